@@ -1,0 +1,127 @@
+/*
+ * lss_hip.h -- C ABI of the MI355X (gfx950) Lift-Splat hot path.
+ *
+ * Drop-in boundary for the reference's hot path (shdragron/LSS-Carla,
+ * src/models.py + src/tools.py). Every entry point takes plain device
+ * pointers and sizes, is asynchronous on the caller's HIP stream, never
+ * synchronises, never allocates, and returns 0 on success, a positive
+ * hipError_t on a launch failure, or a negative LSS_E* code for bad
+ * arguments. No exceptions cross the ABI; there is no global mutable state.
+ * Thread-safe for distinct streams.
+ *
+ * Index conventions (all int32):
+ *   point  p = ((bn*D + d)*H + h)*W + w,   bn = b*N + n      (reference flatten order,
+ *                                                              src/models.py:205-209)
+ *   pixel  q = bn*H*W + h*W + w
+ *   cell   k = ((b*Z + z)*X + x)*Y + y,    -1 = dropped     (griddify order,
+ *                                                              src/models.py:240-244)
+ * H, W are the feature-map sizes (fH, fW = final_dim / 16). C must be 64
+ * (camC is hard-coded, src/models.py:148); D <= 64.
+ */
+#ifndef LSS_HIP_H
+#define LSS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSS_ABI_VERSION 1
+
+typedef struct lss_dims {
+    int32_t B, N, D, H, W, C;
+} lss_dims_t;
+
+/* Voxel grid: lo = bx - dx/2 (fp32, src/models.py:212), dx, nx = (X, Y, Z). */
+typedef struct lss_grid {
+    float lo[3];
+    float dx[3];
+    int32_t nx[3];
+} lss_grid_t;
+
+enum { LSS_F32 = 0, LSS_BF16 = 1 };          /* element types */
+enum { LSS_NCHW = 0, LSS_NHWC = 1 };         /* BEV memory layouts of a (B, Z*C, X, Y) tensor */
+enum { LSS_EINVAL = -1, LSS_EUNSUPPORTED = -2 };
+
+typedef void* lss_stream_t; /* a hipStream_t */
+
+int lss_abi_version(void);
+const char* lss_error_string(int code);
+
+/* Device 3x3 inverses of post_rots and intrins (fp64 adjugate, rounded to fp32).
+ * Replaces torch.inverse(post_rots.cpu()) / torch.inverse(intrins.cpu())
+ * of src/models.py:180,186 without a device->host round trip. */
+int lss_camera_inverse(const float* post_rots, const float* intrins, int32_t n_cams,
+                       float* pinv, float* kinv, lss_stream_t stream);
+
+/* get_geometry (src/models.py:170-190) fused with quantise + bounds filter
+ * (src/models.py:211-223). fp32, sequential non-FMA mat-vecs, IEEE division,
+ * truncation toward zero. out_geom (Nprime*3) may be NULL. cell_of (Nprime)
+ * receives the cell id or -1. If cell_count is non-NULL it must be zeroed
+ * (B*Z*X*Y ints); each kept point atomically increments its cell's count and
+ * slot_of[p] receives the pre-increment value (its slot inside the cell). */
+int lss_geometry_cells(const float* frustum, const float* rots, const float* trans,
+                       const float* kinv, const float* pinv, const float* post_trans,
+                       const lss_dims_t* dims, const lss_grid_t* grid,
+                       float* out_geom, int32_t* cell_of, int32_t* cell_count, int32_t* slot_of,
+                       lss_stream_t stream);
+
+/* Quantise a given (Nprime, 3) fp32 geometry (voxel_pooling(geom_feats, x) boundary,
+ * src/models.py:204-223). Same outputs as lss_geometry_cells; points_per_batch =
+ * Nprime / B (src/models.py:214). */
+int lss_cells_from_geom(const float* geom, int32_t nprime, int32_t points_per_batch,
+                        const lss_grid_t* grid, int32_t* cell_of, int32_t* cell_count,
+                        int32_t* slot_of, lss_stream_t stream);
+
+/* Counting-sort CSR of points by cell (replaces ranks + argsort, src/models.py:225-231):
+ * cell_start (ncells+1) = exclusive scan of cell_count, sorted_pt (Nprime) = point ids
+ * grouped by cell. scratch: lss_csr_scratch_bytes(ncells) bytes. */
+size_t lss_csr_scratch_bytes(int32_t ncells);
+int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime,
+                  const int32_t* cell_count, int32_t ncells, int32_t* cell_start,
+                  int32_t* sorted_pt, void* scratch, lss_stream_t stream);
+
+/* Lift, part 1 (CamEncode.get_depth_dist + layout, src/models.py:49-59, 192-202):
+ * depth (B*N, D, H, W) fp32 = softmax over D of depthnet_out[:, :D];
+ * ctx_t (B*N*H*W, C) fp32 = depthnet_out[:, D:D+C] moved to pixel-major rows.
+ * depthnet_out is (B*N, D+C, H, W) contiguous, element type in_dtype. */
+int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims,
+                  float* depth, float* ctx_t, lss_stream_t stream);
+
+/* Splat forward: segmented per-cell sum written as the dense (B, Z*C, X, Y) BEV
+ * (voxel_pooling + QuickCumsum.forward + griddify, src/models.py:233-246,
+ * src/tools.py:195-209). Fused mode (x_rows == NULL): contribution of point p to
+ * channel c is depth[p] * ctx_t[q(p), c] (the lift's outer product, never
+ * materialised). Lifted mode (depth == ctx_t == NULL): x_rows is (Nprime, C) fp32.
+ * Points of a cell are summed in ascending point id (deterministic). Empty cells
+ * are written as zeros; every element of out is written. */
+int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows,
+                  const int32_t* cell_start, const int32_t* sorted_pt,
+                  const lss_dims_t* dims, const lss_grid_t* grid,
+                  void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream);
+
+/* Backward helpers. A "row" is the C gradient values of one cell.
+ * lss_bev_rows: NCHW dbev -> rows[cell*C + c] for every occupied cell (others untouched). */
+int lss_bev_rows(const void* dbev, int32_t g_dtype, const int32_t* cell_start,
+                 const lss_dims_t* dims, const lss_grid_t* grid, void* rows, lss_stream_t stream);
+
+/* Fused splat + lift backward (QuickCumsum.backward gather, src/tools.py:212-219,
+ * then the outer-product and softmax backward of src/models.py:58-59):
+ * d_depthnet_out (B*N, D+C, H, W), element type d_dtype. rows_layout LSS_NHWC means
+ * g is the channels-last dbev itself; LSS_NCHW means g is the rows buffer of lss_bev_rows. */
+int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int32_t* cell_of,
+                  const float* depth, const float* ctx_t, const lss_dims_t* dims,
+                  const lss_grid_t* grid, void* d_depthnet_out, int32_t d_dtype,
+                  lss_stream_t stream);
+
+/* Lifted-mode backward: dx[p, c] = g_row(cell_of[p])[c], 0 for dropped points (Nprime, C) fp32. */
+int lss_splat_bwd_lifted(const void* g, int32_t g_dtype, int32_t rows_layout, const int32_t* cell_of,
+                         int32_t nprime, const lss_dims_t* dims, const lss_grid_t* grid,
+                         float* dx, lss_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LSS_HIP_H */

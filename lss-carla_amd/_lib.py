@@ -1,0 +1,96 @@
+"""ctypes binding of ``liblss_hip.so`` (the C ABI of ``include/lss_hip.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or
+``python -m lss_carla_amd.build``). There is no fallback: if the library is
+missing or a call fails, a RuntimeError is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch  # noqa: F401  -- loads the HIP runtime (soname libamdhip64.so.7) before our library
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblss_hip.so")
+
+F32, BF16 = 0, 1
+NCHW, NHWC = 0, 1
+ABI_VERSION = 1
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int32), ("N", ctypes.c_int32), ("D", ctypes.c_int32),
+                ("H", ctypes.c_int32), ("W", ctypes.c_int32), ("C", ctypes.c_int32)]
+
+
+class Grid(ctypes.Structure):
+    _fields_ = [("lo", ctypes.c_float * 3), ("dx", ctypes.c_float * 3), ("nx", ctypes.c_int32 * 3)]
+
+
+_p = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_DIMS = ctypes.POINTER(Dims)
+_GRID = ctypes.POINTER(Grid)
+
+# name -> (restype, argtypes); must match include/lss_hip.h exactly.
+SIGNATURES = {
+    "lss_abi_version": (ctypes.c_int, []),
+    "lss_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "lss_camera_inverse": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p]),
+    "lss_geometry_cells": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _p, _p, _p, _p]),
+    "lss_cells_from_geom": (ctypes.c_int, [_p, _i32, _i32, _GRID, _p, _p, _p, _p]),
+    "lss_csr_scratch_bytes": (ctypes.c_size_t, [_i32]),
+    "lss_csr_build": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _p, _p, _p, _p]),
+    "lss_lift_prep": (ctypes.c_int, [_p, _i32, _DIMS, _p, _p, _p]),
+    "lss_splat_fwd": (ctypes.c_int, [_p, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _p]),
+    "lss_bev_rows": (ctypes.c_int, [_p, _i32, _p, _DIMS, _GRID, _p, _p]),
+    "lss_splat_bwd": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p, _DIMS, _GRID, _p, _i32, _p]),
+    "lss_splat_bwd_lifted": (ctypes.c_int, [_p, _i32, _i32, _p, _i32, _DIMS, _GRID, _p, _p]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and type the library; raise if it is absent or of another ABI."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"lss_carla_amd: HIP library not found at {LIB_PATH}. Build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950). "
+            "There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.lss_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"lss_carla_amd: ABI mismatch ({lib.lss_abi_version()} != {ABI_VERSION}); rebuild")
+    _lib = lib
+    return lib
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        msg = load().lss_error_string(code)
+        raise RuntimeError(f"{what} failed: {msg.decode() if msg else code} (code {code})")
+
+
+def ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise RuntimeError(f"lss_carla_amd: unsupported dtype {dt} (float32 / bfloat16 only)")

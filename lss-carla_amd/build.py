@@ -1,0 +1,58 @@
+"""Build ``liblss_hip.so`` in-tree with hipcc for gfx950.
+
+``python -m lss_carla_amd.build`` or ``__graft_entry__.build()``. The shared
+library lands next to this file so it travels with the repo snapshot to the
+GPU box (it is git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+SOURCES = [os.path.join(HERE, "csrc", "lss_hip.hip")]
+HEADERS = [os.path.join(REPO, "include", "lss_hip.h")]
+OUT = os.path.join(HERE, "liblss_hip.so")
+ARCH = os.environ.get("LSS_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build liblss_hip.so)")
+
+
+def command():
+    # -ffp-contract=off: the geometry must keep the reference's un-fused fp32 op order.
+    return [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+            "-Wall", "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}", "-o", OUT] + SOURCES
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(s) <= t for s in SOURCES + HEADERS + [__file__])
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and up_to_date():
+        return OUT
+    cmd = command()
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"hipcc failed ({r.returncode}) building {OUT}")
+    if verbose and r.stderr.strip():
+        sys.stderr.write(r.stderr)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

@@ -1,0 +1,742 @@
+// lss_hip.hip -- gfx950 (MI355X / CDNA4) kernels of the Lift-Splat hot path + C ABI.
+//
+// Compiled with -ffp-contract=off: the geometry must reproduce the reference's
+// un-fused fp32 arithmetic bit for bit. Kernels that may
+// fuse say so explicitly.
+//
+// Pipeline (forward, one training step):
+//   lss_camera_inverse      48 cameras, fp64 adjugate
+//   lss_geometry_cells      1 thread / point: frustum -> ego xyz -> cell id, atomic count
+//   lss_csr_build           counting sort: block reduce -> scan -> scatter
+//   lss_lift_prep           1 block / 64 pixels: depth softmax + context -> pixel-major rows
+//   lss_splat_fwd           1 block / (b, z, x, y-tile): per-cell ordered sum -> LDS -> dense
+//                           coalesced BEV write (zero fill fused)   <- the HBM-bound kernel
+// Backward:
+//   lss_bev_rows            NCHW dbev -> compact per-cell rows (occupied cells only)
+//   lss_splat_bwd           1 wave / pixel: gather D rows to LDS, d_ctx, d_depth, softmax bwd
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <limits.h>
+#include <stdint.h>
+
+#include "lss_hip.h"
+
+namespace {
+
+constexpr int kC = 64;       // camC (src/models.py:148)
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kScanItems = 4096;  // cells per scan block (1024 threads x 4)
+
+using bf16 = __hip_bfloat16;
+
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(bf16 v) { return __bfloat162float(v); }
+
+template <typename T> __device__ __forceinline__ T from_f32(float v);
+template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float v) { return __float2bfloat16(v); }
+
+// 4 consecutive elements, 16 B (fp32) or 8 B (bf16) store.
+__device__ __forceinline__ void store4(float* dst, float a, float b, float c, float d) {
+    *reinterpret_cast<float4*>(dst) = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ void store4(bf16* dst, float a, float b, float c, float d) {
+    bf16 v[4] = {__float2bfloat16(a), __float2bfloat16(b), __float2bfloat16(c), __float2bfloat16(d)};
+    *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(v);
+}
+
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, kWave));
+    return v;
+}
+
+// acc = 0; for k: acc = acc + m[k] * v[k]   -- fp32, each op rounded (CPU torch.matmul order).
+__device__ __forceinline__ float dot3_seq(float m0, float m1, float m2, float v0, float v1, float v2) {
+    float acc = __fmul_rn(m0, v0);
+    acc = __fadd_rn(acc, __fmul_rn(m1, v1));
+    return __fadd_rn(acc, __fmul_rn(m2, v2));
+}
+
+// ----------------------------------------------------------------------------- camera inverse
+__global__ __launch_bounds__(kBlock) void k_camera_inverse(const float* __restrict__ post_rots,
+                                                           const float* __restrict__ intrins, int n_cams,
+                                                           float* __restrict__ pinv, float* __restrict__ kinv) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * n_cams) return;
+    const float* M = i < n_cams ? post_rots + 9 * i : intrins + 9 * (i - n_cams);
+    float* O = i < n_cams ? pinv + 9 * i : kinv + 9 * (i - n_cams);
+    double a[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a[k] = (double)M[k];
+    const double c00 = a[4] * a[8] - a[5] * a[7];
+    const double c01 = a[5] * a[6] - a[3] * a[8];
+    const double c02 = a[3] * a[7] - a[4] * a[6];
+    const double det = a[0] * c00 + a[1] * c01 + a[2] * c02;
+    const double inv[9] = {
+        c00, a[2] * a[7] - a[1] * a[8], a[1] * a[5] - a[2] * a[4],
+        c01, a[0] * a[8] - a[2] * a[6], a[2] * a[3] - a[0] * a[5],
+        c02, a[1] * a[6] - a[0] * a[7], a[0] * a[4] - a[1] * a[3],
+    };
+#pragma unroll
+    for (int k = 0; k < 9; ++k) O[k] = (float)(inv[k] / det);
+}
+
+// ----------------------------------------------------------------------------- geometry -> cells
+__device__ __forceinline__ int quantize_cell(float ex, float ey, float ez, const lss_grid_t& g, int b) {
+    // ((geom - (bx - dx/2)) / dx).long() + bounds filter (src/models.py:212-223).
+    // trunc(v) in [0, n)  <=>  v > -1 && v < n   (NaN fails both).
+    const float vx = __fdiv_rn(__fsub_rn(ex, g.lo[0]), g.dx[0]);
+    const float vy = __fdiv_rn(__fsub_rn(ey, g.lo[1]), g.dx[1]);
+    const float vz = __fdiv_rn(__fsub_rn(ez, g.lo[2]), g.dx[2]);
+    const bool ok = vx > -1.0f && vx < (float)g.nx[0] && vy > -1.0f && vy < (float)g.nx[1] &&
+                    vz > -1.0f && vz < (float)g.nx[2];
+    if (!ok) return -1;
+    const int ix = (int)vx, iy = (int)vy, iz = (int)vz;  // truncation toward zero
+    return ((b * g.nx[2] + iz) * g.nx[0] + ix) * g.nx[1] + iy;
+}
+
+__device__ __forceinline__ void emit_cell(int p, int cell, int32_t* cell_of, int32_t* cell_count, int32_t* slot_of) {
+    cell_of[p] = cell;
+    if (cell_count != nullptr) {
+        int slot = -1;
+        if (cell >= 0) slot = atomicAdd(cell_count + cell, 1);
+        slot_of[p] = slot;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_geometry_cells(
+    const float* __restrict__ frustum, const float* __restrict__ rots, const float* __restrict__ trans,
+    const float* __restrict__ kinv, const float* __restrict__ pinv, const float* __restrict__ post_trans,
+    int N, int DHW, int nprime, lss_grid_t g, float* __restrict__ out_geom, int32_t* __restrict__ cell_of,
+    int32_t* __restrict__ cell_count, int32_t* __restrict__ slot_of) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= nprime) return;
+    const int cam = p / DHW;
+    const int f = p - cam * DHW;
+    const int b = cam / N;
+    const float* P = pinv + 9 * cam;
+    const float* K = kinv + 9 * cam;
+    const float* R = rots + 9 * cam;
+    // points = frustum - post_trans                         (src/models.py:179)
+    const float x0 = __fsub_rn(frustum[3 * f + 0], post_trans[3 * cam + 0]);
+    const float x1 = __fsub_rn(frustum[3 * f + 1], post_trans[3 * cam + 1]);
+    const float x2 = __fsub_rn(frustum[3 * f + 2], post_trans[3 * cam + 2]);
+    // points = inv(post_rots) @ points                      (src/models.py:180)
+    const float q0 = dot3_seq(P[0], P[1], P[2], x0, x1, x2);
+    const float q1 = dot3_seq(P[3], P[4], P[5], x0, x1, x2);
+    const float q2 = dot3_seq(P[6], P[7], P[8], x0, x1, x2);
+    // (x*z, y*z, z)                                         (src/models.py:183-185)
+    const float r0 = __fmul_rn(q0, q2), r1 = __fmul_rn(q1, q2), r2 = q2;
+    // combine = rots @ inv(intrins); points = combine @ points + trans   (src/models.py:186-188)
+    float e[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float c0 = dot3_seq(R[3 * i + 0], R[3 * i + 1], R[3 * i + 2], K[0], K[3], K[6]);
+        const float c1 = dot3_seq(R[3 * i + 0], R[3 * i + 1], R[3 * i + 2], K[1], K[4], K[7]);
+        const float c2 = dot3_seq(R[3 * i + 0], R[3 * i + 1], R[3 * i + 2], K[2], K[5], K[8]);
+        e[i] = __fadd_rn(dot3_seq(c0, c1, c2, r0, r1, r2), trans[3 * cam + i]);
+    }
+    if (out_geom != nullptr) {
+        out_geom[3 * (size_t)p + 0] = e[0];
+        out_geom[3 * (size_t)p + 1] = e[1];
+        out_geom[3 * (size_t)p + 2] = e[2];
+    }
+    emit_cell(p, quantize_cell(e[0], e[1], e[2], g, b), cell_of, cell_count, slot_of);
+}
+
+__global__ __launch_bounds__(kBlock) void k_cells_from_geom(const float* __restrict__ geom, int nprime, int ppb,
+                                                            lss_grid_t g, int32_t* __restrict__ cell_of,
+                                                            int32_t* __restrict__ cell_count,
+                                                            int32_t* __restrict__ slot_of) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= nprime) return;
+    const int cell = quantize_cell(geom[3 * (size_t)p], geom[3 * (size_t)p + 1], geom[3 * (size_t)p + 2], g, p / ppb);
+    emit_cell(p, cell, cell_of, cell_count, slot_of);
+}
+
+// ----------------------------------------------------------------------------- CSR (counting sort)
+// Exclusive scan of 1024 thread totals inside a block; returns the thread's exclusive prefix.
+__device__ int block_exclusive_scan_1024(int v, int* s_wave, int* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, kWave);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    if (wave == 0) {
+        int w = lane < 16 ? s_wave[lane] : 0;
+        int wi = w;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const int t = __shfl_up(wi, o, kWave);
+            if (lane >= o) wi += t;
+        }
+        if (lane < 16) s_wave[16 + lane] = wi - w;
+        if (lane == 15) *total = wi;
+    }
+    __syncthreads();
+    return s_wave[16 + wave] + incl - v;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_partials(const int32_t* __restrict__ cnt, int ncells,
+                                                        int32_t* __restrict__ partial) {
+    __shared__ int s_wave[32];
+    __shared__ int s_total;
+    const int base = blockIdx.x * kScanItems + threadIdx.x * 4;
+    int v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v += (base + i < ncells) ? cnt[base + i] : 0;
+    block_exclusive_scan_1024(v, s_wave, &s_total);
+    if (threadIdx.x == 0) partial[blockIdx.x] = s_total;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_apply(const int32_t* __restrict__ cnt, int ncells,
+                                                     const int32_t* __restrict__ partial,
+                                                     int32_t* __restrict__ cell_start) {
+    __shared__ int s_wave[32];
+    __shared__ int s_total;
+    __shared__ int s_red[16];
+    // prefix = sum of the preceding blocks' totals
+    int pre = 0;
+    for (int i = threadIdx.x; i < (int)blockIdx.x; i += 1024) pre += partial[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, kWave);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = pre;
+    __syncthreads();
+    int prefix = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) prefix += s_red[w];
+    const int base = blockIdx.x * kScanItems + threadIdx.x * 4;
+    int c[4];
+    int v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        c[i] = (base + i < ncells) ? cnt[base + i] : 0;
+        v += c[i];
+    }
+    int run = prefix + block_exclusive_scan_1024(v, s_wave, &s_total);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (base + i < ncells) cell_start[base + i] = run;
+        run += c[i];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) cell_start[ncells] = prefix + s_total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ cell_of,
+                                                    const int32_t* __restrict__ slot_of, int nprime,
+                                                    const int32_t* __restrict__ cell_start,
+                                                    int32_t* __restrict__ sorted_pt) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= nprime) return;
+    const int cell = cell_of[p];
+    if (cell >= 0) sorted_pt[cell_start[cell] + slot_of[p]] = p;
+}
+
+// ----------------------------------------------------------------------------- lift prep
+// One block = 64 consecutive pixels. depth = softmax_D(logits) written in the reference's
+// (B*N, D, H, W) layout (coalesced over pixels); context transposed through LDS to
+// pixel-major rows ctx_t[q*64 + c] (coalesced 256-B rows).
+template <typename InT>
+__global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn, int D, int HW, int npix,
+                                                      float* __restrict__ depth, float* __restrict__ ctx_t) {
+    __shared__ float s_ctx[kC][65];
+    const int q0 = blockIdx.x * 64;
+    const int t = threadIdx.x;
+    const int DC = D + kC;
+    {
+        const int px = t & 63;
+        const int q = q0 + px;
+        if (q < npix) {
+            const int bn = q / HW, hw = q - bn * HW;
+            const InT* src = dn + ((size_t)bn * DC + D) * HW + hw;
+            for (int c = t >> 6; c < kC; c += 4) s_ctx[c][px] = to_f32(src[(size_t)c * HW]);
+        }
+    }
+    if (t < 64) {
+        const int q = q0 + t;
+        if (q < npix) {
+            const int bn = q / HW, hw = q - bn * HW;
+            const InT* src = dn + (size_t)bn * DC * HW + hw;
+            float m = -INFINITY;
+            for (int d = 0; d < D; ++d) m = fmaxf(m, to_f32(src[(size_t)d * HW]));
+            float s = 0.f;
+            for (int d = 0; d < D; ++d) s += expf(to_f32(src[(size_t)d * HW]) - m);
+            float* dst = depth + (size_t)bn * D * HW + hw;
+            for (int d = 0; d < D; ++d) dst[(size_t)d * HW] = expf(to_f32(src[(size_t)d * HW]) - m) / s;
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < 64 * kC; i += kBlock) {
+        const int px = i >> 6, c = i & 63;
+        if (q0 + px < npix) ctx_t[(size_t)(q0 + px) * kC + c] = s_ctx[c][px];
+    }
+}
+
+// ----------------------------------------------------------------------------- splat forward
+struct SplatGeo {
+    int X, Y, Z, YT, ntiles_y;
+};
+
+// Sum over the points of one cell, in ascending point id, lane = channel.
+template <bool FUSED>
+__device__ __forceinline__ float cell_sum(int cs, int n, const int32_t* __restrict__ sorted_pt,
+                                          const float* __restrict__ depth, const float* __restrict__ ctx_t,
+                                          const float* __restrict__ xrows, int DHW, int HW, int lane) {
+    float acc = 0.f;
+    auto contrib = [&](int p) -> float {
+        if (FUSED) {
+            const int cam = p / DHW;
+            const int q = cam * HW + (p - cam * DHW) % HW;
+            return __fmul_rn(depth[p], ctx_t[(size_t)q * kC + lane]);  // the lift's new_x element
+        } else {
+            return xrows[(size_t)p * kC + lane];
+        }
+    };
+    if (n <= kWave) {
+        // rank each lane's id among the cell's ids, permute so lane k holds the k-th smallest.
+        const int id = lane < n ? sorted_pt[cs + lane] : INT_MAX;
+        int rank = 0;
+        for (int j = 0; j < n; ++j) rank += (__builtin_amdgcn_readlane(id, j) < id) ? 1 : 0;
+        const int sid = __builtin_amdgcn_ds_permute(rank << 2, id);
+        int k = 0;
+        for (; k + 4 <= n; k += 4) {
+            const float v0 = contrib(__builtin_amdgcn_readlane(sid, k));
+            const float v1 = contrib(__builtin_amdgcn_readlane(sid, k + 1));
+            const float v2 = contrib(__builtin_amdgcn_readlane(sid, k + 2));
+            const float v3 = contrib(__builtin_amdgcn_readlane(sid, k + 3));
+            acc = __fadd_rn(acc, v0);
+            acc = __fadd_rn(acc, v1);
+            acc = __fadd_rn(acc, v2);
+            acc = __fadd_rn(acc, v3);
+        }
+        for (; k < n; ++k) acc = __fadd_rn(acc, contrib(__builtin_amdgcn_readlane(sid, k)));
+    } else {
+        // rare: more points than lanes -- ordered selection over the global list.
+        int last = -1;
+        for (int k = 0; k < n; ++k) {
+            int best = INT_MAX;
+            for (int i = lane; i < n; i += kWave) {
+                const int v = sorted_pt[cs + i];
+                if (v > last && v < best) best = v;
+            }
+            best = uniform(wave_min(best));
+            acc = __fadd_rn(acc, contrib(best));
+            last = best;
+        }
+    }
+    return acc;
+}
+
+template <bool FUSED, typename OutT, bool NHWC>
+__global__ __launch_bounds__(kBlock) void k_splat_fwd(const float* __restrict__ depth,
+                                                      const float* __restrict__ ctx_t,
+                                                      const float* __restrict__ xrows,
+                                                      const int32_t* __restrict__ cell_start,
+                                                      const int32_t* __restrict__ sorted_pt, int DHW, int HW,
+                                                      SplatGeo sg, OutT* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int tile = blockIdx.x;
+    const int bzx = tile / sg.ntiles_y;
+    const int y0 = (tile - bzx * sg.ntiles_y) * sg.YT;
+    const int ny = min(sg.YT, sg.Y - y0);
+    const int x = bzx % sg.X;
+    const int bz = bzx / sg.X;
+    const int z = bz % sg.Z, b = bz / sg.Z;
+    const int cell0 = bzx * sg.Y + y0;
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    const int S = NHWC ? kC : sg.YT + 4;  // LDS row stride (floats)
+    const bool empty = uniform(cell_start[cell0]) == uniform(cell_start[cell0 + ny]);
+
+    if (!empty) {
+        for (int yy = wave; yy < ny; yy += kBlock / kWave) {
+            const int cs = uniform(cell_start[cell0 + yy]);
+            const int n = uniform(cell_start[cell0 + yy + 1]) - cs;
+            const float acc = n > 0 ? cell_sum<FUSED>(cs, n, sorted_pt, depth, ctx_t, xrows, DHW, HW, lane) : 0.f;
+            if (NHWC) lds[yy * kC + lane] = acc;
+            else lds[lane * S + yy] = acc;
+        }
+        __syncthreads();
+    }
+
+    if (NHWC) {
+        // cell (b, z, x, y) row = out[((b*X + x)*Y + y)*Z*C + z*C + c]
+        const size_t zc = (size_t)sg.Z * kC;
+        OutT* obase = out + (((size_t)b * sg.X + x) * sg.Y + y0) * zc + (size_t)z * kC;
+        for (int i = threadIdx.x; i < ny * (kC / 4); i += kBlock) {
+            const int yy = i >> 4, j = (i & 15) * 4;
+            if (empty) {
+                store4(obase + yy * zc + j, 0.f, 0.f, 0.f, 0.f);
+            } else {
+                const float4 v = *reinterpret_cast<const float4*>(lds + yy * kC + j);
+                store4(obase + yy * zc + j, v.x, v.y, v.z, v.w);
+            }
+        }
+    } else {
+        const size_t XY = (size_t)sg.X * sg.Y;
+        OutT* obase = out + (size_t)bz * kC * XY + (size_t)x * sg.Y + y0;
+        if ((sg.Y & 3) == 0 && (ny & 3) == 0) {
+            const int nq = ny >> 2;
+            for (int i = threadIdx.x; i < kC * nq; i += kBlock) {
+                const int c = i / nq, j = (i - c * nq) * 4;
+                if (empty) {
+                    store4(obase + c * XY + j, 0.f, 0.f, 0.f, 0.f);
+                } else {
+                    const float4 v = *reinterpret_cast<const float4*>(lds + c * S + j);
+                    store4(obase + c * XY + j, v.x, v.y, v.z, v.w);
+                }
+            }
+        } else {
+            for (int i = threadIdx.x; i < kC * ny; i += kBlock) {
+                const int c = i / ny, yy = i - c * ny;
+                obase[c * XY + yy] = from_f32<OutT>(empty ? 0.f : lds[c * S + yy]);
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------- backward
+template <typename GT>
+__global__ __launch_bounds__(kBlock) void k_bev_rows(const GT* __restrict__ dbev, const int32_t* __restrict__ cell_start,
+                                                     SplatGeo sg, GT* __restrict__ rows) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int tile = blockIdx.x;
+    const int bzx = tile / sg.ntiles_y;
+    const int y0 = (tile - bzx * sg.ntiles_y) * sg.YT;
+    const int ny = min(sg.YT, sg.Y - y0);
+    const int x = bzx % sg.X;
+    const int bz = bzx / sg.X;
+    const int cell0 = bzx * sg.Y + y0;
+    if (uniform(cell_start[cell0]) == uniform(cell_start[cell0 + ny])) return;  // nothing pooled here
+    const int S = sg.YT + 1;
+    const size_t XY = (size_t)sg.X * sg.Y;
+    const GT* gbase = dbev + (size_t)bz * kC * XY + (size_t)x * sg.Y + y0;
+    for (int i = threadIdx.x; i < kC * ny; i += kBlock) {
+        const int c = i / ny, yy = i - c * ny;
+        lds[c * S + yy] = to_f32(gbase[c * XY + yy]);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    for (int yy = wave; yy < ny; yy += kBlock / kWave) {
+        const int cell = cell0 + yy;
+        if (uniform(cell_start[cell + 1]) > uniform(cell_start[cell]))
+            rows[(size_t)cell * kC + lane] = from_f32<GT>(lds[lane * S + yy]);
+    }
+}
+
+// Offset of cell k's gradient row: compact rows buffer, or the channels-last dbev itself.
+template <bool NHWC>
+__device__ __forceinline__ size_t row_offset(int cell, const SplatGeo& sg) {
+    if (!NHWC) return (size_t)cell * kC;
+    const int XY = sg.X * sg.Y;
+    const int bz = cell / XY, xy = cell - bz * XY;
+    const int b = bz / sg.Z, z = bz - b * sg.Z;
+    return (((size_t)b * XY + xy) * sg.Z + z) * kC;
+}
+
+// One wave per pixel: the D gradient rows of the pixel's points are gathered into LDS,
+// then (lane = channel) d_ctx[c] = sum_d g[d][c] depth[d], and (lane = depth bin)
+// d_depth[d] = sum_c g[d][c] ctx[c]; softmax backward; write d_depthnet_out.
+template <typename GT, typename DT, bool NHWC>
+__global__ __launch_bounds__(kBlock) void k_splat_bwd(const GT* __restrict__ g, const int32_t* __restrict__ cell_of,
+                                                      const float* __restrict__ depth,
+                                                      const float* __restrict__ ctx_t, int D, int HW, int npix,
+                                                      SplatGeo sg, DT* __restrict__ d_dn) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    const int RS = kC + 1;                 // LDS row stride: conflict-free column reads
+    float* R = lds + wave * (D * RS + kC);  // D rows of this wave's pixel
+    float* cx = R + D * RS;                // the pixel's context row
+    const int q = blockIdx.x * (kBlock / kWave) + wave;
+    const bool live = q < npix;
+    const int bn = live ? q / HW : 0, hw = live ? q - bn * HW : 0;
+    const size_t pbase = (size_t)bn * D * HW + hw;  // point (bn, d=0, hw)
+    float my_depth = 0.f;
+    int my_cell = -1;
+    if (live) {
+        if (lane < D) {
+            my_depth = depth[pbase + (size_t)lane * HW];
+            my_cell = cell_of[pbase + (size_t)lane * HW];
+        }
+        cx[lane] = ctx_t[(size_t)q * kC + lane];
+        int d = 0;
+        for (; d + 4 <= D; d += 4) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int cell = __builtin_amdgcn_readlane(my_cell, d + u);
+                v[u] = cell >= 0 ? to_f32(g[row_offset<NHWC>(cell, sg) + lane]) : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) R[(d + u) * RS + lane] = v[u];
+        }
+        for (; d < D; ++d) {
+            const int cell = __builtin_amdgcn_readlane(my_cell, d);
+            R[d * RS + lane] = cell >= 0 ? to_f32(g[row_offset<NHWC>(cell, sg) + lane]) : 0.f;
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    // d_ctx (lane = c): sum over depth bins in order d = 0..D-1
+    float dctx = 0.f;
+    for (int d = 0; d < D; ++d) dctx = fmaf(R[d * RS + lane], readlane_f(my_depth, d), dctx);
+    // d_depth (lane = d): sum over channels
+    float dd = 0.f;
+    if (lane < D) {
+        const float* row = R + lane * RS;
+        for (int c = 0; c < kC; ++c) dd = fmaf(row[c], cx[c], dd);
+    }
+    // softmax backward: dl = depth * (dd - sum_d depth*dd)
+    const float s = wave_sum(my_depth * dd);
+    const float dl = my_depth * (dd - s);
+    const int DC = D + kC;
+    DT* dst = d_dn + (size_t)bn * DC * HW + hw;
+    if (lane < D) dst[(size_t)lane * HW] = from_f32<DT>(dl);
+    dst[(size_t)(D + lane) * HW] = from_f32<DT>(dctx);
+}
+
+template <typename GT, bool NHWC>
+__global__ __launch_bounds__(kBlock) void k_splat_bwd_lifted(const GT* __restrict__ g, const int32_t* __restrict__ cell_of,
+                                                             int nprime, SplatGeo sg, float* __restrict__ dx) {
+    const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+    const int p = (int)(i >> 4);
+    if (p >= nprime) return;
+    const int j = (int)(i & 15) * 4;
+    const int cell = cell_of[p];
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (cell >= 0) {
+        const GT* r = g + row_offset<NHWC>(cell, sg) + j;
+        v = make_float4(to_f32(r[0]), to_f32(r[1]), to_f32(r[2]), to_f32(r[3]));
+    }
+    *reinterpret_cast<float4*>(dx + (size_t)p * kC + j) = v;
+}
+
+// ----------------------------------------------------------------------------- host helpers
+inline int grid_blocks(long n, int per) { return (int)((n + per - 1) / per); }
+
+inline int choose_yt(int Y) {
+    if (Y <= 128) return Y;
+    for (int t = 128; t >= 16; t -= 4)
+        if (Y % t == 0) return t;
+    return 128;
+}
+
+inline SplatGeo splat_geo(const lss_grid_t* g) {
+    SplatGeo s;
+    s.X = g->nx[0];
+    s.Y = g->nx[1];
+    s.Z = g->nx[2];
+    s.YT = choose_yt(s.Y);
+    s.ntiles_y = (s.Y + s.YT - 1) / s.YT;
+    return s;
+}
+
+inline int launch_status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+inline bool dims_ok(const lss_dims_t* d) {
+    return d && d->B > 0 && d->N > 0 && d->D > 0 && d->H > 0 && d->W > 0 && d->C == kC;
+}
+
+inline bool grid_ok(const lss_grid_t* g) {
+    return g && g->nx[0] > 0 && g->nx[1] > 0 && g->nx[2] > 0 && g->dx[0] > 0.f && g->dx[1] > 0.f && g->dx[2] > 0.f;
+}
+
+}  // namespace
+
+// ============================================================================= C ABI
+extern "C" {
+
+int lss_abi_version(void) { return LSS_ABI_VERSION; }
+
+const char* lss_error_string(int code) {
+    if (code == 0) return "success";
+    if (code == LSS_EINVAL) return "lss: invalid argument";
+    if (code == LSS_EUNSUPPORTED) return "lss: unsupported configuration (need C == 64, D <= 64)";
+    if (code > 0) return hipGetErrorString((hipError_t)code);
+    return "lss: unknown error";
+}
+
+int lss_camera_inverse(const float* post_rots, const float* intrins, int32_t n_cams, float* pinv, float* kinv,
+                       lss_stream_t stream) {
+    if (!post_rots || !intrins || !pinv || !kinv || n_cams <= 0) return LSS_EINVAL;
+    hipLaunchKernelGGL(k_camera_inverse, dim3(grid_blocks(2L * n_cams, kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, post_rots, intrins, n_cams, pinv, kinv);
+    return launch_status();
+}
+
+int lss_geometry_cells(const float* frustum, const float* rots, const float* trans, const float* kinv,
+                       const float* pinv, const float* post_trans, const lss_dims_t* dims, const lss_grid_t* grid,
+                       float* out_geom, int32_t* cell_of, int32_t* cell_count, int32_t* slot_of,
+                       lss_stream_t stream) {
+    if (!dims_ok(dims) || !grid_ok(grid) || !frustum || !rots || !trans || !kinv || !pinv || !post_trans || !cell_of)
+        return LSS_EINVAL;
+    if (cell_count && !slot_of) return LSS_EINVAL;
+    const long DHW = (long)dims->D * dims->H * dims->W;
+    const long nprime = (long)dims->B * dims->N * DHW;
+    if (nprime >= INT_MAX) return LSS_EUNSUPPORTED;
+    hipLaunchKernelGGL(k_geometry_cells, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0, (hipStream_t)stream,
+                       frustum, rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW, (int)nprime, *grid, out_geom,
+                       cell_of, cell_count, slot_of);
+    return launch_status();
+}
+
+int lss_cells_from_geom(const float* geom, int32_t nprime, int32_t points_per_batch, const lss_grid_t* grid,
+                        int32_t* cell_of, int32_t* cell_count, int32_t* slot_of, lss_stream_t stream) {
+    if (!geom || !cell_of || nprime <= 0 || points_per_batch <= 0 || !grid_ok(grid)) return LSS_EINVAL;
+    if (cell_count && !slot_of) return LSS_EINVAL;
+    hipLaunchKernelGGL(k_cells_from_geom, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0, (hipStream_t)stream,
+                       geom, nprime, points_per_batch, *grid, cell_of, cell_count, slot_of);
+    return launch_status();
+}
+
+size_t lss_csr_scratch_bytes(int32_t ncells) {
+    return sizeof(int32_t) * (size_t)((ncells + kScanItems - 1) / kScanItems + 1);
+}
+
+int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, const int32_t* cell_count,
+                  int32_t ncells, int32_t* cell_start, int32_t* sorted_pt, void* scratch, lss_stream_t stream) {
+    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_pt || !scratch || nprime <= 0 || ncells <= 0)
+        return LSS_EINVAL;
+    const int nb = (ncells + kScanItems - 1) / kScanItems;
+    int32_t* partial = static_cast<int32_t*>(scratch);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial);
+    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial, cell_start);
+    hipLaunchKernelGGL(k_scatter, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0, s, cell_of, slot_of, nprime,
+                       cell_start, sorted_pt);
+    return launch_status();
+}
+
+int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims, float* depth, float* ctx_t,
+                  lss_stream_t stream) {
+    if (!dims_ok(dims) || !depthnet_out || !depth || !ctx_t) return LSS_EINVAL;
+    if (dims->D > 64) return LSS_EUNSUPPORTED;
+    const int HW = dims->H * dims->W;
+    const int npix = dims->B * dims->N * HW;
+    const dim3 grid(grid_blocks(npix, 64)), block(kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    if (in_dtype == LSS_F32)
+        hipLaunchKernelGGL(k_lift_prep<float>, grid, block, 0, s, (const float*)depthnet_out, dims->D, HW, npix, depth,
+                           ctx_t);
+    else if (in_dtype == LSS_BF16)
+        hipLaunchKernelGGL(k_lift_prep<bf16>, grid, block, 0, s, (const bf16*)depthnet_out, dims->D, HW, npix, depth,
+                           ctx_t);
+    else
+        return LSS_EINVAL;
+    return launch_status();
+}
+
+int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows, const int32_t* cell_start,
+                  const int32_t* sorted_pt, const lss_dims_t* dims, const lss_grid_t* grid, void* out,
+                  int32_t out_dtype, int32_t out_layout, lss_stream_t stream) {
+    if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_pt || !out) return LSS_EINVAL;
+    const bool fused = x_rows == nullptr;
+    if (fused && (!depth || !ctx_t)) return LSS_EINVAL;
+    const SplatGeo sg = splat_geo(grid);
+    const int DHW = dims->D * dims->H * dims->W;
+    const int HW = dims->H * dims->W;
+    const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
+    const bool nhwc = out_layout == LSS_NHWC;
+    const size_t lds = nhwc ? (size_t)sg.YT * kC * sizeof(float) : (size_t)kC * (sg.YT + 4) * sizeof(float);
+    hipStream_t s = (hipStream_t)stream;
+#define LSS_SPLAT(F, T, L)                                                                                        \
+    hipLaunchKernelGGL((k_splat_fwd<F, T, L>), dim3(nblocks), dim3(kBlock), lds, s, depth, ctx_t, x_rows,         \
+                       cell_start, sorted_pt, DHW, HW, sg, (T*)out)
+    if (out_dtype == LSS_F32) {
+        if (fused) { if (nhwc) LSS_SPLAT(true, float, true); else LSS_SPLAT(true, float, false); }
+        else { if (nhwc) LSS_SPLAT(false, float, true); else LSS_SPLAT(false, float, false); }
+    } else if (out_dtype == LSS_BF16) {
+        if (fused) { if (nhwc) LSS_SPLAT(true, bf16, true); else LSS_SPLAT(true, bf16, false); }
+        else { if (nhwc) LSS_SPLAT(false, bf16, true); else LSS_SPLAT(false, bf16, false); }
+    } else {
+        return LSS_EINVAL;
+    }
+#undef LSS_SPLAT
+    return launch_status();
+}
+
+int lss_bev_rows(const void* dbev, int32_t g_dtype, const int32_t* cell_start, const lss_dims_t* dims,
+                 const lss_grid_t* grid, void* rows, lss_stream_t stream) {
+    if (!dims_ok(dims) || !grid_ok(grid) || !dbev || !cell_start || !rows) return LSS_EINVAL;
+    const SplatGeo sg = splat_geo(grid);
+    const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
+    const size_t lds = (size_t)kC * (sg.YT + 1) * sizeof(float);
+    hipStream_t s = (hipStream_t)stream;
+    if (g_dtype == LSS_F32)
+        hipLaunchKernelGGL(k_bev_rows<float>, dim3(nblocks), dim3(kBlock), lds, s, (const float*)dbev, cell_start, sg,
+                           (float*)rows);
+    else if (g_dtype == LSS_BF16)
+        hipLaunchKernelGGL(k_bev_rows<bf16>, dim3(nblocks), dim3(kBlock), lds, s, (const bf16*)dbev, cell_start, sg,
+                           (bf16*)rows);
+    else
+        return LSS_EINVAL;
+    return launch_status();
+}
+
+int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int32_t* cell_of, const float* depth,
+                  const float* ctx_t, const lss_dims_t* dims, const lss_grid_t* grid, void* d_depthnet_out,
+                  int32_t d_dtype, lss_stream_t stream) {
+    if (!dims_ok(dims) || !grid_ok(grid) || !g || !cell_of || !depth || !ctx_t || !d_depthnet_out) return LSS_EINVAL;
+    if (dims->D > 64) return LSS_EUNSUPPORTED;
+    const SplatGeo sg = splat_geo(grid);
+    const int HW = dims->H * dims->W;
+    const int npix = dims->B * dims->N * HW;
+    const int wpb = kBlock / kWave;
+    const size_t lds = (size_t)wpb * (dims->D * (kC + 1) + kC) * sizeof(float);
+    const dim3 gr(grid_blocks(npix, wpb)), bl(kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    const bool nhwc = rows_layout == LSS_NHWC;
+#define LSS_BWD(GT, DT, L)                                                                                        \
+    hipLaunchKernelGGL((k_splat_bwd<GT, DT, L>), gr, bl, lds, s, (const GT*)g, cell_of, depth, ctx_t, dims->D,    \
+                       HW, npix, sg, (DT*)d_depthnet_out)
+    if (g_dtype == LSS_F32 && d_dtype == LSS_F32) { if (nhwc) LSS_BWD(float, float, true); else LSS_BWD(float, float, false); }
+    else if (g_dtype == LSS_F32 && d_dtype == LSS_BF16) { if (nhwc) LSS_BWD(float, bf16, true); else LSS_BWD(float, bf16, false); }
+    else if (g_dtype == LSS_BF16 && d_dtype == LSS_F32) { if (nhwc) LSS_BWD(bf16, float, true); else LSS_BWD(bf16, float, false); }
+    else if (g_dtype == LSS_BF16 && d_dtype == LSS_BF16) { if (nhwc) LSS_BWD(bf16, bf16, true); else LSS_BWD(bf16, bf16, false); }
+    else return LSS_EINVAL;
+#undef LSS_BWD
+    return launch_status();
+}
+
+int lss_splat_bwd_lifted(const void* g, int32_t g_dtype, int32_t rows_layout, const int32_t* cell_of, int32_t nprime,
+                         const lss_dims_t* dims, const lss_grid_t* grid, float* dx, lss_stream_t stream) {
+    if (!dims_ok(dims) || !grid_ok(grid) || !g || !cell_of || !dx || nprime <= 0) return LSS_EINVAL;
+    const SplatGeo sg = splat_geo(grid);
+    const dim3 gr(grid_blocks(16L * nprime, kBlock)), bl(kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    const bool nhwc = rows_layout == LSS_NHWC;
+    if (g_dtype == LSS_F32) {
+        if (nhwc) hipLaunchKernelGGL((k_splat_bwd_lifted<float, true>), gr, bl, 0, s, (const float*)g, cell_of, nprime, sg, dx);
+        else hipLaunchKernelGGL((k_splat_bwd_lifted<float, false>), gr, bl, 0, s, (const float*)g, cell_of, nprime, sg, dx);
+    } else if (g_dtype == LSS_BF16) {
+        if (nhwc) hipLaunchKernelGGL((k_splat_bwd_lifted<bf16, true>), gr, bl, 0, s, (const bf16*)g, cell_of, nprime, sg, dx);
+        else hipLaunchKernelGGL((k_splat_bwd_lifted<bf16, false>), gr, bl, 0, s, (const bf16*)g, cell_of, nprime, sg, dx);
+    } else {
+        return LSS_EINVAL;
+    }
+    return launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,321 @@
+"""Host orchestration of the HIP hot path: geometry, CSR, fused lift+splat autograd.
+
+Every function here takes device tensors, launches on the current HIP stream
+of that device, never synchronises with the host (except the opt-in
+``inverse='host'`` mode, which mirrors the reference's ``torch.inverse(x.cpu())``
+exactly) and never falls back to another implementation.
+
+Reference boundary replaced (shdragron/LSS-Carla):
+  get_geometry            src/models.py:170-190
+  get_depth_dist/feat     src/models.py:49-61  (lift; fused into the splat)
+  get_cam_feats layout    src/models.py:192-202
+  voxel_pooling           src/models.py:204-246
+  QuickCumsum fwd/bwd     src/tools.py:193-219
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+C_CAM = 64  # camC, src/models.py:148
+
+
+# ----------------------------------------------------------------------------- grid
+@dataclass(frozen=True)
+class GridSpec:
+    """Voxel grid of a grid_conf (``gen_dx_bx``, src/tools.py:174-179; lo = bx - dx/2, src/models.py:212)."""
+    lo: Tuple[float, float, float]
+    dx: Tuple[float, float, float]
+    nx: Tuple[int, int, int]  # X, Y, Z
+
+    @staticmethod
+    def from_conf(grid_conf: dict) -> "GridSpec":
+        rows = (grid_conf["xbound"], grid_conf["ybound"], grid_conf["zbound"])
+        dx = np.array([r[2] for r in rows], dtype=np.float32)
+        bx = np.array([r[0] + r[2] / 2.0 for r in rows], dtype=np.float32)
+        nx = tuple(int((r[1] - r[0]) / r[2]) for r in rows)
+        lo = (bx - dx / np.float32(2.0)).astype(np.float32)
+        return GridSpec(tuple(float(v) for v in lo), tuple(float(v) for v in dx), nx)
+
+    def c_struct(self) -> _lib.Grid:
+        g = _lib.Grid()
+        for i in range(3):
+            g.lo[i] = self.lo[i]
+            g.dx[i] = self.dx[i]
+            g.nx[i] = self.nx[i]
+        return g
+
+    def ncells(self, B: int) -> int:
+        X, Y, Z = self.nx
+        return B * Z * X * Y
+
+
+def make_dims(B: int, N: int, D: int, H: int, W: int) -> _lib.Dims:
+    return _lib.Dims(B, N, D, H, W, C_CAM)
+
+
+def _require_cuda(*ts: Optional[torch.Tensor]) -> torch.device:
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("lss_carla_amd: the hot path runs only on MI355X (HIP) tensors; "
+                               f"got a {t.device} tensor. There is no CPU fallback.")
+        dev = t.device if dev is None else dev
+    return dev
+
+
+def _f32c(t: torch.Tensor) -> torch.Tensor:
+    return t.detach().to(torch.float32).contiguous()
+
+
+# ----------------------------------------------------------------------------- cameras
+def camera_inverses(post_rots: torch.Tensor, intrins: torch.Tensor, mode: str = "host"):
+    """inv(post_rots), inv(intrins) as (B*N, 9) fp32 device tensors.
+
+    mode='host'   : torch.inverse on the CPU, exactly as src/models.py:180,186 (one D2H + H2D copy).
+    mode='device' : lss_camera_inverse (fp64 adjugate rounded to fp32), no host round trip.
+    """
+    dev = _require_cuda(post_rots, intrins)
+    ncam = post_rots.shape[0] * post_rots.shape[1]
+    if mode == "host":
+        pinv = torch.inverse(post_rots.detach().cpu().float()).reshape(ncam, 9)
+        kinv = torch.inverse(intrins.detach().cpu().float()).reshape(ncam, 9)
+        return pinv.to(dev, non_blocking=True), kinv.to(dev, non_blocking=True)
+    if mode != "device":
+        raise ValueError(f"inverse mode must be 'host' or 'device', got {mode!r}")
+    lib = _lib.load()
+    pr, it = _f32c(post_rots), _f32c(intrins)
+    pinv = torch.empty(ncam, 9, device=dev, dtype=torch.float32)
+    kinv = torch.empty(ncam, 9, device=dev, dtype=torch.float32)
+    _lib.check(lib.lss_camera_inverse(_lib.ptr(pr), _lib.ptr(it), ncam, _lib.ptr(pinv), _lib.ptr(kinv),
+                                      _lib.stream_handle(dev)), "lss_camera_inverse")
+    return pinv, kinv
+
+
+# ----------------------------------------------------------------------------- plan
+@dataclass
+class SplatPlan:
+    """Per-forward voxel assignment: cell of every point and the CSR of points by cell."""
+    dims: Tuple[int, int, int, int, int]  # B, N, D, H, W
+    grid: GridSpec
+    cell_of: torch.Tensor      # (Nprime,) int32, -1 = dropped
+    cell_start: torch.Tensor   # (ncells+1,) int32
+    sorted_pt: torch.Tensor    # (Nprime,) int32 (only the first kept entries are meaningful)
+    geom: Optional[torch.Tensor] = None
+
+    @property
+    def c_dims(self) -> _lib.Dims:
+        return make_dims(*self.dims)
+
+    @property
+    def nprime(self) -> int:
+        B, N, D, H, W = self.dims
+        return B * N * D * H * W
+
+
+def _build_csr(cell_of, slot_of, counts, nprime: int, ncells: int, dev) -> Tuple[torch.Tensor, torch.Tensor]:
+    lib = _lib.load()
+    cell_start = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
+    sorted_pt = torch.empty(nprime, device=dev, dtype=torch.int32)
+    scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells)) // 4, device=dev, dtype=torch.int32)
+    _lib.check(lib.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
+                                 _lib.ptr(cell_start), _lib.ptr(sorted_pt), _lib.ptr(scratch),
+                                 _lib.stream_handle(dev)), "lss_csr_build")
+    return cell_start, sorted_pt
+
+
+def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, post_trans, grid: GridSpec,
+                      inverse: str = "host", want_geom: bool = False, want_csr: bool = True) -> SplatPlan:
+    """get_geometry + quantise + filter + counting sort, all on the device (src/models.py:170-231)."""
+    dev = _require_cuda(frustum, rots, trans, intrins, post_rots, post_trans)
+    lib = _lib.load()
+    B, N = trans.shape[:2]
+    D, H, W = frustum.shape[:3]
+    nprime = B * N * D * H * W
+    ncells = grid.ncells(B)
+    pinv, kinv = camera_inverses(post_rots, intrins, inverse)
+    fr, ro, tr, pt = _f32c(frustum), _f32c(rots), _f32c(trans), _f32c(post_trans)
+    cell_of = torch.empty(nprime, device=dev, dtype=torch.int32)
+    geom = torch.empty(B, N, D, H, W, 3, device=dev, dtype=torch.float32) if want_geom else None
+    counts = slot_of = None
+    if want_csr:
+        counts = torch.zeros(ncells, device=dev, dtype=torch.int32)
+        slot_of = torch.empty(nprime, device=dev, dtype=torch.int32)
+    dims = make_dims(B, N, D, H, W)
+    g = grid.c_struct()
+    _lib.check(lib.lss_geometry_cells(_lib.ptr(fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv),
+                                      _lib.ptr(pt), dims, g, _lib.ptr(geom), _lib.ptr(cell_of), _lib.ptr(counts),
+                                      _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
+    cell_start = sorted_pt = None
+    if want_csr:
+        cell_start, sorted_pt = _build_csr(cell_of, slot_of, counts, nprime, ncells, dev)
+    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_pt, geom)
+
+
+def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
+    """Quantise a given (B, N, D, H, W, 3) geometry (voxel_pooling(geom_feats, x) boundary)."""
+    dev = _require_cuda(geom)
+    lib = _lib.load()
+    B, N, D, H, W, _ = geom.shape
+    nprime = B * N * D * H * W
+    ncells = grid.ncells(B)
+    gm = _f32c(geom)
+    cell_of = torch.empty(nprime, device=dev, dtype=torch.int32)
+    counts = torch.zeros(ncells, device=dev, dtype=torch.int32)
+    slot_of = torch.empty(nprime, device=dev, dtype=torch.int32)
+    _lib.check(lib.lss_cells_from_geom(_lib.ptr(gm), nprime, nprime // B, grid.c_struct(), _lib.ptr(cell_of),
+                                       _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)),
+               "lss_cells_from_geom")
+    cell_start, sorted_pt = _build_csr(cell_of, slot_of, counts, nprime, ncells, dev)
+    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_pt, None)
+
+
+# ----------------------------------------------------------------------------- profiling hook
+class _SplatProfile:
+    """Opt-in HIP-event bracketing of every lss_splat_fwd launch (used by bench.py)."""
+
+    def __init__(self):
+        self.enabled = False
+        self.events = []
+
+    def reset(self, enabled: bool = True):
+        self.enabled = enabled
+        self.events = []
+
+    def avg_ms(self) -> Optional[float]:
+        if not self.events:
+            return None
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.events) / len(self.events)
+
+
+SPLAT_PROFILE = _SplatProfile()
+
+
+def _new_bev(B, Z, X, Y, dtype, layout, dev) -> torch.Tensor:
+    if layout == _lib.NHWC:
+        return torch.empty(B, Z * C_CAM, X, Y, device=dev, dtype=dtype, memory_format=torch.channels_last)
+    return torch.empty(B, Z * C_CAM, X, Y, device=dev, dtype=dtype)
+
+
+def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, layout: int):
+    lib = _lib.load()
+    dev = out.device
+    prof = SPLAT_PROFILE.enabled
+    if prof:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), _lib.ptr(x_rows), _lib.ptr(plan.cell_start),
+                                 _lib.ptr(plan.sorted_pt), plan.c_dims, plan.grid.c_struct(), _lib.ptr(out),
+                                 _lib.dtype_code(out.dtype), layout, _lib.stream_handle(dev)), "lss_splat_fwd")
+    if prof:
+        e1.record()
+        SPLAT_PROFILE.events.append((e0, e1))
+
+
+def _grad_rows(plan: SplatPlan, dbev: torch.Tensor) -> Tuple[torch.Tensor, int]:
+    """Gradient rows of the occupied cells: the channels-last dbev itself, or compacted from NCHW."""
+    if dbev.dtype not in (torch.float32, torch.bfloat16):
+        dbev = dbev.float()
+    if dbev.dim() == 4 and dbev.is_contiguous(memory_format=torch.channels_last) and not dbev.is_contiguous():
+        return dbev, _lib.NHWC
+    dbev = dbev.contiguous()
+    lib = _lib.load()
+    B = plan.dims[0]
+    rows = torch.empty(plan.grid.ncells(B) * C_CAM, device=dbev.device, dtype=dbev.dtype)
+    _lib.check(lib.lss_bev_rows(_lib.ptr(dbev), _lib.dtype_code(dbev.dtype), _lib.ptr(plan.cell_start),
+                                plan.c_dims, plan.grid.c_struct(), _lib.ptr(rows), _lib.stream_handle(dbev.device)),
+               "lss_bev_rows")
+    return rows, _lib.NCHW
+
+
+# ----------------------------------------------------------------------------- autograd: fused lift + splat
+class LiftSplat(torch.autograd.Function):
+    """depthnet output (B*N, D+C, H, W) -> BEV (B, Z*C, X, Y).
+
+    Forward = softmax over depth bins, outer product with the context features
+    and voxel pooling (src/models.py:49-61, 192-246), without materialising the
+    (B*N, C, D, H, W) lifted volume. Backward = QuickCumsum's gather
+    (src/tools.py:212-219) fused with the outer-product and softmax backward.
+    """
+
+    @staticmethod
+    def forward(ctx, depthnet_out: torch.Tensor, plan: SplatPlan, out_dtype: torch.dtype, layout: int):
+        dev = _require_cuda(depthnet_out)
+        lib = _lib.load()
+        B, N, D, H, W = plan.dims
+        if depthnet_out.shape != (B * N, D + C_CAM, H, W):
+            raise RuntimeError(f"depthnet output shape {tuple(depthnet_out.shape)} != {(B * N, D + C_CAM, H, W)}")
+        dn = depthnet_out.detach()
+        if dn.dtype not in (torch.float32, torch.bfloat16):
+            dn = dn.float()
+        dn = dn.contiguous()
+        depth = torch.empty(B * N, D, H, W, device=dev, dtype=torch.float32)
+        ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=torch.float32)
+        _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.dtype_code(dn.dtype), plan.c_dims, _lib.ptr(depth),
+                                     _lib.ptr(ctx_t), _lib.stream_handle(dev)), "lss_lift_prep")
+        X, Y, Z = plan.grid.nx
+        out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
+        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout)
+        ctx.save_for_backward(depth, ctx_t)
+        ctx.plan = plan
+        ctx.dn_dtype = depthnet_out.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dbev: torch.Tensor):
+        depth, ctx_t = ctx.saved_tensors
+        plan: SplatPlan = ctx.plan
+        lib = _lib.load()
+        rows, layout = _grad_rows(plan, dbev)
+        B, N, D, H, W = plan.dims
+        d_dn = torch.empty(B * N, D + C_CAM, H, W, device=depth.device, dtype=ctx.dn_dtype)
+        _lib.check(lib.lss_splat_bwd(_lib.ptr(rows), _lib.dtype_code(rows.dtype), layout, _lib.ptr(plan.cell_of),
+                                     _lib.ptr(depth), _lib.ptr(ctx_t), plan.c_dims, plan.grid.c_struct(),
+                                     _lib.ptr(d_dn), _lib.dtype_code(d_dn.dtype), _lib.stream_handle(depth.device)),
+                   "lss_splat_bwd")
+        return d_dn, None, None, None
+
+
+def lift_splat(depthnet_out: torch.Tensor, plan: SplatPlan, out_dtype: torch.dtype = torch.float32,
+               layout: int = _lib.NCHW) -> torch.Tensor:
+    return LiftSplat.apply(depthnet_out, plan, out_dtype, layout)
+
+
+# ----------------------------------------------------------------------------- autograd: unfused voxel pooling
+class VoxelPool(torch.autograd.Function):
+    """(Nprime, C) lifted rows -> BEV (voxel_pooling(geom_feats, x) boundary, src/models.py:204-246)."""
+
+    @staticmethod
+    def forward(ctx, x_rows: torch.Tensor, plan: SplatPlan, layout: int):
+        dev = _require_cuda(x_rows)
+        xr = x_rows.detach().to(torch.float32).contiguous()
+        X, Y, Z = plan.grid.nx
+        out = _new_bev(plan.dims[0], Z, X, Y, torch.float32, layout, dev)
+        _splat_fwd_launch(plan, None, None, xr, out, layout)
+        ctx.plan = plan
+        ctx.x_dtype = x_rows.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dbev: torch.Tensor):
+        plan: SplatPlan = ctx.plan
+        lib = _lib.load()
+        rows, layout = _grad_rows(plan, dbev)
+        dx = torch.empty(plan.nprime, C_CAM, device=rows.device, dtype=torch.float32)
+        _lib.check(lib.lss_splat_bwd_lifted(_lib.ptr(rows), _lib.dtype_code(rows.dtype), layout,
+                                            _lib.ptr(plan.cell_of), plan.nprime, plan.c_dims,
+                                            plan.grid.c_struct(), _lib.ptr(dx), _lib.stream_handle(rows.device)),
+                   "lss_splat_bwd_lifted")
+        return dx.to(ctx.x_dtype), None, None
+
+
+def voxel_pool_rows(x_rows: torch.Tensor, plan: SplatPlan, layout: int = _lib.NCHW) -> torch.Tensor:
+    return VoxelPool.apply(x_rows, plan, layout)

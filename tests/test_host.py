@@ -1,0 +1,103 @@
+"""CPU-only checks: the C ABI library loads and exports every declared symbol, host logic, module surface."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+from oracle import lss_ref as ref
+import lss_carla_amd as L
+from lss_carla_amd import _lib, ops
+from lss_carla_amd import synthetic as syn
+
+HEADER = os.path.join(REPO, "include", "lss_hip.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    return set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(lss_\w+)\s*\(", text, re.M))
+
+
+def test_header_declarations_match_binding():
+    assert _declared() == set(_lib.SIGNATURES), _declared() ^ set(_lib.SIGNATURES)
+
+
+def test_library_loads_and_exports_all_symbols():
+    lib = _lib.load()  # built by __graft_entry__.build(); raises if missing
+    for name in _declared():
+        assert hasattr(lib, name), name
+    assert lib.lss_abi_version() == _lib.ABI_VERSION
+    assert lib.lss_error_string(0) == b"success"
+    assert b"invalid" in lib.lss_error_string(-1)
+    # host-side argument validation (no device work): NULL pointers are rejected
+    assert lib.lss_camera_inverse(None, None, 0, None, None, None) == -1
+    assert lib.lss_csr_scratch_bytes(4096) == 8
+
+
+def test_gridspec_matches_reference_quantiser_constants():
+    gs = ops.GridSpec.from_conf(syn.grid_conf())
+    dx, bx, nx = ref.gen_dx_bx([-50.0, 50.0, 0.5], [-50.0, 50.0, 0.5], [-10.0, 10.0, 20.0])
+    assert gs.nx == tuple(nx.tolist())
+    assert np.array_equal(np.array(gs.lo, dtype=np.float32), (bx - dx / np.float32(2)).astype(np.float32))
+    assert gs.ncells(8) == 8 * 200 * 200
+
+
+def test_module_surface_and_state_dict():
+    gc, dac = syn.grid_conf(), syn.data_aug_conf()
+    m = L.compile_model(gc, dac, outC=1)
+    assert isinstance(m, L.LiftSplatShoot)
+    sd = m.state_dict()
+    keys = list(sd)
+    assert keys[:4] == ["dx", "bx", "nx", "frustum"]
+    assert m.dx.requires_grad is False and m.nx.dtype == torch.long
+    assert m.D == 41 and m.camC == 64 and m.downsample == 16 and m.use_quickcumsum is True
+    np.testing.assert_array_equal(m.frustum.detach().numpy(), ref.create_frustum((128, 352), gc["dbound"]).numpy())
+    for k in ("camencode.trunk._conv_stem.weight", "camencode.trunk._blocks.15._project_conv.weight",
+              "camencode.trunk._blocks.1._expand_conv.weight", "camencode.trunk._blocks.0._se_reduce.bias",
+              "camencode.trunk._fc.weight", "camencode.up1.conv.4.running_var", "camencode.depthnet.weight",
+              "bevencode.conv1.weight", "bevencode.layer2.0.downsample.1.weight", "bevencode.up2.4.bias"):
+        assert k in sd, k
+    assert "camencode.trunk._blocks.0._expand_conv.weight" not in sd  # expand ratio 1 block
+    assert len(m.camencode.trunk._blocks) == 16
+    assert sum(p.numel() for p in m.parameters()) == 14313575
+    assert m.camencode.depthnet.out_channels == 41 + 64
+    # zero_init_residual of the torchvision trunk parts
+    assert m.bevencode.layer1[0].bn2.weight.abs().sum() == 0
+    assert m.bevencode.layer1[0].bn1.weight.sum() == 64
+    # BevEncode parameter order = the reference's (conv1 first)
+    names = [n for n, _ in m.bevencode.named_parameters()]
+    assert names[0] == "conv1.weight" and names[1] == "bn1.weight"
+
+
+def test_efficientnet_static_same_padding():
+    m = L.compile_model(syn.grid_conf(), syn.data_aug_conf(), outC=1)
+    t = m.camencode.trunk
+    assert isinstance(t._conv_stem.static_padding, torch.nn.ZeroPad2d)
+    assert t._conv_stem.static_padding.padding == (0, 1, 0, 1)
+    assert t._blocks[3]._depthwise_conv.static_padding.padding == (1, 2, 1, 2)
+    assert t._blocks[4]._depthwise_conv.padding == (2, 2)
+    # endpoints on a 128x352 image: the depthnet output is 8x22
+    m.eval()
+    with torch.no_grad():
+        feats = m.camencode.get_eff_depth(torch.randn(1, 3, 128, 352))
+    assert feats.shape == (1, 512, 8, 22)
+
+
+def test_cpu_forward_fails_loudly():
+    gc = syn.grid_conf()
+    m = L.compile_model(gc, syn.data_aug_conf((64, 176)), outC=1)
+    rig = syn.make_rig(1, 2, (64, 176))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(torch.randn(1, 2, 3, 64, 176), **rig)
+
+
+def test_synthetic_rig_shapes():
+    rig = syn.make_rig(3, 6, (128, 352))
+    assert rig["rots"].shape == (3, 6, 3, 3) and rig["post_trans"].shape == (3, 6, 3)
+    # val-mode crop of the 224x480 image to 128x352: resize 352/480, crop_h = 164 - 128
+    assert np.isclose(rig["post_rots"][0, 0, 0, 0].item(), 352 / 480)
+    assert rig["post_trans"][0, 0].tolist() == [0.0, -36.0, 0.0]
+    dn = syn.make_depthnet_out(1, 1, 41, 8, 22)
+    assert dn.shape == (1, 105, 8, 22)
