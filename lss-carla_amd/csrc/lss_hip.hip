@@ -7,13 +7,13 @@
 // Pipeline (forward, one training step):
 //   lss_camera_inverse      48 cameras, fp64 adjugate
 //   lss_geometry_cells      1 thread / point: frustum -> ego xyz -> cell id, atomic count
-//   lss_csr_build           counting sort: block reduce -> scan -> scatter
+//   lss_csr_build           counting sort: block reduce -> scan -> scatter of packed (tile-cell, point) keys
 //   lss_lift_prep           1 block / 64 pixels: depth softmax + context -> pixel-major rows
-//   lss_splat_fwd           1 block / (b, z, x, y-tile): per-cell ordered sum -> LDS -> dense
+//   lss_splat_fwd           1 block (8 waves) / (b, z, x, y-tile): per-cell ordered sum -> LDS -> dense
 //                           coalesced BEV write (zero fill fused)   <- the HBM-bound kernel
 // Backward:
 //   lss_bev_rows            NCHW dbev -> compact per-cell rows (occupied cells only)
-//   lss_splat_bwd           1 wave / pixel: gather D rows to LDS, d_ctx, d_depth, softmax bwd
+//   lss_splat_bwd           1 wave / pixel: 16-B gathers of D rows to LDS, d_ctx, d_depth, softmax bwd
 
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
@@ -239,53 +239,71 @@ __global__ __launch_bounds__(1024) void k_scan_apply(const int32_t* __restrict__
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) cell_start[ncells] = prefix + s_total;
 }
 
+// Counting-sort scatter. The sorted entry of point p is the packed key (t << 24) | p with
+// t = the cell's index inside its splat tile (y % YT), so the splat kernel gets cell and
+// point id in one coalesced load and can order a window by key alone.
 __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ cell_of,
                                                     const int32_t* __restrict__ slot_of, int nprime,
-                                                    const int32_t* __restrict__ cell_start,
-                                                    int32_t* __restrict__ sorted_pt) {
+                                                    const int32_t* __restrict__ cell_start, int Y, int YT,
+                                                    int32_t* __restrict__ sorted_key) {
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= nprime) return;
     const int cell = cell_of[p];
-    if (cell >= 0) sorted_pt[cell_start[cell] + slot_of[p]] = p;
+    if (cell >= 0) sorted_key[cell_start[cell] + slot_of[p]] = (((cell % Y) % YT) << 24) | p;
 }
 
 // ----------------------------------------------------------------------------- lift prep
-// One block = 64 consecutive pixels. depth = softmax_D(logits) written in the reference's
-// (B*N, D, H, W) layout (coalesced over pixels); context transposed through LDS to
+// One block = 64 consecutive pixels x 4 waves. Wave w owns depth bins d = w, w+4, ... and
+// context channels 16w..16w+15 of every pixel, so all of a thread's loads are issued back to
+// back (one memory round trip). depth = softmax_D(logits) is written in the reference's
+// (B*N, D, H, W) layout (coalesced over pixels); the context is transposed through LDS to
 // pixel-major rows ctx_t[q*64 + c] (coalesced 256-B rows).
 template <typename InT>
 __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn, int D, int HW, int npix,
                                                       float* __restrict__ depth, float* __restrict__ ctx_t) {
     __shared__ float s_ctx[kC][65];
+    __shared__ float s_red[2][4][64];
     const int q0 = blockIdx.x * 64;
-    const int t = threadIdx.x;
-    const int DC = D + kC;
-    {
-        const int px = t & 63;
-        const int q = q0 + px;
-        if (q < npix) {
-            const int bn = q / HW, hw = q - bn * HW;
-            const InT* src = dn + ((size_t)bn * DC + D) * HW + hw;
-            for (int c = t >> 6; c < kC; c += 4) s_ctx[c][px] = to_f32(src[(size_t)c * HW]);
-        }
+    const int px = threadIdx.x & 63, part = threadIdx.x >> 6;
+    const int q = q0 + px;
+    const bool live = q < npix;
+    const int bn = live ? q / HW : 0, hw = live ? q - bn * HW : 0;
+    const InT* src = dn + (size_t)bn * (D + kC) * HW + hw;
+    float cv[16], l[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cv[i] = live ? to_f32(src[(size_t)(D + part * 16 + i) * HW]) : 0.f;
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int d = part + 4 * i;
+        l[i] = (live && d < D) ? to_f32(src[(size_t)d * HW]) : -INFINITY;
+        m = fmaxf(m, l[i]);
     }
-    if (t < 64) {
-        const int q = q0 + t;
-        if (q < npix) {
-            const int bn = q / HW, hw = q - bn * HW;
-            const InT* src = dn + (size_t)bn * DC * HW + hw;
-            float m = -INFINITY;
-            for (int d = 0; d < D; ++d) m = fmaxf(m, to_f32(src[(size_t)d * HW]));
-            float s = 0.f;
-            for (int d = 0; d < D; ++d) s += expf(to_f32(src[(size_t)d * HW]) - m);
-            float* dst = depth + (size_t)bn * D * HW + hw;
-            for (int d = 0; d < D; ++d) dst[(size_t)d * HW] = expf(to_f32(src[(size_t)d * HW]) - m) / s;
-        }
-    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s_ctx[part * 16 + i][px] = cv[i];
+    s_red[0][part][px] = m;
     __syncthreads();
-    for (int i = t; i < 64 * kC; i += kBlock) {
-        const int px = i >> 6, c = i & 63;
-        if (q0 + px < npix) ctx_t[(size_t)(q0 + px) * kC + c] = s_ctx[c][px];
+    m = fmaxf(fmaxf(s_red[0][0][px], s_red[0][1][px]), fmaxf(s_red[0][2][px], s_red[0][3][px]));
+    float e[16], sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        e[i] = (part + 4 * i < D) ? expf(l[i] - m) : 0.f;
+        sum += e[i];
+    }
+    s_red[1][part][px] = sum;
+    __syncthreads();
+    sum = (s_red[1][0][px] + s_red[1][1][px]) + (s_red[1][2][px] + s_red[1][3][px]);
+    if (live) {
+        float* dst = depth + (size_t)bn * D * HW + hw;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int d = part + 4 * i;
+            if (d < D) dst[(size_t)d * HW] = e[i] / sum;
+        }
+    }
+    for (int i = threadIdx.x; i < 64 * kC; i += kBlock) {
+        const int r = i >> 6, c = i & 63;
+        if (q0 + r < npix) ctx_t[(size_t)(q0 + r) * kC + c] = s_ctx[c][r];
     }
 }
 
@@ -294,64 +312,63 @@ struct SplatGeo {
     int X, Y, Z, YT, ntiles_y;
 };
 
-// Sum over the points of one cell, in ascending point id, lane = channel.
-template <bool FUSED>
-__device__ __forceinline__ float cell_sum(int cs, int n, const int32_t* __restrict__ sorted_pt,
-                                          const float* __restrict__ depth, const float* __restrict__ ctx_t,
-                                          const float* __restrict__ xrows, int DHW, int HW, int lane) {
-    float acc = 0.f;
-    auto contrib = [&](int p) -> float {
-        if (FUSED) {
-            const int cam = p / DHW;
-            const int q = cam * HW + (p - cam * DHW) % HW;
-            return __fmul_rn(depth[p], ctx_t[(size_t)q * kC + lane]);  // the lift's new_x element
-        } else {
-            return xrows[(size_t)p * kC + lane];
-        }
-    };
-    if (n <= kWave) {
-        // rank each lane's id among the cell's ids, permute so lane k holds the k-th smallest.
-        const int id = lane < n ? sorted_pt[cs + lane] : INT_MAX;
-        int rank = 0;
-        for (int j = 0; j < n; ++j) rank += (__builtin_amdgcn_readlane(id, j) < id) ? 1 : 0;
-        const int sid = __builtin_amdgcn_ds_permute(rank << 2, id);
-        int k = 0;
-        for (; k + 4 <= n; k += 4) {
-            const float v0 = contrib(__builtin_amdgcn_readlane(sid, k));
-            const float v1 = contrib(__builtin_amdgcn_readlane(sid, k + 1));
-            const float v2 = contrib(__builtin_amdgcn_readlane(sid, k + 2));
-            const float v3 = contrib(__builtin_amdgcn_readlane(sid, k + 3));
-            acc = __fadd_rn(acc, v0);
-            acc = __fadd_rn(acc, v1);
-            acc = __fadd_rn(acc, v2);
-            acc = __fadd_rn(acc, v3);
-        }
-        for (; k < n; ++k) acc = __fadd_rn(acc, contrib(__builtin_amdgcn_readlane(sid, k)));
-    } else {
-        // rare: more points than lanes -- ordered selection over the global list.
-        int last = -1;
-        for (int k = 0; k < n; ++k) {
-            int best = INT_MAX;
-            for (int i = lane; i < n; i += kWave) {
-                const int v = sorted_pt[cs + i];
-                if (v > last && v < best) best = v;
-            }
-            best = uniform(wave_min(best));
-            acc = __fadd_rn(acc, contrib(best));
-            last = best;
-        }
+constexpr int kMaxYT = 128;       // cells per tile (LDS sizing, 7-bit tile-cell in the keys)
+constexpr int kFwdWaves = 8;      // waves per splat tile
+constexpr int kFwdBlock = kFwdWaves * kWave;
+constexpr int kPrefetch = 16;     // row loads in flight per wave
+
+// 16-byte vector stores of 16/sizeof(T) elements.
+template <typename T> struct Vec;
+template <> struct Vec<float> { static constexpr int n = 4; };
+template <> struct Vec<bf16> { static constexpr int n = 8; };
+
+__device__ __forceinline__ void store_vec(float* dst, const float* src) {
+    *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+}
+__device__ __forceinline__ void store_vec(bf16* dst, const float* src) {
+    const float4 a = *reinterpret_cast<const float4*>(src);
+    const float4 b = *reinterpret_cast<const float4*>(src + 4);
+    bf16 v[8] = {__float2bfloat16(a.x), __float2bfloat16(a.y), __float2bfloat16(a.z), __float2bfloat16(a.w),
+                 __float2bfloat16(b.x), __float2bfloat16(b.y), __float2bfloat16(b.z), __float2bfloat16(b.w)};
+    *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(v);
+}
+__device__ __forceinline__ void store_zero_vec(float* dst) { *reinterpret_cast<float4*>(dst) = make_float4(0.f, 0.f, 0.f, 0.f); }
+__device__ __forceinline__ void store_zero_vec(bf16* dst) { *reinterpret_cast<uint4*>(dst) = make_uint4(0u, 0u, 0u, 0u); }
+
+// First c in [0, ny] with s[c] >= t (s nondecreasing, in LDS).
+__device__ __forceinline__ int tile_lower_bound(const int* s, int ny, int t, int lane) {
+    for (int base = 0; base <= ny; base += kWave) {
+        const int c = base + lane;
+        const unsigned long long hit = __ballot(c <= ny && s[min(c, ny)] >= t);
+        if (hit) return base + __builtin_ctzll(hit);
     }
-    return acc;
+    return ny;
 }
 
+template <bool NHWC>
+__device__ __forceinline__ void flush_row(float* lds, int S, int cell, int lane, float acc) {
+    if (NHWC) lds[cell * kC + lane] = acc;
+    else lds[lane * S + cell] = acc;
+}
+
+// One block = one tile of YT consecutive cells (b, z, x, y0..y0+ny) of the BEV, 8 waves.
+//  1. the tile's cell starts -> LDS; the fp32 accumulator tile is zeroed in LDS.
+//  2. the tile's point range is split over the waves at cell boundaries (equal point counts).
+//  3. each wave streams its range in windows of whole cells holding <= 64 points: one
+//     coalesced load of packed (tile-cell, point) keys; the window is rank-sorted by key so
+//     every cell is summed in ascending point id (deterministic); then the context rows
+//     (256 B, lane = channel) and depth weights are gathered 16 in flight and each cell's sum
+//     is flushed to its LDS row.
+//  4. the tile is written once with 16-B stores, zero rows included (the BEV's zero fill).
 template <bool FUSED, typename OutT, bool NHWC>
-__global__ __launch_bounds__(kBlock) void k_splat_fwd(const float* __restrict__ depth,
-                                                      const float* __restrict__ ctx_t,
-                                                      const float* __restrict__ xrows,
-                                                      const int32_t* __restrict__ cell_start,
-                                                      const int32_t* __restrict__ sorted_pt, int DHW, int HW,
-                                                      SplatGeo sg, OutT* __restrict__ out) {
+__global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict__ depth,
+                                                         const float* __restrict__ ctx_t,
+                                                         const float* __restrict__ xrows,
+                                                         const int32_t* __restrict__ cell_start,
+                                                         const int32_t* __restrict__ sorted_key, int DHW, int HW,
+                                                         SplatGeo sg, OutT* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int s_start[kMaxYT + 1];
     const int tile = blockIdx.x;
     const int bzx = tile / sg.ntiles_y;
     const int y0 = (tile - bzx * sg.ntiles_y) * sg.YT;
@@ -363,38 +380,115 @@ __global__ __launch_bounds__(kBlock) void k_splat_fwd(const float* __restrict__ 
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int S = NHWC ? kC : sg.YT + 4;  // LDS row stride (floats)
-    const bool empty = uniform(cell_start[cell0]) == uniform(cell_start[cell0 + ny]);
+
+    for (int i = threadIdx.x; i <= ny; i += kFwdBlock) s_start[i] = cell_start[cell0 + i];
+    __syncthreads();
+    const int s0 = s_start[0], s1 = s_start[ny];
+    const bool empty = s0 == s1;
 
     if (!empty) {
-        for (int yy = wave; yy < ny; yy += kBlock / kWave) {
-            const int cs = uniform(cell_start[cell0 + yy]);
-            const int n = uniform(cell_start[cell0 + yy + 1]) - cs;
-            const float acc = n > 0 ? cell_sum<FUSED>(cs, n, sorted_pt, depth, ctx_t, xrows, DHW, HW, lane) : 0.f;
-            if (NHWC) lds[yy * kC + lane] = acc;
-            else lds[lane * S + yy] = acc;
+        const int lds_elems = NHWC ? ny * kC : kC * S;
+        for (int i = threadIdx.x * 4; i < lds_elems; i += kFwdBlock * 4)
+            *reinterpret_cast<float4*>(lds + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int span = s1 - s0;
+        const int cb = wave == 0 ? 0 : tile_lower_bound(s_start, ny, s0 + (wave * span) / kFwdWaves, lane);
+        const int ce = wave == kFwdWaves - 1 ? ny
+                                             : tile_lower_bound(s_start, ny, s0 + ((wave + 1) * span) / kFwdWaves, lane);
+        __syncthreads();  // accumulator zeroed before any flush
+        const float* base = FUSED ? ctx_t : xrows;
+        int c = cb;
+        while (c < ce) {
+            const int ws = s_start[c];
+            // window = cells [c, c+m): the longest run of whole cells holding <= 64 points
+            const int cj = c + 1 + lane;
+            const int ej = cj <= ce ? s_start[cj] : INT_MAX;
+            const int m = __popcll(__ballot(ej - ws <= kWave));
+            if (m == 0) {
+                // one cell with more than 64 points: ordered selection over its list (rare)
+                const int n = s_start[c + 1] - ws;
+                float acc = 0.f;
+                int last = -1;
+                for (int k = 0; k < n; ++k) {
+                    int best = INT_MAX;
+                    for (int i = lane; i < n; i += kWave) {
+                        const int v = sorted_key[ws + i];
+                        if (v > last && v < best) best = v;
+                    }
+                    best = uniform(wave_min(best));
+                    const int p = best & 0xFFFFFF;
+                    float v;
+                    if (FUSED) {
+                        const int cam = p / DHW;
+                        v = __fmul_rn(depth[p], ctx_t[(size_t)(cam * HW + (p - cam * DHW) % HW) * kC + lane]);
+                    } else {
+                        v = xrows[(size_t)p * kC + lane];
+                    }
+                    acc = __fadd_rn(acc, v);
+                    last = best;
+                }
+                flush_row<NHWC>(lds, S, c, lane, acc);
+                c += 1;
+                continue;
+            }
+            const int npts = s_start[c + m] - ws;
+            c += m;
+            if (npts == 0) continue;  // a run of empty cells: their rows stay zero
+            const int key = lane < npts ? sorted_key[ws + lane] : INT_MAX;
+            int rank = 0;
+            for (int j = 0; j < npts; ++j) rank += (__builtin_amdgcn_readlane(key, j) < key) ? 1 : 0;
+            const int sk = __builtin_amdgcn_ds_permute(rank << 2, key);
+            const int p = sk & 0xFFFFFF;
+            int row = p;
+            if (FUSED) {
+                const int cam = p / DHW;
+                row = cam * HW + (p - cam * DHW) % HW;
+            }
+            const float w = (FUSED && lane < npts) ? depth[p] : 1.f;
+            float acc = 0.f;
+            int cur = __builtin_amdgcn_readlane(sk, 0) >> 24;
+            for (int k0 = 0; k0 < npts; k0 += kPrefetch) {
+                float v[kPrefetch];
+#pragma unroll
+                for (int j = 0; j < kPrefetch; ++j) {
+                    const int k = min(k0 + j, npts - 1);
+                    v[j] = base[(size_t)__builtin_amdgcn_readlane(row, k) * kC + lane];
+                }
+#pragma unroll
+                for (int j = 0; j < kPrefetch; ++j) {
+                    const int k = k0 + j;
+                    if (k < npts) {
+                        const int cr = __builtin_amdgcn_readlane(sk, k) >> 24;
+                        if (cr != cur) {
+                            flush_row<NHWC>(lds, S, cur, lane, acc);
+                            acc = 0.f;
+                            cur = cr;
+                        }
+                        acc = __fadd_rn(acc, FUSED ? __fmul_rn(readlane_f(w, k), v[j]) : v[j]);
+                    }
+                }
+            }
+            flush_row<NHWC>(lds, S, cur, lane, acc);
         }
         __syncthreads();
     }
 
+    constexpr int VN = Vec<OutT>::n;
     if (NHWC) {
         // cell (b, z, x, y) row = out[((b*X + x)*Y + y)*Z*C + z*C + c]
         const size_t zc = (size_t)sg.Z * kC;
         OutT* obase = out + (((size_t)b * sg.X + x) * sg.Y + y0) * zc + (size_t)z * kC;
-        for (int i = threadIdx.x; i < ny * (kC / 4); i += kBlock) {
-            const int yy = i >> 4, j = (i & 15) * 4;
-            if (empty) {
-                store4(obase + yy * zc + j, 0.f, 0.f, 0.f, 0.f);
-            } else {
-                const float4 v = *reinterpret_cast<const float4*>(lds + yy * kC + j);
-                store4(obase + yy * zc + j, v.x, v.y, v.z, v.w);
-            }
+        constexpr int per_row = kC / VN;
+        for (int i = threadIdx.x; i < ny * per_row; i += kFwdBlock) {
+            const int yy = i / per_row, j = (i - yy * per_row) * VN;
+            if (empty) store_zero_vec(obase + yy * zc + j);
+            else store_vec(obase + yy * zc + j, lds + yy * kC + j);
         }
     } else {
         const size_t XY = (size_t)sg.X * sg.Y;
         OutT* obase = out + (size_t)bz * kC * XY + (size_t)x * sg.Y + y0;
         if ((sg.Y & 3) == 0 && (ny & 3) == 0) {
             const int nq = ny >> 2;
-            for (int i = threadIdx.x; i < kC * nq; i += kBlock) {
+            for (int i = threadIdx.x; i < kC * nq; i += kFwdBlock) {
                 const int c = i / nq, j = (i - c * nq) * 4;
                 if (empty) {
                     store4(obase + c * XY + j, 0.f, 0.f, 0.f, 0.f);
@@ -404,7 +498,7 @@ __global__ __launch_bounds__(kBlock) void k_splat_fwd(const float* __restrict__ 
                 }
             }
         } else {
-            for (int i = threadIdx.x; i < kC * ny; i += kBlock) {
+            for (int i = threadIdx.x; i < kC * ny; i += kFwdBlock) {
                 const int c = i / ny, yy = i - c * ny;
                 obase[c * XY + yy] = from_f32<OutT>(empty ? 0.f : lds[c * S + yy]);
             }
@@ -452,64 +546,85 @@ __device__ __forceinline__ size_t row_offset(int cell, const SplatGeo& sg) {
     return (((size_t)b * XY + xy) * sg.Z + z) * kC;
 }
 
-// One wave per pixel: the D gradient rows of the pixel's points are gathered into LDS,
-// then (lane = channel) d_ctx[c] = sum_d g[d][c] depth[d], and (lane = depth bin)
-// d_depth[d] = sum_c g[d][c] ctx[c]; softmax backward; write d_depthnet_out.
+// 16-byte gradient-row chunk -> fp32.
+__device__ __forceinline__ void unpack16(const uint4& u, const float*, float* o) {
+    o[0] = __uint_as_float(u.x); o[1] = __uint_as_float(u.y); o[2] = __uint_as_float(u.z); o[3] = __uint_as_float(u.w);
+}
+__device__ __forceinline__ void unpack16(const uint4& u, const bf16*, float* o) {
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        o[2 * i] = __uint_as_float(w[i] << 16);
+        o[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+}
+
+// One wave per pixel. The D gradient rows of the pixel's points are gathered into LDS with
+// 16-B lane loads (every load of the pixel in flight at once), then (lane = channel)
+// d_ctx[c] = sum_d g[d][c] depth[d] and (lane = depth bin) d_depth[d] = sum_c g[d][c] ctx[c],
+// softmax backward, write d_depthnet_out.
 template <typename GT, typename DT, bool NHWC>
 __global__ __launch_bounds__(kBlock) void k_splat_bwd(const GT* __restrict__ g, const int32_t* __restrict__ cell_of,
                                                       const float* __restrict__ depth,
                                                       const float* __restrict__ ctx_t, int D, int HW, int npix,
                                                       SplatGeo sg, DT* __restrict__ d_dn) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int EPL = 16 / sizeof(GT);    // row elements per 16-B lane load
+    constexpr int LPR = kC / EPL;           // lanes per row
+    constexpr int RPI = kWave / LPR;        // rows per wave-instruction
+    constexpr int NI = kWave / RPI;         // instructions for 64 rows
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
-    const int RS = kC + 1;                 // LDS row stride: conflict-free column reads
-    float* R = lds + wave * (D * RS + kC);  // D rows of this wave's pixel
-    float* cx = R + D * RS;                // the pixel's context row
+    const int RS = kC + 1;                  // LDS row stride: conflict-free column reads
+    float* R = lds + wave * (D * RS + kC);
+    float* cx = R + D * RS;
     const int q = blockIdx.x * (kBlock / kWave) + wave;
     const bool live = q < npix;
     const int bn = live ? q / HW : 0, hw = live ? q - bn * HW : 0;
-    const size_t pbase = (size_t)bn * D * HW + hw;  // point (bn, d=0, hw)
+    const size_t pbase = (size_t)bn * D * HW + hw;  // point (bn, d = 0, hw)
     float my_depth = 0.f;
     int my_cell = -1;
-    if (live) {
-        if (lane < D) {
-            my_depth = depth[pbase + (size_t)lane * HW];
-            my_cell = cell_of[pbase + (size_t)lane * HW];
-        }
-        cx[lane] = ctx_t[(size_t)q * kC + lane];
-        int d = 0;
-        for (; d + 4 <= D; d += 4) {
-            float v[4];
+    if (live && lane < D) {
+        my_depth = depth[pbase + (size_t)lane * HW];
+        my_cell = cell_of[pbase + (size_t)lane * HW];
+    }
+    if (live) cx[lane] = ctx_t[(size_t)q * kC + lane];
+    const int sub = lane / LPR, chunk = (lane % LPR) * EPL;
+    uint4 raw[NI];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int cell = __builtin_amdgcn_readlane(my_cell, d + u);
-                v[u] = cell >= 0 ? to_f32(g[row_offset<NHWC>(cell, sg) + lane]) : 0.f;
-            }
+    for (int k = 0; k < NI; ++k) {
+        const int r = k * RPI + sub;
+        const int cell = __shfl(my_cell, r & 63, kWave);  // -1 beyond D
+        raw[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (live && k * RPI < D && cell >= 0)
+            raw[k] = *reinterpret_cast<const uint4*>(g + row_offset<NHWC>(cell, sg) + chunk);
+    }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) R[(d + u) * RS + lane] = v[u];
-        }
-        for (; d < D; ++d) {
-            const int cell = __builtin_amdgcn_readlane(my_cell, d);
-            R[d * RS + lane] = cell >= 0 ? to_f32(g[row_offset<NHWC>(cell, sg) + lane]) : 0.f;
+    for (int k = 0; k < NI; ++k) {
+        const int r = k * RPI + sub;
+        if (k * RPI < D && r < D) {
+            float f[EPL];
+            unpack16(raw[k], (const GT*)nullptr, f);
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) R[r * RS + chunk + e] = f[e];
         }
     }
     __syncthreads();
     if (!live) return;
-    // d_ctx (lane = c): sum over depth bins in order d = 0..D-1
+    // d_ctx (lane = c): over depth bins in order d = 0..D-1
     float dctx = 0.f;
     for (int d = 0; d < D; ++d) dctx = fmaf(R[d * RS + lane], readlane_f(my_depth, d), dctx);
-    // d_depth (lane = d): sum over channels
+    // d_depth (lane = d): over channels
     float dd = 0.f;
     if (lane < D) {
         const float* row = R + lane * RS;
+#pragma unroll 16
         for (int c = 0; c < kC; ++c) dd = fmaf(row[c], cx[c], dd);
     }
     // softmax backward: dl = depth * (dd - sum_d depth*dd)
     const float s = wave_sum(my_depth * dd);
     const float dl = my_depth * (dd - s);
-    const int DC = D + kC;
-    DT* dst = d_dn + (size_t)bn * DC * HW + hw;
+    DT* dst = d_dn + (size_t)bn * (D + kC) * HW + hw;
     if (lane < D) dst[(size_t)lane * HW] = from_f32<DT>(dl);
     dst[(size_t)(D + lane) * HW] = from_f32<DT>(dctx);
 }
@@ -616,16 +731,21 @@ size_t lss_csr_scratch_bytes(int32_t ncells) {
 }
 
 int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, const int32_t* cell_count,
-                  int32_t ncells, int32_t* cell_start, int32_t* sorted_pt, void* scratch, lss_stream_t stream) {
-    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_pt || !scratch || nprime <= 0 || ncells <= 0)
+                  int32_t ncells, const lss_grid_t* grid, int32_t* cell_start, int32_t* sorted_key, void* scratch,
+                  lss_stream_t stream) {
+    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !scratch || nprime <= 0 ||
+        ncells <= 0 || !grid_ok(grid))
         return LSS_EINVAL;
+    if (nprime >= (1 << 24)) return LSS_EUNSUPPORTED;  // 24-bit point ids in the packed keys
+    const SplatGeo sg = splat_geo(grid);
+    if (sg.YT > kMaxYT) return LSS_EUNSUPPORTED;
     const int nb = (ncells + kScanItems - 1) / kScanItems;
     int32_t* partial = static_cast<int32_t*>(scratch);
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial);
     hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial, cell_start);
     hipLaunchKernelGGL(k_scatter, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0, s, cell_of, slot_of, nprime,
-                       cell_start, sorted_pt);
+                       cell_start, sg.Y, sg.YT, sorted_key);
     return launch_status();
 }
 
@@ -649,21 +769,22 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
 }
 
 int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows, const int32_t* cell_start,
-                  const int32_t* sorted_pt, const lss_dims_t* dims, const lss_grid_t* grid, void* out,
+                  const int32_t* sorted_key, const lss_dims_t* dims, const lss_grid_t* grid, void* out,
                   int32_t out_dtype, int32_t out_layout, lss_stream_t stream) {
-    if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_pt || !out) return LSS_EINVAL;
+    if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_key || !out) return LSS_EINVAL;
     const bool fused = x_rows == nullptr;
     if (fused && (!depth || !ctx_t)) return LSS_EINVAL;
     const SplatGeo sg = splat_geo(grid);
     const int DHW = dims->D * dims->H * dims->W;
     const int HW = dims->H * dims->W;
+    if ((long)dims->B * dims->N * DHW >= (1L << 24) || sg.YT > kMaxYT) return LSS_EUNSUPPORTED;
     const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
     const bool nhwc = out_layout == LSS_NHWC;
     const size_t lds = nhwc ? (size_t)sg.YT * kC * sizeof(float) : (size_t)kC * (sg.YT + 4) * sizeof(float);
     hipStream_t s = (hipStream_t)stream;
 #define LSS_SPLAT(F, T, L)                                                                                        \
-    hipLaunchKernelGGL((k_splat_fwd<F, T, L>), dim3(nblocks), dim3(kBlock), lds, s, depth, ctx_t, x_rows,         \
-                       cell_start, sorted_pt, DHW, HW, sg, (T*)out)
+    hipLaunchKernelGGL((k_splat_fwd<F, T, L>), dim3(nblocks), dim3(kFwdBlock), lds, s, depth, ctx_t, x_rows,      \
+                       cell_start, sorted_key, DHW, HW, sg, (T*)out)
     if (out_dtype == LSS_F32) {
         if (fused) { if (nhwc) LSS_SPLAT(true, float, true); else LSS_SPLAT(true, float, false); }
         else { if (nhwc) LSS_SPLAT(false, float, true); else LSS_SPLAT(false, float, false); }

@@ -107,7 +107,8 @@ class SplatPlan:
     grid: GridSpec
     cell_of: torch.Tensor      # (Nprime,) int32, -1 = dropped
     cell_start: torch.Tensor   # (ncells+1,) int32
-    sorted_pt: torch.Tensor    # (Nprime,) int32 (only the first kept entries are meaningful)
+    sorted_pt: torch.Tensor    # (Nprime,) int32 packed (tile-cell << 24 | point) keys grouped by cell;
+                               # only the first cell_start[-1] entries are meaningful
     geom: Optional[torch.Tensor] = None
 
     @property
@@ -120,13 +121,13 @@ class SplatPlan:
         return B * N * D * H * W
 
 
-def _build_csr(cell_of, slot_of, counts, nprime: int, ncells: int, dev) -> Tuple[torch.Tensor, torch.Tensor]:
+def _build_csr(cell_of, slot_of, counts, nprime: int, ncells: int, grid: GridSpec, dev):
     lib = _lib.load()
     cell_start = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
     sorted_pt = torch.empty(nprime, device=dev, dtype=torch.int32)
     scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells)) // 4, device=dev, dtype=torch.int32)
     _lib.check(lib.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
-                                 _lib.ptr(cell_start), _lib.ptr(sorted_pt), _lib.ptr(scratch),
+                                 grid.c_struct(), _lib.ptr(cell_start), _lib.ptr(sorted_pt), _lib.ptr(scratch),
                                  _lib.stream_handle(dev)), "lss_csr_build")
     return cell_start, sorted_pt
 
@@ -155,7 +156,7 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
                                       _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
     cell_start = sorted_pt = None
     if want_csr:
-        cell_start, sorted_pt = _build_csr(cell_of, slot_of, counts, nprime, ncells, dev)
+        cell_start, sorted_pt = _build_csr(cell_of, slot_of, counts, nprime, ncells, grid, dev)
     return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_pt, geom)
 
 
@@ -173,7 +174,7 @@ def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
     _lib.check(lib.lss_cells_from_geom(_lib.ptr(gm), nprime, nprime // B, grid.c_struct(), _lib.ptr(cell_of),
                                        _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)),
                "lss_cells_from_geom")
-    cell_start, sorted_pt = _build_csr(cell_of, slot_of, counts, nprime, ncells, dev)
+    cell_start, sorted_pt = _build_csr(cell_of, slot_of, counts, nprime, ncells, grid, dev)
     return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_pt, None)
 
 

@@ -94,8 +94,14 @@ def test_voxel_ids_bit_exact_full_size(name, inverse):
     np.testing.assert_array_equal(np.diff(cs), counts)
     order = np.argsort(cell[kept], kind="stable")
     want_sorted = np.nonzero(kept)[0][order]
-    got_sorted = np.concatenate([np.sort(sp[cs[k]:cs[k + 1]]) for k in np.nonzero(counts)[0]])
+    got_sorted = np.concatenate([np.sort(sp[cs[k]:cs[k + 1]] & 0xFFFFFF) for k in np.nonzero(counts)[0]])
     np.testing.assert_array_equal(got_sorted, want_sorted)
+    # packed key high bits = the cell's index inside its splat tile (y % tile width)
+    Y = m_grid.nx[1]
+    yt = Y if Y <= 128 else next(t for t in range(128, 15, -4) if Y % t == 0)
+    tile_cell = sp[:cs[-1]] >> 24
+    cell_sorted = np.repeat(np.arange(counts.size), counts)
+    np.testing.assert_array_equal(tile_cell, (cell_sorted % Y) % yt)
 
 
 # ----------------------------------------------------------------------------- splat forward
