@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--bev-layout", default="nhwc", choices=["nhwc", "nchw"])
     ap.add_argument("--trunk-channels-last", type=int, default=0)
+    ap.add_argument("--trunk-fp32", type=int, default=0, help="run CamEncode outside autocast")
+    ap.add_argument("--dw-fp32", type=int, default=0, help="depthwise convs of the trunk in fp32")
+    ap.add_argument("--miopen-find", type=int, default=0, help="torch.backends.cudnn.benchmark (MIOpen find)")
     ap.add_argument("--inverse", default="host", choices=["host", "device"])
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -86,6 +89,17 @@ def build_model(args, dev, cfg, gc, dac):
         model.bevencode.to(memory_format=torch.channels_last)
     if args.trunk_channels_last:
         model.camencode.to(memory_format=torch.channels_last)
+    if args.dw_fp32:
+        from lss_carla_amd.efficientnet import set_depthwise_fp32
+        set_depthwise_fp32(model.camencode.trunk, True)
+    if args.trunk_fp32:
+        ce = model.camencode
+        fwd = ce.depthnet_out
+
+        def depthnet_out_fp32(x):
+            with torch.autocast("cuda", enabled=False):
+                return fwd(x.float())
+        ce.depthnet_out = depthnet_out_fp32
     model.train()
     return model
 
@@ -139,22 +153,15 @@ def cpu_baseline(model, cfg, gc, seconds: float):
 def main():
     args = parse()
     world, rank, dev = setup_dist()
-    torch.backends.cudnn.benchmark = False
-    from lss_carla_amd import ops, synthetic as syn
+    torch.backends.cudnn.benchmark = bool(args.miopen_find)
+    from lss_carla_amd import ops, parallel, synthetic as syn
     import lss_carla_amd as L
 
     cfg, gc, dac = syn.config_confs(args.config)
     B, N, fd = args.batch, cfg["N"], cfg["final_dim"]
     torch.manual_seed(1234 + rank)
     model = build_model(args, dev, cfg, gc, dac)
-    ddp = model
-    if world > 1:
-        # the classification head of the trunk is never used by LSS (no grads): keep it out of DDP's buckets
-        for n_, p in model.named_parameters():
-            if n_.startswith(("camencode.trunk._conv_head", "camencode.trunk._bn1", "camencode.trunk._fc")):
-                p.requires_grad_(False)
-        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index], bucket_cap_mb=25,
-                                                        broadcast_buffers=False, gradient_as_bucket_view=True)
+    ddp = parallel.make_data_parallel(model, dev) if world > 1 else model
     loss_fn = L.SimpleLoss(2.13).to(dev)
     opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-7,
                            fused=True)

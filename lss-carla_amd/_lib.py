@@ -53,25 +53,29 @@ SIGNATURES = {
 _lib: Optional[ctypes.CDLL] = None
 
 
-def load() -> ctypes.CDLL:
-    """Load (once) and type the library; raise if it is absent or of another ABI."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+def open_library(path: str) -> ctypes.CDLL:
+    """dlopen a build of the C ABI and attach the signatures (also used for tuning variants)."""
+    if not os.path.exists(path):
         raise RuntimeError(
-            f"lss_carla_amd: HIP library not found at {LIB_PATH}. Build it with "
+            f"lss_carla_amd: HIP library not found at {path}. Build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950). "
             "There is no CPU fallback.")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     if lib.lss_abi_version() != ABI_VERSION:
         raise RuntimeError(f"lss_carla_amd: ABI mismatch ({lib.lss_abi_version()} != {ABI_VERSION}); rebuild")
-    _lib = lib
     return lib
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and type the product library; raise if it is absent or of another ABI."""
+    global _lib
+    if _lib is None:
+        _lib = open_library(LIB_PATH)
+    return _lib
 
 
 def check(code: int, what: str) -> None:

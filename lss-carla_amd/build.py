@@ -26,10 +26,23 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build liblss_hip.so)")
 
 
-def command():
+def command(out: str = OUT, defines=()):
     # -ffp-contract=off: the geometry must keep the reference's un-fused fp32 op order.
     return [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-            "-Wall", "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}", "-o", OUT] + SOURCES
+            "-Wall", "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}"] + \
+        [f"-D{d}" for d in defines] + ["-o", out] + SOURCES
+
+
+def build_variant(name: str, defines) -> str:
+    """Tuning build with extra -D knobs into lss-carla_amd/variants/<name>.so (scripts/kbench.py)."""
+    vdir = os.path.join(HERE, "variants")
+    os.makedirs(vdir, exist_ok=True)
+    out = os.path.join(vdir, f"{name}.so")
+    r = subprocess.run(command(out, defines), capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"hipcc failed building variant {name}")
+    return out
 
 
 def up_to_date() -> bool:

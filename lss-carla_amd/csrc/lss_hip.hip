@@ -312,10 +312,26 @@ struct SplatGeo {
     int X, Y, Z, YT, ntiles_y;
 };
 
+// Tuning knobs (compile-time; scripts/kbench.py builds variants with -D to measure them).
+#ifndef LSS_FWD_WAVES
+#define LSS_FWD_WAVES 8
+#endif
+#ifndef LSS_FWD_PREFETCH
+#define LSS_FWD_PREFETCH 16
+#endif
+#ifndef LSS_FWD_PHASES  // bit 0: compute the cell sums, bit 1: write the tile (3 = the kernel)
+#define LSS_FWD_PHASES 3
+#endif
+#ifndef LSS_YT_MAX
+#define LSS_YT_MAX 128
+#endif
+#ifndef LSS_FWD_SKIP  // timing-only ablations: bit 0 window loop, bit 1 rank sort, bit 2 row gathers
+#define LSS_FWD_SKIP 0
+#endif
 constexpr int kMaxYT = 128;       // cells per tile (LDS sizing, 7-bit tile-cell in the keys)
-constexpr int kFwdWaves = 8;      // waves per splat tile
+constexpr int kFwdWaves = LSS_FWD_WAVES;  // waves per splat tile
 constexpr int kFwdBlock = kFwdWaves * kWave;
-constexpr int kPrefetch = 16;     // row loads in flight per wave
+constexpr int kPrefetch = LSS_FWD_PREFETCH;  // row loads in flight per wave
 
 // 16-byte vector stores of 16/sizeof(T) elements.
 template <typename T> struct Vec;
@@ -386,7 +402,7 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
     const int s0 = s_start[0], s1 = s_start[ny];
     const bool empty = s0 == s1;
 
-    if (!empty) {
+    if (!empty && (LSS_FWD_PHASES & 1)) {
         const int lds_elems = NHWC ? ny * kC : kC * S;
         for (int i = threadIdx.x * 4; i < lds_elems; i += kFwdBlock * 4)
             *reinterpret_cast<float4*>(lds + i) = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -396,7 +412,7 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
                                              : tile_lower_bound(s_start, ny, s0 + ((wave + 1) * span) / kFwdWaves, lane);
         __syncthreads();  // accumulator zeroed before any flush
         const float* base = FUSED ? ctx_t : xrows;
-        int c = cb;
+        int c = (LSS_FWD_SKIP & 1) ? ce : cb;
         while (c < ce) {
             const int ws = s_start[c];
             // window = cells [c, c+m): the longest run of whole cells holding <= 64 points
@@ -434,8 +450,9 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
             c += m;
             if (npts == 0) continue;  // a run of empty cells: their rows stay zero
             const int key = lane < npts ? sorted_key[ws + lane] : INT_MAX;
-            int rank = 0;
-            for (int j = 0; j < npts; ++j) rank += (__builtin_amdgcn_readlane(key, j) < key) ? 1 : 0;
+            int rank = (LSS_FWD_SKIP & 2) ? lane : 0;
+            if (!(LSS_FWD_SKIP & 2))
+                for (int j = 0; j < npts; ++j) rank += (__builtin_amdgcn_readlane(key, j) < key) ? 1 : 0;
             const int sk = __builtin_amdgcn_ds_permute(rank << 2, key);
             const int p = sk & 0xFFFFFF;
             int row = p;
@@ -451,7 +468,7 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
 #pragma unroll
                 for (int j = 0; j < kPrefetch; ++j) {
                     const int k = min(k0 + j, npts - 1);
-                    v[j] = base[(size_t)__builtin_amdgcn_readlane(row, k) * kC + lane];
+                    v[j] = (LSS_FWD_SKIP & 4) ? (float)k : base[(size_t)__builtin_amdgcn_readlane(row, k) * kC + lane];
                 }
 #pragma unroll
                 for (int j = 0; j < kPrefetch; ++j) {
@@ -472,6 +489,7 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
         __syncthreads();
     }
 
+    if (!(LSS_FWD_PHASES & 2)) return;
     constexpr int VN = Vec<OutT>::n;
     if (NHWC) {
         // cell (b, z, x, y) row = out[((b*X + x)*Y + y)*Z*C + z*C + c]
@@ -503,6 +521,148 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
                 obase[c * XY + yy] = from_f32<OutT>(empty ? 0.f : lds[c * S + yy]);
             }
         }
+    }
+}
+
+// ----------------------------------------------------------------------------- splat forward, channels-last
+// The production layout (BevEncode runs channels-last): every BEV cell is one contiguous row
+// of C values, so no LDS transpose is needed. One wave per "unit" of UY <= 63 consecutive cells
+// (b, z, x, y0..y0+ny), four independent waves per block, no barriers:
+//   - lane j holds cell_start of cell j of the unit (one coalesced load);
+//   - the rows of empty cells are zero-filled with 16-B stores (mask from a ballot);
+//   - windows of whole cells holding <= 64 points are formed from the lane-held starts;
+//     the next window's keys are loaded while the current one is reduced;
+//   - a window is rank-sorted by packed (tile-cell, point) key (ascending point id per cell:
+//     deterministic), its context rows (256 B, lane = channel) and depth weights gathered
+//     16 in flight, and each finished cell's sum stored straight to its row.
+struct UnitGeo {
+    int X, Y, Z, YT, UY, nuy;  // tile width (key encoding), unit width, units per BEV row
+};
+
+struct Window {
+    int c, m, ws, npts;  // first cell, cells, first sorted entry, points
+};
+
+__device__ __forceinline__ Window next_window(int sv, int c, int ny, int lane) {
+    while (c < ny) {
+        const int ws = __builtin_amdgcn_readlane(sv, c);
+        const int src = c + 1 + lane;
+        const int ej = __shfl(sv, src & 63, kWave);
+        const int m = __popcll(__ballot(src <= ny && ej - ws <= kWave));
+        if (m == 0) return {c, 0, ws, __builtin_amdgcn_readlane(sv, c + 1) - ws};
+        const int npts = __builtin_amdgcn_readlane(sv, c + m) - ws;
+        if (npts > 0) return {c, m, ws, npts};
+        c += m;  // a run of empty cells (already zero-filled)
+    }
+    return {ny, 0, 0, 0};
+}
+
+template <bool FUSED, typename OutT>
+__global__ __launch_bounds__(kBlock) void k_splat_fwd_rows(const float* __restrict__ depth,
+                                                           const float* __restrict__ ctx_t,
+                                                           const float* __restrict__ xrows,
+                                                           const int32_t* __restrict__ cell_start,
+                                                           const int32_t* __restrict__ sorted_key, int DHW, int HW,
+                                                           UnitGeo ug, int nunits, OutT* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int unit = blockIdx.x * (kBlock / kWave) + uniform(threadIdx.x >> 6);
+    if (unit >= nunits) return;
+    const int bzx = unit / ug.nuy;
+    const int y0 = (unit - bzx * ug.nuy) * ug.UY;
+    const int ny = min(ug.UY, ug.Y - y0);
+    const int x = bzx % ug.X;
+    const int bz = bzx / ug.X;
+    const int z = bz % ug.Z, b = bz / ug.Z;
+    const int cell0 = bzx * ug.Y + y0;
+    const int yoff = y0 % ug.YT;  // this unit's first cell inside its CSR tile
+    const size_t zc = (size_t)ug.Z * kC;
+    OutT* obase = out + (((size_t)b * ug.X + x) * ug.Y + y0) * zc + (size_t)z * kC;
+
+    const int sv = lane <= ny ? cell_start[cell0 + lane] : 0;
+    // zero-fill the rows of empty cells, 16-B stores
+    {
+        const int snext = __shfl(sv, (lane + 1) & 63, kWave);
+        const unsigned long long emask = __ballot(lane < ny && snext == sv);
+        constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
+        if (emask) {
+            for (int r0 = 0; r0 < ny; r0 += RPS) {
+                const int r = r0 + lane / LPR;
+                if (r < ny && ((emask >> r) & 1ull)) store_zero_vec(obase + r * zc + (lane % LPR) * EPL);
+            }
+        }
+    }
+    const float* base = FUSED ? ctx_t : xrows;
+    Window w = next_window(sv, 0, ny, lane);
+    int key = (w.m > 0 && lane < w.npts) ? sorted_key[w.ws + lane] : INT_MAX;
+    while (w.c < ny) {
+        if (w.m == 0) {
+            // one cell with more than 64 points: ordered selection over its list (rare)
+            float acc = 0.f;
+            int last = -1;
+            for (int k = 0; k < w.npts; ++k) {
+                int best = INT_MAX;
+                for (int i = lane; i < w.npts; i += kWave) {
+                    const int v = sorted_key[w.ws + i];
+                    if (v > last && v < best) best = v;
+                }
+                best = uniform(wave_min(best));
+                const int p = best & 0xFFFFFF;
+                float v;
+                if (FUSED) {
+                    const int cam = p / DHW;
+                    v = __fmul_rn(depth[p], ctx_t[(size_t)(cam * HW + (p - cam * DHW) % HW) * kC + lane]);
+                } else {
+                    v = xrows[(size_t)p * kC + lane];
+                }
+                acc = __fadd_rn(acc, v);
+                last = best;
+            }
+            obase[w.c * zc + lane] = from_f32<OutT>(acc);
+            w = next_window(sv, w.c + 1, ny, lane);
+            key = (w.m > 0 && lane < w.npts) ? sorted_key[w.ws + lane] : INT_MAX;
+            continue;
+        }
+        // prefetch the next window's keys
+        const Window wn = next_window(sv, w.c + w.m, ny, lane);
+        const int key_n = (wn.m > 0 && lane < wn.npts) ? sorted_key[wn.ws + lane] : INT_MAX;
+        const int npts = w.npts;
+        int rank = (LSS_FWD_SKIP & 2) ? lane : 0;
+        if (!(LSS_FWD_SKIP & 2))
+            for (int j = 0; j < npts; ++j) rank += (__builtin_amdgcn_readlane(key, j) < key) ? 1 : 0;
+        const int sk = __builtin_amdgcn_ds_permute(rank << 2, key);
+        const int p = sk & 0xFFFFFF;
+        int row = p;
+        if (FUSED) {
+            const int cam = p / DHW;
+            row = cam * HW + (p - cam * DHW) % HW;
+        }
+        const float wt = (FUSED && lane < npts) ? depth[p] : 1.f;
+        float acc = 0.f;
+        int cur = (__builtin_amdgcn_readlane(sk, 0) >> 24) - yoff;
+        for (int k0 = 0; k0 < npts; k0 += kPrefetch) {
+            float v[kPrefetch];
+#pragma unroll
+            for (int j = 0; j < kPrefetch; ++j) {
+                const int k = min(k0 + j, npts - 1);
+                v[j] = base[(size_t)__builtin_amdgcn_readlane(row, k) * kC + lane];
+            }
+#pragma unroll
+            for (int j = 0; j < kPrefetch; ++j) {
+                const int k = k0 + j;
+                if (k < npts) {
+                    const int cr = (__builtin_amdgcn_readlane(sk, k) >> 24) - yoff;
+                    if (cr != cur) {
+                        obase[cur * zc + lane] = from_f32<OutT>(acc);
+                        acc = 0.f;
+                        cur = cr;
+                    }
+                    acc = __fadd_rn(acc, FUSED ? __fmul_rn(readlane_f(wt, k), v[j]) : v[j]);
+                }
+            }
+        }
+        obase[cur * zc + lane] = from_f32<OutT>(acc);
+        w = wn;
+        key = key_n;
     }
 }
 
@@ -649,10 +809,22 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd_lifted(const GT* __restric
 inline int grid_blocks(long n, int per) { return (int)((n + per - 1) / per); }
 
 inline int choose_yt(int Y) {
-    if (Y <= 128) return Y;
-    for (int t = 128; t >= 16; t -= 4)
+    if (Y <= LSS_YT_MAX) return Y;
+    for (int t = LSS_YT_MAX; t >= 16; t -= 4)
         if (Y % t == 0) return t;
-    return 128;
+    return LSS_YT_MAX;
+}
+
+#ifndef LSS_UNIT_MAX
+#define LSS_UNIT_MAX 63
+#endif
+#ifndef LSS_FWD_ROWS  // 1: channels-last output through k_splat_fwd_rows (wave per unit) instead of the tile kernel
+#define LSS_FWD_ROWS 0
+#endif
+inline int choose_unit(int YT) {
+    for (int u = LSS_UNIT_MAX; u >= 8; --u)
+        if (YT % u == 0) return u;
+    return YT <= 63 ? YT : 63;
 }
 
 inline SplatGeo splat_geo(const lss_grid_t* g) {
@@ -778,10 +950,27 @@ int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows, c
     const int DHW = dims->D * dims->H * dims->W;
     const int HW = dims->H * dims->W;
     if ((long)dims->B * dims->N * DHW >= (1L << 24) || sg.YT > kMaxYT) return LSS_EUNSUPPORTED;
-    const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
     const bool nhwc = out_layout == LSS_NHWC;
-    const size_t lds = nhwc ? (size_t)sg.YT * kC * sizeof(float) : (size_t)kC * (sg.YT + 4) * sizeof(float);
     hipStream_t s = (hipStream_t)stream;
+    if (nhwc && LSS_FWD_ROWS) {
+        UnitGeo ug;
+        ug.X = sg.X; ug.Y = sg.Y; ug.Z = sg.Z; ug.YT = sg.YT;
+        ug.UY = choose_unit(sg.YT);
+        if (sg.YT % ug.UY != 0) return LSS_EUNSUPPORTED;
+        ug.nuy = (sg.Y + ug.UY - 1) / ug.UY;
+        const int nunits = dims->B * sg.Z * sg.X * ug.nuy;
+        const dim3 gr(grid_blocks(nunits, kBlock / kWave)), bl(kBlock);
+#define LSS_ROWS(F, T)                                                                                            \
+    hipLaunchKernelGGL((k_splat_fwd_rows<F, T>), gr, bl, 0, s, depth, ctx_t, x_rows, cell_start, sorted_key, DHW, \
+                       HW, ug, nunits, (T*)out)
+        if (out_dtype == LSS_F32) { if (fused) LSS_ROWS(true, float); else LSS_ROWS(false, float); }
+        else if (out_dtype == LSS_BF16) { if (fused) LSS_ROWS(true, bf16); else LSS_ROWS(false, bf16); }
+        else return LSS_EINVAL;
+#undef LSS_ROWS
+        return launch_status();
+    }
+    const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
+    const size_t lds = nhwc ? (size_t)sg.YT * kC * sizeof(float) : (size_t)kC * (sg.YT + 4) * sizeof(float);
 #define LSS_SPLAT(F, T, L)                                                                                        \
     hipLaunchKernelGGL((k_splat_fwd<F, T, L>), dim3(nblocks), dim3(kFwdBlock), lds, s, depth, ctx_t, x_rows,      \
                        cell_start, sorted_key, DHW, HW, sg, (T*)out)

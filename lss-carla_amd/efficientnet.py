@@ -97,12 +97,18 @@ class MBConvBlock(nn.Module):
         self._se_expand = Conv2dStaticSamePadding(sq, mid, 1, image_size=(1, 1))
         self._project_conv = Conv2dStaticSamePadding(mid, out_f, 1, bias=False, image_size=image_size)
         self._bn2 = nn.BatchNorm2d(out_f, momentum=BN_MOMENTUM, eps=BN_EPS)
+        self.depthwise_fp32 = False  # run the depthwise conv outside autocast (MIOpen solver choice)
 
     def forward(self, inputs: torch.Tensor, drop_connect_rate=None) -> torch.Tensor:
         x = inputs
         if self.expand != 1:
             x = F.silu(self._bn0(self._expand_conv(x)))
-        x = F.silu(self._bn1(self._depthwise_conv(x)))
+        if self.depthwise_fp32 and x.is_cuda and torch.is_autocast_enabled("cuda"):
+            with torch.autocast("cuda", enabled=False):
+                x = self._depthwise_conv(x.float())
+        else:
+            x = self._depthwise_conv(x)
+        x = F.silu(self._bn1(x))
         s = F.adaptive_avg_pool2d(x, 1)
         s = self._se_expand(F.silu(self._se_reduce(s)))
         x = torch.sigmoid(s) * x
@@ -112,6 +118,12 @@ class MBConvBlock(nn.Module):
                 x = drop_connect(x, drop_connect_rate, self.training)
             x = x + inputs
         return x
+
+
+def set_depthwise_fp32(module: nn.Module, flag: bool = True) -> None:
+    for m in module.modules():
+        if isinstance(m, MBConvBlock):
+            m.depthwise_fp32 = flag
 
 
 class EfficientNetB0(nn.Module):

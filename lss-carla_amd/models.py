@@ -50,7 +50,13 @@ class Up(nn.Module):
         )
 
     def forward(self, x1, x2):
-        return self.conv(torch.cat([x2, self.up(x1)], dim=1))
+        if x1.is_cuda and not x1.is_contiguous(memory_format=torch.channels_last):
+            # PyTorch's NCHW bilinear kernel parallelises over output pixels only (a 8x22 map:
+            # 176 threads, each looping over N*C); the channels-last kernel covers every element.
+            x1 = self.up(x1.contiguous(memory_format=torch.channels_last)).contiguous()
+        else:
+            x1 = self.up(x1)
+        return self.conv(torch.cat([x2, x1], dim=1))
 
 
 class CamEncode(nn.Module):

@@ -1,0 +1,121 @@
+"""World-size-2 data parallelism on CPU (gloo): DDP-averaged gradients of the LSS model equal the
+average of per-replica single-process gradients (BatchNorm is per replica, as in the reference).
+
+The HIP hot path has no CPU implementation, so on CPU the hot path runs through the oracle
+(test infrastructure) while the conv stacks, the DP wrapper and the all-reduce are the product's.
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import lss_carla_amd as L
+from lss_carla_amd import parallel
+from lss_carla_amd import synthetic as syn
+
+FD = (64, 192)
+GC = syn.grid_conf(xy=(-16.0, 16.0, 0.5))  # 64x64 BEV (BevEncode needs X, Y multiples of 8)
+
+
+class _CpuLSS(torch.nn.Module):
+    """Wraps the product model; forward goes through the oracle hot path (CPU only)."""
+
+    def __init__(self, model):
+        super().__init__()
+        self.model = model
+
+    def forward(self, x, rots, trans, intrins, post_rots, post_trans):
+        from oracle import lss_ref as ref
+        m = self.model
+        dx, bx, nx = ref.gen_dx_bx(GC["xbound"], GC["ybound"], GC["zbound"])
+        return ref.full_forward(m.camencode.depthnet_out, m.bevencode, m.frustum.detach(), x, rots, trans, intrins,
+                                post_rots, post_trans, dx, bx, nx, m.D)
+
+
+def _model():
+    torch.manual_seed(0)
+    m = L.compile_model(GC, syn.data_aug_conf(FD, 2), outC=1)
+    for mod in m.modules():
+        if isinstance(mod, (torch.nn.Dropout, torch.nn.Dropout2d)):
+            mod.p = 0.0
+    m.camencode.trunk._global_params.drop_connect_rate = 0.0
+    m.train()
+    return m
+
+
+def _batch(seed):
+    rig = syn.make_rig(1, 2, FD, seed=seed)
+    imgs = syn.make_images(1, 2, FD, seed=seed)
+    labels = syn.make_labels(1, 64, 64, seed=seed)
+    return imgs, rig, labels
+
+
+def _grads(module, seed):
+    imgs, rig, labels = _batch(seed)
+    out = module(imgs, rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"])
+    L.SimpleLoss(2.13)(out, labels).backward()
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    w, r, _, dev = parallel.init_from_env("gloo")
+    assert (w, r) == (world, rank)
+    m = _model()
+    ddp = parallel.make_data_parallel(_CpuLSS(m), dev)
+    assert isinstance(ddp, torch.nn.parallel.DistributedDataParallel)
+    _grads(ddp, seed=10 + rank)
+    if rank == 0:
+        torch.save({n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None},
+                   os.path.join(outdir, "ddp.pt"))
+    t = parallel.max_over_ranks(float(rank), dev)
+    assert t == world - 1
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.timeout(600)
+def test_ddp_gradients_equal_mean_of_replicas():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        ddp = torch.load(os.path.join(d, "ddp.pt"), weights_only=True)
+    ref = {}
+    nthreads = torch.get_num_threads()
+    torch.set_num_threads(2)  # the workers' thread count: same conv algorithms and reduction order
+    for rank in range(world):
+        m = _model()
+        parallel.freeze_unused(m)
+        _grads(_CpuLSS(m), seed=10 + rank)
+        for n, p in m.named_parameters():
+            if p.grad is not None:
+                ref[n] = ref.get(n, 0) + p.grad / world
+    torch.set_num_threads(nthreads)
+    assert set(ddp) == set(ref)
+    for n in ref:
+        scale = ref[n].abs().max().clamp_min(1e-12)
+        err = (ddp[n] - ref[n]).abs().max() / scale
+        assert err < 1e-3, (n, float(err), float(scale))
+    assert not any(n.startswith(parallel.UNUSED_PREFIXES) for n in ddp)
+
+
+def test_freeze_unused_through_wrapper():
+    w = _CpuLSS(_model())
+    assert parallel.freeze_unused(w) == parallel.freeze_unused(_model()) > 0
+
+
+def test_freeze_unused_counts_head_params():
+    m = _model()
+    frozen = parallel.freeze_unused(m)
+    assert frozen == 320 * 1280 + 2 * 1280 + 1280 * 1000 + 1000
+    assert all(not p.requires_grad for n, p in m.named_parameters() if n.startswith(parallel.UNUSED_PREFIXES))
