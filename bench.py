@@ -24,6 +24,11 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+# MIOpen find results (which conv solver per shape) and compiled kernels, kept in-tree so a
+# fresh box does not repeat the exhaustive search (tuning/README.md). Must precede torch init.
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(REPO, "tuning", "miopen", "db"))
+os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(REPO, "tuning", "miopen", "cache"))
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -47,7 +52,7 @@ def parse():
     ap.add_argument("--trunk-channels-last", type=int, default=0)
     ap.add_argument("--trunk-fp32", type=int, default=0, help="run CamEncode outside autocast")
     ap.add_argument("--dw-fp32", type=int, default=0, help="depthwise convs of the trunk in fp32")
-    ap.add_argument("--miopen-find", type=int, default=0, help="torch.backends.cudnn.benchmark (MIOpen find)")
+    ap.add_argument("--miopen-find", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
     ap.add_argument("--inverse", default="host", choices=["host", "device"])
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)

@@ -1,9 +1,14 @@
-# Bench variants back to back (one JSON line each), then a kernel-trace profile of one of them.
+# Bench variants back to back (one JSON line each). MIOpen's user find-db and kernel cache go to
+# gpurun_out/miopen so they can be inspected / reused.
 set -o pipefail
-mkdir -p gpurun_out/prof
+mkdir -p gpurun_out/prof gpurun_out/miopen/db gpurun_out/miopen/cache
+export MIOPEN_USER_DB_PATH="$PWD/gpurun_out/miopen/db" MIOPEN_CUSTOM_CACHE_DIR="$PWD/gpurun_out/miopen/cache"
 for v in "$@"; do
   echo "== variant: $v"
-  timeout -k 10 400 python bench.py --steps 10 --warmup 3 --cpu-baseline 0 $v > gpurun_out/var.log 2>&1; rc=$?
-  tail -1 gpurun_out/var.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'], d['roofline']['frac'])" || tail -5 gpurun_out/var.log
-  if [ $rc -ne 0 ]; then exit $rc; fi
+  t0=$(date +%s)
+  timeout -k 10 420 python bench.py --steps 10 --warmup 3 --cpu-baseline 0 $v > gpurun_out/var.log 2>&1; rc=$?
+  grep -h "first step\|warmup" gpurun_out/var.log | tr '\n' ' '; echo "(wall $(( $(date +%s) - t0 )) s)"
+  if [ $rc -ne 0 ]; then tail -3 gpurun_out/var.log; exit $rc; fi
+  tail -1 gpurun_out/var.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'], d['roofline']['frac'])"
 done
+du -sh gpurun_out/miopen/db gpurun_out/miopen/cache
