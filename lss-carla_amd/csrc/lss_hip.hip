@@ -7,10 +7,12 @@
 // Pipeline (forward, one training step):
 //   lss_camera_inverse      48 cameras, fp64 adjugate
 //   lss_geometry_cells      1 thread / point: frustum -> ego xyz -> cell id, atomic count
-//   lss_csr_build           counting sort: block reduce -> scan -> scatter of packed (tile-cell, point) keys
+//   lss_csr_build           counting sort: block reduce -> scan (+ point-balanced item cuts) -> scatter of
+//                           (cell, point) keys
 //   lss_lift_prep           1 block / 64 pixels: depth softmax + context -> pixel-major rows
-//   lss_splat_fwd           1 block (8 waves) / (b, z, x, y-tile): per-cell ordered sum -> LDS -> dense
-//                           coalesced BEV write (zero fill fused)   <- the HBM-bound kernel
+//   lss_splat_fwd           channels-last: 1 wave / ~32-point item (ordered per-cell sums, rows stored
+//                           directly) + 1 wave / 64 cells zero-filling empty rows  <- the HBM-bound kernel
+//                           NCHW: 1 block (8 waves) / BEV row tile, LDS accumulator, transposed write
 // Backward:
 //   lss_bev_rows            NCHW dbev -> compact per-cell rows (occupied cells only)
 //   lss_splat_bwd           1 wave / pixel: 16-B gathers of D rows to LDS, d_ctx, d_depth, softmax bwd
@@ -206,9 +208,13 @@ __global__ __launch_bounds__(1024) void k_scan_partials(const int32_t* __restric
     if (threadIdx.x == 0) partial[blockIdx.x] = s_total;
 }
 
+// Exclusive scan of the cell counts -> cell_start. It also cuts the sorted point list into
+// splat "items" of ~G points aligned to cell boundaries: item j starts at the first cell
+// boundary >= G*j (item_start pre-filled with INT_MAX; readers clamp to the total).
 __global__ __launch_bounds__(1024) void k_scan_apply(const int32_t* __restrict__ cnt, int ncells,
                                                      const int32_t* __restrict__ partial,
-                                                     int32_t* __restrict__ cell_start) {
+                                                     int32_t* __restrict__ cell_start, int item_g, int n_items,
+                                                     int32_t* __restrict__ item_start) {
     __shared__ int s_wave[32];
     __shared__ int s_total;
     __shared__ int s_red[16];
@@ -233,23 +239,30 @@ __global__ __launch_bounds__(1024) void k_scan_apply(const int32_t* __restrict__
     int run = prefix + block_exclusive_scan_1024(v, s_wave, &s_total);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        if (base + i < ncells) cell_start[base + i] = run;
+        if (base + i < ncells) {
+            cell_start[base + i] = run;
+            if (item_start != nullptr && c[i] > 0) {
+                // entries g*j inside [run, run + c): item j starts here (g*j == run) or at the cell's end
+                const int jhi = min((run + c[i] - 1) / item_g, n_items - 1);
+                for (int j = (run + item_g - 1) / item_g; j <= jhi; ++j)
+                    item_start[j] = (j * item_g == run) ? run : run + c[i];
+            }
+        }
         run += c[i];
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) cell_start[ncells] = prefix + s_total;
 }
 
-// Counting-sort scatter. The sorted entry of point p is the packed key (t << 24) | p with
-// t = the cell's index inside its splat tile (y % YT), so the splat kernel gets cell and
-// point id in one coalesced load and can order a window by key alone.
+// Counting-sort scatter: the sorted entry of point p is the key (cell << 32) | p, so a splat
+// wave gets both with one coalesced 8-B load per lane.
 __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ cell_of,
                                                     const int32_t* __restrict__ slot_of, int nprime,
-                                                    const int32_t* __restrict__ cell_start, int Y, int YT,
-                                                    int32_t* __restrict__ sorted_key) {
+                                                    const int32_t* __restrict__ cell_start,
+                                                    long long* __restrict__ sorted_key) {
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= nprime) return;
     const int cell = cell_of[p];
-    if (cell >= 0) sorted_key[cell_start[cell] + slot_of[p]] = (((cell % Y) % YT) << 24) | p;
+    if (cell >= 0) sorted_key[cell_start[cell] + slot_of[p]] = ((long long)cell << 32) | (unsigned)p;
 }
 
 // ----------------------------------------------------------------------------- lift prep
@@ -367,6 +380,18 @@ __device__ __forceinline__ void flush_row(float* lds, int S, int cell, int lane,
     else lds[lane * S + cell] = acc;
 }
 
+// Contribution of point p to channel `lane`: the lift's new_x element depth[p] * ctx[q(p), c]
+// (fused) or the lifted row (x_rows).
+template <bool FUSED>
+__device__ __forceinline__ float point_contrib(int p, const float* __restrict__ depth, const float* __restrict__ ctx_t,
+                                               const float* __restrict__ xrows, int DHW, int HW, int lane) {
+    if (FUSED) {
+        const int cam = p / DHW;
+        return __fmul_rn(depth[p], ctx_t[(size_t)(cam * HW + (p - cam * DHW) % HW) * kC + lane]);
+    }
+    return xrows[(size_t)p * kC + lane];
+}
+
 // One block = one tile of YT consecutive cells (b, z, x, y0..y0+ny) of the BEV, 8 waves.
 //  1. the tile's cell starts -> LDS; the fp32 accumulator tile is zeroed in LDS.
 //  2. the tile's point range is split over the waves at cell boundaries (equal point counts).
@@ -381,7 +406,7 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
                                                          const float* __restrict__ ctx_t,
                                                          const float* __restrict__ xrows,
                                                          const int32_t* __restrict__ cell_start,
-                                                         const int32_t* __restrict__ sorted_key, int DHW, int HW,
+                                                         const long long* __restrict__ sorted_key, int DHW, int HW,
                                                          SplatGeo sg, OutT* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_start[kMaxYT + 1];
@@ -427,19 +452,11 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
                 for (int k = 0; k < n; ++k) {
                     int best = INT_MAX;
                     for (int i = lane; i < n; i += kWave) {
-                        const int v = sorted_key[ws + i];
+                        const int v = (int)(sorted_key[ws + i] & 0xFFFFFFFF);
                         if (v > last && v < best) best = v;
                     }
                     best = uniform(wave_min(best));
-                    const int p = best & 0xFFFFFF;
-                    float v;
-                    if (FUSED) {
-                        const int cam = p / DHW;
-                        v = __fmul_rn(depth[p], ctx_t[(size_t)(cam * HW + (p - cam * DHW) % HW) * kC + lane]);
-                    } else {
-                        v = xrows[(size_t)p * kC + lane];
-                    }
-                    acc = __fadd_rn(acc, v);
+                    acc = __fadd_rn(acc, point_contrib<FUSED>(best, depth, ctx_t, xrows, DHW, HW, lane));
                     last = best;
                 }
                 flush_row<NHWC>(lds, S, c, lane, acc);
@@ -449,7 +466,11 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
             const int npts = s_start[c + m] - ws;
             c += m;
             if (npts == 0) continue;  // a run of empty cells: their rows stay zero
-            const int key = lane < npts ? sorted_key[ws + lane] : INT_MAX;
+            int key = INT_MAX;  // (cell inside the tile) << 24 | point id
+            if (lane < npts) {
+                const long long k64 = sorted_key[ws + lane];
+                key = (((int)(k64 >> 32) - cell0) << 24) | (int)(k64 & 0xFFFFFF);
+            }
             int rank = (LSS_FWD_SKIP & 2) ? lane : 0;
             if (!(LSS_FWD_SKIP & 2))
                 for (int j = 0; j < npts; ++j) rank += (__builtin_amdgcn_readlane(key, j) < key) ? 1 : 0;
@@ -525,144 +546,159 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
 }
 
 // ----------------------------------------------------------------------------- splat forward, channels-last
-// The production layout (BevEncode runs channels-last): every BEV cell is one contiguous row
-// of C values, so no LDS transpose is needed. One wave per "unit" of UY <= 63 consecutive cells
-// (b, z, x, y0..y0+ny), four independent waves per block, no barriers:
-//   - lane j holds cell_start of cell j of the unit (one coalesced load);
-//   - the rows of empty cells are zero-filled with 16-B stores (mask from a ballot);
-//   - windows of whole cells holding <= 64 points are formed from the lane-held starts;
-//     the next window's keys are loaded while the current one is reduced;
-//   - a window is rank-sorted by packed (tile-cell, point) key (ascending point id per cell:
-//     deterministic), its context rows (256 B, lane = channel) and depth weights gathered
-//     16 in flight, and each finished cell's sum stored straight to its row.
-struct UnitGeo {
-    int X, Y, Z, YT, UY, nuy;  // tile width (key encoding), unit width, units per BEV row
+// The production layout (BevEncode runs channels-last): every BEV cell is one contiguous row of
+// C values, so no LDS transpose is needed and the work can be balanced by points, not cells.
+// One launch, two wave roles, four independent waves per block (no barriers):
+//   item waves (first, so they are dispatched first): item j = the sorted points from the first
+//     cell boundary >= G*j to the next item's start (lss_csr_build), <= G + max-cell points, all
+//     whole cells. Lanes load (cell, point) keys in one 8-B load; windows of whole cells with
+//     <= 64 points are rank-sorted by (cell ordinal, point id) -> every cell is summed in
+//     ascending point id (deterministic); depth weights and context rows (256 B, lane =
+//     channel) are gathered 16 in flight; each finished cell's row is stored directly.
+//   zero waves: 64 consecutive cells each; the rows of the empty cells are written as zeros with
+//     16-B stores (every BEV element is written exactly once).
+#ifndef LSS_ITEM_G
+#define LSS_ITEM_G 256
+#endif
+constexpr int kItemG = LSS_ITEM_G;
+
+struct BevGeo {
+    int X, Y, Z;
+    int ncells, n_items, item_waves;
 };
 
-struct Window {
-    int c, m, ws, npts;  // first cell, cells, first sorted entry, points
-};
-
-__device__ __forceinline__ Window next_window(int sv, int c, int ny, int lane) {
-    while (c < ny) {
-        const int ws = __builtin_amdgcn_readlane(sv, c);
-        const int src = c + 1 + lane;
-        const int ej = __shfl(sv, src & 63, kWave);
-        const int m = __popcll(__ballot(src <= ny && ej - ws <= kWave));
-        if (m == 0) return {c, 0, ws, __builtin_amdgcn_readlane(sv, c + 1) - ws};
-        const int npts = __builtin_amdgcn_readlane(sv, c + m) - ws;
-        if (npts > 0) return {c, m, ws, npts};
-        c += m;  // a run of empty cells (already zero-filled)
-    }
-    return {ny, 0, 0, 0};
+template <typename OutT>
+__device__ __forceinline__ OutT* cell_row(OutT* out, int cell, const BevGeo& g) {
+    // channels-last (B, X, Y, Z*C): cell ((b*Z + z)*X + x)*Y + y -> ((b*X + x)*Y + y)*Z*C + z*C
+    const int XY = g.X * g.Y;
+    const int bz = cell / XY, xy = cell - bz * XY;
+    const int b = bz / g.Z, z = bz - b * g.Z;
+    return out + ((((size_t)b * XY + xy) * g.Z + z) * kC);
 }
 
 template <bool FUSED, typename OutT>
-__global__ __launch_bounds__(kBlock) void k_splat_fwd_rows(const float* __restrict__ depth,
-                                                           const float* __restrict__ ctx_t,
-                                                           const float* __restrict__ xrows,
-                                                           const int32_t* __restrict__ cell_start,
-                                                           const int32_t* __restrict__ sorted_key, int DHW, int HW,
-                                                           UnitGeo ug, int nunits, OutT* __restrict__ out) {
-    const int lane = threadIdx.x & 63;
-    const int unit = blockIdx.x * (kBlock / kWave) + uniform(threadIdx.x >> 6);
-    if (unit >= nunits) return;
-    const int bzx = unit / ug.nuy;
-    const int y0 = (unit - bzx * ug.nuy) * ug.UY;
-    const int ny = min(ug.UY, ug.Y - y0);
-    const int x = bzx % ug.X;
-    const int bz = bzx / ug.X;
-    const int z = bz % ug.Z, b = bz / ug.Z;
-    const int cell0 = bzx * ug.Y + y0;
-    const int yoff = y0 % ug.YT;  // this unit's first cell inside its CSR tile
-    const size_t zc = (size_t)ug.Z * kC;
-    OutT* obase = out + (((size_t)b * ug.X + x) * ug.Y + y0) * zc + (size_t)z * kC;
-
-    const int sv = lane <= ny ? cell_start[cell0 + lane] : 0;
-    // zero-fill the rows of empty cells, 16-B stores
-    {
-        const int snext = __shfl(sv, (lane + 1) & 63, kWave);
-        const unsigned long long emask = __ballot(lane < ny && snext == sv);
-        constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
-        if (emask) {
-            for (int r0 = 0; r0 < ny; r0 += RPS) {
-                const int r = r0 + lane / LPR;
-                if (r < ny && ((emask >> r) & 1ull)) store_zero_vec(obase + r * zc + (lane % LPR) * EPL);
-            }
-        }
-    }
+__device__ void splat_item(int j, const float* __restrict__ depth, const float* __restrict__ ctx_t,
+                           const float* __restrict__ xrows, const int32_t* __restrict__ cell_start,
+                           const long long* __restrict__ sorted_key, const int32_t* __restrict__ item_start,
+                           int DHW, int HW, const BevGeo& g, OutT* __restrict__ out, int lane) {
+    const int total = cell_start[g.ncells];
+    const int e1 = min(item_start[j + 1], total);
+    int w0 = min(item_start[j], total);
     const float* base = FUSED ? ctx_t : xrows;
-    Window w = next_window(sv, 0, ny, lane);
-    int key = (w.m > 0 && lane < w.npts) ? sorted_key[w.ws + lane] : INT_MAX;
-    while (w.c < ny) {
-        if (w.m == 0) {
-            // one cell with more than 64 points: ordered selection over its list (rare)
-            float acc = 0.f;
-            int last = -1;
-            for (int k = 0; k < w.npts; ++k) {
-                int best = INT_MAX;
-                for (int i = lane; i < w.npts; i += kWave) {
-                    const int v = sorted_key[w.ws + i];
-                    if (v > last && v < best) best = v;
+    while (w0 < e1) {
+        const int avail = e1 - w0;
+        // keys of the next (up to) 65 entries: lanes 0..63 + entry 64 for the split test
+        long long k64 = lane < avail ? sorted_key[w0 + lane] : -1ll;
+        const int cell = (int)(k64 >> 32);
+        int L = min(avail, kWave);
+        if (avail > kWave) {
+            const int cell64 = (int)(sorted_key[w0 + kWave] >> 32);
+            const unsigned long long same = __ballot(cell == cell64);
+            L = same ? __builtin_ctzll(same) : kWave;  // do not split the cell holding entry 64
+            if (L == 0) {
+                // one cell with more than 64 points: ordered selection over its list (rare)
+                const int n = cell_start[cell64 + 1] - w0;
+                float acc = 0.f;
+                int last = -1;
+                for (int k = 0; k < n; ++k) {
+                    int best = INT_MAX;
+                    for (int i = lane; i < n; i += kWave) {
+                        const int v = (int)(sorted_key[w0 + i] & 0xFFFFFFFF);
+                        if (v > last && v < best) best = v;
+                    }
+                    best = uniform(wave_min(best));
+                    acc = __fadd_rn(acc, point_contrib<FUSED>(best, depth, ctx_t, xrows, DHW, HW, lane));
+                    last = best;
                 }
-                best = uniform(wave_min(best));
-                const int p = best & 0xFFFFFF;
-                float v;
-                if (FUSED) {
-                    const int cam = p / DHW;
-                    v = __fmul_rn(depth[p], ctx_t[(size_t)(cam * HW + (p - cam * DHW) % HW) * kC + lane]);
-                } else {
-                    v = xrows[(size_t)p * kC + lane];
-                }
-                acc = __fadd_rn(acc, v);
-                last = best;
+                cell_row(out, cell64, g)[lane] = from_f32<OutT>(acc);
+                w0 += n;
+                continue;
             }
-            obase[w.c * zc + lane] = from_f32<OutT>(acc);
-            w = next_window(sv, w.c + 1, ny, lane);
-            key = (w.m > 0 && lane < w.npts) ? sorted_key[w.ws + lane] : INT_MAX;
-            continue;
         }
-        // prefetch the next window's keys
-        const Window wn = next_window(sv, w.c + w.m, ny, lane);
-        const int key_n = (wn.m > 0 && lane < wn.npts) ? sorted_key[wn.ws + lane] : INT_MAX;
-        const int npts = w.npts;
-        int rank = (LSS_FWD_SKIP & 2) ? lane : 0;
-        if (!(LSS_FWD_SKIP & 2))
-            for (int j = 0; j < npts; ++j) rank += (__builtin_amdgcn_readlane(key, j) < key) ? 1 : 0;
+        // cell ordinal inside the window (entries are grouped by cell), rank by (ordinal, point)
+        const int prev = __shfl(cell, (lane + 63) & 63, kWave);
+        const unsigned long long starts = __ballot(lane < L && (lane == 0 || cell != prev));
+        const int ord = __popcll(starts & (~0ull >> (63 - lane))) - 1;  // starts at lanes <= this one
+        const int key = lane < L ? ((ord << 24) | (int)(k64 & 0xFFFFFF)) : INT_MAX;
+        int rank = 0;
+        for (int i = 0; i < L; ++i) rank += (__builtin_amdgcn_readlane(key, i) < key) ? 1 : 0;
         const int sk = __builtin_amdgcn_ds_permute(rank << 2, key);
+        const int scell = __builtin_amdgcn_ds_permute(rank << 2, cell);
         const int p = sk & 0xFFFFFF;
         int row = p;
         if (FUSED) {
             const int cam = p / DHW;
             row = cam * HW + (p - cam * DHW) % HW;
         }
-        const float wt = (FUSED && lane < npts) ? depth[p] : 1.f;
+        const float wt = (FUSED && lane < L) ? depth[p] : 1.f;
         float acc = 0.f;
-        int cur = (__builtin_amdgcn_readlane(sk, 0) >> 24) - yoff;
-        for (int k0 = 0; k0 < npts; k0 += kPrefetch) {
+        int cur = __builtin_amdgcn_readlane(sk, 0) >> 24;
+        for (int k0 = 0; k0 < L; k0 += kPrefetch) {
             float v[kPrefetch];
 #pragma unroll
-            for (int j = 0; j < kPrefetch; ++j) {
-                const int k = min(k0 + j, npts - 1);
-                v[j] = base[(size_t)__builtin_amdgcn_readlane(row, k) * kC + lane];
+            for (int u = 0; u < kPrefetch; ++u) {
+                const int k = min(k0 + u, L - 1);
+                v[u] = base[(size_t)__builtin_amdgcn_readlane(row, k) * kC + lane];
             }
 #pragma unroll
-            for (int j = 0; j < kPrefetch; ++j) {
-                const int k = k0 + j;
-                if (k < npts) {
-                    const int cr = (__builtin_amdgcn_readlane(sk, k) >> 24) - yoff;
-                    if (cr != cur) {
-                        obase[cur * zc + lane] = from_f32<OutT>(acc);
+            for (int u = 0; u < kPrefetch; ++u) {
+                const int k = k0 + u;
+                if (k < L) {
+                    const int o = __builtin_amdgcn_readlane(sk, k) >> 24;
+                    if (o != cur) {
+                        cell_row(out, __builtin_amdgcn_readlane(scell, k - 1), g)[lane] = from_f32<OutT>(acc);
                         acc = 0.f;
-                        cur = cr;
+                        cur = o;
                     }
-                    acc = __fadd_rn(acc, FUSED ? __fmul_rn(readlane_f(wt, k), v[j]) : v[j]);
+                    acc = __fadd_rn(acc, FUSED ? __fmul_rn(readlane_f(wt, k), v[u]) : v[u]);
                 }
             }
         }
-        obase[cur * zc + lane] = from_f32<OutT>(acc);
-        w = wn;
-        key = key_n;
+        cell_row(out, __builtin_amdgcn_readlane(scell, L - 1), g)[lane] = from_f32<OutT>(acc);
+        w0 += L;
+    }
+}
+
+template <typename OutT>
+__device__ void zero_empty_rows(int u, const int32_t* __restrict__ cell_start, const BevGeo& g,
+                                OutT* __restrict__ out, int lane) {
+    const int k0 = u * kWave;
+    const int k = k0 + lane;
+    bool empty = false;
+    if (k < g.ncells) empty = cell_start[k] == cell_start[k + 1];
+    const unsigned long long emask = __ballot(empty);
+    constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
+    if (g.Z == 1) {
+        // rows of consecutive cells are contiguous
+        OutT* base = out + (size_t)k0 * kC;
+        for (int r0 = 0; r0 < kWave; r0 += RPS) {
+            const int r = r0 + lane / LPR;
+            if ((emask >> r) & 1ull) store_zero_vec(base + (size_t)r * kC + (lane % LPR) * EPL);
+        }
+    } else {
+        for (int r0 = 0; r0 < kWave; r0 += RPS) {
+            const int r = r0 + lane / LPR;
+            if ((emask >> r) & 1ull) store_zero_vec(cell_row(out, k0 + r, g) + (lane % LPR) * EPL);
+        }
+    }
+}
+
+template <bool FUSED, typename OutT>
+__global__ __launch_bounds__(kBlock) void k_splat_fwd_items(const float* __restrict__ depth,
+                                                            const float* __restrict__ ctx_t,
+                                                            const float* __restrict__ xrows,
+                                                            const int32_t* __restrict__ cell_start,
+                                                            const long long* __restrict__ sorted_key,
+                                                            const int32_t* __restrict__ item_start, int DHW, int HW,
+                                                            BevGeo g, OutT* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * (kBlock / kWave) + uniform(threadIdx.x >> 6);
+    if (w < g.item_waves) {
+        if (w < g.n_items) splat_item<FUSED, OutT>(w, depth, ctx_t, xrows, cell_start, sorted_key, item_start, DHW, HW,
+                                                   g, out, lane);
+    } else {
+        const int u = w - g.item_waves;
+        if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, g, out, lane);
     }
 }
 
@@ -815,18 +851,6 @@ inline int choose_yt(int Y) {
     return LSS_YT_MAX;
 }
 
-#ifndef LSS_UNIT_MAX
-#define LSS_UNIT_MAX 63
-#endif
-#ifndef LSS_FWD_ROWS  // 1: channels-last output through k_splat_fwd_rows (wave per unit) instead of the tile kernel
-#define LSS_FWD_ROWS 0
-#endif
-inline int choose_unit(int YT) {
-    for (int u = LSS_UNIT_MAX; u >= 8; --u)
-        if (YT % u == 0) return u;
-    return YT <= 63 ? YT : 63;
-}
-
 inline SplatGeo splat_geo(const lss_grid_t* g) {
     SplatGeo s;
     s.X = g->nx[0];
@@ -902,22 +926,27 @@ size_t lss_csr_scratch_bytes(int32_t ncells) {
     return sizeof(int32_t) * (size_t)((ncells + kScanItems - 1) / kScanItems + 1);
 }
 
+int32_t lss_splat_item_count(int32_t nprime) { return nprime / kItemG + 1; }
+
 int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, const int32_t* cell_count,
-                  int32_t ncells, const lss_grid_t* grid, int32_t* cell_start, int32_t* sorted_key, void* scratch,
+                  int32_t ncells, int32_t* cell_start, long long* sorted_key, int32_t* item_start, void* scratch,
                   lss_stream_t stream) {
-    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !scratch || nprime <= 0 ||
-        ncells <= 0 || !grid_ok(grid))
+    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !scratch || nprime <= 0 || ncells <= 0)
         return LSS_EINVAL;
-    if (nprime >= (1 << 24)) return LSS_EUNSUPPORTED;  // 24-bit point ids in the packed keys
-    const SplatGeo sg = splat_geo(grid);
-    if (sg.YT > kMaxYT) return LSS_EUNSUPPORTED;
+    if (nprime >= (1 << 24)) return LSS_EUNSUPPORTED;  // 24-bit point ids in the window keys
     const int nb = (ncells + kScanItems - 1) / kScanItems;
+    const int n_items = lss_splat_item_count(nprime);
     int32_t* partial = static_cast<int32_t*>(scratch);
     hipStream_t s = (hipStream_t)stream;
+    if (item_start != nullptr) {
+        const hipError_t e = hipMemsetD32Async(item_start, INT_MAX, (size_t)n_items + 1, s);
+        if (e != hipSuccess) return (int)e;
+    }
     hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial);
-    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial, cell_start);
+    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial, cell_start, kItemG,
+                       n_items, item_start);
     hipLaunchKernelGGL(k_scatter, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0, s, cell_of, slot_of, nprime,
-                       cell_start, sg.Y, sg.YT, sorted_key);
+                       cell_start, sorted_key);
     return launch_status();
 }
 
@@ -941,34 +970,36 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
 }
 
 int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows, const int32_t* cell_start,
-                  const int32_t* sorted_key, const lss_dims_t* dims, const lss_grid_t* grid, void* out,
-                  int32_t out_dtype, int32_t out_layout, lss_stream_t stream) {
+                  const long long* sorted_key, const int32_t* item_start, const lss_dims_t* dims,
+                  const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream) {
     if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_key || !out) return LSS_EINVAL;
     const bool fused = x_rows == nullptr;
     if (fused && (!depth || !ctx_t)) return LSS_EINVAL;
     const SplatGeo sg = splat_geo(grid);
     const int DHW = dims->D * dims->H * dims->W;
     const int HW = dims->H * dims->W;
-    if ((long)dims->B * dims->N * DHW >= (1L << 24) || sg.YT > kMaxYT) return LSS_EUNSUPPORTED;
+    const long nprime = (long)dims->B * dims->N * DHW;
+    if (nprime >= (1L << 24)) return LSS_EUNSUPPORTED;
     const bool nhwc = out_layout == LSS_NHWC;
     hipStream_t s = (hipStream_t)stream;
-    if (nhwc && LSS_FWD_ROWS) {
-        UnitGeo ug;
-        ug.X = sg.X; ug.Y = sg.Y; ug.Z = sg.Z; ug.YT = sg.YT;
-        ug.UY = choose_unit(sg.YT);
-        if (sg.YT % ug.UY != 0) return LSS_EUNSUPPORTED;
-        ug.nuy = (sg.Y + ug.UY - 1) / ug.UY;
-        const int nunits = dims->B * sg.Z * sg.X * ug.nuy;
-        const dim3 gr(grid_blocks(nunits, kBlock / kWave)), bl(kBlock);
-#define LSS_ROWS(F, T)                                                                                            \
-    hipLaunchKernelGGL((k_splat_fwd_rows<F, T>), gr, bl, 0, s, depth, ctx_t, x_rows, cell_start, sorted_key, DHW, \
-                       HW, ug, nunits, (T*)out)
-        if (out_dtype == LSS_F32) { if (fused) LSS_ROWS(true, float); else LSS_ROWS(false, float); }
-        else if (out_dtype == LSS_BF16) { if (fused) LSS_ROWS(true, bf16); else LSS_ROWS(false, bf16); }
+    if (nhwc && item_start != nullptr) {
+        BevGeo g;
+        g.X = sg.X; g.Y = sg.Y; g.Z = sg.Z;
+        g.ncells = dims->B * sg.Z * sg.X * sg.Y;
+        g.n_items = lss_splat_item_count((int32_t)nprime);
+        g.item_waves = (g.n_items + 3) & ~3;  // whole blocks of item waves, zero waves after
+        const int zero_waves = (g.ncells + kWave - 1) / kWave;
+        const dim3 gr((g.item_waves + zero_waves + 3) / 4), bl(kBlock);
+#define LSS_ITEMS(F, T)                                                                                           \
+    hipLaunchKernelGGL((k_splat_fwd_items<F, T>), gr, bl, 0, s, depth, ctx_t, x_rows, cell_start, sorted_key,     \
+                       item_start, DHW, HW, g, (T*)out)
+        if (out_dtype == LSS_F32) { if (fused) LSS_ITEMS(true, float); else LSS_ITEMS(false, float); }
+        else if (out_dtype == LSS_BF16) { if (fused) LSS_ITEMS(true, bf16); else LSS_ITEMS(false, bf16); }
         else return LSS_EINVAL;
-#undef LSS_ROWS
+#undef LSS_ITEMS
         return launch_status();
     }
+    if (sg.YT > kMaxYT) return LSS_EUNSUPPORTED;
     const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
     const size_t lds = nhwc ? (size_t)sg.YT * kC * sizeof(float) : (size_t)kC * (sg.YT + 4) * sizeof(float);
 #define LSS_SPLAT(F, T, L)                                                                                        \

@@ -107,8 +107,9 @@ class SplatPlan:
     grid: GridSpec
     cell_of: torch.Tensor      # (Nprime,) int32, -1 = dropped
     cell_start: torch.Tensor   # (ncells+1,) int32
-    sorted_pt: torch.Tensor    # (Nprime,) int32 packed (tile-cell << 24 | point) keys grouped by cell;
+    sorted_key: torch.Tensor   # (Nprime,) int64 (cell << 32 | point) grouped by cell;
                                # only the first cell_start[-1] entries are meaningful
+    item_start: Optional[torch.Tensor] = None  # point-balanced splat items (lss_csr_build)
     geom: Optional[torch.Tensor] = None
 
     @property
@@ -121,15 +122,16 @@ class SplatPlan:
         return B * N * D * H * W
 
 
-def _build_csr(cell_of, slot_of, counts, nprime: int, ncells: int, grid: GridSpec, dev):
+def _build_csr(cell_of, slot_of, counts, nprime: int, ncells: int, dev):
     lib = _lib.load()
     cell_start = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
-    sorted_pt = torch.empty(nprime, device=dev, dtype=torch.int32)
+    sorted_key = torch.empty(nprime, device=dev, dtype=torch.int64)
+    item_start = torch.empty(int(lib.lss_splat_item_count(nprime)) + 1, device=dev, dtype=torch.int32)
     scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells)) // 4, device=dev, dtype=torch.int32)
     _lib.check(lib.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
-                                 grid.c_struct(), _lib.ptr(cell_start), _lib.ptr(sorted_pt), _lib.ptr(scratch),
+                                 _lib.ptr(cell_start), _lib.ptr(sorted_key), _lib.ptr(item_start), _lib.ptr(scratch),
                                  _lib.stream_handle(dev)), "lss_csr_build")
-    return cell_start, sorted_pt
+    return cell_start, sorted_key, item_start
 
 
 def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, post_trans, grid: GridSpec,
@@ -154,10 +156,10 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
     _lib.check(lib.lss_geometry_cells(_lib.ptr(fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv),
                                       _lib.ptr(pt), dims, g, _lib.ptr(geom), _lib.ptr(cell_of), _lib.ptr(counts),
                                       _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
-    cell_start = sorted_pt = None
+    cell_start = sorted_key = item_start = None
     if want_csr:
-        cell_start, sorted_pt = _build_csr(cell_of, slot_of, counts, nprime, ncells, grid, dev)
-    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_pt, geom)
+        cell_start, sorted_key, item_start = _build_csr(cell_of, slot_of, counts, nprime, ncells, dev)
+    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, item_start, geom)
 
 
 def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
@@ -174,8 +176,8 @@ def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
     _lib.check(lib.lss_cells_from_geom(_lib.ptr(gm), nprime, nprime // B, grid.c_struct(), _lib.ptr(cell_of),
                                        _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)),
                "lss_cells_from_geom")
-    cell_start, sorted_pt = _build_csr(cell_of, slot_of, counts, nprime, ncells, grid, dev)
-    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_pt, None)
+    cell_start, sorted_key, item_start = _build_csr(cell_of, slot_of, counts, nprime, ncells, dev)
+    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, item_start, None)
 
 
 # ----------------------------------------------------------------------------- profiling hook
@@ -214,7 +216,7 @@ def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, 
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
     _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), _lib.ptr(x_rows), _lib.ptr(plan.cell_start),
-                                 _lib.ptr(plan.sorted_pt), plan.c_dims, plan.grid.c_struct(), _lib.ptr(out),
+                                 _lib.ptr(plan.sorted_key), _lib.ptr(plan.item_start), plan.c_dims, plan.grid.c_struct(), _lib.ptr(out),
                                  _lib.dtype_code(out.dtype), layout, _lib.stream_handle(dev)), "lss_splat_fwd")
     if prof:
         e1.record()

@@ -15,11 +15,13 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
-    "pf8": ["LSS_FWD_PREFETCH=8"],
-    "pf32": ["LSS_FWD_PREFETCH=32"],
-    "unit25": ["LSS_UNIT_MAX=32"],
-    "unit20": ["LSS_UNIT_MAX=24"],
-    "skip_rank": ["LSS_FWD_SKIP=2"],
+    "g64": ["LSS_ITEM_G=64"],
+    "g96": ["LSS_ITEM_G=96"],
+    "g128": ["LSS_ITEM_G=128"],
+    "g192": ["LSS_ITEM_G=192"],
+    "g256": ["LSS_ITEM_G=256"],
+    "g128_pf8": ["LSS_ITEM_G=128", "LSS_FWD_PREFETCH=8"],
+    "g128_pf32": ["LSS_ITEM_G=128", "LSS_FWD_PREFETCH=32"],
 }
 
 
@@ -90,10 +92,14 @@ def main():
 
     def fwd(l, out, layout):
         return lambda: _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), None, _lib.ptr(plan.cell_start),
-                                                  _lib.ptr(plan.sorted_pt), dims, g, _lib.ptr(out),
+                                                  _lib.ptr(plan.sorted_key), _lib.ptr(items), dims, g, _lib.ptr(out),
                                                   _lib.dtype_code(out.dtype), layout, st()), "fwd")
 
+    items = plan.item_start
     res["splat_fwd nhwc bf16"] = named("splat_fwd nhwc bf16", fwd(lib, bev_bf, _lib.NHWC))
+    items = None
+    res["splat_fwd nhwc bf16 [tile kernel]"] = named("splat_fwd nhwc bf16 [tile kernel]", fwd(lib, bev_bf, _lib.NHWC))
+    items = plan.item_start
     res["splat_fwd nchw f32"] = named("splat_fwd nchw f32", fwd(lib, bev_f, _lib.NCHW))
     for path in sorted(glob.glob(os.path.join(REPO, "lss-carla_amd", "variants", "*.so"))):
         vl = _lib.open_library(path)

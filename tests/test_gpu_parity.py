@@ -87,21 +87,40 @@ def test_voxel_ids_bit_exact_full_size(name, inverse):
         np.testing.assert_array_equal(plan.geom.cpu().numpy(), geom)
     # CSR: every cell's point set equals the oracle's
     cs = plan.cell_start.cpu().numpy().astype(np.int64)
-    sp = plan.sorted_pt.cpu().numpy()
+    sk = plan.sorted_key.cpu().numpy()
     kept = cell >= 0
     assert cs[-1] == kept.sum()
     counts = np.bincount(cell[kept], minlength=m_grid.ncells(cfg["B"]))
     np.testing.assert_array_equal(np.diff(cs), counts)
     order = np.argsort(cell[kept], kind="stable")
     want_sorted = np.nonzero(kept)[0][order]
-    got_sorted = np.concatenate([np.sort(sp[cs[k]:cs[k + 1]] & 0xFFFFFF) for k in np.nonzero(counts)[0]])
+    got_sorted = np.concatenate([np.sort(sk[cs[k]:cs[k + 1]] & 0xFFFFFFFF) for k in np.nonzero(counts)[0]])
     np.testing.assert_array_equal(got_sorted, want_sorted)
-    # packed key high bits = the cell's index inside its splat tile (y % tile width)
-    Y = m_grid.nx[1]
-    yt = Y if Y <= 128 else next(t for t in range(128, 15, -4) if Y % t == 0)
-    tile_cell = sp[:cs[-1]] >> 24
-    cell_sorted = np.repeat(np.arange(counts.size), counts)
-    np.testing.assert_array_equal(tile_cell, (cell_sorted % Y) % yt)
+    # key high word = the entry's cell
+    np.testing.assert_array_equal(sk[:cs[-1]] >> 32, np.repeat(np.arange(counts.size), counts))
+    # point-balanced items: cut at cell boundaries, nondecreasing, cover every entry
+    total = int(cs[-1])
+    items = np.minimum(plan.item_start.cpu().numpy().astype(np.int64), total)
+    assert items[0] == 0 and items[-1] == total and np.all(np.diff(items) >= 0)
+    assert np.isin(items, cs).all()
+    G = 256
+    assert np.diff(items).max() <= G + counts.max() - 1
+
+
+def test_splat_items_tile_agree_bitwise():
+    """The NHWC item kernel and the NHWC tile kernel sum every cell in the same order."""
+    cfg, gc, rig, frustum, dn, plan, bev = _lift_splat("c3", _lib.NHWC)
+    lib = _lib.load()
+    B, N, D, H, W = plan.dims
+    depth = torch.empty(B * N, D, H, W, device=DEV)
+    ctx_t = torch.empty(B * N * H * W, 64, device=DEV)
+    _lib.check(lib.lss_lift_prep(_lib.ptr(dn.to(DEV)), _lib.F32, plan.c_dims, _lib.ptr(depth), _lib.ptr(ctx_t),
+                                 _lib.stream_handle(DEV)), "lift")
+    out = torch.full_like(bev, float("nan"))
+    _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), None, _lib.ptr(plan.cell_start),
+                                 _lib.ptr(plan.sorted_key), None, plan.c_dims, plan.grid.c_struct(), _lib.ptr(out),
+                                 _lib.F32, _lib.NHWC, _lib.stream_handle(DEV)), "tile")
+    assert torch.equal(out, bev)
 
 
 # ----------------------------------------------------------------------------- splat forward

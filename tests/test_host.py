@@ -17,7 +17,7 @@ HEADER = os.path.join(REPO, "include", "lss_hip.h")
 
 def _declared():
     text = open(HEADER).read()
-    return set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(lss_\w+)\s*\(", text, re.M))
+    return set(re.findall(r"^\s*(?:int|int32_t|size_t|const char\*)\s+(lss_\w+)\s*\(", text, re.M))
 
 
 def test_header_declarations_match_binding():
