@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--trunk-fp32", type=int, default=0, help="run CamEncode outside autocast")
     ap.add_argument("--dw-fp32", type=int, default=0, help="depthwise convs of the trunk in fp32")
     ap.add_argument("--miopen-find", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
+    ap.add_argument("--dw-native", type=int, default=0, help="depthwise convs on PyTorch's native kernels")
+    ap.add_argument("--bn-native", default="", help="BatchNorm on native kernels: '', 'trunk', 'bev', 'all'")
     ap.add_argument("--inverse", default="host", choices=["host", "device"])
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -94,6 +96,15 @@ def build_model(args, dev, cfg, gc, dac):
         model.bevencode.to(memory_format=torch.channels_last)
     if args.trunk_channels_last:
         model.camencode.to(memory_format=torch.channels_last)
+    if args.dw_native:
+        from lss_carla_amd.efficientnet import set_depthwise_native
+        set_depthwise_native(model.camencode.trunk, True)
+    if args.bn_native:
+        from lss_carla_amd.efficientnet import set_batchnorm_native
+        if args.bn_native in ("trunk", "all"):
+            set_batchnorm_native(model.camencode)
+        if args.bn_native in ("bev", "all"):
+            set_batchnorm_native(model.bevencode)
     if args.dw_fp32:
         from lss_carla_amd.efficientnet import set_depthwise_fp32
         set_depthwise_fp32(model.camencode.trunk, True)
@@ -210,6 +221,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ops.SPLAT_PROFILE.enabled = False
     splat_ms = ops.SPLAT_PROFILE.avg_ms()
+    ops.SPLAT_PROFILE.release()
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 4
+#define LSS_ABI_VERSION 5
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -46,9 +46,15 @@ enum { LSS_NCHW = 0, LSS_NHWC = 1 };         /* BEV memory layouts of a (B, Z*C,
 enum { LSS_EINVAL = -1, LSS_EUNSUPPORTED = -2 };
 
 typedef void* lss_stream_t; /* a hipStream_t */
+typedef void* lss_event_t;  /* a hipEvent_t */
 
 int lss_abi_version(void);
 const char* lss_error_string(int code);
+
+/* Profiling helpers: hipEvents for the optional kernel-timestamp arguments of lss_splat_fwd. */
+int lss_event_create(lss_event_t* ev);
+int lss_event_destroy(lss_event_t ev);
+int lss_event_elapsed_ms(lss_event_t start, lss_event_t stop, float* ms); /* synchronises on stop */
 
 /* Device 3x3 inverses of post_rots and intrins (fp64 adjugate, rounded to fp32).
  * Replaces torch.inverse(post_rots.cpu()) / torch.inverse(intrins.cpu())
@@ -103,11 +109,14 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
  * Points of a cell are summed in ascending point id (deterministic). Empty cells
  * are written as zeros; every element of out is written once. LSS_NHWC with item_start
  * uses the point-balanced item kernel; otherwise a BEV-row tile kernel (<= 128 cells per
- * tile along Y) is used. Requires Nprime < 2^24 (LSS_EUNSUPPORTED otherwise). */
+ * tile along Y) is used. Requires Nprime < 2^24 (LSS_EUNSUPPORTED otherwise).
+ * ev_start / ev_stop (nullable) are stamped with the kernel's own start / end
+ * (hipExtLaunchKernel), so their elapsed time is the kernel alone, never launch latency. */
 int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows,
                   const int32_t* cell_start, const long long* sorted_key, const int32_t* item_start,
                   const lss_dims_t* dims, const lss_grid_t* grid,
-                  void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream);
+                  void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream,
+                  lss_event_t ev_start, lss_event_t ev_stop);
 
 /* Backward helpers. A "row" is the C gradient values of one cell.
  * lss_bev_rows: NCHW dbev -> rows[cell*C + c] for every occupied cell (others untouched). */

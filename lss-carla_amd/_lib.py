@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(_HERE, "liblss_hip.so")
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class Dims(ctypes.Structure):
@@ -38,6 +38,9 @@ _GRID = ctypes.POINTER(Grid)
 SIGNATURES = {
     "lss_abi_version": (ctypes.c_int, []),
     "lss_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "lss_event_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
+    "lss_event_destroy": (ctypes.c_int, [_p]),
+    "lss_event_elapsed_ms": (ctypes.c_int, [_p, _p, ctypes.POINTER(ctypes.c_float)]),
     "lss_camera_inverse": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p]),
     "lss_geometry_cells": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _p, _p, _p, _p]),
     "lss_cells_from_geom": (ctypes.c_int, [_p, _i32, _i32, _GRID, _p, _p, _p, _p]),
@@ -45,7 +48,7 @@ SIGNATURES = {
     "lss_splat_item_count": (ctypes.c_int32, [_i32]),
     "lss_csr_build": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _p, _p, _p, _p, _p]),
     "lss_lift_prep": (ctypes.c_int, [_p, _i32, _DIMS, _p, _p, _p]),
-    "lss_splat_fwd": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _p]),
+    "lss_splat_fwd": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _p, _p, _p]),
     "lss_bev_rows": (ctypes.c_int, [_p, _i32, _p, _DIMS, _GRID, _p, _p]),
     "lss_splat_bwd": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p, _DIMS, _GRID, _p, _i32, _p]),
     "lss_splat_bwd_lifted": (ctypes.c_int, [_p, _i32, _i32, _p, _i32, _DIMS, _GRID, _p, _p]),

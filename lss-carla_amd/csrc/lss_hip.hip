@@ -19,6 +19,7 @@
 
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
+#include <hip/hip_ext.h>
 #include <limits.h>
 #include <stdint.h>
 
@@ -881,6 +882,23 @@ extern "C" {
 
 int lss_abi_version(void) { return LSS_ABI_VERSION; }
 
+int lss_event_create(lss_event_t* ev) {
+    if (!ev) return LSS_EINVAL;
+    hipEvent_t e;
+    const hipError_t r = hipEventCreate(&e);
+    *ev = (lss_event_t)e;
+    return (int)r;
+}
+
+int lss_event_destroy(lss_event_t ev) { return ev ? (int)hipEventDestroy((hipEvent_t)ev) : LSS_EINVAL; }
+
+int lss_event_elapsed_ms(lss_event_t start, lss_event_t stop, float* ms) {
+    if (!start || !stop || !ms) return LSS_EINVAL;
+    hipError_t r = hipEventSynchronize((hipEvent_t)stop);
+    if (r != hipSuccess) return (int)r;
+    return (int)hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop);
+}
+
 const char* lss_error_string(int code) {
     if (code == 0) return "success";
     if (code == LSS_EINVAL) return "lss: invalid argument";
@@ -971,7 +989,9 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
 
 int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows, const int32_t* cell_start,
                   const long long* sorted_key, const int32_t* item_start, const lss_dims_t* dims,
-                  const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream) {
+                  const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream,
+                  lss_event_t ev_start, lss_event_t ev_stop) {
+    hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
     if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_key || !out) return LSS_EINVAL;
     const bool fused = x_rows == nullptr;
     if (fused && (!depth || !ctx_t)) return LSS_EINVAL;
@@ -991,8 +1011,8 @@ int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows, c
         const int zero_waves = (g.ncells + kWave - 1) / kWave;
         const dim3 gr((g.item_waves + zero_waves + 3) / 4), bl(kBlock);
 #define LSS_ITEMS(F, T)                                                                                           \
-    hipLaunchKernelGGL((k_splat_fwd_items<F, T>), gr, bl, 0, s, depth, ctx_t, x_rows, cell_start, sorted_key,     \
-                       item_start, DHW, HW, g, (T*)out)
+    hipExtLaunchKernelGGL((k_splat_fwd_items<F, T>), gr, bl, 0, s, e0, e1, 0, depth, ctx_t, x_rows, cell_start, \
+                          sorted_key, item_start, DHW, HW, g, (T*)out)
         if (out_dtype == LSS_F32) { if (fused) LSS_ITEMS(true, float); else LSS_ITEMS(false, float); }
         else if (out_dtype == LSS_BF16) { if (fused) LSS_ITEMS(true, bf16); else LSS_ITEMS(false, bf16); }
         else return LSS_EINVAL;
@@ -1003,8 +1023,8 @@ int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows, c
     const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
     const size_t lds = nhwc ? (size_t)sg.YT * kC * sizeof(float) : (size_t)kC * (sg.YT + 4) * sizeof(float);
 #define LSS_SPLAT(F, T, L)                                                                                        \
-    hipLaunchKernelGGL((k_splat_fwd<F, T, L>), dim3(nblocks), dim3(kFwdBlock), lds, s, depth, ctx_t, x_rows,      \
-                       cell_start, sorted_key, DHW, HW, sg, (T*)out)
+    hipExtLaunchKernelGGL((k_splat_fwd<F, T, L>), dim3(nblocks), dim3(kFwdBlock), (uint32_t)lds, s, e0, e1, 0, depth, \
+                          ctx_t, x_rows, cell_start, sorted_key, DHW, HW, sg, (T*)out)
     if (out_dtype == LSS_F32) {
         if (fused) { if (nhwc) LSS_SPLAT(true, float, true); else LSS_SPLAT(true, float, false); }
         else { if (nhwc) LSS_SPLAT(false, float, true); else LSS_SPLAT(false, float, false); }

@@ -71,6 +71,36 @@ class Conv2dStaticSamePadding(nn.Conv2d):
         return self._conv_forward(self.static_padding(x), self.weight, self.bias)
 
 
+class _NativeConv2d(torch.autograd.Function):
+    """conv2d forward AND backward with MIOpen disabled, i.e. on PyTorch's native kernels.
+
+    PyTorch picks the convolution backend again in backward (from the global cuDNN/MIOpen
+    flag), so disabling MIOpen around the forward alone is not enough. Used for the depthwise
+    convolutions, for which MIOpen has no bf16 NCHW solver and falls back to naive kernels.
+    """
+
+    @staticmethod
+    def forward(ctx, x, w, stride, padding, dilation, groups):
+        if x.is_cuda and torch.is_autocast_enabled("cuda"):
+            dt = torch.get_autocast_dtype("cuda")
+            x, w = x.to(dt), w.to(dt)
+        with torch.autocast("cuda", enabled=False), torch.backends.cudnn.flags(enabled=False):
+            y = F.conv2d(x, w, None, stride, padding, dilation, groups)
+        ctx.save_for_backward(x, w)
+        ctx.conf = (stride, padding, dilation, groups)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        stride, padding, dilation, groups = ctx.conf
+        with torch.autocast("cuda", enabled=False), torch.backends.cudnn.flags(enabled=False):
+            gx, gw, _ = torch.ops.aten.convolution_backward(
+                gy.to(x.dtype).contiguous(), x, w, None, list(stride), list(padding), list(dilation), False, [0, 0],
+                groups, [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        return gx, gw, None, None, None, None
+
+
 def drop_connect(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
     """Per-sample stochastic depth (efficientnet_pytorch ``drop_connect``)."""
     if not training or not p:
@@ -98,12 +128,16 @@ class MBConvBlock(nn.Module):
         self._project_conv = Conv2dStaticSamePadding(mid, out_f, 1, bias=False, image_size=image_size)
         self._bn2 = nn.BatchNorm2d(out_f, momentum=BN_MOMENTUM, eps=BN_EPS)
         self.depthwise_fp32 = False  # run the depthwise conv outside autocast (MIOpen solver choice)
+        self.depthwise_native = False  # run the depthwise conv on PyTorch's native kernels (not MIOpen)
 
     def forward(self, inputs: torch.Tensor, drop_connect_rate=None) -> torch.Tensor:
         x = inputs
         if self.expand != 1:
             x = F.silu(self._bn0(self._expand_conv(x)))
-        if self.depthwise_fp32 and x.is_cuda and torch.is_autocast_enabled("cuda"):
+        if self.depthwise_native and x.is_cuda:
+            dw = self._depthwise_conv
+            x = _NativeConv2d.apply(dw.static_padding(x), dw.weight, dw.stride, dw.padding, dw.dilation, dw.groups)
+        elif self.depthwise_fp32 and x.is_cuda and torch.is_autocast_enabled("cuda"):
             with torch.autocast("cuda", enabled=False):
                 x = self._depthwise_conv(x.float())
         else:
@@ -124,6 +158,31 @@ def set_depthwise_fp32(module: nn.Module, flag: bool = True) -> None:
     for m in module.modules():
         if isinstance(m, MBConvBlock):
             m.depthwise_fp32 = flag
+
+
+def set_depthwise_native(module: nn.Module, flag: bool = True) -> None:
+    for m in module.modules():
+        if isinstance(m, MBConvBlock):
+            m.depthwise_native = flag
+
+
+class _NativeBatchNorm2d(nn.BatchNorm2d):
+    """BatchNorm2d on PyTorch's native kernels (MIOpen disabled for the forward, which also
+    fixes the backward: the autograd node is NativeBatchNormBackward)."""
+
+    def forward(self, x):
+        with torch.backends.cudnn.flags(enabled=False):
+            return super().forward(x)
+
+
+def set_batchnorm_native(module: nn.Module) -> int:
+    """Swap the class of every BatchNorm2d under `module` (state_dict unchanged)."""
+    n = 0
+    for m in module.modules():
+        if type(m) is nn.BatchNorm2d:
+            m.__class__ = _NativeBatchNorm2d
+            n += 1
+    return n
 
 
 class EfficientNetB0(nn.Module):

@@ -14,6 +14,7 @@ Reference boundary replaced (shdragron/LSS-Carla):
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 from typing import Optional, Sequence, Tuple
 
@@ -182,21 +183,46 @@ def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
 
 # ----------------------------------------------------------------------------- profiling hook
 class _SplatProfile:
-    """Opt-in HIP-event bracketing of every lss_splat_fwd launch (used by bench.py)."""
+    """Opt-in timing of every lss_splat_fwd launch (used by bench.py).
+
+    The ABI stamps a pair of hipEvents with the kernel's own start/end (hipExtLaunchKernel), so
+    the average is kernel time only -- the same quantity rocprofv3 --kernel-trace reports.
+    """
 
     def __init__(self):
         self.enabled = False
-        self.events = []
+        self.pairs = []
 
     def reset(self, enabled: bool = True):
+        self.release()
         self.enabled = enabled
-        self.events = []
+
+    def new_pair(self):
+        lib = _lib.load()
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(lib.lss_event_create(ctypes.byref(a)), "lss_event_create")
+        _lib.check(lib.lss_event_create(ctypes.byref(b)), "lss_event_create")
+        self.pairs.append((a, b))
+        return a, b
 
     def avg_ms(self) -> Optional[float]:
-        if not self.events:
+        if not self.pairs:
             return None
-        torch.cuda.synchronize()
-        return sum(a.elapsed_time(b) for a, b in self.events) / len(self.events)
+        lib = _lib.load()
+        tot = 0.0
+        for a, b in self.pairs:
+            ms = ctypes.c_float()
+            _lib.check(lib.lss_event_elapsed_ms(a, b, ctypes.byref(ms)), "lss_event_elapsed_ms")
+            tot += ms.value
+        return tot / len(self.pairs)
+
+    def release(self):
+        if self.pairs:
+            lib = _lib.load()
+            for a, b in self.pairs:
+                lib.lss_event_destroy(a)
+                lib.lss_event_destroy(b)
+        self.pairs = []
 
 
 SPLAT_PROFILE = _SplatProfile()
@@ -211,16 +237,11 @@ def _new_bev(B, Z, X, Y, dtype, layout, dev) -> torch.Tensor:
 def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, layout: int):
     lib = _lib.load()
     dev = out.device
-    prof = SPLAT_PROFILE.enabled
-    if prof:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
+    e0, e1 = SPLAT_PROFILE.new_pair() if SPLAT_PROFILE.enabled else (None, None)
     _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), _lib.ptr(x_rows), _lib.ptr(plan.cell_start),
-                                 _lib.ptr(plan.sorted_key), _lib.ptr(plan.item_start), plan.c_dims, plan.grid.c_struct(), _lib.ptr(out),
-                                 _lib.dtype_code(out.dtype), layout, _lib.stream_handle(dev)), "lss_splat_fwd")
-    if prof:
-        e1.record()
-        SPLAT_PROFILE.events.append((e0, e1))
+                                 _lib.ptr(plan.sorted_key), _lib.ptr(plan.item_start), plan.c_dims,
+                                 plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype), layout,
+                                 _lib.stream_handle(dev), e0, e1), "lss_splat_fwd")
 
 
 def _grad_rows(plan: SplatPlan, dbev: torch.Tensor) -> Tuple[torch.Tensor, int]:

@@ -93,7 +93,7 @@ def main():
     def fwd(l, out, layout):
         return lambda: _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), None, _lib.ptr(plan.cell_start),
                                                   _lib.ptr(plan.sorted_key), _lib.ptr(items), dims, g, _lib.ptr(out),
-                                                  _lib.dtype_code(out.dtype), layout, st()), "fwd")
+                                                  _lib.dtype_code(out.dtype), layout, st(), None, None), "fwd")
 
     items = plan.item_start
     res["splat_fwd nhwc bf16"] = named("splat_fwd nhwc bf16", fwd(lib, bev_bf, _lib.NHWC))

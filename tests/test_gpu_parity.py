@@ -119,7 +119,7 @@ def test_splat_items_tile_agree_bitwise():
     out = torch.full_like(bev, float("nan"))
     _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), None, _lib.ptr(plan.cell_start),
                                  _lib.ptr(plan.sorted_key), None, plan.c_dims, plan.grid.c_struct(), _lib.ptr(out),
-                                 _lib.F32, _lib.NHWC, _lib.stream_handle(DEV)), "tile")
+                                 _lib.F32, _lib.NHWC, _lib.stream_handle(DEV), None, None), "tile")
     assert torch.equal(out, bev)
 
 
