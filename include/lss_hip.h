@@ -86,7 +86,7 @@ int lss_cells_from_geom(const float* geom, int32_t nprime, int32_t points_per_ba
  * grouped by cell, each as the key (cell << 32) | p (order inside a cell is arbitrary: the
  * splat orders by point id). If item_start is non-NULL (lss_splat_item_count(Nprime) + 1
  * ints) it also cuts the sorted list into point-balanced splat items: item j begins at the
- * first cell boundary >= G*j (G = 256); entries past the end hold INT_MAX (readers clamp to
+ * first cell boundary >= G*j (G = 32); entries past the end hold INT_MAX (readers clamp to
  * cell_start[ncells]). Requires Nprime < 2^24. scratch: lss_csr_scratch_bytes(ncells) bytes. */
 size_t lss_csr_scratch_bytes(int32_t ncells);
 int32_t lss_splat_item_count(int32_t nprime);

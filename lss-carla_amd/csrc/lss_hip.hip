@@ -559,7 +559,7 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
 //   zero waves: 64 consecutive cells each; the rows of the empty cells are written as zeros with
 //     16-B stores (every BEV element is written exactly once).
 #ifndef LSS_ITEM_G
-#define LSS_ITEM_G 256
+#define LSS_ITEM_G 32
 #endif
 constexpr int kItemG = LSS_ITEM_G;
 

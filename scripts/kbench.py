@@ -15,13 +15,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
+    "g8": ["LSS_ITEM_G=8"],
+    "g16": ["LSS_ITEM_G=16"],
+    "g32": ["LSS_ITEM_G=32"],
     "g64": ["LSS_ITEM_G=64"],
-    "g96": ["LSS_ITEM_G=96"],
     "g128": ["LSS_ITEM_G=128"],
-    "g192": ["LSS_ITEM_G=192"],
-    "g256": ["LSS_ITEM_G=256"],
-    "g128_pf8": ["LSS_ITEM_G=128", "LSS_FWD_PREFETCH=8"],
-    "g128_pf32": ["LSS_ITEM_G=128", "LSS_FWD_PREFETCH=32"],
 }
 
 
@@ -37,6 +35,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", default="", help="run only ops whose name contains this (for rocprofv3 --pmc)")
+    ap.add_argument("--cold", type=int, default=1, help="also time splat_fwd with caches flushed before each launch")
     args = ap.parse_args()
     if args.build_variants:
         build_variants()
@@ -73,6 +72,27 @@ def main():
 
     res = {}
 
+    def lib_plan(l):
+        """cell_start / sorted_key / item_start built by library `l` (its own item granularity)."""
+        import ctypes as ct
+        ncells = grid.ncells(B)
+        nprime = plan.nprime
+        counts = torch.zeros(ncells, device=dev, dtype=torch.int32)
+        slot = torch.empty(nprime, device=dev, dtype=torch.int32)
+        cell_of = torch.empty(nprime, device=dev, dtype=torch.int32)
+        pinv, kinv = ops.camera_inverses(rig["post_rots"], rig["intrins"], "device")
+        ro, tr, pt = [t.float().contiguous() for t in (rig["rots"], rig["trans"], rig["post_trans"])]
+        _lib.check(l.lss_geometry_cells(_lib.ptr(frustum), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv),
+                                        _lib.ptr(pinv), _lib.ptr(pt), dims, g, None, _lib.ptr(cell_of),
+                                        _lib.ptr(counts), _lib.ptr(slot), st()), "geom")
+        cs = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
+        sk = torch.empty(nprime, device=dev, dtype=torch.int64)
+        its = torch.empty(int(l.lss_splat_item_count(nprime)) + 1, device=dev, dtype=torch.int32)
+        scr = torch.empty(int(l.lss_csr_scratch_bytes(ncells)) // 4, device=dev, dtype=torch.int32)
+        _lib.check(l.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot), nprime, _lib.ptr(counts), ncells, _lib.ptr(cs),
+                                   _lib.ptr(sk), _lib.ptr(its), _lib.ptr(scr), st()), "csr")
+        return cs, sk, its
+
     def named(name, fn, *a):
         timeit.name = name
         return timeit(fn, *a)
@@ -90,9 +110,10 @@ def main():
     res["lift_prep"] = named("lift_prep", lambda: _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth),
                                                                     _lib.ptr(ctx_t), st()), "lift"))
 
-    def fwd(l, out, layout):
-        return lambda: _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), None, _lib.ptr(plan.cell_start),
-                                                  _lib.ptr(plan.sorted_key), _lib.ptr(items), dims, g, _lib.ptr(out),
+    def fwd(l, out, layout, csr=None):
+        cs, sk, its = csr if csr is not None else (plan.cell_start, plan.sorted_key, items)
+        return lambda: _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), None, _lib.ptr(cs),
+                                                  _lib.ptr(sk), _lib.ptr(its), dims, g, _lib.ptr(out),
                                                   _lib.dtype_code(out.dtype), layout, st(), None, None), "fwd")
 
     items = plan.item_start
@@ -101,10 +122,47 @@ def main():
     res["splat_fwd nhwc bf16 [tile kernel]"] = named("splat_fwd nhwc bf16 [tile kernel]", fwd(lib, bev_bf, _lib.NHWC))
     items = plan.item_start
     res["splat_fwd nchw f32"] = named("splat_fwd nchw f32", fwd(lib, bev_f, _lib.NCHW))
+    fwd(lib, bev_bf, _lib.NHWC)()
+    ref_out = bev_bf.clone()
+    variants = {}
     for path in sorted(glob.glob(os.path.join(REPO, "lss-carla_amd", "variants", "*.so"))):
         vl = _lib.open_library(path)
         name = os.path.basename(path)[:-3]
-        res[f"splat_fwd nhwc bf16 [{name}]"] = named(f"splat_fwd nhwc bf16 [{name}]", fwd(vl, bev_bf, _lib.NHWC))
+        variants[name] = (vl, lib_plan(vl))
+        res[f"splat_fwd nhwc bf16 [{name}]"] = named(f"splat_fwd nhwc bf16 [{name}]",
+                                                     fwd(vl, bev_bf, _lib.NHWC, variants[name][1]))
+        if not torch.equal(bev_bf, ref_out):
+            print(f"WARNING variant {name}: output differs from the product kernel", flush=True)
+    if args.cold:
+        # cold caches, as inside a training step (the trunk runs between the CSR build and the splat):
+        # 512 MiB written before every launch, kernel time from kernel-stamped events (hipExtLaunchKernel)
+        flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+
+        def cold(l, out, layout, csr, iters=20):
+            import ctypes as ct
+            cs, sk, its = csr
+            tot = 0.0
+            for _ in range(iters):
+                flush.zero_()
+                a, b = ct.c_void_p(), ct.c_void_p()
+                l.lss_event_create(ct.byref(a))
+                l.lss_event_create(ct.byref(b))
+                _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), None, _lib.ptr(cs),
+                                           _lib.ptr(sk), _lib.ptr(its), dims, g, _lib.ptr(out),
+                                           _lib.dtype_code(out.dtype), layout, st(), a, b), "fwd")
+                ms = ct.c_float()
+                l.lss_event_elapsed_ms(a, b, ct.byref(ms))
+                tot += ms.value
+                l.lss_event_destroy(a)
+                l.lss_event_destroy(b)
+            return tot / iters * 1e3
+
+        if not args.only or "cold" in args.only:
+            pc = (plan.cell_start, plan.sorted_key, plan.item_start)
+            res["COLD splat_fwd nhwc bf16"] = cold(lib, bev_bf, _lib.NHWC, pc)
+            res["COLD splat_fwd nhwc bf16 [tile kernel]"] = cold(lib, bev_bf, _lib.NHWC, pc[:2] + (None,))
+            for name, (vl, csr) in variants.items():
+                res[f"COLD splat_fwd nhwc bf16 [{name}]"] = cold(vl, bev_bf, _lib.NHWC, csr)
     g_bf = torch.randn(B, Z * 64, X, Y, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     d_dn = torch.empty_like(dn)
     res["splat_bwd nhwc bf16"] = named("splat_bwd nhwc bf16", lambda: _lib.check(lib.lss_splat_bwd(
@@ -117,7 +175,7 @@ def main():
     nbytes = (B * N * D * H * W * 4 + B * N * H * W * 64 * 4 + kept * 4 + (grid.ncells(B) + 1) * 4
               + grid.ncells(B) * 64 * 2)
     for k, v in res.items():
-        extra = f"  {nbytes / v / 1e3:7.1f} GB/s alg" if k.startswith("splat_fwd nhwc bf16") else ""
+        extra = f"  {nbytes / v / 1e3:7.1f} GB/s alg" if "splat_fwd nhwc bf16" in k else ""
         print(f"{k:40s} {v:9.2f} us{extra}")
     print(json.dumps({"kept": kept, "alg_bytes_fwd_bf16": nbytes}))
 

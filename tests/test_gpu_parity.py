@@ -103,7 +103,7 @@ def test_voxel_ids_bit_exact_full_size(name, inverse):
     items = np.minimum(plan.item_start.cpu().numpy().astype(np.int64), total)
     assert items[0] == 0 and items[-1] == total and np.all(np.diff(items) >= 0)
     assert np.isin(items, cs).all()
-    G = 256
+    G = 32
     assert np.diff(items).max() <= G + counts.max() - 1
 
 
