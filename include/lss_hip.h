@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 5
+#define LSS_ABI_VERSION 6
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -82,17 +82,17 @@ int lss_cells_from_geom(const float* geom, int32_t nprime, int32_t points_per_ba
                         int32_t* slot_of, lss_stream_t stream);
 
 /* Counting-sort CSR of points by cell (replaces ranks + argsort, src/models.py:225-231):
- * cell_start (ncells+1) = exclusive scan of cell_count; sorted_key (Nprime) = the kept points
- * grouped by cell, each as the key (cell << 32) | p (order inside a cell is arbitrary: the
- * splat orders by point id). If item_start is non-NULL (lss_splat_item_count(Nprime) + 1
- * ints) it also cuts the sorted list into point-balanced splat items: item j begins at the
- * first cell boundary >= G*j (G = 32); entries past the end hold INT_MAX (readers clamp to
- * cell_start[ncells]). Requires Nprime < 2^24. scratch: lss_csr_scratch_bytes(ncells) bytes. */
-size_t lss_csr_scratch_bytes(int32_t ncells);
-int32_t lss_splat_item_count(int32_t nprime);
+ * cell_start (ncells+1) = exclusive scan of cell_count; sorted_key (Nprime capacity) = the kept
+ * points grouped by cell in canonical order -- ascending cell, then ascending point id inside a
+ * cell (the order the reference's stable argsort gives points of equal rank) -- each as the key
+ * (cell << 32) | p; sorted_row (Nprime capacity) = the row each entry's features are read from:
+ * the pixel q(p) when dims is given (fused lift), p itself when dims is NULL (per-point rows).
+ * Only the first cell_start[ncells] entries are defined. scratch: lss_csr_scratch_bytes bytes. */
+size_t lss_csr_scratch_bytes(int32_t ncells, int32_t nprime);
 int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime,
-                  const int32_t* cell_count, int32_t ncells, int32_t* cell_start,
-                  long long* sorted_key, int32_t* item_start, void* scratch, lss_stream_t stream);
+                  const int32_t* cell_count, int32_t ncells, const lss_dims_t* dims,
+                  int32_t* cell_start, long long* sorted_key, int32_t* sorted_row, void* scratch,
+                  lss_stream_t stream);
 
 /* Lift, part 1 (CamEncode.get_depth_dist + layout, src/models.py:49-59, 192-202):
  * depth (B*N, D, H, W) fp32 = softmax over D of depthnet_out[:, :D];
@@ -107,13 +107,14 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
  * channel c is depth[p] * ctx_t[q(p), c] (the lift's outer product, never
  * materialised). Lifted mode (depth == ctx_t == NULL): x_rows is (Nprime, C) fp32.
  * Points of a cell are summed in ascending point id (deterministic). Empty cells
- * are written as zeros; every element of out is written once. LSS_NHWC with item_start
- * uses the point-balanced item kernel; otherwise a BEV-row tile kernel (<= 128 cells per
- * tile along Y) is used. Requires Nprime < 2^24 (LSS_EUNSUPPORTED otherwise).
+ * are written as zeros; every element of out is written once. LSS_NHWC: one wave per
+ * 64-entry chunk of the CSR, rows stored directly; LSS_NCHW: a BEV-row tile kernel (<= 128
+ * cells per tile along Y) with an LDS transpose. sorted_key / sorted_row as lss_csr_build
+ * wrote them (sorted_row is unused in lifted mode, where the rows are the point ids).
  * ev_start / ev_stop (nullable) are stamped with the kernel's own start / end
  * (hipExtLaunchKernel), so their elapsed time is the kernel alone, never launch latency. */
 int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows,
-                  const int32_t* cell_start, const long long* sorted_key, const int32_t* item_start,
+                  const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
                   const lss_dims_t* dims, const lss_grid_t* grid,
                   void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream,
                   lss_event_t ev_start, lss_event_t ev_stop);

@@ -7,10 +7,10 @@
 // Pipeline (forward, one training step):
 //   lss_camera_inverse      48 cameras, fp64 adjugate
 //   lss_geometry_cells      1 thread / point: frustum -> ego xyz -> cell id, atomic count
-//   lss_csr_build           counting sort: block reduce -> scan (+ point-balanced item cuts) -> scatter of
-//                           (cell, point) keys
+//   lss_csr_build           counting sort: block reduce -> scan -> scatter of (cell, point) keys ->
+//                           canonical order (point id inside a cell) + context-row index per entry
 //   lss_lift_prep           1 block / 64 pixels: depth softmax + context -> pixel-major rows
-//   lss_splat_fwd           channels-last: 1 wave / ~32-point item (ordered per-cell sums, rows stored
+//   lss_splat_fwd           channels-last: 1 wave / 64-entry CSR chunk (ordered per-cell sums, rows stored
 //                           directly) + 1 wave / 64 cells zero-filling empty rows  <- the HBM-bound kernel
 //                           NCHW: 1 block (8 waves) / BEV row tile, LDS accumulator, transposed write
 // Backward:
@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <hip/hip_ext.h>
+#include <algorithm>
 #include <limits.h>
 #include <stdint.h>
 
@@ -209,13 +210,9 @@ __global__ __launch_bounds__(1024) void k_scan_partials(const int32_t* __restric
     if (threadIdx.x == 0) partial[blockIdx.x] = s_total;
 }
 
-// Exclusive scan of the cell counts -> cell_start. It also cuts the sorted point list into
-// splat "items" of ~G points aligned to cell boundaries: item j starts at the first cell
-// boundary >= G*j (item_start pre-filled with INT_MAX; readers clamp to the total).
 __global__ __launch_bounds__(1024) void k_scan_apply(const int32_t* __restrict__ cnt, int ncells,
                                                      const int32_t* __restrict__ partial,
-                                                     int32_t* __restrict__ cell_start, int item_g, int n_items,
-                                                     int32_t* __restrict__ item_start) {
+                                                     int32_t* __restrict__ cell_start) {
     __shared__ int s_wave[32];
     __shared__ int s_total;
     __shared__ int s_red[16];
@@ -240,30 +237,135 @@ __global__ __launch_bounds__(1024) void k_scan_apply(const int32_t* __restrict__
     int run = prefix + block_exclusive_scan_1024(v, s_wave, &s_total);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        if (base + i < ncells) {
-            cell_start[base + i] = run;
-            if (item_start != nullptr && c[i] > 0) {
-                // entries g*j inside [run, run + c): item j starts here (g*j == run) or at the cell's end
-                const int jhi = min((run + c[i] - 1) / item_g, n_items - 1);
-                for (int j = (run + item_g - 1) / item_g; j <= jhi; ++j)
-                    item_start[j] = (j * item_g == run) ? run : run + c[i];
-            }
-        }
+        if (base + i < ncells) cell_start[base + i] = run;
         run += c[i];
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) cell_start[ncells] = prefix + s_total;
 }
 
-// Counting-sort scatter: the sorted entry of point p is the key (cell << 32) | p, so a splat
-// wave gets both with one coalesced 8-B load per lane.
+// Counting-sort scatter: point p lands at cell_start[cell] + slot as the key (cell << 32) | p
+// (slot order inside a cell is the atomics' arrival order; k_csr_canon fixes it).
 __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ cell_of,
                                                     const int32_t* __restrict__ slot_of, int nprime,
                                                     const int32_t* __restrict__ cell_start,
-                                                    long long* __restrict__ sorted_key) {
+                                                    long long* __restrict__ key_out) {
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= nprime) return;
     const int cell = cell_of[p];
-    if (cell >= 0) sorted_key[cell_start[cell] + slot_of[p]] = ((long long)cell << 32) | (unsigned)p;
+    if (cell >= 0) key_out[cell_start[cell] + slot_of[p]] = ((long long)cell << 32) | (unsigned)p;
+}
+
+// The sorted list is cut into 64-entry chunks; the wave of chunk w owns the cells that START
+// in [64w, 64w + 64). It reads entries [64w - 1, 64w + 128): the owned cells (<= 64 entries each;
+// a longer last cell is flagged `big`) and the entry before the chunk (a cell that started earlier).
+struct ChunkCells {
+    int s, end;           // owned entries [s, end) held in the two registers (end <= base + 128)
+    int big_start;        // start of an owned cell that runs past base + 127, or -1
+};
+
+__device__ __forceinline__ ChunkCells chunk_cells(int base, int total, int c0, int c1, int prevcell, int lane,
+                                                  int ch = kWave) {
+    // ch <= 64: the chunk is [base, base + ch) (cells of <= 64 entries starting there end below base + 128)
+    ChunkCells r{0, 0, -1};
+    const int up = __shfl(c0, (lane + 63) & 63, kWave);
+    const int before = lane == 0 ? prevcell : up;
+    const unsigned long long sm = __ballot(lane < ch && base + lane < total && c0 != before);
+    if (!sm) {
+        r.s = r.end = base;
+        return r;
+    }
+    const int first = __builtin_ctzll(sm), last = 63 - __builtin_clzll(sm);
+    const int lastcell = __builtin_amdgcn_readlane(c0, last);
+    r.s = base + first;
+    const unsigned long long m0 = __ballot(lane > last && c0 != lastcell);  // c = -1 past the total
+    if (m0) {
+        r.end = base + __builtin_ctzll(m0);
+        return r;
+    }
+    const unsigned long long m1 = __ballot(c1 != lastcell);
+    if (m1) {
+        r.end = base + 64 + __builtin_ctzll(m1);
+        return r;
+    }
+    r.end = base + last;  // the last owned cell has more than 64 entries
+    r.big_start = base + last;
+    return r;
+}
+
+__device__ __forceinline__ int pick(int r0, int r1, int idx) {  // idx uniform, 0..127
+    return idx < kWave ? __builtin_amdgcn_readlane(r0, idx) : __builtin_amdgcn_readlane(r1, idx - kWave);
+}
+
+__device__ __forceinline__ int point_row(int p, int DHW, int HW) {
+    const int cam = p / DHW;
+    return cam * HW + (p - cam * DHW) % HW;  // pixel of point p = its context row
+}
+
+// Canonical CSR order: inside every cell the entries are sorted by point id (so every later
+// reduction over a cell is deterministic without sorting again), and each entry's context-row
+// index (its pixel) is stored beside it. One wave per 64-entry chunk, cells owned as above.
+__global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restrict__ key_in,
+                                                      const int32_t* __restrict__ total_ptr, int nchunks, int DHW,
+                                                      int HW, long long* __restrict__ key_out,
+                                                      int32_t* __restrict__ row_out) {
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * (kBlock / kWave) + uniform(threadIdx.x >> 6);
+    if (w >= nchunks) return;
+    const int total = *total_ptr;
+    const int base = w * kWave;
+    if (base >= total) return;
+    const int e0 = base + lane, e1 = base + kWave + lane;
+    const long long k0 = e0 < total ? key_in[e0] : -1ll;
+    const long long k1 = e1 < total ? key_in[e1] : -1ll;
+    const int prevcell = base > 0 ? (int)(key_in[base - 1] >> 32) : -2;
+    const int c0 = (int)(k0 >> 32), c1 = (int)(k1 >> 32);
+    const int p0 = (int)(k0 & 0xFFFFFFFF), p1 = (int)(k1 & 0xFFFFFFFF);
+    const ChunkCells cc = chunk_cells(base, total, c0, c1, prevcell, lane);
+    // start (global entry index) of the cell of each held entry
+    // (cross-lane reads hoisted out of the lane-0 select: a permute from a lane that is switched
+    // off returns 0)
+    const int up0 = __shfl(c0, (lane + 63) & 63, kWave), up1 = __shfl(c1, (lane + 63) & 63, kWave);
+    const int c0_last = __builtin_amdgcn_readlane(c0, 63);
+    const unsigned long long st0 = __ballot(c0 != (lane == 0 ? prevcell : up0));
+    const unsigned long long st1 = __ballot(c1 != (lane == 0 ? c0_last : up1));
+    const unsigned long long le = ~0ull >> (63 - lane);
+    const int cs0 = base + 63 - __builtin_clzll((st0 & le) | 1ull);  // bit 0 guard: owned entries have a start
+    const int cs1 = (st1 & le) ? base + kWave + 63 - __builtin_clzll(st1 & le)
+                               : base + 63 - __builtin_clzll(st0 | 1ull);
+    int r0 = 0, r1 = 0;
+    for (int j = cc.s; j < cc.end; ++j) {
+        const int cj = pick(c0, c1, j - base), pj = pick(p0, p1, j - base);
+        r0 += (cj == c0 && pj < p0) ? 1 : 0;
+        r1 += (cj == c1 && pj < p1) ? 1 : 0;
+    }
+    if (e0 >= cc.s && e0 < cc.end) {
+        key_out[cs0 + r0] = k0;
+        row_out[cs0 + r0] = point_row(p0, DHW, HW);
+    }
+    if (e1 >= cc.s && e1 < cc.end) {
+        key_out[cs1 + r1] = k1;
+        row_out[cs1 + r1] = point_row(p1, DHW, HW);
+    }
+    if (cc.big_start >= 0) {
+        // one cell with more than 64 entries: ordered selection straight from memory (rare)
+        const int cell = (int)(key_in[cc.big_start] >> 32);
+        int n = 0;
+        while (cc.big_start + n < total && (int)(key_in[cc.big_start + n] >> 32) == cell) ++n;
+        int last = -1;
+        for (int k = 0; k < n; ++k) {
+            int best = INT_MAX;
+            for (int i = lane; i < n; i += kWave) {
+                const int v = (int)(key_in[cc.big_start + i] & 0xFFFFFFFF);
+                if (v > last && v < best) best = v;
+            }
+            best = uniform(wave_min(best));
+            if (lane == 0) {
+                key_out[cc.big_start + k] = ((long long)cell << 32) | (unsigned)best;
+                row_out[cc.big_start + k] = point_row(best, DHW, HW);
+            }
+            last = best;
+        }
+    }
 }
 
 // ----------------------------------------------------------------------------- lift prep
@@ -326,26 +428,43 @@ struct SplatGeo {
     int X, Y, Z, YT, ntiles_y;
 };
 
-// Tuning knobs (compile-time; scripts/kbench.py builds variants with -D to measure them).
-#ifndef LSS_FWD_WAVES
-#define LSS_FWD_WAVES 8
-#endif
-#ifndef LSS_FWD_PREFETCH
-#define LSS_FWD_PREFETCH 16
-#endif
-#ifndef LSS_FWD_PHASES  // bit 0: compute the cell sums, bit 1: write the tile (3 = the kernel)
-#define LSS_FWD_PHASES 3
+#ifndef LSS_PREFETCH
+#define LSS_PREFETCH 16
 #endif
 #ifndef LSS_YT_MAX
 #define LSS_YT_MAX 128
 #endif
-#ifndef LSS_FWD_SKIP  // timing-only ablations: bit 0 window loop, bit 1 rank sort, bit 2 row gathers
-#define LSS_FWD_SKIP 0
+#ifndef LSS_CHUNK
+#define LSS_CHUNK 64
 #endif
-constexpr int kMaxYT = 128;       // cells per tile (LDS sizing, 7-bit tile-cell in the keys)
-constexpr int kFwdWaves = LSS_FWD_WAVES;  // waves per splat tile
+constexpr int kChunk = LSS_CHUNK;
+#ifndef LSS_BATCH
+#define LSS_BATCH 8
+#endif
+constexpr int kBatch = LSS_BATCH;  // entries staged in LDS per pass of a channels-last splat wave  // CSR entries whose cells one channels-last splat wave owns (<= 64)
+#ifndef LSS_WAVES_PER_CU
+#define LSS_WAVES_PER_CU 32  // resident waves of the channels-last splat (0: one wave per possible unit)
+#endif
+#ifndef LSS_GROUPS
+#define LSS_GROUPS 1  // 1: 4 lane groups each summing a run of whole cells; 0: LDS-staged batches
+#endif
+#ifndef LSS_UNROLL
+#define LSS_UNROLL 4
+#endif
+constexpr int kUnroll = LSS_UNROLL;  // entries in flight per lane group
+#ifndef LSS_PIPELINE
+#define LSS_PIPELINE 1  // issue the next batch's gathers before the current batch's ordered sums
+#endif
+#ifndef LSS_FWD_SKIP
+#define LSS_FWD_SKIP 0  // timing experiments only: 1 skips the chunks, 2 the zero fill (wrong output)
+#endif
+#ifndef LSS_NHWC_TILES
+#define LSS_NHWC_TILES 0  // 1: channels-last through the tile kernel (comparison builds)
+#endif
+constexpr int kMaxYT = 128;            // cells per NCHW tile (LDS sizing)
+constexpr int kFwdWaves = 8;           // waves per NCHW tile
 constexpr int kFwdBlock = kFwdWaves * kWave;
-constexpr int kPrefetch = LSS_FWD_PREFETCH;  // row loads in flight per wave
+constexpr int kPrefetch = LSS_PREFETCH;  // context-row loads in flight per wave
 
 // 16-byte vector stores of 16/sizeof(T) elements.
 template <typename T> struct Vec;
@@ -365,7 +484,69 @@ __device__ __forceinline__ void store_vec(bf16* dst, const float* src) {
 __device__ __forceinline__ void store_zero_vec(float* dst) { *reinterpret_cast<float4*>(dst) = make_float4(0.f, 0.f, 0.f, 0.f); }
 __device__ __forceinline__ void store_zero_vec(bf16* dst) { *reinterpret_cast<uint4*>(dst) = make_uint4(0u, 0u, 0u, 0u); }
 
-// First c in [0, ny] with s[c] >= t (s nondecreasing, in LDS).
+// Ordered reduction of canonical CSR entries [s, end) held in registers (entry base+l in lane l of
+// (key0, row0, w0), base+64+l in (key1, row1, w1)); lane = channel. `flush(cell, sum)` is called
+// once per cell, cells in order, points of a cell in ascending point id.
+template <typename Flush>
+__device__ __forceinline__ void reduce_entries(int base, int s, int end, int c0, int c1, int row0, int row1, float w0,
+                                               float w1, const float* __restrict__ rows_base, bool weighted,
+                                               int lane, Flush&& flush) {
+    float acc = 0.f;
+    int cur = s < end ? pick(c0, c1, s - base) : 0;
+    for (int k0 = s; k0 < end; k0 += kPrefetch) {
+        float v[kPrefetch];
+#pragma unroll
+        for (int u = 0; u < kPrefetch; ++u) {
+            const int k = min(k0 + u, end - 1) - base;
+            v[u] = rows_base[(size_t)pick(row0, row1, k) * kC + lane];
+        }
+#pragma unroll
+        for (int u = 0; u < kPrefetch; ++u) {
+            const int k = k0 + u;
+            if (k < end) {
+                const int c = pick(c0, c1, k - base);
+                if (c != cur) {
+                    flush(cur, acc);
+                    acc = 0.f;
+                    cur = c;
+                }
+                const float wk = __int_as_float(pick(__float_as_int(w0), __float_as_int(w1), k - base));
+                acc = __fadd_rn(acc, weighted ? __fmul_rn(wk, v[u]) : v[u]);
+            }
+        }
+    }
+    if (s < end) flush(cur, acc);
+}
+
+// A cell with more than 64 entries, canonical order: streamed 64 at a time (rare).
+template <bool FUSED>
+__device__ float reduce_big_cell(int start, int total, const long long* __restrict__ key,
+                                 const int32_t* __restrict__ row, const float* __restrict__ depth,
+                                 const float* __restrict__ rows_base, int lane, int* cell_out) {
+    const int cell = (int)(key[start] >> 32);
+    *cell_out = cell;
+    float acc = 0.f;
+    for (int b = start;; b += kWave) {
+        const int e = b + lane;
+        const long long k = e < total ? key[e] : -1ll;
+        const bool mine = (int)(k >> 32) == cell;
+        const unsigned long long m = __ballot(mine);
+        const int n = __popcll(m);  // entries of the cell are contiguous from b
+        const int r = mine ? (FUSED ? row[e] : (int)(k & 0xFFFFFFFF)) : 0;
+        const float w = (FUSED && mine) ? depth[(int)(k & 0xFFFFFFFF)] : 1.f;
+        for (int i = 0; i < n; ++i) {
+            const float v = rows_base[(size_t)__builtin_amdgcn_readlane(r, i) * kC + lane];
+            acc = __fadd_rn(acc, FUSED ? __fmul_rn(readlane_f(w, i), v) : v);
+        }
+        if (n < kWave) break;
+    }
+    return acc;
+}
+
+// ---- NCHW (the reference layout): one block = one tile of YT consecutive cells (b, z, x, y0..)
+// of a BEV row, 8 waves; the tile's canonical entries are split over the waves at cell
+// boundaries; sums go to an LDS tile that is written transposed (channel-major) with 16-B
+// stores, zero rows included.
 __device__ __forceinline__ int tile_lower_bound(const int* s, int ny, int t, int lane) {
     for (int base = 0; base <= ny; base += kWave) {
         const int c = base + lane;
@@ -375,39 +556,13 @@ __device__ __forceinline__ int tile_lower_bound(const int* s, int ny, int t, int
     return ny;
 }
 
-template <bool NHWC>
-__device__ __forceinline__ void flush_row(float* lds, int S, int cell, int lane, float acc) {
-    if (NHWC) lds[cell * kC + lane] = acc;
-    else lds[lane * S + cell] = acc;
-}
-
-// Contribution of point p to channel `lane`: the lift's new_x element depth[p] * ctx[q(p), c]
-// (fused) or the lifted row (x_rows).
-template <bool FUSED>
-__device__ __forceinline__ float point_contrib(int p, const float* __restrict__ depth, const float* __restrict__ ctx_t,
-                                               const float* __restrict__ xrows, int DHW, int HW, int lane) {
-    if (FUSED) {
-        const int cam = p / DHW;
-        return __fmul_rn(depth[p], ctx_t[(size_t)(cam * HW + (p - cam * DHW) % HW) * kC + lane]);
-    }
-    return xrows[(size_t)p * kC + lane];
-}
-
-// One block = one tile of YT consecutive cells (b, z, x, y0..y0+ny) of the BEV, 8 waves.
-//  1. the tile's cell starts -> LDS; the fp32 accumulator tile is zeroed in LDS.
-//  2. the tile's point range is split over the waves at cell boundaries (equal point counts).
-//  3. each wave streams its range in windows of whole cells holding <= 64 points: one
-//     coalesced load of packed (tile-cell, point) keys; the window is rank-sorted by key so
-//     every cell is summed in ascending point id (deterministic); then the context rows
-//     (256 B, lane = channel) and depth weights are gathered 16 in flight and each cell's sum
-//     is flushed to its LDS row.
-//  4. the tile is written once with 16-B stores, zero rows included (the BEV's zero fill).
 template <bool FUSED, typename OutT, bool NHWC>
 __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict__ depth,
                                                          const float* __restrict__ ctx_t,
                                                          const float* __restrict__ xrows,
                                                          const int32_t* __restrict__ cell_start,
-                                                         const long long* __restrict__ sorted_key, int DHW, int HW,
+                                                         const long long* __restrict__ sorted_key,
+                                                         const int32_t* __restrict__ sorted_row,
                                                          SplatGeo sg, OutT* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_start[kMaxYT + 1];
@@ -422,13 +577,14 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int S = NHWC ? kC : sg.YT + 4;  // LDS row stride (floats)
+    const float* rows_base = FUSED ? ctx_t : xrows;
 
     for (int i = threadIdx.x; i <= ny; i += kFwdBlock) s_start[i] = cell_start[cell0 + i];
     __syncthreads();
     const int s0 = s_start[0], s1 = s_start[ny];
     const bool empty = s0 == s1;
 
-    if (!empty && (LSS_FWD_PHASES & 1)) {
+    if (!empty) {
         const int lds_elems = NHWC ? ny * kC : kC * S;
         for (int i = threadIdx.x * 4; i < lds_elems; i += kFwdBlock * 4)
             *reinterpret_cast<float4*>(lds + i) = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -437,84 +593,46 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
         const int ce = wave == kFwdWaves - 1 ? ny
                                              : tile_lower_bound(s_start, ny, s0 + ((wave + 1) * span) / kFwdWaves, lane);
         __syncthreads();  // accumulator zeroed before any flush
-        const float* base = FUSED ? ctx_t : xrows;
-        int c = (LSS_FWD_SKIP & 1) ? ce : cb;
-        while (c < ce) {
-            const int ws = s_start[c];
-            // window = cells [c, c+m): the longest run of whole cells holding <= 64 points
-            const int cj = c + 1 + lane;
-            const int ej = cj <= ce ? s_start[cj] : INT_MAX;
-            const int m = __popcll(__ballot(ej - ws <= kWave));
-            if (m == 0) {
-                // one cell with more than 64 points: ordered selection over its list (rare)
-                const int n = s_start[c + 1] - ws;
-                float acc = 0.f;
-                int last = -1;
-                for (int k = 0; k < n; ++k) {
-                    int best = INT_MAX;
-                    for (int i = lane; i < n; i += kWave) {
-                        const int v = (int)(sorted_key[ws + i] & 0xFFFFFFFF);
-                        if (v > last && v < best) best = v;
-                    }
-                    best = uniform(wave_min(best));
-                    acc = __fadd_rn(acc, point_contrib<FUSED>(best, depth, ctx_t, xrows, DHW, HW, lane));
-                    last = best;
-                }
-                flush_row<NHWC>(lds, S, c, lane, acc);
-                c += 1;
-                continue;
-            }
-            const int npts = s_start[c + m] - ws;
-            c += m;
-            if (npts == 0) continue;  // a run of empty cells: their rows stay zero
-            int key = INT_MAX;  // (cell inside the tile) << 24 | point id
-            if (lane < npts) {
-                const long long k64 = sorted_key[ws + lane];
-                key = (((int)(k64 >> 32) - cell0) << 24) | (int)(k64 & 0xFFFFFF);
-            }
-            int rank = (LSS_FWD_SKIP & 2) ? lane : 0;
-            if (!(LSS_FWD_SKIP & 2))
-                for (int j = 0; j < npts; ++j) rank += (__builtin_amdgcn_readlane(key, j) < key) ? 1 : 0;
-            const int sk = __builtin_amdgcn_ds_permute(rank << 2, key);
-            const int p = sk & 0xFFFFFF;
-            int row = p;
-            if (FUSED) {
-                const int cam = p / DHW;
-                row = cam * HW + (p - cam * DHW) % HW;
-            }
-            const float w = (FUSED && lane < npts) ? depth[p] : 1.f;
-            float acc = 0.f;
-            int cur = __builtin_amdgcn_readlane(sk, 0) >> 24;
-            for (int k0 = 0; k0 < npts; k0 += kPrefetch) {
-                float v[kPrefetch];
-#pragma unroll
-                for (int j = 0; j < kPrefetch; ++j) {
-                    const int k = min(k0 + j, npts - 1);
-                    v[j] = (LSS_FWD_SKIP & 4) ? (float)k : base[(size_t)__builtin_amdgcn_readlane(row, k) * kC + lane];
-                }
-#pragma unroll
-                for (int j = 0; j < kPrefetch; ++j) {
-                    const int k = k0 + j;
-                    if (k < npts) {
-                        const int cr = __builtin_amdgcn_readlane(sk, k) >> 24;
-                        if (cr != cur) {
-                            flush_row<NHWC>(lds, S, cur, lane, acc);
-                            acc = 0.f;
-                            cur = cr;
-                        }
-                        acc = __fadd_rn(acc, FUSED ? __fmul_rn(readlane_f(w, k), v[j]) : v[j]);
-                    }
+        auto flush = [&](int cell, float acc) {
+            const int t = cell - cell0;
+            if (NHWC) lds[t * kC + lane] = acc;
+            else lds[lane * S + t] = acc;
+        };
+        int e = s_start[cb];
+        const int eend = s_start[ce];
+        while (e < eend) {
+            // up to 128 entries of whole cells: [e, stop)
+            const int e0 = e + lane, e1 = e + kWave + lane;
+            const long long k0 = e0 < eend ? sorted_key[e0] : -1ll;
+            const long long k1 = e1 < eend ? sorted_key[e1] : -1ll;
+            const int c0 = (int)(k0 >> 32), c1 = (int)(k1 >> 32);
+            int stop = min(eend, e + 2 * kWave);
+            if (stop < eend) {  // do not split the cell holding entry e + 128: stop at its first entry
+                const int cl = __builtin_amdgcn_readlane(c1, 63);
+                const unsigned long long m0 = __ballot(c0 == cl), m1 = __ballot(c1 == cl);
+                stop = m0 ? e + __builtin_ctzll(m0) : e + kWave + __builtin_ctzll(m1);
+                if (stop == e) {  // one cell longer than 128 entries
+                    int cell;
+                    const float acc = reduce_big_cell<FUSED>(e, eend, sorted_key, sorted_row, depth, rows_base,
+                                                             lane, &cell);
+                    flush(cell, acc);
+                    e = s_start[min(cell - cell0 + 1, ny)];
+                    continue;
                 }
             }
-            flush_row<NHWC>(lds, S, cur, lane, acc);
+            const int p0 = (int)(k0 & 0xFFFFFFFF), p1 = (int)(k1 & 0xFFFFFFFF);
+            const int row0 = FUSED ? (e0 < eend ? sorted_row[e0] : 0) : p0;
+            const int row1 = FUSED ? (e1 < eend ? sorted_row[e1] : 0) : p1;
+            const float w0 = (FUSED && e0 < stop) ? depth[p0] : 1.f;
+            const float w1 = (FUSED && e1 < stop) ? depth[p1] : 1.f;
+            reduce_entries(e, e, stop, c0, c1, row0, row1, w0, w1, rows_base, FUSED, lane, flush);
+            e = stop;
         }
         __syncthreads();
     }
 
-    if (!(LSS_FWD_PHASES & 2)) return;
     constexpr int VN = Vec<OutT>::n;
     if (NHWC) {
-        // cell (b, z, x, y) row = out[((b*X + x)*Y + y)*Z*C + z*C + c]
         const size_t zc = (size_t)sg.Z * kC;
         OutT* obase = out + (((size_t)b * sg.X + x) * sg.Y + y0) * zc + (size_t)z * kC;
         constexpr int per_row = kC / VN;
@@ -547,117 +665,28 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
 }
 
 // ----------------------------------------------------------------------------- splat forward, channels-last
-// The production layout (BevEncode runs channels-last): every BEV cell is one contiguous row of
-// C values, so no LDS transpose is needed and the work can be balanced by points, not cells.
-// One launch, two wave roles, four independent waves per block (no barriers):
-//   item waves (first, so they are dispatched first): item j = the sorted points from the first
-//     cell boundary >= G*j to the next item's start (lss_csr_build), <= G + max-cell points, all
-//     whole cells. Lanes load (cell, point) keys in one 8-B load; windows of whole cells with
-//     <= 64 points are rank-sorted by (cell ordinal, point id) -> every cell is summed in
-//     ascending point id (deterministic); depth weights and context rows (256 B, lane =
-//     channel) are gathered 16 in flight; each finished cell's row is stored directly.
+// The production layout (BevEncode runs channels-last): every BEV cell is one contiguous row of C
+// values, so no LDS transpose is needed. One launch, two wave roles, four independent waves per
+// block, no barriers:
+//   chunk waves (first, so they are dispatched first): the wave of chunk w owns the cells that
+//     start among canonical entries [64w, 64w + 64) (k_csr_canon). One round trip loads keys and
+//     context-row indices, a second the depth weights and the context rows (256 B, lane =
+//     channel, 16 in flight); each finished cell's row is stored straight to the BEV.
 //   zero waves: 64 consecutive cells each; the rows of the empty cells are written as zeros with
-//     16-B stores (every BEV element is written exactly once).
-#ifndef LSS_ITEM_G
-#define LSS_ITEM_G 32
-#endif
-constexpr int kItemG = LSS_ITEM_G;
-
+//     16-B stores, so every BEV element is written exactly once.
 struct BevGeo {
     int X, Y, Z;
-    int ncells, n_items, item_waves;
+    int ncells;
 };
 
 template <typename OutT>
 __device__ __forceinline__ OutT* cell_row(OutT* out, int cell, const BevGeo& g) {
     // channels-last (B, X, Y, Z*C): cell ((b*Z + z)*X + x)*Y + y -> ((b*X + x)*Y + y)*Z*C + z*C
+    if (g.Z == 1) return out + (size_t)cell * kC;  // rows of consecutive cells are contiguous
     const int XY = g.X * g.Y;
     const int bz = cell / XY, xy = cell - bz * XY;
     const int b = bz / g.Z, z = bz - b * g.Z;
     return out + ((((size_t)b * XY + xy) * g.Z + z) * kC);
-}
-
-template <bool FUSED, typename OutT>
-__device__ void splat_item(int j, const float* __restrict__ depth, const float* __restrict__ ctx_t,
-                           const float* __restrict__ xrows, const int32_t* __restrict__ cell_start,
-                           const long long* __restrict__ sorted_key, const int32_t* __restrict__ item_start,
-                           int DHW, int HW, const BevGeo& g, OutT* __restrict__ out, int lane) {
-    const int total = cell_start[g.ncells];
-    const int e1 = min(item_start[j + 1], total);
-    int w0 = min(item_start[j], total);
-    const float* base = FUSED ? ctx_t : xrows;
-    while (w0 < e1) {
-        const int avail = e1 - w0;
-        // keys of the next (up to) 65 entries: lanes 0..63 + entry 64 for the split test
-        long long k64 = lane < avail ? sorted_key[w0 + lane] : -1ll;
-        const int cell = (int)(k64 >> 32);
-        int L = min(avail, kWave);
-        if (avail > kWave) {
-            const int cell64 = (int)(sorted_key[w0 + kWave] >> 32);
-            const unsigned long long same = __ballot(cell == cell64);
-            L = same ? __builtin_ctzll(same) : kWave;  // do not split the cell holding entry 64
-            if (L == 0) {
-                // one cell with more than 64 points: ordered selection over its list (rare)
-                const int n = cell_start[cell64 + 1] - w0;
-                float acc = 0.f;
-                int last = -1;
-                for (int k = 0; k < n; ++k) {
-                    int best = INT_MAX;
-                    for (int i = lane; i < n; i += kWave) {
-                        const int v = (int)(sorted_key[w0 + i] & 0xFFFFFFFF);
-                        if (v > last && v < best) best = v;
-                    }
-                    best = uniform(wave_min(best));
-                    acc = __fadd_rn(acc, point_contrib<FUSED>(best, depth, ctx_t, xrows, DHW, HW, lane));
-                    last = best;
-                }
-                cell_row(out, cell64, g)[lane] = from_f32<OutT>(acc);
-                w0 += n;
-                continue;
-            }
-        }
-        // cell ordinal inside the window (entries are grouped by cell), rank by (ordinal, point)
-        const int prev = __shfl(cell, (lane + 63) & 63, kWave);
-        const unsigned long long starts = __ballot(lane < L && (lane == 0 || cell != prev));
-        const int ord = __popcll(starts & (~0ull >> (63 - lane))) - 1;  // starts at lanes <= this one
-        const int key = lane < L ? ((ord << 24) | (int)(k64 & 0xFFFFFF)) : INT_MAX;
-        int rank = 0;
-        for (int i = 0; i < L; ++i) rank += (__builtin_amdgcn_readlane(key, i) < key) ? 1 : 0;
-        const int sk = __builtin_amdgcn_ds_permute(rank << 2, key);
-        const int scell = __builtin_amdgcn_ds_permute(rank << 2, cell);
-        const int p = sk & 0xFFFFFF;
-        int row = p;
-        if (FUSED) {
-            const int cam = p / DHW;
-            row = cam * HW + (p - cam * DHW) % HW;
-        }
-        const float wt = (FUSED && lane < L) ? depth[p] : 1.f;
-        float acc = 0.f;
-        int cur = __builtin_amdgcn_readlane(sk, 0) >> 24;
-        for (int k0 = 0; k0 < L; k0 += kPrefetch) {
-            float v[kPrefetch];
-#pragma unroll
-            for (int u = 0; u < kPrefetch; ++u) {
-                const int k = min(k0 + u, L - 1);
-                v[u] = base[(size_t)__builtin_amdgcn_readlane(row, k) * kC + lane];
-            }
-#pragma unroll
-            for (int u = 0; u < kPrefetch; ++u) {
-                const int k = k0 + u;
-                if (k < L) {
-                    const int o = __builtin_amdgcn_readlane(sk, k) >> 24;
-                    if (o != cur) {
-                        cell_row(out, __builtin_amdgcn_readlane(scell, k - 1), g)[lane] = from_f32<OutT>(acc);
-                        acc = 0.f;
-                        cur = o;
-                    }
-                    acc = __fadd_rn(acc, FUSED ? __fmul_rn(readlane_f(wt, k), v[u]) : v[u]);
-                }
-            }
-        }
-        cell_row(out, __builtin_amdgcn_readlane(scell, L - 1), g)[lane] = from_f32<OutT>(acc);
-        w0 += L;
-    }
 }
 
 template <typename OutT>
@@ -669,37 +698,200 @@ __device__ void zero_empty_rows(int u, const int32_t* __restrict__ cell_start, c
     if (k < g.ncells) empty = cell_start[k] == cell_start[k + 1];
     const unsigned long long emask = __ballot(empty);
     constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
-    if (g.Z == 1) {
-        // rows of consecutive cells are contiguous
-        OutT* base = out + (size_t)k0 * kC;
-        for (int r0 = 0; r0 < kWave; r0 += RPS) {
-            const int r = r0 + lane / LPR;
-            if ((emask >> r) & 1ull) store_zero_vec(base + (size_t)r * kC + (lane % LPR) * EPL);
-        }
-    } else {
-        for (int r0 = 0; r0 < kWave; r0 += RPS) {
-            const int r = r0 + lane / LPR;
-            if ((emask >> r) & 1ull) store_zero_vec(cell_row(out, k0 + r, g) + (lane % LPR) * EPL);
+    for (int r0 = 0; r0 < kWave; r0 += RPS) {
+        const int r = r0 + lane / LPR;
+        if ((emask >> r) & 1ull) {
+            store_zero_vec(cell_row(out, k0 + r, g) + (lane % LPR) * EPL);
         }
     }
 }
 
 template <bool FUSED, typename OutT>
-__global__ __launch_bounds__(kBlock) void k_splat_fwd_items(const float* __restrict__ depth,
-                                                            const float* __restrict__ ctx_t,
-                                                            const float* __restrict__ xrows,
-                                                            const int32_t* __restrict__ cell_start,
-                                                            const long long* __restrict__ sorted_key,
-                                                            const int32_t* __restrict__ item_start, int DHW, int HW,
-                                                            BevGeo g, OutT* __restrict__ out) {
+__device__ __forceinline__ void splat_chunk(int w, int total, const float* __restrict__ depth,
+                                            const float* __restrict__ ctx_t, const float* __restrict__ xrows,
+                                            const long long* __restrict__ sorted_key,
+                                            const int32_t* __restrict__ sorted_row, const BevGeo& g,
+                                            OutT* __restrict__ out, int lane) {
+    // round trip 1: keys, context rows and the previous entry's cell
+    const int base = w * kChunk;
+    const float* rows_base = FUSED ? ctx_t : xrows;
+    const int e0 = base + lane, e1 = base + kWave + lane;
+    const long long k0 = e0 < total ? sorted_key[e0] : -1ll;
+    const long long k1 = e1 < total ? sorted_key[e1] : -1ll;
+    const int rr0 = (FUSED && e0 < total) ? sorted_row[e0] : 0;
+    const int rr1 = (FUSED && e1 < total) ? sorted_row[e1] : 0;
+    const int prevcell = base > 0 ? (int)(sorted_key[base - 1] >> 32) : -2;
+    const int c0 = (int)(k0 >> 32), c1 = (int)(k1 >> 32);
+    const int p0 = (int)(k0 & 0xFFFFFFFF), p1 = (int)(k1 & 0xFFFFFFFF);
+    const ChunkCells cc = chunk_cells(base, total, c0, c1, prevcell, lane, kChunk);
+    auto flush = [&](int cell, float acc) { cell_row(out, cell, g)[lane] = from_f32<OutT>(acc); };
+    // cell starts among the held entries (bit i of st0 / st1: entry base + i / base + 64 + i)
+    const int up0 = __shfl(c0, (lane + 63) & 63, kWave), up1 = __shfl(c1, (lane + 63) & 63, kWave);
+    const int c0_last = __builtin_amdgcn_readlane(c0, 63);
+    const unsigned long long st0 = __ballot(c0 != (lane == 0 ? prevcell : up0));
+    const unsigned long long st1 = __ballot(c1 != (lane == 0 ? c0_last : up1));
+    const int rs0 = FUSED ? rr0 : p0, rs1 = FUSED ? rr1 : p1;
+    const int n = cc.end - cc.s;
+#if LSS_GROUPS
+    // Round trip 2: the wave splits the owned entries [s, end) into 4 contiguous runs of whole
+    // cells, one per 16-lane group, cut at the cell start nearest each quarter. Lane (g4, j) owns
+    // channels 4j..4j+3 of its group's current cell: it gathers 16 B of each entry's context row
+    // (kUnroll entries in flight) and the depth weight, and sums the entries of a cell in order
+    // (ascending point id, the tile kernel's order) -- no LDS staging, no per-entry scalar work.
+    if (n > 0) {
+        const int g4 = lane >> 4, j = lane & 15;
+        const int srel = cc.s - base, erel = cc.end - base;
+        unsigned long long own = (kChunk >= kWave ? ~0ull : ((1ull << kChunk) - 1)) & (~0ull << srel);
+        if (erel < kWave) own &= (1ull << erel) - 1;
+        own &= st0;  // starts of owned cells (all in the first register)
+        auto run_start = [&](int q) {  // first owned cell start >= s + n*q/4 (q = 0: s, q = 4: end)
+            if (q == 0) return srel;
+            if (q >= 4) return erel;
+            const int t = srel + (n * q) / 4;
+            if (t >= kWave) return erel;
+            const unsigned long long m = own & (~0ull << t);
+            return m ? (int)__builtin_ctzll(m) : erel;
+        };
+        const int gs = run_start(g4), ge = run_start(g4 + 1);
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        int cell = -1;
+        auto flush4 = [&](int c, const float4& a) {
+            OutT* dst = cell_row(out, c, g) + 4 * j;
+            store4(dst, a.x, a.y, a.z, a.w);
+        };
+        for (int e = gs; __ballot(e < ge); e += kUnroll) {
+            float4 v[kUnroll];
+            float wt[kUnroll];
+            int cl[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int rel = min(e + u, erel - 1);  // 0..127
+                const int ra = __shfl(rs0, rel & 63, kWave), rb = __shfl(rs1, rel & 63, kWave);
+                const int ca = __shfl(c0, rel & 63, kWave), cb = __shfl(c1, rel & 63, kWave);
+                const int pa = __shfl(p0, rel & 63, kWave), pb = __shfl(p1, rel & 63, kWave);
+                cl[u] = rel < kWave ? ca : cb;  // (every cross-lane read above runs with all lanes on)
+                v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                wt[u] = 1.f;
+                if (e + u < ge) {
+                    v[u] = *reinterpret_cast<const float4*>(rows_base + (size_t)(rel < kWave ? ra : rb) * kC + 4 * j);
+                    if (FUSED) wt[u] = depth[rel < kWave ? pa : pb];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                if (e + u < ge) {
+                    if (cl[u] != cell) {
+                        if (cell >= 0) flush4(cell, acc);
+                        acc = make_float4(0.f, 0.f, 0.f, 0.f);
+                        cell = cl[u];
+                    }
+                    const float4 q = v[u];
+                    if (FUSED) {
+                        acc.x = __fadd_rn(acc.x, __fmul_rn(wt[u], q.x));
+                        acc.y = __fadd_rn(acc.y, __fmul_rn(wt[u], q.y));
+                        acc.z = __fadd_rn(acc.z, __fmul_rn(wt[u], q.z));
+                        acc.w = __fadd_rn(acc.w, __fmul_rn(wt[u], q.w));
+                    } else {
+                        acc.x = __fadd_rn(acc.x, q.x);
+                        acc.y = __fadd_rn(acc.y, q.y);
+                        acc.z = __fadd_rn(acc.z, q.z);
+                        acc.w = __fadd_rn(acc.w, q.w);
+                    }
+                }
+            }
+        }
+        if (cell >= 0) flush4(cell, acc);
+    }
+#else
+    // round trip 2, kBatch entries at a time: lane (g4, j) loads channels 4j..4j+3 of entry 4i + g4
+    // (16-B loads, one 256-B context row per 16 lanes) and the entry's depth weight; the products go
+    // to this wave's LDS slice, then lane = channel sums each cell's entries in ascending point id.
+    __shared__ float4 s_prod[kBlock / kWave][kBatch][16];
+    float4(*prod)[16] = s_prod[threadIdx.x >> 6];
+    const int g4 = lane >> 4, j = lane & 15;
+    float acc = 0.f;
+    int cur = n > 0 ? pick(c0, c1, cc.s - base) : 0;
+    float4 v[kBatch / 4];
+    float wt[kBatch / 4];
+    auto issue = [&](int kb) {  // gathers of batch kb (software-pipelined one batch ahead)
+#pragma unroll
+        for (int i = 0; i < kBatch / 4; ++i) {
+            const int rel = min(cc.s + kb + 4 * i + g4, cc.end - 1) - base;  // 0..127
+            const int ra = __shfl(rs0, rel & 63, kWave), rb = __shfl(rs1, rel & 63, kWave);
+            const int r = rel < kWave ? ra : rb;
+            v[i] = *reinterpret_cast<const float4*>(rows_base + (size_t)r * kC + 4 * j);
+            if (FUSED) {
+                const int pa = __shfl(p0, rel & 63, kWave), pb = __shfl(p1, rel & 63, kWave);
+                wt[i] = depth[rel < kWave ? pa : pb];
+            }
+        }
+    };
+    if (n > 0) issue(0);
+    for (int kb = 0; kb < n; kb += kBatch) {
+#pragma unroll
+        for (int i = 0; i < kBatch / 4; ++i) {
+            float4 q = v[i];
+            if (FUSED) q = make_float4(__fmul_rn(wt[i], q.x), __fmul_rn(wt[i], q.y), __fmul_rn(wt[i], q.z),
+                                       __fmul_rn(wt[i], q.w));
+            prod[4 * i + g4][j] = q;
+        }
+        if (LSS_PIPELINE && kb + kBatch < n) issue(kb + kBatch);
+        __builtin_amdgcn_wave_barrier();
+        const int m = min(kBatch, n - kb);
+        const float* pr = reinterpret_cast<const float*>(prod);
+        float pv[kBatch];  // all LDS reads in flight before the ordered adds
+#pragma unroll
+        for (int kk = 0; kk < kBatch; ++kk) pv[kk] = pr[kk * kC + lane];
+#pragma unroll
+        for (int kk = 0; kk < kBatch; ++kk) {
+            if (kk < m) {
+                const int rel = cc.s + kb + kk - base;
+                const bool start = rel < kWave ? (st0 >> rel) & 1ull : (st1 >> (rel - kWave)) & 1ull;
+                if (kb + kk > 0 && start) {
+                    flush(cur, acc);
+                    acc = 0.f;
+                    cur = pick(c0, c1, rel);
+                }
+                acc = __fadd_rn(acc, pv[kk]);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (!LSS_PIPELINE && kb + kBatch < n) issue(kb + kBatch);
+    }
+    if (n > 0) flush(cur, acc);
+#endif
+    if (cc.big_start >= 0) {
+        int cell;
+        const float a2 = reduce_big_cell<FUSED>(cc.big_start, total, sorted_key, sorted_row, depth, rows_base, lane,
+                                                &cell);
+        flush(cell, a2);
+    }
+}
+
+// Work units: the chunks (as many as the entry count needs), then the 64-cell zero-fill units.
+// A grid of resident waves strides over them (g.waves_per_cu per CU), so no wave is launched
+// just to find it has nothing to do.
+template <bool FUSED, typename OutT>
+__global__ __launch_bounds__(kBlock) void k_splat_fwd_chunks(const float* __restrict__ depth,
+                                                             const float* __restrict__ ctx_t,
+                                                             const float* __restrict__ xrows,
+                                                             const int32_t* __restrict__ cell_start,
+                                                             const long long* __restrict__ sorted_key,
+                                                             const int32_t* __restrict__ sorted_row, BevGeo g,
+                                                             OutT* __restrict__ out) {
     const int lane = threadIdx.x & 63;
-    const int w = blockIdx.x * (kBlock / kWave) + uniform(threadIdx.x >> 6);
-    if (w < g.item_waves) {
-        if (w < g.n_items) splat_item<FUSED, OutT>(w, depth, ctx_t, xrows, cell_start, sorted_key, item_start, DHW, HW,
-                                                   g, out, lane);
-    } else {
-        const int u = w - g.item_waves;
-        if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, g, out, lane);
+    const int nw = gridDim.x * (kBlock / kWave);
+    const int wid = blockIdx.x * (kBlock / kWave) + uniform(threadIdx.x >> 6);
+    const int total = uniform(cell_start[g.ncells]);
+    const int nchunks = (total + kChunk - 1) / kChunk;
+    const int nunits = nchunks + (g.ncells + kWave - 1) / kWave;
+    for (int t = wid; t < nunits; t += nw) {
+        if (t < nchunks) {
+            if (!(LSS_FWD_SKIP & 1))
+                splat_chunk<FUSED, OutT>(t, total, depth, ctx_t, xrows, sorted_key, sorted_row, g, out, lane);
+        } else if (!(LSS_FWD_SKIP & 2)) {
+            zero_empty_rows<OutT>(t - nchunks, cell_start, g, out, lane);
+        }
     }
 }
 
@@ -862,6 +1054,19 @@ inline SplatGeo splat_geo(const lss_grid_t* g) {
     return s;
 }
 
+inline int cu_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            n = v;
+        else
+            n = 256;
+    }
+    return n;
+}
+
 inline int launch_status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
@@ -940,31 +1145,36 @@ int lss_cells_from_geom(const float* geom, int32_t nprime, int32_t points_per_ba
     return launch_status();
 }
 
-size_t lss_csr_scratch_bytes(int32_t ncells) {
-    return sizeof(int32_t) * (size_t)((ncells + kScanItems - 1) / kScanItems + 1);
+size_t lss_csr_scratch_bytes(int32_t ncells, int32_t nprime) {
+    const size_t partial = sizeof(int32_t) * (size_t)((ncells + kScanItems - 1) / kScanItems + 1);
+    return ((partial + 255) & ~(size_t)255) + sizeof(long long) * (size_t)nprime;
 }
 
-int32_t lss_splat_item_count(int32_t nprime) { return nprime / kItemG + 1; }
-
 int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, const int32_t* cell_count,
-                  int32_t ncells, int32_t* cell_start, long long* sorted_key, int32_t* item_start, void* scratch,
-                  lss_stream_t stream) {
-    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !scratch || nprime <= 0 || ncells <= 0)
+                  int32_t ncells, const lss_dims_t* dims, int32_t* cell_start, long long* sorted_key,
+                  int32_t* sorted_row, void* scratch, lss_stream_t stream) {
+    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !sorted_row || !scratch || nprime <= 0 ||
+        ncells <= 0)
         return LSS_EINVAL;
-    if (nprime >= (1 << 24)) return LSS_EUNSUPPORTED;  // 24-bit point ids in the window keys
-    const int nb = (ncells + kScanItems - 1) / kScanItems;
-    const int n_items = lss_splat_item_count(nprime);
-    int32_t* partial = static_cast<int32_t*>(scratch);
-    hipStream_t s = (hipStream_t)stream;
-    if (item_start != nullptr) {
-        const hipError_t e = hipMemsetD32Async(item_start, INT_MAX, (size_t)n_items + 1, s);
-        if (e != hipSuccess) return (int)e;
+    int DHW = nprime, HW = nprime;  // no dims: the row of point p is p (per-point rows)
+    if (dims != nullptr) {
+        if (!dims_ok(dims)) return LSS_EINVAL;
+        DHW = dims->D * dims->H * dims->W;
+        HW = dims->H * dims->W;
+        if ((long)dims->B * dims->N * DHW != nprime) return LSS_EINVAL;
     }
+    const int nb = (ncells + kScanItems - 1) / kScanItems;
+    int32_t* partial = static_cast<int32_t*>(scratch);
+    const size_t poff = ((sizeof(int32_t) * (size_t)(nb + 1)) + 255) & ~(size_t)255;
+    long long* tmp_key = reinterpret_cast<long long*>(static_cast<char*>(scratch) + poff);
+    hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial);
-    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial, cell_start, kItemG,
-                       n_items, item_start);
+    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial, cell_start);
     hipLaunchKernelGGL(k_scatter, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0, s, cell_of, slot_of, nprime,
-                       cell_start, sorted_key);
+                       cell_start, tmp_key);
+    const int nchunks = (nprime + kWave - 1) / kWave;
+    hipLaunchKernelGGL(k_csr_canon, dim3(grid_blocks(nchunks, kBlock / kWave)), dim3(kBlock), 0, s, tmp_key,
+                       cell_start + ncells, nchunks, DHW, HW, sorted_key, sorted_row);
     return launch_status();
 }
 
@@ -988,35 +1198,32 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
 }
 
 int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows, const int32_t* cell_start,
-                  const long long* sorted_key, const int32_t* item_start, const lss_dims_t* dims,
+                  const long long* sorted_key, const int32_t* sorted_row, const lss_dims_t* dims,
                   const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream,
                   lss_event_t ev_start, lss_event_t ev_stop) {
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
     if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_key || !out) return LSS_EINVAL;
     const bool fused = x_rows == nullptr;
-    if (fused && (!depth || !ctx_t)) return LSS_EINVAL;
+    if (fused && (!depth || !ctx_t || !sorted_row)) return LSS_EINVAL;
     const SplatGeo sg = splat_geo(grid);
-    const int DHW = dims->D * dims->H * dims->W;
-    const int HW = dims->H * dims->W;
-    const long nprime = (long)dims->B * dims->N * DHW;
-    if (nprime >= (1L << 24)) return LSS_EUNSUPPORTED;
+    const long nprime = (long)dims->B * dims->N * dims->D * dims->H * dims->W;
+    if (nprime >= INT_MAX) return LSS_EUNSUPPORTED;
     const bool nhwc = out_layout == LSS_NHWC;
     hipStream_t s = (hipStream_t)stream;
-    if (nhwc && item_start != nullptr) {
+    if (nhwc && !LSS_NHWC_TILES) {
         BevGeo g;
         g.X = sg.X; g.Y = sg.Y; g.Z = sg.Z;
         g.ncells = dims->B * sg.Z * sg.X * sg.Y;
-        g.n_items = lss_splat_item_count((int32_t)nprime);
-        g.item_waves = (g.n_items + 3) & ~3;  // whole blocks of item waves, zero waves after
-        const int zero_waves = (g.ncells + kWave - 1) / kWave;
-        const dim3 gr((g.item_waves + zero_waves + 3) / 4), bl(kBlock);
-#define LSS_ITEMS(F, T)                                                                                           \
-    hipExtLaunchKernelGGL((k_splat_fwd_items<F, T>), gr, bl, 0, s, e0, e1, 0, depth, ctx_t, x_rows, cell_start, \
-                          sorted_key, item_start, DHW, HW, g, (T*)out)
-        if (out_dtype == LSS_F32) { if (fused) LSS_ITEMS(true, float); else LSS_ITEMS(false, float); }
-        else if (out_dtype == LSS_BF16) { if (fused) LSS_ITEMS(true, bf16); else LSS_ITEMS(false, bf16); }
+        const int units_max = ((int)nprime + kChunk - 1) / kChunk + (g.ncells + kWave - 1) / kWave;
+        const int waves = LSS_WAVES_PER_CU > 0 ? std::min(units_max, LSS_WAVES_PER_CU * cu_count()) : units_max;
+        const dim3 gr((waves + 3) / 4), bl(kBlock);
+#define LSS_CHUNKS(F, T)                                                                                           \
+    hipExtLaunchKernelGGL((k_splat_fwd_chunks<F, T>), gr, bl, 0, s, e0, e1, 0, depth, ctx_t, x_rows, cell_start, \
+                          sorted_key, sorted_row, g, (T*)out)
+        if (out_dtype == LSS_F32) { if (fused) LSS_CHUNKS(true, float); else LSS_CHUNKS(false, float); }
+        else if (out_dtype == LSS_BF16) { if (fused) LSS_CHUNKS(true, bf16); else LSS_CHUNKS(false, bf16); }
         else return LSS_EINVAL;
-#undef LSS_ITEMS
+#undef LSS_CHUNKS
         return launch_status();
     }
     if (sg.YT > kMaxYT) return LSS_EUNSUPPORTED;
@@ -1024,7 +1231,7 @@ int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows, c
     const size_t lds = nhwc ? (size_t)sg.YT * kC * sizeof(float) : (size_t)kC * (sg.YT + 4) * sizeof(float);
 #define LSS_SPLAT(F, T, L)                                                                                        \
     hipExtLaunchKernelGGL((k_splat_fwd<F, T, L>), dim3(nblocks), dim3(kFwdBlock), (uint32_t)lds, s, e0, e1, 0, depth, \
-                          ctx_t, x_rows, cell_start, sorted_key, DHW, HW, sg, (T*)out)
+                          ctx_t, x_rows, cell_start, sorted_key, sorted_row, sg, (T*)out)
     if (out_dtype == LSS_F32) {
         if (fused) { if (nhwc) LSS_SPLAT(true, float, true); else LSS_SPLAT(true, float, false); }
         else { if (nhwc) LSS_SPLAT(false, float, true); else LSS_SPLAT(false, float, false); }

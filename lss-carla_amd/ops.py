@@ -108,9 +108,9 @@ class SplatPlan:
     grid: GridSpec
     cell_of: torch.Tensor      # (Nprime,) int32, -1 = dropped
     cell_start: torch.Tensor   # (ncells+1,) int32
-    sorted_key: torch.Tensor   # (Nprime,) int64 (cell << 32 | point) grouped by cell;
+    sorted_key: torch.Tensor   # (Nprime,) int64 (cell << 32 | point): ascending cell, then point id;
                                # only the first cell_start[-1] entries are meaningful
-    item_start: Optional[torch.Tensor] = None  # point-balanced splat items (lss_csr_build)
+    sorted_row: torch.Tensor   # (Nprime,) int32 context row (pixel) of each sorted entry
     geom: Optional[torch.Tensor] = None
 
     @property
@@ -123,16 +123,19 @@ class SplatPlan:
         return B * N * D * H * W
 
 
-def _build_csr(cell_of, slot_of, counts, nprime: int, ncells: int, dev):
+def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev):
+    """Counting sort into the canonical CSR (lss_csr_build): cell_start, sorted_key, sorted_row."""
     lib = _lib.load()
+    B, N, D, H, W = dims
+    nprime = B * N * D * H * W
     cell_start = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
     sorted_key = torch.empty(nprime, device=dev, dtype=torch.int64)
-    item_start = torch.empty(int(lib.lss_splat_item_count(nprime)) + 1, device=dev, dtype=torch.int32)
-    scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells)) // 4, device=dev, dtype=torch.int32)
+    sorted_row = torch.empty(nprime, device=dev, dtype=torch.int32)
+    scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
     _lib.check(lib.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
-                                 _lib.ptr(cell_start), _lib.ptr(sorted_key), _lib.ptr(item_start), _lib.ptr(scratch),
-                                 _lib.stream_handle(dev)), "lss_csr_build")
-    return cell_start, sorted_key, item_start
+                                 make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key), _lib.ptr(sorted_row),
+                                 _lib.ptr(scratch), _lib.stream_handle(dev)), "lss_csr_build")
+    return cell_start, sorted_key, sorted_row
 
 
 def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, post_trans, grid: GridSpec,
@@ -157,10 +160,10 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
     _lib.check(lib.lss_geometry_cells(_lib.ptr(fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv),
                                       _lib.ptr(pt), dims, g, _lib.ptr(geom), _lib.ptr(cell_of), _lib.ptr(counts),
                                       _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
-    cell_start = sorted_key = item_start = None
+    cell_start = sorted_key = sorted_row = None
     if want_csr:
-        cell_start, sorted_key, item_start = _build_csr(cell_of, slot_of, counts, nprime, ncells, dev)
-    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, item_start, geom)
+        cell_start, sorted_key, sorted_row = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev)
+    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom)
 
 
 def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
@@ -177,8 +180,8 @@ def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
     _lib.check(lib.lss_cells_from_geom(_lib.ptr(gm), nprime, nprime // B, grid.c_struct(), _lib.ptr(cell_of),
                                        _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)),
                "lss_cells_from_geom")
-    cell_start, sorted_key, item_start = _build_csr(cell_of, slot_of, counts, nprime, ncells, dev)
-    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, item_start, None)
+    cell_start, sorted_key, sorted_row = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev)
+    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, None)
 
 
 # ----------------------------------------------------------------------------- profiling hook
@@ -239,7 +242,7 @@ def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, 
     dev = out.device
     e0, e1 = SPLAT_PROFILE.new_pair() if SPLAT_PROFILE.enabled else (None, None)
     _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), _lib.ptr(x_rows), _lib.ptr(plan.cell_start),
-                                 _lib.ptr(plan.sorted_key), _lib.ptr(plan.item_start), plan.c_dims,
+                                 _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), plan.c_dims,
                                  plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype), layout,
                                  _lib.stream_handle(dev), e0, e1), "lss_splat_fwd")
 

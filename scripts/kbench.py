@@ -15,11 +15,13 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
-    "g8": ["LSS_ITEM_G=8"],
-    "g16": ["LSS_ITEM_G=16"],
-    "g32": ["LSS_ITEM_G=32"],
-    "g64": ["LSS_ITEM_G=64"],
-    "g128": ["LSS_ITEM_G=128"],
+    "lds_b8": ["LSS_GROUPS=0", "LSS_BATCH=8"],
+    "lds_b16": ["LSS_GROUPS=0", "LSS_BATCH=16"],
+    "u2": ["LSS_UNROLL=2"],
+    "u3": ["LSS_UNROLL=3"],
+    "u6": ["LSS_UNROLL=6"],
+    "wpc16": ["LSS_WAVES_PER_CU=16"],
+    "wpc0": ["LSS_WAVES_PER_CU=0"],
 }
 
 
@@ -35,6 +37,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", default="", help="run only ops whose name contains this (for rocprofv3 --pmc)")
+    ap.add_argument("--variants", type=int, default=1, help="also time the variants/*.so builds")
     ap.add_argument("--cold", type=int, default=1, help="also time splat_fwd with caches flushed before each launch")
     args = ap.parse_args()
     if args.build_variants:
@@ -73,7 +76,7 @@ def main():
     res = {}
 
     def lib_plan(l):
-        """cell_start / sorted_key / item_start built by library `l` (its own item granularity)."""
+        """cell_start / sorted_key / sorted_row built by library `l`."""
         import ctypes as ct
         ncells = grid.ncells(B)
         nprime = plan.nprime
@@ -87,11 +90,11 @@ def main():
                                         _lib.ptr(counts), _lib.ptr(slot), st()), "geom")
         cs = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
         sk = torch.empty(nprime, device=dev, dtype=torch.int64)
-        its = torch.empty(int(l.lss_splat_item_count(nprime)) + 1, device=dev, dtype=torch.int32)
-        scr = torch.empty(int(l.lss_csr_scratch_bytes(ncells)) // 4, device=dev, dtype=torch.int32)
-        _lib.check(l.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot), nprime, _lib.ptr(counts), ncells, _lib.ptr(cs),
-                                   _lib.ptr(sk), _lib.ptr(its), _lib.ptr(scr), st()), "csr")
-        return cs, sk, its
+        sr = torch.empty(nprime, device=dev, dtype=torch.int32)
+        scr = torch.empty(int(l.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
+        _lib.check(l.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot), nprime, _lib.ptr(counts), ncells, dims,
+                                   _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), _lib.ptr(scr), st()), "csr")
+        return cs, sk, sr
 
     def named(name, fn, *a):
         timeit.name = name
@@ -110,22 +113,20 @@ def main():
     res["lift_prep"] = named("lift_prep", lambda: _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth),
                                                                     _lib.ptr(ctx_t), st()), "lift"))
 
-    def fwd(l, out, layout, csr=None):
-        cs, sk, its = csr if csr is not None else (plan.cell_start, plan.sorted_key, items)
+    pcsr = (plan.cell_start, plan.sorted_key, plan.sorted_row)
+
+    def fwd(l, out, layout, csr=pcsr):
+        cs, sk, its = csr
         return lambda: _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), None, _lib.ptr(cs),
                                                   _lib.ptr(sk), _lib.ptr(its), dims, g, _lib.ptr(out),
                                                   _lib.dtype_code(out.dtype), layout, st(), None, None), "fwd")
 
-    items = plan.item_start
     res["splat_fwd nhwc bf16"] = named("splat_fwd nhwc bf16", fwd(lib, bev_bf, _lib.NHWC))
-    items = None
-    res["splat_fwd nhwc bf16 [tile kernel]"] = named("splat_fwd nhwc bf16 [tile kernel]", fwd(lib, bev_bf, _lib.NHWC))
-    items = plan.item_start
     res["splat_fwd nchw f32"] = named("splat_fwd nchw f32", fwd(lib, bev_f, _lib.NCHW))
     fwd(lib, bev_bf, _lib.NHWC)()
     ref_out = bev_bf.clone()
     variants = {}
-    for path in sorted(glob.glob(os.path.join(REPO, "lss-carla_amd", "variants", "*.so"))):
+    for path in sorted(glob.glob(os.path.join(REPO, "lss-carla_amd", "variants", "*.so"))) if args.variants else []:
         vl = _lib.open_library(path)
         name = os.path.basename(path)[:-3]
         variants[name] = (vl, lib_plan(vl))
@@ -158,9 +159,7 @@ def main():
             return tot / iters * 1e3
 
         if not args.only or "cold" in args.only:
-            pc = (plan.cell_start, plan.sorted_key, plan.item_start)
-            res["COLD splat_fwd nhwc bf16"] = cold(lib, bev_bf, _lib.NHWC, pc)
-            res["COLD splat_fwd nhwc bf16 [tile kernel]"] = cold(lib, bev_bf, _lib.NHWC, pc[:2] + (None,))
+            res["COLD splat_fwd nhwc bf16"] = cold(lib, bev_bf, _lib.NHWC, pcsr)
             for name, (vl, csr) in variants.items():
                 res[f"COLD splat_fwd nhwc bf16 [{name}]"] = cold(vl, bev_bf, _lib.NHWC, csr)
     g_bf = torch.randn(B, Z * 64, X, Y, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)

@@ -85,42 +85,73 @@ def test_voxel_ids_bit_exact_full_size(name, inverse):
     np.testing.assert_array_equal(plan.cell_of.cpu().numpy(), cell)
     if inverse == "host":
         np.testing.assert_array_equal(plan.geom.cpu().numpy(), geom)
-    # CSR: every cell's point set equals the oracle's
+    _check_canonical_csr(plan, cell, m_grid.ncells(cfg["B"]))
+
+
+def _check_canonical_csr(plan, cell, ncells):
+    """lss_csr_build: ascending cell, then ascending point id (= the reference's stable argsort of
+    ranks, src/models.py:228-231); sorted_row = the pixel of each point."""
     cs = plan.cell_start.cpu().numpy().astype(np.int64)
-    sk = plan.sorted_key.cpu().numpy()
-    kept = cell >= 0
-    assert cs[-1] == kept.sum()
-    counts = np.bincount(cell[kept], minlength=m_grid.ncells(cfg["B"]))
-    np.testing.assert_array_equal(np.diff(cs), counts)
-    order = np.argsort(cell[kept], kind="stable")
-    want_sorted = np.nonzero(kept)[0][order]
-    got_sorted = np.concatenate([np.sort(sk[cs[k]:cs[k + 1]] & 0xFFFFFFFF) for k in np.nonzero(counts)[0]])
-    np.testing.assert_array_equal(got_sorted, want_sorted)
-    # key high word = the entry's cell
-    np.testing.assert_array_equal(sk[:cs[-1]] >> 32, np.repeat(np.arange(counts.size), counts))
-    # point-balanced items: cut at cell boundaries, nondecreasing, cover every entry
     total = int(cs[-1])
-    items = np.minimum(plan.item_start.cpu().numpy().astype(np.int64), total)
-    assert items[0] == 0 and items[-1] == total and np.all(np.diff(items) >= 0)
-    assert np.isin(items, cs).all()
-    G = 32
-    assert np.diff(items).max() <= G + counts.max() - 1
-
-
-def test_splat_items_tile_agree_bitwise():
-    """The NHWC item kernel and the NHWC tile kernel sum every cell in the same order."""
-    cfg, gc, rig, frustum, dn, plan, bev = _lift_splat("c3", _lib.NHWC)
-    lib = _lib.load()
+    sk = plan.sorted_key.cpu().numpy()[:total]
+    kept = cell >= 0
+    assert total == kept.sum()
+    counts = np.bincount(cell[kept], minlength=ncells)
+    np.testing.assert_array_equal(np.diff(cs), counts)
+    want_p = np.nonzero(kept)[0][np.argsort(cell[kept], kind="stable")]
+    np.testing.assert_array_equal(sk & 0xFFFFFFFF, want_p)
+    np.testing.assert_array_equal(sk >> 32, np.repeat(np.arange(counts.size), counts))
     B, N, D, H, W = plan.dims
-    depth = torch.empty(B * N, D, H, W, device=DEV)
-    ctx_t = torch.empty(B * N * H * W, 64, device=DEV)
-    _lib.check(lib.lss_lift_prep(_lib.ptr(dn.to(DEV)), _lib.F32, plan.c_dims, _lib.ptr(depth), _lib.ptr(ctx_t),
-                                 _lib.stream_handle(DEV)), "lift")
-    out = torch.full_like(bev, float("nan"))
-    _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), None, _lib.ptr(plan.cell_start),
-                                 _lib.ptr(plan.sorted_key), None, plan.c_dims, plan.grid.c_struct(), _lib.ptr(out),
-                                 _lib.F32, _lib.NHWC, _lib.stream_handle(DEV), None, None), "tile")
-    assert torch.equal(out, bev)
+    cam, rem = np.divmod(want_p, D * H * W)
+    np.testing.assert_array_equal(plan.sorted_row.cpu().numpy()[:total], cam * H * W + rem % (H * W))
+
+
+def test_splat_chunk_and_tile_kernels_agree_bitwise():
+    """The channels-last chunk kernel and the NCHW tile kernel sum every cell in the same order."""
+    *_, bev_nhwc = _lift_splat("c3", _lib.NHWC)
+    *_, bev_nchw = _lift_splat("c3", _lib.NCHW)
+    assert torch.equal(bev_nhwc.contiguous(), bev_nchw)
+
+
+def _dense_cell_geom(B, N, D, H, W, seed=0):
+    """A geometry with a few very full cells (> 64 and > 128 points: the kernels' long-cell paths)
+    and the rest scattered; grid 16 x 16 x 1 over [-8, 8)."""
+    rng = np.random.default_rng(seed)
+    nprime = B * N * D * H * W
+    g = rng.uniform(-8, 8, size=(nprime, 3)).astype(np.float32)
+    g[:, 2] = rng.uniform(-1, 1, size=nprime).astype(np.float32)
+    perm = rng.permutation(nprime // B)  # the full cells in batch 0
+    for n, xy in ((300, (0.25, 0.25)), (129, (3.5, -2.5)), (65, (-7.5, 7.5)), (64, (-0.75, 0.25))):
+        pts, perm = perm[:n], perm[n:]
+        g[pts, 0], g[pts, 1] = xy
+    g[perm[:50], 0] = 100.0  # out of grid
+    return g.reshape(B, N, D, H, W, 3)
+
+
+@pytest.mark.parametrize("layout", [_lib.NCHW, _lib.NHWC])
+def test_dense_cells_long_paths(layout):
+    gc = syn.grid_conf(xy=(-8.0, 8.0, 1.0), z=(-2.0, 2.0, 4.0), dbound=(4.0, 45.0, 1.0))
+    B, N, D, H, W = 2, 2, 41, 4, 22
+    geom = _dense_cell_geom(B, N, D, H, W)
+    dx, bx, nx = ref.gen_dx_bx(gc["xbound"], gc["ybound"], gc["zbound"])
+    ids, kept = ref.quantize(geom, dx, bx, nx)
+    cell = np.where(kept, ref.output_cell(ids, nx), -1).astype(np.int32)
+    assert np.bincount(cell[cell >= 0]).max() >= 300
+    grid = ops.GridSpec.from_conf(gc)
+    plan = ops.plan_from_geom(torch.from_numpy(geom).to(DEV), grid)
+    np.testing.assert_array_equal(plan.cell_of.cpu().numpy(), cell)
+    _check_canonical_csr(plan, cell, grid.ncells(B))
+    dn = syn.make_depthnet_out(B, N, D, H, W, seed=5)
+    bev = ops.lift_splat(dn.to(DEV), plan, torch.float32, layout)
+    _, new_x = ref.lift(dn, D, 64)
+    x = ref.cam_feats_layout(new_x, B, N)
+    exact = ref.voxel_pooling_fp64(geom, x.numpy(), dx, bx, nx)
+    np.testing.assert_allclose(bev.float().cpu().numpy(), exact, rtol=0, atol=ATOL)
+    # lifted rows through the same plan
+    m = L.compile_model(gc, syn.data_aug_conf((64, 352)), 1).to(DEV)
+    m.bev_layout = "nhwc" if layout == _lib.NHWC else "nchw"
+    bev2 = m.voxel_pooling(torch.from_numpy(geom).to(DEV), x.to(DEV))
+    np.testing.assert_allclose(bev2.float().cpu().numpy(), exact, rtol=0, atol=ATOL)
 
 
 # ----------------------------------------------------------------------------- splat forward

@@ -33,7 +33,7 @@ def test_library_loads_and_exports_all_symbols():
     assert b"invalid" in lib.lss_error_string(-1)
     # host-side argument validation (no device work): NULL pointers are rejected
     assert lib.lss_camera_inverse(None, None, 0, None, None, None) == -1
-    assert lib.lss_csr_scratch_bytes(4096) == 8
+    assert lib.lss_csr_scratch_bytes(4096, 100) == 256 + 8 * 100  # scan partials (aligned) + unsorted keys
 
 
 def test_gridspec_matches_reference_quantiser_constants():
