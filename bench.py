@@ -75,12 +75,12 @@ def setup_dist():
     return world, rank, torch.device("cuda", local if world > 1 else 0)
 
 
-def splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes) -> int:
+def splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes, ctx_bytes) -> int:
     """Algorithmic bytes of one lss_splat_fwd launch."""
     nprime = B * N * D * H * W
     ncells = B * Z * X * Y
     return (nprime * 4                    # depth (fp32)
-            + B * N * H * W * 64 * 4      # context rows (fp32)
+            + B * N * H * W * 64 * ctx_bytes  # context rows (the depthnet output's type: bf16 under autocast)
             + kept * 4                    # sorted point ids
             + (ncells + 1) * 4            # cell_start
             + ncells * 64 * out_bytes)    # dense BEV, every element written once
@@ -234,7 +234,7 @@ def main():
             plan = model.plan(rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"])
             kept = int(plan.cell_start[-1].item())
         out_bytes = 2 if amp_dtype is not None else 4
-        nbytes = splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes)
+        nbytes = splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes, ctx_bytes=out_bytes)
         achieved = nbytes / (splat_ms * 1e-3) / 1e9 if splat_ms else None
         traffic = None
         if os.path.exists(args.traffic_json):

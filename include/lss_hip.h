@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 6
+#define LSS_ABI_VERSION 7
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -85,9 +85,10 @@ int lss_cells_from_geom(const float* geom, int32_t nprime, int32_t points_per_ba
  * cell_start (ncells+1) = exclusive scan of cell_count; sorted_key (Nprime capacity) = the kept
  * points grouped by cell in canonical order -- ascending cell, then ascending point id inside a
  * cell (the order the reference's stable argsort gives points of equal rank) -- each as the key
- * (cell << 32) | p; sorted_row (Nprime capacity) = the row each entry's features are read from:
- * the pixel q(p) when dims is given (fused lift), p itself when dims is NULL (per-point rows).
- * Only the first cell_start[ncells] entries are defined. scratch: lss_csr_scratch_bytes bytes. */
+ * (cell << 32) | p, followed by the sentinel key -1 in every slot from cell_start[ncells] to
+ * Nprime; sorted_row (Nprime capacity) = the row each entry's features are read from: the pixel
+ * q(p) when dims is given (fused lift), p itself when dims is NULL (per-point rows); defined for
+ * the first cell_start[ncells] entries. scratch: lss_csr_scratch_bytes bytes. */
 size_t lss_csr_scratch_bytes(int32_t ncells, int32_t nprime);
 int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime,
                   const int32_t* cell_count, int32_t ncells, const lss_dims_t* dims,
@@ -96,24 +97,27 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
 
 /* Lift, part 1 (CamEncode.get_depth_dist + layout, src/models.py:49-59, 192-202):
  * depth (B*N, D, H, W) fp32 = softmax over D of depthnet_out[:, :D];
- * ctx_t (B*N*H*W, C) fp32 = depthnet_out[:, D:D+C] moved to pixel-major rows.
+ * ctx_t (B*N*H*W, C), element type ctx_dtype = depthnet_out[:, D:D+C] moved to pixel-major rows
+ * (bf16 rows are exact when depthnet_out is bf16, as under autocast).
  * depthnet_out is (B*N, D+C, H, W) contiguous, element type in_dtype. */
 int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims,
-                  float* depth, float* ctx_t, lss_stream_t stream);
+                  float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream);
 
 /* Splat forward: segmented per-cell sum written as the dense (B, Z*C, X, Y) BEV
  * (voxel_pooling + QuickCumsum.forward + griddify, src/models.py:233-246,
  * src/tools.py:195-209). Fused mode (x_rows == NULL): contribution of point p to
  * channel c is depth[p] * ctx_t[q(p), c] (the lift's outer product, never
- * materialised). Lifted mode (depth == ctx_t == NULL): x_rows is (Nprime, C) fp32.
- * Points of a cell are summed in ascending point id (deterministic). Empty cells
- * are written as zeros; every element of out is written once. LSS_NHWC: one wave per
- * 64-entry chunk of the CSR, rows stored directly; LSS_NCHW: a BEV-row tile kernel (<= 128
- * cells per tile along Y) with an LDS transpose. sorted_key / sorted_row as lss_csr_build
- * wrote them (sorted_row is unused in lifted mode, where the rows are the point ids).
+ * materialised; ctx_t of element type ctx_dtype). Lifted mode (depth == ctx_t == NULL):
+ * x_rows is (Nprime, C) fp32. Points of a cell are summed in ascending point id, in fp32, one
+ * rounded multiply and add per point (deterministic; both layouts give identical bits). Empty
+ * cells are written as zeros; every element of out is written once. LSS_NHWC: one wave per
+ * 64-entry chunk of the CSR (one gather round trip, LDS-staged ordered sums, rows stored
+ * directly) plus zero-fill waves; LSS_NCHW: a BEV-row tile kernel (<= 128 cells per tile along Y)
+ * with an LDS transpose. sorted_key / sorted_row as lss_csr_build wrote them (sorted_row is
+ * unused in lifted mode, where the rows are the point ids).
  * ev_start / ev_stop (nullable) are stamped with the kernel's own start / end
  * (hipExtLaunchKernel), so their elapsed time is the kernel alone, never launch latency. */
-int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows,
+int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
                   const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
                   const lss_dims_t* dims, const lss_grid_t* grid,
                   void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream,
@@ -129,7 +133,7 @@ int lss_bev_rows(const void* dbev, int32_t g_dtype, const int32_t* cell_start,
  * d_depthnet_out (B*N, D+C, H, W), element type d_dtype. rows_layout LSS_NHWC means
  * g is the channels-last dbev itself; LSS_NCHW means g is the rows buffer of lss_bev_rows. */
 int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int32_t* cell_of,
-                  const float* depth, const float* ctx_t, const lss_dims_t* dims,
+                  const float* depth, const void* ctx_t, int32_t ctx_dtype, const lss_dims_t* dims,
                   const lss_grid_t* grid, void* d_depthnet_out, int32_t d_dtype,
                   lss_stream_t stream);
 

@@ -34,6 +34,8 @@ constexpr int kBlock = 256;
 constexpr int kScanItems = 4096;  // cells per scan block (1024 threads x 4)
 
 using bf16 = __hip_bfloat16;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+using u32x2 = __attribute__((ext_vector_type(2))) unsigned;
 
 __device__ __forceinline__ float to_f32(float v) { return v; }
 __device__ __forceinline__ float to_f32(bf16 v) { return __bfloat162float(v); }
@@ -305,7 +307,8 @@ __device__ __forceinline__ int point_row(int p, int DHW, int HW) {
 // reduction over a cell is deterministic without sorting again), and each entry's context-row
 // index (its pixel) is stored beside it. One wave per 64-entry chunk, cells owned as above.
 __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restrict__ key_in,
-                                                      const int32_t* __restrict__ total_ptr, int nchunks, int DHW,
+                                                      const int32_t* __restrict__ total_ptr, int nchunks, int nprime,
+                                                      int DHW,
                                                       int HW, long long* __restrict__ key_out,
                                                       int32_t* __restrict__ row_out) {
     const int lane = threadIdx.x & 63;
@@ -313,8 +316,10 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
     if (w >= nchunks) return;
     const int total = *total_ptr;
     const int base = w * kWave;
-    if (base >= total) return;
     const int e0 = base + lane, e1 = base + kWave + lane;
+    // sentinel tail: entries [total, nprime) hold key -1 (cell -1), so a reader needs no entry count
+    if (e0 >= total && e0 < nprime) key_out[e0] = -1ll;
+    if (base >= total) return;
     const long long k0 = e0 < total ? key_in[e0] : -1ll;
     const long long k1 = e1 < total ? key_in[e1] : -1ll;
     const int prevcell = base > 0 ? (int)(key_in[base - 1] >> 32) : -2;
@@ -374,9 +379,9 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
 // back (one memory round trip). depth = softmax_D(logits) is written in the reference's
 // (B*N, D, H, W) layout (coalesced over pixels); the context is transposed through LDS to
 // pixel-major rows ctx_t[q*64 + c] (coalesced 256-B rows).
-template <typename InT>
+template <typename InT, typename CT>
 __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn, int D, int HW, int npix,
-                                                      float* __restrict__ depth, float* __restrict__ ctx_t) {
+                                                      float* __restrict__ depth, CT* __restrict__ ctx_t) {
     __shared__ float s_ctx[kC][65];
     __shared__ float s_red[2][4][64];
     const int q0 = blockIdx.x * 64;
@@ -419,7 +424,20 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
     }
     for (int i = threadIdx.x; i < 64 * kC; i += kBlock) {
         const int r = i >> 6, c = i & 63;
-        if (q0 + r < npix) ctx_t[(size_t)(q0 + r) * kC + c] = s_ctx[c][r];
+        if (q0 + r < npix) ctx_t[(size_t)(q0 + r) * kC + c] = from_f32<CT>(s_ctx[c][r]);
+    }
+}
+
+// 16 bytes of fp32 or bf16 row elements -> fp32.
+__device__ __forceinline__ void unpack16(const uint4& u, const float*, float* o) {
+    o[0] = __uint_as_float(u.x); o[1] = __uint_as_float(u.y); o[2] = __uint_as_float(u.z); o[3] = __uint_as_float(u.w);
+}
+__device__ __forceinline__ void unpack16(const uint4& u, const bf16*, float* o) {
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        o[2 * i] = __uint_as_float(w[i] << 16);
+        o[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
     }
 }
 
@@ -434,32 +452,37 @@ struct SplatGeo {
 #ifndef LSS_YT_MAX
 #define LSS_YT_MAX 128
 #endif
-#ifndef LSS_CHUNK
-#define LSS_CHUNK 64
+#ifndef LSS_MIN_WAVES
+#define LSS_MIN_WAVES 5  // occupancy floor of the channels-last splat (waves per SIMD; VGPR budget 512 / this)
 #endif
-constexpr int kChunk = LSS_CHUNK;
-#ifndef LSS_BATCH
-#define LSS_BATCH 8
+#ifndef LSS_INTERLEAVE
+#define LSS_INTERLEAVE 0  // dispatch order of the block groups: 0 chunks first, 1 interleaved, 2 zero fill first
 #endif
-constexpr int kBatch = LSS_BATCH;  // entries staged in LDS per pass of a channels-last splat wave  // CSR entries whose cells one channels-last splat wave owns (<= 64)
-#ifndef LSS_WAVES_PER_CU
-#define LSS_WAVES_PER_CU 32  // resident waves of the channels-last splat (0: one wave per possible unit)
+#ifndef LSS_XCD_MAP
+#define LSS_XCD_MAP 1     // 1: chunk blocks of one XCD take a contiguous run of chunks (L2 holds ~1/8 of the rows)
 #endif
-#ifndef LSS_GROUPS
-#define LSS_GROUPS 1  // 1: 4 lane groups each summing a run of whole cells; 0: LDS-staged batches
+#ifndef LSS_CHUNK_STOP
+#define LSS_CHUNK_STOP 0  // timing experiments only: chunk waves stop after round trip 1 (1) or 2 (2)
 #endif
-#ifndef LSS_UNROLL
-#define LSS_UNROLL 4
+#ifndef LSS_NO_DEPTH
+#define LSS_NO_DEPTH 0  // timing experiments only: 1 skips the depth-weight gathers (wrong output)
 #endif
-constexpr int kUnroll = LSS_UNROLL;  // entries in flight per lane group
-#ifndef LSS_PIPELINE
-#define LSS_PIPELINE 1  // issue the next batch's gathers before the current batch's ordered sums
+#ifndef LSS_TRACE
+#define LSS_TRACE 0  // diagnostics build: per-wave s_memrealtime stamps of the channels-last splat
+#endif
+#if LSS_TRACE
+// [wave slot][0: start, 1: after round trip 1, 2: after the first gather batch, 3: end, 4: kind | hw id]
+__device__ unsigned long long g_lss_trace[16384][5];
+#define LSS_STAMP(slot, i)                                                                                     \
+    do {                                                                                                       \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                        \
+        if ((threadIdx.x & 63) == 0 && (slot) < 16384) g_lss_trace[(slot)][(i)] = t_;                          \
+    } while (0)
+#else
+#define LSS_STAMP(slot, i) do { } while (0)
 #endif
 #ifndef LSS_FWD_SKIP
 #define LSS_FWD_SKIP 0  // timing experiments only: 1 skips the chunks, 2 the zero fill (wrong output)
-#endif
-#ifndef LSS_NHWC_TILES
-#define LSS_NHWC_TILES 0  // 1: channels-last through the tile kernel (comparison builds)
 #endif
 constexpr int kMaxYT = 128;            // cells per NCHW tile (LDS sizing)
 constexpr int kFwdWaves = 8;           // waves per NCHW tile
@@ -487,9 +510,9 @@ __device__ __forceinline__ void store_zero_vec(bf16* dst) { *reinterpret_cast<ui
 // Ordered reduction of canonical CSR entries [s, end) held in registers (entry base+l in lane l of
 // (key0, row0, w0), base+64+l in (key1, row1, w1)); lane = channel. `flush(cell, sum)` is called
 // once per cell, cells in order, points of a cell in ascending point id.
-template <typename Flush>
+template <typename RT, typename Flush>
 __device__ __forceinline__ void reduce_entries(int base, int s, int end, int c0, int c1, int row0, int row1, float w0,
-                                               float w1, const float* __restrict__ rows_base, bool weighted,
+                                               float w1, const RT* __restrict__ rows_base, bool weighted,
                                                int lane, Flush&& flush) {
     float acc = 0.f;
     int cur = s < end ? pick(c0, c1, s - base) : 0;
@@ -498,7 +521,7 @@ __device__ __forceinline__ void reduce_entries(int base, int s, int end, int c0,
 #pragma unroll
         for (int u = 0; u < kPrefetch; ++u) {
             const int k = min(k0 + u, end - 1) - base;
-            v[u] = rows_base[(size_t)pick(row0, row1, k) * kC + lane];
+            v[u] = to_f32(rows_base[(size_t)pick(row0, row1, k) * kC + lane]);
         }
 #pragma unroll
         for (int u = 0; u < kPrefetch; ++u) {
@@ -511,7 +534,7 @@ __device__ __forceinline__ void reduce_entries(int base, int s, int end, int c0,
                     cur = c;
                 }
                 const float wk = __int_as_float(pick(__float_as_int(w0), __float_as_int(w1), k - base));
-                acc = __fadd_rn(acc, weighted ? __fmul_rn(wk, v[u]) : v[u]);
+                acc = weighted ? fmaf(wk, v[u], acc) : __fadd_rn(acc, v[u]);
             }
         }
     }
@@ -519,24 +542,24 @@ __device__ __forceinline__ void reduce_entries(int base, int s, int end, int c0,
 }
 
 // A cell with more than 64 entries, canonical order: streamed 64 at a time (rare).
-template <bool FUSED>
-__device__ float reduce_big_cell(int start, int total, const long long* __restrict__ key,
+template <bool FUSED, typename RT>
+__device__ float reduce_big_cell(int start, int nprime, const long long* __restrict__ key,
                                  const int32_t* __restrict__ row, const float* __restrict__ depth,
-                                 const float* __restrict__ rows_base, int lane, int* cell_out) {
+                                 const RT* __restrict__ rows_base, int lane, int* cell_out) {
     const int cell = (int)(key[start] >> 32);
     *cell_out = cell;
     float acc = 0.f;
     for (int b = start;; b += kWave) {
         const int e = b + lane;
-        const long long k = e < total ? key[e] : -1ll;
+        const long long k = e < nprime ? key[e] : -1ll;
         const bool mine = (int)(k >> 32) == cell;
         const unsigned long long m = __ballot(mine);
         const int n = __popcll(m);  // entries of the cell are contiguous from b
         const int r = mine ? (FUSED ? row[e] : (int)(k & 0xFFFFFFFF)) : 0;
         const float w = (FUSED && mine) ? depth[(int)(k & 0xFFFFFFFF)] : 1.f;
         for (int i = 0; i < n; ++i) {
-            const float v = rows_base[(size_t)__builtin_amdgcn_readlane(r, i) * kC + lane];
-            acc = __fadd_rn(acc, FUSED ? __fmul_rn(readlane_f(w, i), v) : v);
+            const float v = to_f32(rows_base[(size_t)__builtin_amdgcn_readlane(r, i) * kC + lane]);
+            acc = FUSED ? fmaf(readlane_f(w, i), v, acc) : __fadd_rn(acc, v);
         }
         if (n < kWave) break;
     }
@@ -556,14 +579,13 @@ __device__ __forceinline__ int tile_lower_bound(const int* s, int ny, int t, int
     return ny;
 }
 
-template <bool FUSED, typename OutT, bool NHWC>
+template <bool FUSED, typename RT, typename OutT, bool NHWC>
 __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict__ depth,
-                                                         const float* __restrict__ ctx_t,
-                                                         const float* __restrict__ xrows,
+                                                         const RT* __restrict__ rows_base,
                                                          const int32_t* __restrict__ cell_start,
                                                          const long long* __restrict__ sorted_key,
                                                          const int32_t* __restrict__ sorted_row,
-                                                         SplatGeo sg, OutT* __restrict__ out) {
+                                                         SplatGeo sg, int nprime, OutT* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_start[kMaxYT + 1];
     const int tile = blockIdx.x;
@@ -577,7 +599,6 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int S = NHWC ? kC : sg.YT + 4;  // LDS row stride (floats)
-    const float* rows_base = FUSED ? ctx_t : xrows;
 
     for (int i = threadIdx.x; i <= ny; i += kFwdBlock) s_start[i] = cell_start[cell0 + i];
     __syncthreads();
@@ -613,8 +634,8 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
                 stop = m0 ? e + __builtin_ctzll(m0) : e + kWave + __builtin_ctzll(m1);
                 if (stop == e) {  // one cell longer than 128 entries
                     int cell;
-                    const float acc = reduce_big_cell<FUSED>(e, eend, sorted_key, sorted_row, depth, rows_base,
-                                                             lane, &cell);
+                    const float acc = reduce_big_cell<FUSED, RT>(e, nprime, sorted_key, sorted_row, depth, rows_base,
+                                                                 lane, &cell);
                     flush(cell, acc);
                     e = s_start[min(cell - cell0 + 1, ny)];
                     continue;
@@ -666,14 +687,18 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
 
 // ----------------------------------------------------------------------------- splat forward, channels-last
 // The production layout (BevEncode runs channels-last): every BEV cell is one contiguous row of C
-// values, so no LDS transpose is needed. One launch, two wave roles, four independent waves per
-// block, no barriers:
-//   chunk waves (first, so they are dispatched first): the wave of chunk w owns the cells that
-//     start among canonical entries [64w, 64w + 64) (k_csr_canon). One round trip loads keys and
-//     context-row indices, a second the depth weights and the context rows (256 B, lane =
-//     channel, 16 in flight); each finished cell's row is stored straight to the BEV.
+// values. One launch, two block roles, four independent waves per block, no block barriers:
+//   chunk waves: the wave of chunk w owns the cells that START among canonical entries
+//     [64w, 64w + 64) and reads the window [64w - 1, 64w + 128) (cells have <= 64 entries there;
+//     a longer one is streamed by reduce_big_cell). Round trip 1: keys and context-row indices.
+//     Round trip 2: the depth weights and every owned entry's context row, 16-B lane slices, all in
+//     flight at once. The rows are staged in the wave's LDS slice and summed lane = channel in
+//     canonical order (ascending point id per cell, the NCHW tile kernel's order, so both layouts
+//     agree bit for bit); each finished cell's row is stored straight to the BEV. No global load
+//     follows a store, so stores never sit in front of a load's wait.
 //   zero waves: 64 consecutive cells each; the rows of the empty cells are written as zeros with
 //     16-B stores, so every BEV element is written exactly once.
+// The CSR's sentinel tail (key -1 past the last entry, lss_csr_build) spares a load of the count.
 struct BevGeo {
     int X, Y, Z;
     int ncells;
@@ -689,209 +714,300 @@ __device__ __forceinline__ OutT* cell_row(OutT* out, int cell, const BevGeo& g) 
     return out + ((((size_t)b * XY + xy) * g.Z + z) * kC);
 }
 
+#ifndef LSS_ZERO_STORE
+#define LSS_ZERO_STORE 1  // zero-fill stores: 0 plain, 1 non-temporal
+#endif
+#ifndef LSS_ZERO_UNITS
+#define LSS_ZERO_UNITS 1  // 64-cell zero-fill units per wave (their cell_start loads in flight together)
+#endif
+constexpr int kZeroUnits = LSS_ZERO_UNITS;
+
+// Zero-fill units [u0, u0 + kZeroUnits): cells [64u, 64u + 64) each; empty cells' rows written as zeros.
 template <typename OutT>
-__device__ void zero_empty_rows(int u, const int32_t* __restrict__ cell_start, const BevGeo& g,
+__device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start, const BevGeo& g,
                                 OutT* __restrict__ out, int lane) {
-    const int k0 = u * kWave;
-    const int k = k0 + lane;
-    bool empty = false;
-    if (k < g.ncells) empty = cell_start[k] == cell_start[k + 1];
-    const unsigned long long emask = __ballot(empty);
+    unsigned long long emask[kZeroUnits];
+#pragma unroll
+    for (int i = 0; i < kZeroUnits; ++i) {
+        const int k = (u0 + i) * kWave + lane;
+        bool empty = false;
+        if (k < g.ncells) empty = cell_start[k] == cell_start[k + 1];
+        emask[i] = __ballot(empty);
+    }
     constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
-    for (int r0 = 0; r0 < kWave; r0 += RPS) {
-        const int r = r0 + lane / LPR;
-        if ((emask >> r) & 1ull) {
-            store_zero_vec(cell_row(out, k0 + r, g) + (lane % LPR) * EPL);
+#pragma unroll
+    for (int i = 0; i < kZeroUnits; ++i) {
+        const int k0 = (u0 + i) * kWave;
+        for (int r0 = 0; r0 < kWave; r0 += RPS) {
+            const int r = r0 + lane / LPR;
+            if ((emask[i] >> r) & 1ull) {
+                OutT* dst = cell_row(out, k0 + r, g) + (lane % LPR) * EPL;
+                if (LSS_ZERO_STORE == 1) {
+                    __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, reinterpret_cast<u32x4*>(dst));
+                } else {
+                    store_zero_vec(dst);
+                }
+            }
         }
     }
 }
 
-template <bool FUSED, typename OutT>
-__device__ __forceinline__ void splat_chunk(int w, int total, const float* __restrict__ depth,
-                                            const float* __restrict__ ctx_t, const float* __restrict__ xrows,
+// Owned entries of a chunk, relative to its base: [s, end); big >= 0: the last owned cell starts at
+// `big` and runs past the 128-entry window (it is excluded from [s, end)).
+struct Span {
+    int s, end, big;
+};
+
+__device__ __forceinline__ Span chunk_span(int c0, int c1, int prevcell, int lane) {
+    const int up = __shfl(c0, (lane + 63) & 63, kWave);
+    const int before = lane == 0 ? prevcell : up;
+    const unsigned long long sm = __ballot(c0 >= 0 && c0 != before);  // cell starts (cell -1: past the end)
+    if (!sm) return Span{0, 0, -1};
+    const int first = __builtin_ctzll(sm), last = 63 - __builtin_clzll(sm);
+    const int lastcell = __builtin_amdgcn_readlane(c0, last);
+    const unsigned long long m0 = __ballot(lane > last && c0 != lastcell);
+    if (m0) return Span{first, (int)__builtin_ctzll(m0), -1};
+    const unsigned long long m1 = __ballot(c1 != lastcell);
+    if (m1) return Span{first, kWave + (int)__builtin_ctzll(m1), -1};
+    return Span{first, last, last};
+}
+
+template <typename RT> struct RowSlice {
+    static constexpr int EPL = 16 / sizeof(RT);  // row elements per 16-B lane slice
+    static constexpr int LPR = kC / EPL;         // lanes per row = lanes per group: 16 (fp32), 8 (bf16)
+    static constexpr int NG = kWave / LPR;       // groups per wave: 4, 8
+};
+
+#ifndef LSS_ROW_NT
+#define LSS_ROW_NT 0  // 1: the chunk waves' row stores are non-temporal too
+#endif
+template <int EPL>
+__device__ __forceinline__ void store_slice(float* dst, const float* a) {
+#pragma unroll
+    for (int i = 0; i < EPL; i += 4) {
+        if (LSS_ROW_NT) {
+            const u32x4 v = {__float_as_uint(a[i]), __float_as_uint(a[i + 1]), __float_as_uint(a[i + 2]),
+                             __float_as_uint(a[i + 3])};
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + i));
+        } else {
+            *reinterpret_cast<float4*>(dst + i) = make_float4(a[i], a[i + 1], a[i + 2], a[i + 3]);
+        }
+    }
+}
+template <int EPL>
+__device__ __forceinline__ void store_slice(bf16* dst, const float* a) {
+    bf16 v[EPL];
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) v[i] = __float2bfloat16(a[i]);
+    if constexpr (EPL == 4) {
+        if (LSS_ROW_NT) __builtin_nontemporal_store(*reinterpret_cast<const u32x2*>(v), reinterpret_cast<u32x2*>(dst));
+        else *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(v);
+    } else {
+        if (LSS_ROW_NT) __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(v), reinterpret_cast<u32x4*>(dst));
+        else *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(v);
+    }
+}
+
+#ifndef LSS_UNROLL
+#define LSS_UNROLL 8
+#endif
+// Entries in flight per lane group. A group holds at most ceil(128 / NG) entries (16 with bf16 rows),
+// so with 16 every group issues all its gathers before its first row store: a load issued after a
+// store would wait for that store too (vmcnt counts both, in order), and stores are slow while the
+// zero fill saturates the write path.
+constexpr int kUnroll = LSS_UNROLL;
+
+// Entry metadata of a chunk's 128-entry window, staged once in LDS: (row, point, cell).
+struct EntryMeta {
+    int row, p, cell, pad;
+};
+
+template <bool FUSED, typename RT, typename OutT>
+__device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __restrict__ depth,
+                                            const RT* __restrict__ rows_base,
                                             const long long* __restrict__ sorted_key,
                                             const int32_t* __restrict__ sorted_row, const BevGeo& g,
-                                            OutT* __restrict__ out, int lane) {
-    // round trip 1: keys, context rows and the previous entry's cell
-    const int base = w * kChunk;
-    const float* rows_base = FUSED ? ctx_t : xrows;
+                                            OutT* __restrict__ out, EntryMeta* __restrict__ meta,
+                                            float* __restrict__ part, int lane) {
+    using RS = RowSlice<RT>;
+    // round trip 1: keys (cell << 32 | point), context rows, the previous entry's cell
+    const int base = w * kWave;
     const int e0 = base + lane, e1 = base + kWave + lane;
-    const long long k0 = e0 < total ? sorted_key[e0] : -1ll;
-    const long long k1 = e1 < total ? sorted_key[e1] : -1ll;
-    const int rr0 = (FUSED && e0 < total) ? sorted_row[e0] : 0;
-    const int rr1 = (FUSED && e1 < total) ? sorted_row[e1] : 0;
+    const long long k0 = e0 < nprime ? sorted_key[e0] : -1ll;
+    const long long k1 = e1 < nprime ? sorted_key[e1] : -1ll;
+    int rs0 = 0, rs1 = 0;
+    if (FUSED) {
+        rs0 = e0 < nprime ? sorted_row[e0] : 0;
+        rs1 = e1 < nprime ? sorted_row[e1] : 0;
+    }
     const int prevcell = base > 0 ? (int)(sorted_key[base - 1] >> 32) : -2;
     const int c0 = (int)(k0 >> 32), c1 = (int)(k1 >> 32);
     const int p0 = (int)(k0 & 0xFFFFFFFF), p1 = (int)(k1 & 0xFFFFFFFF);
-    const ChunkCells cc = chunk_cells(base, total, c0, c1, prevcell, lane, kChunk);
-    auto flush = [&](int cell, float acc) { cell_row(out, cell, g)[lane] = from_f32<OutT>(acc); };
-    // cell starts among the held entries (bit i of st0 / st1: entry base + i / base + 64 + i)
-    const int up0 = __shfl(c0, (lane + 63) & 63, kWave), up1 = __shfl(c1, (lane + 63) & 63, kWave);
-    const int c0_last = __builtin_amdgcn_readlane(c0, 63);
-    const unsigned long long st0 = __ballot(c0 != (lane == 0 ? prevcell : up0));
-    const unsigned long long st1 = __ballot(c1 != (lane == 0 ? c0_last : up1));
-    const int rs0 = FUSED ? rr0 : p0, rs1 = FUSED ? rr1 : p1;
-    const int n = cc.end - cc.s;
-#if LSS_GROUPS
-    // Round trip 2: the wave splits the owned entries [s, end) into 4 contiguous runs of whole
-    // cells, one per 16-lane group, cut at the cell start nearest each quarter. Lane (g4, j) owns
-    // channels 4j..4j+3 of its group's current cell: it gathers 16 B of each entry's context row
-    // (kUnroll entries in flight) and the depth weight, and sums the entries of a cell in order
-    // (ascending point id, the tile kernel's order) -- no LDS staging, no per-entry scalar work.
-    if (n > 0) {
-        const int g4 = lane >> 4, j = lane & 15;
-        const int srel = cc.s - base, erel = cc.end - base;
-        unsigned long long own = (kChunk >= kWave ? ~0ull : ((1ull << kChunk) - 1)) & (~0ull << srel);
-        if (erel < kWave) own &= (1ull << erel) - 1;
-        own &= st0;  // starts of owned cells (all in the first register)
-        auto run_start = [&](int q) {  // first owned cell start >= s + n*q/4 (q = 0: s, q = 4: end)
-            if (q == 0) return srel;
-            if (q >= 4) return erel;
-            const int t = srel + (n * q) / 4;
-            if (t >= kWave) return erel;
-            const unsigned long long m = own & (~0ull << t);
-            return m ? (int)__builtin_ctzll(m) : erel;
+    if (!FUSED) {
+        rs0 = p0;
+        rs1 = p1;
+    }
+    LSS_STAMP(w, 1);
+    const Span sp = chunk_span(c0, c1, prevcell, lane);
+    const int s = uniform(sp.s), end = uniform(sp.end), big = uniform(sp.big);
+    if (LSS_CHUNK_STOP == 1) {
+        if (s == 12345 && end == 777 && (rs0 ^ rs1) == 99) out[0] = from_f32<OutT>(1.f);
+        return;
+    }
+    if (end > 0) {
+        meta[lane] = EntryMeta{rs0, p0, c0, 0};
+        meta[kWave + lane] = EntryMeta{rs1, p1, c1, 0};
+        __builtin_amdgcn_wave_barrier();
+        const int up = __shfl(c0, (lane + 63) & 63, kWave);
+        const unsigned long long starts = __ballot(c0 != (lane == 0 ? prevcell : up)) &
+                                          (~0ull << s) & (end >= kWave ? ~0ull : ((1ull << end) - 1));
+        // The owned entries [s, end) (n <= 128) are split evenly over the NG groups of LPR lanes:
+        // group q sums entries [s + n*q/NG, s + n*(q+1)/NG) cell by cell; lane j of a group owns row
+        // elements [EPL*j, EPL*j + EPL). A cell cut by group boundaries is summed in pieces: the
+        // group holding its first entry leaves its piece in part_last[q], every later group holding
+        // some of it leaves its piece in part_first[q]; after a wave barrier the group holding the
+        // cell's last entry adds the pieces in group order and stores the row. The association
+        // depends only on the CSR (deterministic), never on timing.
+        const int n = end - s;
+        const int grp = lane / RS::LPR, col = (lane % RS::LPR) * RS::EPL;
+        auto gbeg = [&](int q) { return s + (n * q) / RS::NG; };
+        const int gs = gbeg(grp), ge = gbeg(grp + 1);
+        const int first_cell = gs < ge ? meta[gs].cell : -1;
+        const bool head_split = gs < ge && gs > s && meta[gs - 1].cell == first_cell;
+        const bool tail_split = gs < ge && ge < end && meta[ge].cell == meta[ge - 1].cell;
+        float acc[RS::EPL];
+#pragma unroll
+        for (int i = 0; i < RS::EPL; ++i) acc[i] = 0.f;
+        int cur = -1;
+        auto put = [&](float* dst) {
+#pragma unroll
+            for (int i = 0; i < RS::EPL; i += 4)
+                *reinterpret_cast<float4*>(dst + col + i) = make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
         };
-        const int gs = run_start(g4), ge = run_start(g4 + 1);
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        int cell = -1;
-        auto flush4 = [&](int c, const float4& a) {
-            OutT* dst = cell_row(out, c, g) + 4 * j;
-            store4(dst, a.x, a.y, a.z, a.w);
+        auto finish = [&](bool last) {  // the cell `cur` ends at this point of the group
+            if (cur == first_cell && head_split) put(part + (RS::NG + grp) * kC);   // part_first[grp]
+            else if (last && tail_split) put(part + grp * kC);                       // part_last[grp]
+            else store_slice<RS::EPL>(cell_row(out, cur, g) + col, acc);
         };
-        for (int e = gs; __ballot(e < ge); e += kUnroll) {
-            float4 v[kUnroll];
+        // round trip 2 (one per kUnroll entries of a group): row slices and depth weights in flight together
+        for (int e = gs; e < ge; e += kUnroll) {
+            uint4 v[kUnroll];
             float wt[kUnroll];
-            int cl[kUnroll];
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
-                const int rel = min(e + u, erel - 1);  // 0..127
-                const int ra = __shfl(rs0, rel & 63, kWave), rb = __shfl(rs1, rel & 63, kWave);
-                const int ca = __shfl(c0, rel & 63, kWave), cb = __shfl(c1, rel & 63, kWave);
-                const int pa = __shfl(p0, rel & 63, kWave), pb = __shfl(p1, rel & 63, kWave);
-                cl[u] = rel < kWave ? ca : cb;  // (every cross-lane read above runs with all lanes on)
-                v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                wt[u] = 1.f;
-                if (e + u < ge) {
-                    v[u] = *reinterpret_cast<const float4*>(rows_base + (size_t)(rel < kWave ? ra : rb) * kC + 4 * j);
-                    if (FUSED) wt[u] = depth[rel < kWave ? pa : pb];
-                }
+                const int2 m = *reinterpret_cast<const int2*>(&meta[min(e + u, ge - 1)]);  // (row, p)
+                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)m.x * kC + col);
+                wt[u] = (FUSED && !LSS_NO_DEPTH) ? depth[m.y] : 1.f;
             }
+            if (LSS_CHUNK_STOP == 2) {
+                unsigned x = 0;
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) x ^= v[u].x ^ v[u].w ^ __float_as_uint(wt[u]);
+                if (x == 0x12345u) out[0] = from_f32<OutT>(1.f);
+                continue;
+            }
+            if (LSS_TRACE && e == gs && grp == 0) LSS_STAMP(w, 2);
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
                 if (e + u < ge) {
-                    if (cl[u] != cell) {
-                        if (cell >= 0) flush4(cell, acc);
-                        acc = make_float4(0.f, 0.f, 0.f, 0.f);
-                        cell = cl[u];
+                    const int cl = meta[e + u].cell;
+                    if (cl != cur) {
+                        if (cur >= 0) finish(false);
+#pragma unroll
+                        for (int i = 0; i < RS::EPL; ++i) acc[i] = 0.f;
+                        cur = cl;
                     }
-                    const float4 q = v[u];
-                    if (FUSED) {
-                        acc.x = __fadd_rn(acc.x, __fmul_rn(wt[u], q.x));
-                        acc.y = __fadd_rn(acc.y, __fmul_rn(wt[u], q.y));
-                        acc.z = __fadd_rn(acc.z, __fmul_rn(wt[u], q.z));
-                        acc.w = __fadd_rn(acc.w, __fmul_rn(wt[u], q.w));
-                    } else {
-                        acc.x = __fadd_rn(acc.x, q.x);
-                        acc.y = __fadd_rn(acc.y, q.y);
-                        acc.z = __fadd_rn(acc.z, q.z);
-                        acc.w = __fadd_rn(acc.w, q.w);
-                    }
+                    float x[RS::EPL];
+                    unpack16(v[u], (const RT*)nullptr, x);
+#pragma unroll
+                    for (int i = 0; i < RS::EPL; ++i) acc[i] = FUSED ? fmaf(wt[u], x[i], acc[i]) : __fadd_rn(acc[i], x[i]);
                 }
             }
         }
-        if (cell >= 0) flush4(cell, acc);
-    }
-#else
-    // round trip 2, kBatch entries at a time: lane (g4, j) loads channels 4j..4j+3 of entry 4i + g4
-    // (16-B loads, one 256-B context row per 16 lanes) and the entry's depth weight; the products go
-    // to this wave's LDS slice, then lane = channel sums each cell's entries in ascending point id.
-    __shared__ float4 s_prod[kBlock / kWave][kBatch][16];
-    float4(*prod)[16] = s_prod[threadIdx.x >> 6];
-    const int g4 = lane >> 4, j = lane & 15;
-    float acc = 0.f;
-    int cur = n > 0 ? pick(c0, c1, cc.s - base) : 0;
-    float4 v[kBatch / 4];
-    float wt[kBatch / 4];
-    auto issue = [&](int kb) {  // gathers of batch kb (software-pipelined one batch ahead)
-#pragma unroll
-        for (int i = 0; i < kBatch / 4; ++i) {
-            const int rel = min(cc.s + kb + 4 * i + g4, cc.end - 1) - base;  // 0..127
-            const int ra = __shfl(rs0, rel & 63, kWave), rb = __shfl(rs1, rel & 63, kWave);
-            const int r = rel < kWave ? ra : rb;
-            v[i] = *reinterpret_cast<const float4*>(rows_base + (size_t)r * kC + 4 * j);
-            if (FUSED) {
-                const int pa = __shfl(p0, rel & 63, kWave), pb = __shfl(p1, rel & 63, kWave);
-                wt[i] = depth[rel < kWave ? pa : pb];
-            }
-        }
-    };
-    if (n > 0) issue(0);
-    for (int kb = 0; kb < n; kb += kBatch) {
-#pragma unroll
-        for (int i = 0; i < kBatch / 4; ++i) {
-            float4 q = v[i];
-            if (FUSED) q = make_float4(__fmul_rn(wt[i], q.x), __fmul_rn(wt[i], q.y), __fmul_rn(wt[i], q.z),
-                                       __fmul_rn(wt[i], q.w));
-            prod[4 * i + g4][j] = q;
-        }
-        if (LSS_PIPELINE && kb + kBatch < n) issue(kb + kBatch);
+        if (cur >= 0 && LSS_CHUNK_STOP != 2) finish(true);
         __builtin_amdgcn_wave_barrier();
-        const int m = min(kBatch, n - kb);
-        const float* pr = reinterpret_cast<const float*>(prod);
-        float pv[kBatch];  // all LDS reads in flight before the ordered adds
+        // pieces of the cell cut at this group's start: summed here if the cell ends in this group
+        if (head_split && !(tail_split && meta[ge - 1].cell == first_cell) && LSS_CHUNK_STOP != 2) {
+            // the group holding the cell's first entry (owned cells start below 64: bit in `starts`)
+            const unsigned long long upto = starts & (gs >= kWave ? ~0ull : ((2ull << gs) - 1));
+            const int cstart = 63 - __builtin_clzll(upto);
+            int g0 = 0;
+            while (gbeg(g0 + 1) <= cstart) ++g0;
+            float sum[RS::EPL];
 #pragma unroll
-        for (int kk = 0; kk < kBatch; ++kk) pv[kk] = pr[kk * kC + lane];
+            for (int i = 0; i < RS::EPL; ++i) sum[i] = part[g0 * kC + col + i];
+            for (int q = g0 + 1; q <= grp; ++q) {
+                if (gbeg(q) == gbeg(q + 1)) continue;  // empty group
 #pragma unroll
-        for (int kk = 0; kk < kBatch; ++kk) {
-            if (kk < m) {
-                const int rel = cc.s + kb + kk - base;
-                const bool start = rel < kWave ? (st0 >> rel) & 1ull : (st1 >> (rel - kWave)) & 1ull;
-                if (kb + kk > 0 && start) {
-                    flush(cur, acc);
-                    acc = 0.f;
-                    cur = pick(c0, c1, rel);
-                }
-                acc = __fadd_rn(acc, pv[kk]);
+                for (int i = 0; i < RS::EPL; ++i) sum[i] = __fadd_rn(sum[i], part[(RS::NG + q) * kC + col + i]);
             }
+            store_slice<RS::EPL>(cell_row(out, first_cell, g) + col, sum);
         }
-        __builtin_amdgcn_wave_barrier();
-        if (!LSS_PIPELINE && kb + kBatch < n) issue(kb + kBatch);
     }
-    if (n > 0) flush(cur, acc);
-#endif
-    if (cc.big_start >= 0) {
+    if (big >= 0) {
         int cell;
-        const float a2 = reduce_big_cell<FUSED>(cc.big_start, total, sorted_key, sorted_row, depth, rows_base, lane,
-                                                &cell);
-        flush(cell, a2);
+        const float a2 = reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base,
+                                                    lane, &cell);
+        cell_row(out, cell, g)[lane] = from_f32<OutT>(a2);
     }
 }
 
-// Work units: the chunks (as many as the entry count needs), then the 64-cell zero-fill units.
-// A grid of resident waves strides over them (g.waves_per_cu per CU), so no wave is launched
-// just to find it has nothing to do.
-template <bool FUSED, typename OutT>
-__global__ __launch_bounds__(kBlock) void k_splat_fwd_chunks(const float* __restrict__ depth,
-                                                             const float* __restrict__ ctx_t,
-                                                             const float* __restrict__ xrows,
-                                                             const int32_t* __restrict__ cell_start,
-                                                             const long long* __restrict__ sorted_key,
-                                                             const int32_t* __restrict__ sorted_row, BevGeo g,
-                                                             OutT* __restrict__ out) {
+template <bool FUSED, typename RT, typename OutT>
+__global__ __launch_bounds__(kBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const float* __restrict__ depth,
+                                                           const RT* __restrict__ rows_base,
+                                                           const int32_t* __restrict__ cell_start,
+                                                           const long long* __restrict__ sorted_key,
+                                                           const int32_t* __restrict__ sorted_row, BevGeo g,
+                                                           int nprime, int nchunk_blocks, int nzero_blocks,
+                                                           OutT* __restrict__ out) {
+    __shared__ EntryMeta s_meta[kBlock / kWave][2 * kWave];
+    __shared__ __attribute__((aligned(16))) float s_part[kBlock / kWave][2 * RowSlice<RT>::NG * kC];
     const int lane = threadIdx.x & 63;
-    const int nw = gridDim.x * (kBlock / kWave);
-    const int wid = blockIdx.x * (kBlock / kWave) + uniform(threadIdx.x >> 6);
-    const int total = uniform(cell_start[g.ncells]);
-    const int nchunks = (total + kChunk - 1) / kChunk;
-    const int nunits = nchunks + (g.ncells + kWave - 1) / kWave;
-    for (int t = wid; t < nunits; t += nw) {
-        if (t < nchunks) {
-            if (!(LSS_FWD_SKIP & 1))
-                splat_chunk<FUSED, OutT>(t, total, depth, ctx_t, xrows, sorted_key, sorted_row, g, out, lane);
-        } else if (!(LSS_FWD_SKIP & 2)) {
-            zero_empty_rows<OutT>(t - nchunks, cell_start, g, out, lane);
-        }
+    const int wave = uniform(threadIdx.x >> 6);
+    // Blocks come in groups of 8, one per XCD (blocks are dealt round-robin over the 8 XCDs). Chunk
+    // groups and zero-fill groups are interleaved evenly in dispatch order, so the HBM-write-bound
+    // zero fill runs beside the L2-bound chunk gathers from the start; the chunk blocks of XCD x
+    // take one contiguous run of chunks, whose context rows (a few cameras) then stay in that L2.
+    const int ncg = (nchunk_blocks + 7) >> 3, nzg = (nzero_blocks + 7) >> 3;
+    const int gi = blockIdx.x >> 3, x = blockIdx.x & 7;
+    int zgi = gi - ncg, cgi = gi;
+    bool zero_role = gi >= ncg;
+    if (LSS_INTERLEAVE == 2) {
+        zero_role = gi < nzg;
+        zgi = gi;
+        cgi = gi - nzg;
+    } else if (LSS_INTERLEAVE == 1) {
+        const int G = ncg + nzg;
+        zgi = (gi * nzg) / G;
+        zero_role = ((gi + 1) * nzg) / G > zgi;
+        cgi = gi - zgi;
+    }
+    if (!zero_role) {
+        if (LSS_FWD_SKIP & 1) return;
+        const int cb = LSS_XCD_MAP ? x * ncg + cgi : cgi * 8 + x;
+        if (cb >= nchunk_blocks) return;
+        const int w = cb * (kBlock / kWave) + wave;
+        LSS_STAMP(w, 0);
+        splat_chunk<FUSED, RT, OutT>(w, nprime, depth, rows_base, sorted_key, sorted_row, g, out, s_meta[wave],
+                                     s_part[wave], lane);
+        LSS_STAMP(w, 3);
+#if LSS_TRACE
+        if (lane == 0 && w < 16384) g_lss_trace[w][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
+                                                    (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+#endif
+    } else {
+        if (LSS_FWD_SKIP & 2) return;
+        const int zb = zgi * 8 + x;
+        if (zb >= nzero_blocks) return;
+        const int u = (zb * (kBlock / kWave) + wave) * kZeroUnits;
+        const int zslot = nchunk_blocks * (kBlock / kWave) + zb * (kBlock / kWave) + wave;
+        LSS_STAMP(zslot, 0);
+        if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, g, out, lane);
+        LSS_STAMP(zslot, 3);
+#if LSS_TRACE
+        if (lane == 0 && zslot < 16384) g_lss_trace[zslot][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
+                                                        (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+#endif
     }
 }
 
@@ -935,27 +1051,14 @@ __device__ __forceinline__ size_t row_offset(int cell, const SplatGeo& sg) {
     return (((size_t)b * XY + xy) * sg.Z + z) * kC;
 }
 
-// 16-byte gradient-row chunk -> fp32.
-__device__ __forceinline__ void unpack16(const uint4& u, const float*, float* o) {
-    o[0] = __uint_as_float(u.x); o[1] = __uint_as_float(u.y); o[2] = __uint_as_float(u.z); o[3] = __uint_as_float(u.w);
-}
-__device__ __forceinline__ void unpack16(const uint4& u, const bf16*, float* o) {
-    const unsigned w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        o[2 * i] = __uint_as_float(w[i] << 16);
-        o[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
-    }
-}
-
 // One wave per pixel. The D gradient rows of the pixel's points are gathered into LDS with
 // 16-B lane loads (every load of the pixel in flight at once), then (lane = channel)
 // d_ctx[c] = sum_d g[d][c] depth[d] and (lane = depth bin) d_depth[d] = sum_c g[d][c] ctx[c],
 // softmax backward, write d_depthnet_out.
-template <typename GT, typename DT, bool NHWC>
+template <typename GT, typename DT, typename CT, bool NHWC>
 __global__ __launch_bounds__(kBlock) void k_splat_bwd(const GT* __restrict__ g, const int32_t* __restrict__ cell_of,
                                                       const float* __restrict__ depth,
-                                                      const float* __restrict__ ctx_t, int D, int HW, int npix,
+                                                      const CT* __restrict__ ctx_t, int D, int HW, int npix,
                                                       SplatGeo sg, DT* __restrict__ d_dn) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int EPL = 16 / sizeof(GT);    // row elements per 16-B lane load
@@ -977,7 +1080,7 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd(const GT* __restrict__ g, 
         my_depth = depth[pbase + (size_t)lane * HW];
         my_cell = cell_of[pbase + (size_t)lane * HW];
     }
-    if (live) cx[lane] = ctx_t[(size_t)q * kC + lane];
+    if (live) cx[lane] = to_f32(ctx_t[(size_t)q * kC + lane]);
     const int sub = lane / LPR, chunk = (lane % LPR) * EPL;
     uint4 raw[NI];
 #pragma unroll
@@ -1054,19 +1157,6 @@ inline SplatGeo splat_geo(const lss_grid_t* g) {
     return s;
 }
 
-inline int cu_count() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-            n = v;
-        else
-            n = 256;
-    }
-    return n;
-}
-
 inline int launch_status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
@@ -1086,6 +1176,19 @@ inline bool grid_ok(const lss_grid_t* g) {
 extern "C" {
 
 int lss_abi_version(void) { return LSS_ABI_VERSION; }
+
+#if LSS_TRACE
+// Diagnostics builds only (not in lss_hip.h): copy the per-wave stamps of the last splat to the host.
+int lss_debug_trace(unsigned long long* host, int nrows) {
+    if (nrows > 16384) nrows = 16384;
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lss_trace), sizeof(unsigned long long) * 5 * nrows, 0,
+                                    hipMemcpyDeviceToHost);
+}
+int lss_debug_trace_clear(void) {
+    static unsigned long long zeros[16384][5];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_lss_trace), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
+}
+#endif
 
 int lss_event_create(lss_event_t* ev) {
     if (!ev) return LSS_EINVAL;
@@ -1174,72 +1277,84 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
                        cell_start, tmp_key);
     const int nchunks = (nprime + kWave - 1) / kWave;
     hipLaunchKernelGGL(k_csr_canon, dim3(grid_blocks(nchunks, kBlock / kWave)), dim3(kBlock), 0, s, tmp_key,
-                       cell_start + ncells, nchunks, DHW, HW, sorted_key, sorted_row);
+                       cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row);
     return launch_status();
 }
 
-int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims, float* depth, float* ctx_t,
-                  lss_stream_t stream) {
+int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims, float* depth, void* ctx_t,
+                  int32_t ctx_dtype, lss_stream_t stream) {
     if (!dims_ok(dims) || !depthnet_out || !depth || !ctx_t) return LSS_EINVAL;
     if (dims->D > 64) return LSS_EUNSUPPORTED;
     const int HW = dims->H * dims->W;
     const int npix = dims->B * dims->N * HW;
     const dim3 grid(grid_blocks(npix, 64)), block(kBlock);
     hipStream_t s = (hipStream_t)stream;
-    if (in_dtype == LSS_F32)
-        hipLaunchKernelGGL(k_lift_prep<float>, grid, block, 0, s, (const float*)depthnet_out, dims->D, HW, npix, depth,
-                           ctx_t);
-    else if (in_dtype == LSS_BF16)
-        hipLaunchKernelGGL(k_lift_prep<bf16>, grid, block, 0, s, (const bf16*)depthnet_out, dims->D, HW, npix, depth,
-                           ctx_t);
-    else
-        return LSS_EINVAL;
+#define LSS_PREP(IT, CT) \
+    hipLaunchKernelGGL((k_lift_prep<IT, CT>), grid, block, 0, s, (const IT*)depthnet_out, dims->D, HW, npix, depth, (CT*)ctx_t)
+    if (in_dtype == LSS_F32 && ctx_dtype == LSS_F32) LSS_PREP(float, float);
+    else if (in_dtype == LSS_F32 && ctx_dtype == LSS_BF16) LSS_PREP(float, bf16);
+    else if (in_dtype == LSS_BF16 && ctx_dtype == LSS_F32) LSS_PREP(bf16, float);
+    else if (in_dtype == LSS_BF16 && ctx_dtype == LSS_BF16) LSS_PREP(bf16, bf16);
+    else return LSS_EINVAL;
+#undef LSS_PREP
     return launch_status();
 }
 
-int lss_splat_fwd(const float* depth, const float* ctx_t, const float* x_rows, const int32_t* cell_start,
-                  const long long* sorted_key, const int32_t* sorted_row, const lss_dims_t* dims,
-                  const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream,
-                  lss_event_t ev_start, lss_event_t ev_stop) {
+int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
+                  const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
+                  const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout,
+                  lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop) {
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
     if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_key || !out) return LSS_EINVAL;
     const bool fused = x_rows == nullptr;
     if (fused && (!depth || !ctx_t || !sorted_row)) return LSS_EINVAL;
+    if (fused && ctx_dtype != LSS_F32 && ctx_dtype != LSS_BF16) return LSS_EINVAL;
+    if (out_dtype != LSS_F32 && out_dtype != LSS_BF16) return LSS_EINVAL;
     const SplatGeo sg = splat_geo(grid);
-    const long nprime = (long)dims->B * dims->N * dims->D * dims->H * dims->W;
-    if (nprime >= INT_MAX) return LSS_EUNSUPPORTED;
+    const long nprime_l = (long)dims->B * dims->N * dims->D * dims->H * dims->W;
+    if (nprime_l >= INT_MAX - 2 * kWave) return LSS_EUNSUPPORTED;
+    const int nprime = (int)nprime_l;
     const bool nhwc = out_layout == LSS_NHWC;
+    const bool ctx_bf16 = fused && ctx_dtype == LSS_BF16;
+    const void* rows = fused ? ctx_t : (const void*)x_rows;
     hipStream_t s = (hipStream_t)stream;
-    if (nhwc && !LSS_NHWC_TILES) {
+    if (nhwc) {
         BevGeo g;
         g.X = sg.X; g.Y = sg.Y; g.Z = sg.Z;
         g.ncells = dims->B * sg.Z * sg.X * sg.Y;
-        const int units_max = ((int)nprime + kChunk - 1) / kChunk + (g.ncells + kWave - 1) / kWave;
-        const int waves = LSS_WAVES_PER_CU > 0 ? std::min(units_max, LSS_WAVES_PER_CU * cu_count()) : units_max;
-        const dim3 gr((waves + 3) / 4), bl(kBlock);
-#define LSS_CHUNKS(F, T)                                                                                           \
-    hipExtLaunchKernelGGL((k_splat_fwd_chunks<F, T>), gr, bl, 0, s, e0, e1, 0, depth, ctx_t, x_rows, cell_start, \
-                          sorted_key, sorted_row, g, (T*)out)
-        if (out_dtype == LSS_F32) { if (fused) LSS_CHUNKS(true, float); else LSS_CHUNKS(false, float); }
-        else if (out_dtype == LSS_BF16) { if (fused) LSS_CHUNKS(true, bf16); else LSS_CHUNKS(false, bf16); }
-        else return LSS_EINVAL;
-#undef LSS_CHUNKS
+        const int wpb = kBlock / kWave;
+        const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), wpb);
+        const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), wpb);
+        const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kBlock);
+#define LSS_NHWC_FWD(F, RT, T)                                                                                     \
+    hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, (const RT*)rows,           \
+                          cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, (T*)out)
+        if (out_dtype == LSS_F32) {
+            if (!fused) LSS_NHWC_FWD(false, float, float);
+            else if (ctx_bf16) LSS_NHWC_FWD(true, bf16, float);
+            else LSS_NHWC_FWD(true, float, float);
+        } else {
+            if (!fused) LSS_NHWC_FWD(false, float, bf16);
+            else if (ctx_bf16) LSS_NHWC_FWD(true, bf16, bf16);
+            else LSS_NHWC_FWD(true, float, bf16);
+        }
+#undef LSS_NHWC_FWD
         return launch_status();
     }
     if (sg.YT > kMaxYT) return LSS_EUNSUPPORTED;
     const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
-    const size_t lds = nhwc ? (size_t)sg.YT * kC * sizeof(float) : (size_t)kC * (sg.YT + 4) * sizeof(float);
-#define LSS_SPLAT(F, T, L)                                                                                        \
-    hipExtLaunchKernelGGL((k_splat_fwd<F, T, L>), dim3(nblocks), dim3(kFwdBlock), (uint32_t)lds, s, e0, e1, 0, depth, \
-                          ctx_t, x_rows, cell_start, sorted_key, sorted_row, sg, (T*)out)
+    const size_t lds = (size_t)kC * (sg.YT + 4) * sizeof(float);
+#define LSS_SPLAT(F, RT, T)                                                                                       \
+    hipExtLaunchKernelGGL((k_splat_fwd<F, RT, T, false>), dim3(nblocks), dim3(kFwdBlock), (uint32_t)lds, s, e0, e1, \
+                          0, depth, (const RT*)rows, cell_start, sorted_key, sorted_row, sg, nprime, (T*)out)
     if (out_dtype == LSS_F32) {
-        if (fused) { if (nhwc) LSS_SPLAT(true, float, true); else LSS_SPLAT(true, float, false); }
-        else { if (nhwc) LSS_SPLAT(false, float, true); else LSS_SPLAT(false, float, false); }
-    } else if (out_dtype == LSS_BF16) {
-        if (fused) { if (nhwc) LSS_SPLAT(true, bf16, true); else LSS_SPLAT(true, bf16, false); }
-        else { if (nhwc) LSS_SPLAT(false, bf16, true); else LSS_SPLAT(false, bf16, false); }
+        if (!fused) LSS_SPLAT(false, float, float);
+        else if (ctx_bf16) LSS_SPLAT(true, bf16, float);
+        else LSS_SPLAT(true, float, float);
     } else {
-        return LSS_EINVAL;
+        if (!fused) LSS_SPLAT(false, float, bf16);
+        else if (ctx_bf16) LSS_SPLAT(true, bf16, bf16);
+        else LSS_SPLAT(true, float, bf16);
     }
 #undef LSS_SPLAT
     return launch_status();
@@ -1264,8 +1379,8 @@ int lss_bev_rows(const void* dbev, int32_t g_dtype, const int32_t* cell_start, c
 }
 
 int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int32_t* cell_of, const float* depth,
-                  const float* ctx_t, const lss_dims_t* dims, const lss_grid_t* grid, void* d_depthnet_out,
-                  int32_t d_dtype, lss_stream_t stream) {
+                  const void* ctx_t, int32_t ctx_dtype, const lss_dims_t* dims, const lss_grid_t* grid,
+                  void* d_depthnet_out, int32_t d_dtype, lss_stream_t stream) {
     if (!dims_ok(dims) || !grid_ok(grid) || !g || !cell_of || !depth || !ctx_t || !d_depthnet_out) return LSS_EINVAL;
     if (dims->D > 64) return LSS_EUNSUPPORTED;
     const SplatGeo sg = splat_geo(grid);
@@ -1276,14 +1391,24 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
     const dim3 gr(grid_blocks(npix, wpb)), bl(kBlock);
     hipStream_t s = (hipStream_t)stream;
     const bool nhwc = rows_layout == LSS_NHWC;
-#define LSS_BWD(GT, DT, L)                                                                                        \
-    hipLaunchKernelGGL((k_splat_bwd<GT, DT, L>), gr, bl, lds, s, (const GT*)g, cell_of, depth, ctx_t, dims->D,    \
-                       HW, npix, sg, (DT*)d_depthnet_out)
-    if (g_dtype == LSS_F32 && d_dtype == LSS_F32) { if (nhwc) LSS_BWD(float, float, true); else LSS_BWD(float, float, false); }
-    else if (g_dtype == LSS_F32 && d_dtype == LSS_BF16) { if (nhwc) LSS_BWD(float, bf16, true); else LSS_BWD(float, bf16, false); }
-    else if (g_dtype == LSS_BF16 && d_dtype == LSS_F32) { if (nhwc) LSS_BWD(bf16, float, true); else LSS_BWD(bf16, float, false); }
-    else if (g_dtype == LSS_BF16 && d_dtype == LSS_BF16) { if (nhwc) LSS_BWD(bf16, bf16, true); else LSS_BWD(bf16, bf16, false); }
+#define LSS_BWD(GT, DT, CT)                                                                                       \
+    do {                                                                                                          \
+        if (nhwc)                                                                                                 \
+            hipLaunchKernelGGL((k_splat_bwd<GT, DT, CT, true>), gr, bl, lds, s, (const GT*)g, cell_of, depth,     \
+                               (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_splat_bwd<GT, DT, CT, false>), gr, bl, lds, s, (const GT*)g, cell_of, depth,    \
+                               (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
+    } while (0)
+#define LSS_BWD2(GT, DT) \
+    do { if (ctx_dtype == LSS_BF16) LSS_BWD(GT, DT, bf16); else LSS_BWD(GT, DT, float); } while (0)
+    if (ctx_dtype != LSS_F32 && ctx_dtype != LSS_BF16) return LSS_EINVAL;
+    if (g_dtype == LSS_F32 && d_dtype == LSS_F32) LSS_BWD2(float, float);
+    else if (g_dtype == LSS_F32 && d_dtype == LSS_BF16) LSS_BWD2(float, bf16);
+    else if (g_dtype == LSS_BF16 && d_dtype == LSS_F32) LSS_BWD2(bf16, float);
+    else if (g_dtype == LSS_BF16 && d_dtype == LSS_BF16) LSS_BWD2(bf16, bf16);
     else return LSS_EINVAL;
+#undef LSS_BWD2
 #undef LSS_BWD
     return launch_status();
 }

@@ -251,10 +251,17 @@ class LiftSplatShoot(nn.Module):
         return ops.voxel_pool_rows(x.reshape(B * N * D * H * W, C), plan, self._layout())
 
     def get_voxels(self, x, rots, trans, intrins, post_rots, post_trans):
-        """Fused hot path: geometry/CSR, trunk, lift+splat (src/models.py:248-254)."""
+        """Fused hot path: trunk, geometry/CSR, lift+splat (src/models.py:248-254).
+
+        Schedule: the camera inverses first (inverse='host' copies the rig to the host, which must
+        not wait behind the trunk), then the trunk, then the plan kernels right before the splat,
+        so the splat reads the CSR from the caches instead of HBM.
+        """
         B, N, C, imH, imW = x.shape
-        plan = self.plan(rots, trans, intrins, post_rots, post_trans)
+        inv = ops.camera_inverses(post_rots, intrins, self.inverse)
         dn = self.camencode.depthnet_out(x.view(B * N, C, imH, imW))
+        plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
+                                     inverses=inv)
         return ops.lift_splat(dn, plan, self._bev_dtype(x.device), self._layout())
 
     def forward(self, x, rots, trans, intrins, post_rots, post_trans):

@@ -139,15 +139,20 @@ def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev):
 
 
 def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, post_trans, grid: GridSpec,
-                      inverse: str = "host", want_geom: bool = False, want_csr: bool = True) -> SplatPlan:
-    """get_geometry + quantise + filter + counting sort, all on the device (src/models.py:170-231)."""
+                      inverse: str = "host", want_geom: bool = False, want_csr: bool = True,
+                      inverses: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> SplatPlan:
+    """get_geometry + quantise + filter + counting sort, all on the device (src/models.py:170-231).
+
+    `inverses` = a (pinv, kinv) pair from camera_inverses, if already computed (models.py computes
+    them before the trunk, so the host round trip of inverse='host' never waits for device work).
+    """
     dev = _require_cuda(frustum, rots, trans, intrins, post_rots, post_trans)
     lib = _lib.load()
     B, N = trans.shape[:2]
     D, H, W = frustum.shape[:3]
     nprime = B * N * D * H * W
     ncells = grid.ncells(B)
-    pinv, kinv = camera_inverses(post_rots, intrins, inverse)
+    pinv, kinv = inverses if inverses is not None else camera_inverses(post_rots, intrins, inverse)
     fr, ro, tr, pt = _f32c(frustum), _f32c(rots), _f32c(trans), _f32c(post_trans)
     cell_of = torch.empty(nprime, device=dev, dtype=torch.int32)
     geom = torch.empty(B, N, D, H, W, 3, device=dev, dtype=torch.float32) if want_geom else None
@@ -241,7 +246,9 @@ def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, 
     lib = _lib.load()
     dev = out.device
     e0, e1 = SPLAT_PROFILE.new_pair() if SPLAT_PROFILE.enabled else (None, None)
-    _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), _lib.ptr(x_rows), _lib.ptr(plan.cell_start),
+    ctx_code = _lib.dtype_code(ctx_t.dtype) if ctx_t is not None else _lib.F32
+    _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), ctx_code, _lib.ptr(x_rows),
+                                 _lib.ptr(plan.cell_start),
                                  _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), plan.c_dims,
                                  plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype), layout,
                                  _lib.stream_handle(dev), e0, e1), "lss_splat_fwd")
@@ -285,9 +292,12 @@ class LiftSplat(torch.autograd.Function):
             dn = dn.float()
         dn = dn.contiguous()
         depth = torch.empty(B * N, D, H, W, device=dev, dtype=torch.float32)
-        ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=torch.float32)
+        # context rows keep the input's element type: bf16 rows are exact for a bf16 depthnet output
+        # and halve the splat's gathered bytes
+        ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=dn.dtype)
         _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.dtype_code(dn.dtype), plan.c_dims, _lib.ptr(depth),
-                                     _lib.ptr(ctx_t), _lib.stream_handle(dev)), "lss_lift_prep")
+                                     _lib.ptr(ctx_t), _lib.dtype_code(ctx_t.dtype), _lib.stream_handle(dev)),
+                   "lss_lift_prep")
         X, Y, Z = plan.grid.nx
         out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
         _splat_fwd_launch(plan, depth, ctx_t, None, out, layout)
@@ -305,7 +315,8 @@ class LiftSplat(torch.autograd.Function):
         B, N, D, H, W = plan.dims
         d_dn = torch.empty(B * N, D + C_CAM, H, W, device=depth.device, dtype=ctx.dn_dtype)
         _lib.check(lib.lss_splat_bwd(_lib.ptr(rows), _lib.dtype_code(rows.dtype), layout, _lib.ptr(plan.cell_of),
-                                     _lib.ptr(depth), _lib.ptr(ctx_t), plan.c_dims, plan.grid.c_struct(),
+                                     _lib.ptr(depth), _lib.ptr(ctx_t), _lib.dtype_code(ctx_t.dtype), plan.c_dims,
+                                     plan.grid.c_struct(),
                                      _lib.ptr(d_dn), _lib.dtype_code(d_dn.dtype), _lib.stream_handle(depth.device)),
                    "lss_splat_bwd")
         return d_dn, None, None, None

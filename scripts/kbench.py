@@ -1,11 +1,18 @@
-"""Kernel micro-benchmark: every hot-path op of config 3 timed in isolation (HIP events), plus
-tuning variants of lss_splat_fwd built with -D knobs (lss-carla_amd/variants/*.so).
+"""Kernel micro-benchmark: every hot-path op of config 3 timed in isolation, plus tuning variants of
+lss_splat_fwd built with -D knobs (lss-carla_amd/variants/*.so).
+
+Splat times come from kernel-stamped events (hipExtLaunchKernel: the kernel alone, no launch
+overhead) in three cache states:
+  warm  back-to-back launches
+  cold  512 MiB written before each launch (L2 and Infinity Cache flushed)
+  step  caches flushed, then the CSR and the lift prep rebuilt right before the splat -- the order of
+        a training step, where the plan is built after the trunk (models.LiftSplatShoot.get_voxels)
 
   python scripts/kbench.py --build-variants     # here (hipcc), before gpurun
   python scripts/kbench.py                      # on the GPU box
 """
 import argparse
-import ctypes
+import ctypes as ct
 import glob
 import json
 import os
@@ -15,13 +22,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
-    "lds_b8": ["LSS_GROUPS=0", "LSS_BATCH=8"],
-    "lds_b16": ["LSS_GROUPS=0", "LSS_BATCH=16"],
-    "u2": ["LSS_UNROLL=2"],
-    "u3": ["LSS_UNROLL=3"],
-    "u6": ["LSS_UNROLL=6"],
-    "wpc16": ["LSS_WAVES_PER_CU=16"],
-    "wpc0": ["LSS_WAVES_PER_CU=0"],
+    "plain_zero": ["LSS_ZERO_STORE=0"],
+    "row_nt": ["LSS_ROW_NT=1"],
+    "z2": ["LSS_ZERO_UNITS=2"],
+    "z2_row_nt": ["LSS_ZERO_UNITS=2", "LSS_ROW_NT=1"],
+    "u6": ["LSS_UNROLL=6", "LSS_MIN_WAVES=6"],
 }
 
 
@@ -38,7 +43,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", default="", help="run only ops whose name contains this (for rocprofv3 --pmc)")
     ap.add_argument("--variants", type=int, default=1, help="also time the variants/*.so builds")
-    ap.add_argument("--cold", type=int, default=1, help="also time splat_fwd with caches flushed before each launch")
+    ap.add_argument("--cold", type=int, default=1, help="also time splat_fwd in the cold and step cache states")
     args = ap.parse_args()
     if args.build_variants:
         build_variants()
@@ -60,6 +65,7 @@ def main():
     st = lambda: _lib.stream_handle(dev)  # noqa: E731
 
     def timeit(fn, iters=args.iters):
+        """Launch-to-launch time (includes the host's launch overhead for short kernels)."""
         if args.only and args.only not in timeit.name:
             return float("nan")
         for _ in range(3):
@@ -74,23 +80,27 @@ def main():
         return e0.elapsed_time(e1) / iters * 1e3  # us
 
     res = {}
+    plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device")
+    kept = int(plan.cell_start[-1])
+    dims, g = plan.c_dims, grid.c_struct()
+    ncells, nprime = grid.ncells(B), plan.nprime
+    pinv, kinv = ops.camera_inverses(rig["post_rots"], rig["intrins"], "device")
+    ro, tr, pt = [t.float().contiguous() for t in (rig["rots"], rig["trans"], rig["post_trans"])]
 
-    def lib_plan(l):
-        """cell_start / sorted_key / sorted_row built by library `l`."""
-        import ctypes as ct
-        ncells = grid.ncells(B)
-        nprime = plan.nprime
+    def lib_plan(l, into=None):
+        """cell_start / sorted_key / sorted_row built by library `l` (into the given buffers, if any)."""
         counts = torch.zeros(ncells, device=dev, dtype=torch.int32)
         slot = torch.empty(nprime, device=dev, dtype=torch.int32)
         cell_of = torch.empty(nprime, device=dev, dtype=torch.int32)
-        pinv, kinv = ops.camera_inverses(rig["post_rots"], rig["intrins"], "device")
-        ro, tr, pt = [t.float().contiguous() for t in (rig["rots"], rig["trans"], rig["post_trans"])]
         _lib.check(l.lss_geometry_cells(_lib.ptr(frustum), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv),
                                         _lib.ptr(pinv), _lib.ptr(pt), dims, g, None, _lib.ptr(cell_of),
                                         _lib.ptr(counts), _lib.ptr(slot), st()), "geom")
-        cs = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
-        sk = torch.empty(nprime, device=dev, dtype=torch.int64)
-        sr = torch.empty(nprime, device=dev, dtype=torch.int32)
+        if into is not None:
+            cs, sk, sr = into
+        else:
+            cs = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
+            sk = torch.empty(nprime, device=dev, dtype=torch.int64)
+            sr = torch.empty(nprime, device=dev, dtype=torch.int32)
         scr = torch.empty(int(l.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
         _lib.check(l.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot), nprime, _lib.ptr(counts), ncells, dims,
                                    _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), _lib.ptr(scr), st()), "csr")
@@ -99,84 +109,95 @@ def main():
     def named(name, fn, *a):
         timeit.name = name
         return timeit(fn, *a)
-    plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device")
-    kept = int(plan.cell_start[-1])
-    dims, g = plan.c_dims, grid.c_struct()
+
     depth = torch.empty(B * N, D, H, W, device=dev)
-    ctx_t = torch.empty(B * N * H * W, 64, device=dev)
+    ctx_t = torch.empty(B * N * H * W, 64, device=dev, dtype=torch.bfloat16)  # as ops.LiftSplat for bf16 input
     bev_bf = torch.empty(B, Z * 64, X, Y, device=dev, dtype=torch.bfloat16, memory_format=torch.channels_last)
     bev_f = torch.empty(B, Z * 64, X, Y, device=dev)
     res["memset_bev_bf16_41MB"] = named("memset_bev_bf16_41MB", lambda: bev_bf.zero_())
     res["memset_bev_f32_82MB"] = named("memset_bev_f32_82MB", lambda: bev_f.zero_())
     res["copy_bev_f32_82MB"] = named("copy_bev_f32_82MB", lambda: bev_f.copy_(bev_bf))
-    res["plan_total(device inv)"] = named("plan_total(device inv)", lambda: ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device"))
-    res["lift_prep"] = named("lift_prep", lambda: _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth),
-                                                                    _lib.ptr(ctx_t), st()), "lift"))
+    res["plan_total(device inv)"] = named("plan_total(device inv)",
+                                          lambda: ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device"))
+    res["lift_prep"] = named("lift_prep", lambda: _lib.check(lib.lss_lift_prep(
+        _lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, st()), "lift"))
+    ctx_f = torch.empty(B * N * H * W, 64, device=dev)
+    _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_f), _lib.F32, st()),
+               "lift")
 
     pcsr = (plan.cell_start, plan.sorted_key, plan.sorted_row)
 
-    def fwd(l, out, layout, csr=pcsr):
+    def fwd(l, out, layout, csr=pcsr, ctx=None):
         cs, sk, its = csr
-        return lambda: _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), None, _lib.ptr(cs),
-                                                  _lib.ptr(sk), _lib.ptr(its), dims, g, _lib.ptr(out),
+        ctx = ctx_t if ctx is None else ctx
+        return lambda: _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx), _lib.dtype_code(ctx.dtype), None,
+                                                  _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(its), dims, g, _lib.ptr(out),
                                                   _lib.dtype_code(out.dtype), layout, st(), None, None), "fwd")
 
-    res["splat_fwd nhwc bf16"] = named("splat_fwd nhwc bf16", fwd(lib, bev_bf, _lib.NHWC))
-    res["splat_fwd nchw f32"] = named("splat_fwd nchw f32", fwd(lib, bev_f, _lib.NCHW))
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+
+    def stamped(l, out, layout, csr=pcsr, ctx=None, mode="warm", iters=20):
+        cs, sk, its = csr
+        ctx = ctx_t if ctx is None else ctx
+        tot = 0.0
+        for i in range(iters + 3):
+            if mode in ("cold", "step"):
+                flush.zero_()
+            if mode == "step":
+                lib_plan(l, csr)
+                _lib.check(l.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx),
+                                           _lib.dtype_code(ctx.dtype), st()), "lift")
+            a, b = ct.c_void_p(), ct.c_void_p()
+            l.lss_event_create(ct.byref(a))
+            l.lss_event_create(ct.byref(b))
+            _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx), _lib.dtype_code(ctx.dtype), None, _lib.ptr(cs),
+                                       _lib.ptr(sk), _lib.ptr(its), dims, g, _lib.ptr(out),
+                                       _lib.dtype_code(out.dtype), layout, st(), a, b), "fwd")
+            ms = ct.c_float()
+            l.lss_event_elapsed_ms(a, b, ct.byref(ms))
+            if i >= 3:
+                tot += ms.value
+            l.lss_event_destroy(a)
+            l.lss_event_destroy(b)
+        return tot / iters * 1e3
+
+    modes = ["warm"] + (["cold", "step"] if args.cold else [])
     fwd(lib, bev_bf, _lib.NHWC)()
     ref_out = bev_bf.clone()
-    variants = {}
+    fwd(lib, bev_bf, _lib.NHWC, ctx=ctx_f)()
+    if not torch.equal(bev_bf, ref_out):
+        print("WARNING: fp32 and bf16 context rows give different outputs", flush=True)
+    if not args.only or "splat_fwd" in args.only:
+        res["launch-to-launch splat_fwd nhwc bf16"] = named("splat_fwd nhwc bf16", fwd(lib, bev_bf, _lib.NHWC))
+        for m in modes:
+            res[f"{m} splat_fwd nhwc bf16"] = stamped(lib, bev_bf, _lib.NHWC, mode=m)
+            res[f"{m} splat_fwd nhwc bf16 (f32 ctx)"] = stamped(lib, bev_bf, _lib.NHWC, ctx=ctx_f, mode=m)
+        res["warm splat_fwd nchw f32"] = stamped(lib, bev_f, _lib.NCHW)
     for path in sorted(glob.glob(os.path.join(REPO, "lss-carla_amd", "variants", "*.so"))) if args.variants else []:
         vl = _lib.open_library(path)
         name = os.path.basename(path)[:-3]
-        variants[name] = (vl, lib_plan(vl))
-        res[f"splat_fwd nhwc bf16 [{name}]"] = named(f"splat_fwd nhwc bf16 [{name}]",
-                                                     fwd(vl, bev_bf, _lib.NHWC, variants[name][1]))
+        vcsr = lib_plan(vl)
+        fwd(vl, bev_bf, _lib.NHWC, vcsr)()
         if not torch.equal(bev_bf, ref_out):
             print(f"WARNING variant {name}: output differs from the product kernel", flush=True)
-    if args.cold:
-        # cold caches, as inside a training step (the trunk runs between the CSR build and the splat):
-        # 512 MiB written before every launch, kernel time from kernel-stamped events (hipExtLaunchKernel)
-        flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
-
-        def cold(l, out, layout, csr, iters=20):
-            import ctypes as ct
-            cs, sk, its = csr
-            tot = 0.0
-            for _ in range(iters):
-                flush.zero_()
-                a, b = ct.c_void_p(), ct.c_void_p()
-                l.lss_event_create(ct.byref(a))
-                l.lss_event_create(ct.byref(b))
-                _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), None, _lib.ptr(cs),
-                                           _lib.ptr(sk), _lib.ptr(its), dims, g, _lib.ptr(out),
-                                           _lib.dtype_code(out.dtype), layout, st(), a, b), "fwd")
-                ms = ct.c_float()
-                l.lss_event_elapsed_ms(a, b, ct.byref(ms))
-                tot += ms.value
-                l.lss_event_destroy(a)
-                l.lss_event_destroy(b)
-            return tot / iters * 1e3
-
-        if not args.only or "cold" in args.only:
-            res["COLD splat_fwd nhwc bf16"] = cold(lib, bev_bf, _lib.NHWC, pcsr)
-            for name, (vl, csr) in variants.items():
-                res[f"COLD splat_fwd nhwc bf16 [{name}]"] = cold(vl, bev_bf, _lib.NHWC, csr)
+        for m in modes:
+            res[f"{m} splat_fwd nhwc bf16 [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m)
+            res[f"{m} splat_fwd nhwc bf16 (f32 ctx) [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, ctx=ctx_f,
+                                                                          mode=m)
     g_bf = torch.randn(B, Z * 64, X, Y, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     d_dn = torch.empty_like(dn)
     res["splat_bwd nhwc bf16"] = named("splat_bwd nhwc bf16", lambda: _lib.check(lib.lss_splat_bwd(
-        _lib.ptr(g_bf), _lib.BF16, _lib.NHWC, _lib.ptr(plan.cell_of), _lib.ptr(depth), _lib.ptr(ctx_t), dims, g,
-        _lib.ptr(d_dn), _lib.BF16, st()), "bwd"))
-    rows = torch.empty(grid.ncells(B) * 64, device=dev)
+        _lib.ptr(g_bf), _lib.BF16, _lib.NHWC, _lib.ptr(plan.cell_of), _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
+        dims, g, _lib.ptr(d_dn), _lib.BF16, st()), "bwd"))
+    rows = torch.empty(ncells * 64, device=dev)
     g_f = torch.randn(B, Z * 64, X, Y, device=dev)
     res["bev_rows nchw f32"] = named("bev_rows nchw f32", lambda: _lib.check(lib.lss_bev_rows(
         _lib.ptr(g_f), _lib.F32, _lib.ptr(plan.cell_start), dims, g, _lib.ptr(rows), st()), "rows"))
-    nbytes = (B * N * D * H * W * 4 + B * N * H * W * 64 * 4 + kept * 4 + (grid.ncells(B) + 1) * 4
-              + grid.ncells(B) * 64 * 2)
+    nbytes = (nprime * 4 + B * N * H * W * 64 * 2 + kept * 4 + (ncells + 1) * 4 + ncells * 64 * 2)
     for k, v in res.items():
         extra = f"  {nbytes / v / 1e3:7.1f} GB/s alg" if "splat_fwd nhwc bf16" in k else ""
-        print(f"{k:40s} {v:9.2f} us{extra}")
-    print(json.dumps({"kept": kept, "alg_bytes_fwd_bf16": nbytes}))
+        print(f"{k:52s} {v:9.2f} us{extra}")
+    print(json.dumps({"kept": kept, "alg_bytes_fwd_bf16_ctx": nbytes}))
 
 
 if __name__ == "__main__":

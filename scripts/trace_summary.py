@@ -58,9 +58,11 @@ if fetch is not None and write is not None:
     traffic = {"config": a.config, "out_bytes": a.out_bytes, "kernel": "k_splat_fwd",
                "fetch_size_kb": round(fetch, 1), "write_size_kb": round(write, 1),
                "hbm_bytes_per_launch": int((fetch + write) * 1024),
-               "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, KB units x1024. The reads are "
-                       "4-B-per-lane gathers (not the 16-B streaming pattern whose FETCH_SIZE gfx950 halves), so no "
-                       "x2 correction is applied to the read side; the 16-B streaming stores make WRITE_SIZE exact."}
+               "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over the bench's training steps, "
+                       "KB x1024, averaged over the splat launches. FETCH_SIZE counts the reads that left L2 for the "
+                       "fabric (Infinity Cache or HBM); the context-row gathers are 16-B lane slices of L2-resident "
+                       "rows, not a streaming read, so no x2 correction is applied. WRITE_SIZE is exact for the "
+                       "16-B row stores."}
     with open(os.path.join(a.out_dir, "splat_fwd_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     summary["splat_fwd_traffic"] = traffic

@@ -106,11 +106,15 @@ def _check_canonical_csr(plan, cell, ncells):
     np.testing.assert_array_equal(plan.sorted_row.cpu().numpy()[:total], cam * H * W + rem % (H * W))
 
 
-def test_splat_chunk_and_tile_kernels_agree_bitwise():
-    """The channels-last chunk kernel and the NCHW tile kernel sum every cell in the same order."""
+def test_splat_chunk_and_tile_kernels_agree():
+    """The channels-last chunk kernel and the NCHW tile kernel differ only in how a cell cut by a
+    lane-group boundary is associated (both fp32, FMA per point)."""
     *_, bev_nhwc = _lift_splat("c3", _lib.NHWC)
     *_, bev_nchw = _lift_splat("c3", _lib.NCHW)
-    assert torch.equal(bev_nhwc.contiguous(), bev_nchw)
+    torch.testing.assert_close(bev_nhwc.contiguous(), bev_nchw, rtol=0, atol=1e-5)
+    # cells whose points all fall in one lane group are summed in the same order: most rows agree bitwise
+    same = (bev_nhwc.contiguous() == bev_nchw).all(dim=1).float().mean().item()
+    assert same > 0.9, same
 
 
 def _dense_cell_geom(B, N, D, H, W, seed=0):
@@ -213,8 +217,9 @@ def test_golden_pool_small():
     np.testing.assert_allclose(bev, z["bev_quick"], rtol=0, atol=ATOL)
 
 
-def test_deterministic_bitwise():
-    outs = [_lift_splat("c3", _lib.NCHW)[-1].cpu() for _ in range(2)]
+@pytest.mark.parametrize("layout", [_lib.NCHW, _lib.NHWC])
+def test_deterministic_bitwise(layout):
+    outs = [_lift_splat("c3", layout)[-1].cpu() for _ in range(2)]
     assert torch.equal(outs[0], outs[1])
 
 
