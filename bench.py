@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--dw-native", type=int, default=0, help="depthwise convs on PyTorch's native kernels")
     ap.add_argument("--bn-native", default="", help="BatchNorm on native kernels: '', 'trunk', 'bev', 'all'")
     ap.add_argument("--inverse", default="host", choices=["host", "device"])
+    ap.add_argument("--fuse-depthnet", type=int, default=1, help="depthnet 1x1 conv inside the lift kernel (MFMA)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "splat_fwd_traffic.json"))
@@ -92,6 +93,7 @@ def build_model(args, dev, cfg, gc, dac):
     model = L.compile_model(gc, dac, outC=1).to(dev)
     model.bev_layout = args.bev_layout
     model.inverse = args.inverse
+    model.fuse_depthnet = bool(args.fuse_depthnet)
     if args.bev_layout == "nhwc":
         model.bevencode.to(memory_format=torch.channels_last)
     if args.trunk_channels_last:
@@ -254,7 +256,7 @@ def main():
             "config": {"workload": f"{args.config}: B={B}/GPU x {N} cams x {fd[0]}x{fd[1]}, D={D}, {X}x{Y} BEV, "
                                    "full train step (fwd+loss+bwd+clip+Adam)",
                        "global_batch": world * B, "parallelism": f"dp{world}", "bev_layout": args.bev_layout,
-                       "inverse": args.inverse},
+                       "inverse": args.inverse, "fuse_depthnet": bool(args.fuse_depthnet)},
             "roofline": {"kernel": "lss_splat_fwd", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 7
+#define LSS_ABI_VERSION 8
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -102,6 +102,18 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
  * depthnet_out is (B*N, D+C, H, W) contiguous, element type in_dtype. */
 int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims,
                   float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream);
+
+/* Depthnet + lift, part 1, fused (CamEncode.depthnet 1x1 conv + get_depth_dist + layout,
+ * src/models.py:47, 55-59, 192-202): logits = weight . feat + bias on MFMA (bf16 in, fp32
+ * accumulate, rounded to bf16 like the autocast conv output), depth (B*N, D, H, W) fp32 = softmax
+ * over the first D logits, ctx_t (B*N*H*W, C) bf16 = the last C logits as pixel-major rows. The
+ * depthnet output (B*N, D+C, H, W) is never written. feat (B*N, K, H, W) contiguous, weight
+ * (D+C, K) row-major, bias (D+C); dtype and ctx_dtype must be LSS_BF16; K % 16 == 0, K <= 512,
+ * D + C <= 128 (else LSS_EUNSUPPORTED). The backward stays the conv's: d(logits) from
+ * lss_splat_bwd feeds the 1x1 conv's weight / input gradients. */
+int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
+                      const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype,
+                      lss_stream_t stream);
 
 /* Splat forward: segmented per-cell sum written as the dense (B, Z*C, X, Y) BEV
  * (voxel_pooling + QuickCumsum.forward + griddify, src/models.py:233-246,

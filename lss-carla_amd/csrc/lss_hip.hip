@@ -428,6 +428,105 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
     }
 }
 
+// ----------------------------------------------------------------------------- depthnet + lift prep (fused)
+// CamEncode's depthnet 1x1 conv (K -> D + C channels, with bias) fused with the lift's first half
+// (src/models.py:47, 55-59): logits = W.x + b on MFMA (v_mfma_f32_32x32x16_bf16: bf16 in, fp32
+// accumulate), rounded to bf16 as the autocast conv's output is, then depth = softmax over the D
+// bins (fp32, the reference's (B*N, D, H, W) layout) and the context rows ctx_t (bf16,
+// pixel-major) -- the depthnet output itself is never written. One block = 32 pixels x 4 waves:
+// the pixels' K input channels are staged in LDS as [pixel][k] (one 16-B LDS read per MFMA B
+// fragment); wave w computes output channels [32w, 32w + 32) over all of K with A fragments (16 B
+// of a weight row) read straight from L2.
+constexpr int kDnPix = 32;    // pixels per block
+constexpr int kDnMaxK = 512;  // input channels (up1 outputs 512, src/models.py:45)
+constexpr int kDnMaxO = 128;  // D + C <= 4 waves x 32 output channels
+
+__global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict__ feat, const bf16* __restrict__ weight,
+                                                          const bf16* __restrict__ bias, int K, int D, int HW,
+                                                          int npix, float* __restrict__ depth, bf16* __restrict__ ctx_t) {
+    using bf16x8 = __attribute__((ext_vector_type(8))) short;
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    __shared__ __attribute__((aligned(16))) bf16 s_x[kDnPix][kDnMaxK + 8];  // [pixel][k]; +8: spread the banks
+    __shared__ float s_lg[kDnMaxO][kDnPix + 1];                               // bf16-rounded logits [o][pixel]
+    __shared__ float s_red[2][kBlock / kDnPix][kDnPix];
+    const int q0 = blockIdx.x * kDnPix;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // stage: element (k, p), pixels fastest. With HW % 8 == 0 an aligned run of 8 pixels never
+    // crosses an image, so each thread moves 16 B (8 pixels of one channel) per load.
+    if ((HW & 7) == 0) {
+        for (int i = threadIdx.x; i < K * (kDnPix / 8); i += kBlock) {
+            const int k = i / (kDnPix / 8), p8 = (i - k * (kDnPix / 8)) * 8, q = q0 + p8;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (q < npix) {
+                const int bn = q / HW, hw = q - bn * HW;
+                v = *reinterpret_cast<const uint4*>(feat + ((size_t)bn * K + k) * HW + hw);
+            }
+            const unsigned short* e = reinterpret_cast<const unsigned short*>(&v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) reinterpret_cast<unsigned short*>(&s_x[p8 + j][0])[k] = e[j];
+        }
+    } else {
+        for (int i = threadIdx.x; i < K * kDnPix; i += kBlock) {
+            const int k = i / kDnPix, p = i - k * kDnPix, q = q0 + p;
+            bf16 v = __float2bfloat16(0.f);
+            if (q < npix) {
+                const int bn = q / HW, hw = q - bn * HW;
+                v = feat[((size_t)bn * K + k) * HW + hw];
+            }
+            s_x[p][k] = v;
+        }
+    }
+    __syncthreads();
+    const int O = D + kC;
+    const int r = lane & 31, h = lane >> 5;
+    const int o = wave * 32 + r;
+    const bf16* wrow = weight + (size_t)min(o, O - 1) * K + 8 * h;
+    f32x16 acc = {};
+#pragma unroll 4
+    for (int k0 = 0; k0 < K; k0 += 16) {
+        // A[row o][k = k0 + 8h + j] (weight row), B[k = k0 + 8h + j][col p = r] (staged pixel r)
+        bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + k0);
+        if (o >= O) a = bf16x8{};
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&s_x[r][k0 + 8 * h]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+    }
+    // D/C layout: column (pixel) = lane & 31, row (output channel) = (i & 3) + 8 (i >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int og = wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (og < O) s_lg[og][r] = __bfloat162float(__float2bfloat16(acc[i] + __bfloat162float(bias[og])));
+    }
+    __syncthreads();
+    // softmax over the D bins of each pixel: thread (part, p) covers bins part, part + 8, ...
+    constexpr int kParts = kBlock / kDnPix;
+    const int p = threadIdx.x % kDnPix, part = threadIdx.x / kDnPix;
+    float m = -INFINITY;
+    for (int d = part; d < D; d += kParts) m = fmaxf(m, s_lg[d][p]);
+    s_red[0][part][p] = m;
+    __syncthreads();
+    m = s_red[0][0][p];
+#pragma unroll
+    for (int j = 1; j < kParts; ++j) m = fmaxf(m, s_red[0][j][p]);
+    float sum = 0.f;
+    for (int d = part; d < D; d += kParts) sum += expf(s_lg[d][p] - m);
+    s_red[1][part][p] = sum;
+    __syncthreads();
+    sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < kParts; ++j) sum += s_red[1][j][p];
+    const int q = q0 + p;
+    if (q < npix) {
+        const int bn = q / HW, hw = q - bn * HW;
+        float* dst = depth + (size_t)bn * D * HW + hw;
+        for (int d = part; d < D; d += kParts) dst[(size_t)d * HW] = expf(s_lg[d][p] - m) / sum;
+    }
+    // context rows: 64 consecutive channels of a pixel = one 128-B row
+    for (int i = threadIdx.x; i < kDnPix * kC; i += kBlock) {
+        const int pp = i / kC, c = i - pp * kC;
+        if (q0 + pp < npix) ctx_t[(size_t)(q0 + pp) * kC + c] = __float2bfloat16(s_lg[D + c][pp]);
+    }
+}
+
 // 16 bytes of fp32 or bf16 row elements -> fp32.
 __device__ __forceinline__ void unpack16(const uint4& u, const float*, float* o) {
     o[0] = __uint_as_float(u.x); o[1] = __uint_as_float(u.y); o[2] = __uint_as_float(u.z); o[3] = __uint_as_float(u.w);
@@ -1297,6 +1396,20 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
     else if (in_dtype == LSS_BF16 && ctx_dtype == LSS_BF16) LSS_PREP(bf16, bf16);
     else return LSS_EINVAL;
 #undef LSS_PREP
+    return launch_status();
+}
+
+int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
+                      const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream) {
+    if (!dims_ok(dims) || !feat || !weight || !bias || !depth || !ctx_t) return LSS_EINVAL;
+    if (dtype != LSS_BF16 || ctx_dtype != LSS_BF16) return LSS_EUNSUPPORTED;
+    if (K <= 0 || K % 16 != 0 || K > kDnMaxK || dims->D + kC > kDnMaxO) return LSS_EUNSUPPORTED;
+    const int HW = dims->H * dims->W;
+    const long npix = (long)dims->B * dims->N * HW;
+    if (npix >= INT_MAX) return LSS_EUNSUPPORTED;
+    hipLaunchKernelGGL(k_depthnet_lift, dim3(grid_blocks(npix, kDnPix)), dim3(kBlock), 0, (hipStream_t)stream,
+                       (const bf16*)feat, (const bf16*)weight, (const bf16*)bias, K, dims->D, HW, (int)npix, depth,
+                       (bf16*)ctx_t);
     return launch_status();
 }
 

@@ -18,10 +18,12 @@ outer product) and the splat run as gfx950 HIP kernels (``ops.py`` ->
 stock PyTorch-ROCm modules (MIOpen / MFMA). The hot path refuses CPU tensors.
 
 Extra knobs (not in the reference, defaults reproduce it):
-  ``bev_layout``  'nchw' (reference layout) or 'nhwc' (channels-last BEV, feeds a
-                  channels-last BevEncode without a transpose)
-  ``inverse``     'host' (torch.inverse on the CPU, as src/models.py:180,186) or
-                  'device' (no host round trip)
+  ``bev_layout``     'nchw' (reference layout) or 'nhwc' (channels-last BEV, feeds a
+                     channels-last BevEncode without a transpose)
+  ``inverse``        'host' (torch.inverse on the CPU, as src/models.py:180,186) or
+                     'device' (no host round trip)
+  ``fuse_depthnet``  under bf16 autocast, run the depthnet 1x1 conv inside the lift kernel
+                     (MFMA); off: the conv runs as its own op (MIOpen)
 """
 from __future__ import annotations
 
@@ -205,6 +207,7 @@ class LiftSplatShoot(nn.Module):
         self.use_quickcumsum = True
         self.bev_layout = "nchw"
         self.inverse = "host"
+        self.fuse_depthnet = True  # bf16 autocast: depthnet conv fused into the lift kernel
         self._grid = ops.GridSpec.from_conf(grid_conf)
 
     def create_frustum(self):
@@ -259,10 +262,16 @@ class LiftSplatShoot(nn.Module):
         """
         B, N, C, imH, imW = x.shape
         inv = ops.camera_inverses(post_rots, intrins, self.inverse)
-        dn = self.camencode.depthnet_out(x.view(B * N, C, imH, imW))
+        ce = self.camencode
+        feat = ce.dropout(ce.get_eff_depth(x.view(B * N, C, imH, imW)))
         plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
                                      inverses=inv)
-        return ops.lift_splat(dn, plan, self._bev_dtype(x.device), self._layout())
+        out_dtype = self._bev_dtype(x.device)
+        if self.fuse_depthnet and out_dtype == torch.bfloat16:
+            # depthnet 1x1 conv + softmax + context layout in one MFMA kernel
+            return ops.depthnet_lift_splat(feat, ce.depthnet.weight, ce.depthnet.bias, plan, out_dtype,
+                                           self._layout())
+        return ops.lift_splat(ce.depthnet(feat), plan, out_dtype, self._layout())
 
     def forward(self, x, rots, trans, intrins, post_rots, post_trans):
         x = self.get_voxels(x, rots, trans, intrins, post_rots, post_trans)

@@ -327,6 +327,69 @@ def lift_splat(depthnet_out: torch.Tensor, plan: SplatPlan, out_dtype: torch.dty
     return LiftSplat.apply(depthnet_out, plan, out_dtype, layout)
 
 
+# ----------------------------------------------------------------------------- autograd: depthnet + lift + splat
+class DepthnetLiftSplat(torch.autograd.Function):
+    """depthnet(feat) -> lift -> splat in two kernels: lss_depthnet_lift (the 1x1 conv on MFMA fused
+    with the depth softmax and the context-row layout, src/models.py:47, 55-59) and lss_splat_fwd.
+    The (B*N, D+C, H, W) depthnet output is never materialised in the forward.
+
+    bf16 only (the autocast training path): under autocast the inputs are cast to bf16 as the
+    reference's ``nn.Conv2d`` would be. Backward: lss_splat_bwd gives d(logits); the conv's own
+    backward (MIOpen) turns it into d(feat), d(weight), d(bias).
+    """
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
+    def forward(ctx, feat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, plan: SplatPlan,
+                out_dtype: torch.dtype, layout: int):
+        dev = _require_cuda(feat, weight, bias)
+        lib = _lib.load()
+        B, N, D, H, W = plan.dims
+        O, K = weight.shape[0], weight.shape[1]
+        if feat.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16 or bias.dtype != torch.bfloat16:
+            raise RuntimeError("lss_carla_amd: the fused depthnet path is bf16 (run it under torch.autocast)")
+        if feat.shape != (B * N, K, H, W) or O != D + C_CAM or tuple(weight.shape[2:]) != (1, 1):
+            raise RuntimeError(f"depthnet shapes feat {tuple(feat.shape)} weight {tuple(weight.shape)} do not match "
+                               f"the plan (B*N={B * N}, D+C={D + C_CAM}, H={H}, W={W})")
+        f = feat.detach().contiguous()
+        w = weight.detach().reshape(O, K).contiguous()
+        b = bias.detach().contiguous()
+        depth = torch.empty(B * N, D, H, W, device=dev, dtype=torch.float32)
+        ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=torch.bfloat16)
+        _lib.check(lib.lss_depthnet_lift(_lib.ptr(f), _lib.ptr(w), _lib.ptr(b), _lib.BF16, K, plan.c_dims,
+                                         _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, _lib.stream_handle(dev)),
+                   "lss_depthnet_lift")
+        X, Y, Z = plan.grid.nx
+        out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
+        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout)
+        ctx.save_for_backward(f, weight, depth, ctx_t)
+        ctx.plan = plan
+        return out
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dbev: torch.Tensor):
+        feat, weight, depth, ctx_t = ctx.saved_tensors
+        plan: SplatPlan = ctx.plan
+        lib = _lib.load()
+        rows, layout = _grad_rows(plan, dbev)
+        B, N, D, H, W = plan.dims
+        d_dn = torch.empty(B * N, D + C_CAM, H, W, device=depth.device, dtype=torch.bfloat16)
+        _lib.check(lib.lss_splat_bwd(_lib.ptr(rows), _lib.dtype_code(rows.dtype), layout, _lib.ptr(plan.cell_of),
+                                     _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, plan.c_dims, plan.grid.c_struct(),
+                                     _lib.ptr(d_dn), _lib.BF16, _lib.stream_handle(depth.device)), "lss_splat_bwd")
+        need = ctx.needs_input_grad
+        d_feat, d_w, d_b = torch.ops.aten.convolution_backward(
+            d_dn, feat, weight, [weight.shape[0]], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+            [need[0], need[1], need[2]])
+        return d_feat, d_w, d_b, None, None, None
+
+
+def depthnet_lift_splat(feat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, plan: SplatPlan,
+                        out_dtype: torch.dtype = torch.bfloat16, layout: int = _lib.NHWC) -> torch.Tensor:
+    return DepthnetLiftSplat.apply(feat, weight, bias, plan, out_dtype, layout)
+
+
 # ----------------------------------------------------------------------------- autograd: unfused voxel pooling
 class VoxelPool(torch.autograd.Function):
     """(Nprime, C) lifted rows -> BEV (voxel_pooling(geom_feats, x) boundary, src/models.py:204-246)."""

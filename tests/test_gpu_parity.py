@@ -345,3 +345,81 @@ def test_cpu_tensors_fail_loudly():
     cfg, gc, rig, frustum, _ = _setup("c1")
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ops.plan_from_cameras(frustum, **rig, grid=ops.GridSpec.from_conf(gc))
+
+
+# ----------------------------------------------------------------------------- depthnet fused into the lift (§8f row 1)
+def _depthnet_inputs(name, seed=0, K=512):
+    cfg, gc, rig, frustum, _ = _setup(name, seed)
+    D, H, W = frustum.shape[:3]
+    BN = cfg["B"] * cfg["N"]
+    g = torch.Generator().manual_seed(seed + 100)
+    feat = torch.randn(BN, K, H, W, generator=g).to(torch.bfloat16)
+    weight = (torch.randn(D + 64, K, 1, 1, generator=g) * 0.05).to(torch.bfloat16)
+    bias = (torch.randn(D + 64, generator=g) * 0.1).to(torch.bfloat16)
+    plan = ops.plan_from_cameras(frustum.to(DEV), **_rig_dev(rig), grid=ops.GridSpec.from_conf(gc))
+    return cfg, gc, rig, frustum, feat, weight, bias, plan
+
+
+@pytest.mark.parametrize("name", ["c1", "c3"])
+def test_depthnet_lift_kernel_vs_conv_then_lift_prep(name):
+    """lss_depthnet_lift == bf16(conv1x1 in fp32) followed by lss_lift_prep, up to the rounding of a
+    logit that lies on a bf16 rounding boundary (GEMM accumulation order)."""
+    cfg, gc, rig, frustum, feat, weight, bias, plan = _depthnet_inputs(name)
+    lib = _lib.load()
+    B, N, D, H, W = plan.dims
+    f, w, b = feat.to(DEV), weight.to(DEV), bias.to(DEV)
+    depth = torch.empty(B * N, D, H, W, device=DEV)
+    ctx_t = torch.empty(B * N * H * W, 64, device=DEV, dtype=torch.bfloat16)
+    _lib.check(lib.lss_depthnet_lift(_lib.ptr(f), _lib.ptr(w.reshape(D + 64, -1).contiguous()), _lib.ptr(b),
+                                     _lib.BF16, 512, plan.c_dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
+                                     _lib.stream_handle(DEV)), "depthnet_lift")
+    # reference: the conv in fp64 from the same bf16 operands, rounded to bf16 like the autocast conv output
+    logits = torch.einsum("nkhw,ok->nohw", feat.double(), weight.double().flatten(1)) + bias.double().view(1, -1, 1, 1)
+    dn = logits.to(torch.bfloat16)
+    want_depth, _ = ref.lift(dn.float(), D, 64)
+    want_ctx = dn[:, D:].permute(0, 2, 3, 1).reshape(-1, 64)
+    got_ctx = ctx_t.cpu()
+    ulp_flips = (got_ctx != want_ctx)
+    assert ulp_flips.float().mean().item() < 1e-3
+    np.testing.assert_allclose(got_ctx.float().numpy(), want_ctx.float().numpy(), rtol=1e-2, atol=1e-2)
+    np.testing.assert_allclose(depth.cpu().numpy(), want_depth.numpy(), rtol=2e-2, atol=1e-4)
+
+
+def test_depthnet_lift_splat_fwd_bwd_vs_unfused():
+    """Fused depthnet+lift+splat vs the unfused path (MIOpen conv under autocast, then lift_splat)."""
+    cfg, gc, rig, frustum, feat, weight, bias, plan = _depthnet_inputs("c2")
+    fw = [t.to(DEV).float().requires_grad_(True) for t in (feat, weight, bias)]
+    uw = [t.to(DEV).float().requires_grad_(True) for t in (feat, weight, bias)]
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        fused = ops.depthnet_lift_splat(fw[0], fw[1], fw[2], plan, torch.bfloat16, _lib.NHWC)
+        dn = torch.nn.functional.conv2d(uw[0], uw[1], uw[2])
+        unfused = ops.lift_splat(dn, plan, torch.bfloat16, _lib.NHWC)
+    assert fused.dtype == torch.bfloat16 and fused.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(fused.float(), unfused.float(), rtol=2e-2, atol=2e-2)
+    g = torch.randn(fused.shape, generator=torch.Generator().manual_seed(7)).to(DEV)
+    g = g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    fused.backward(g)
+    unfused.backward(g)
+    for a, b_, what in zip(fw, uw, ("feat", "weight", "bias")):
+        assert a.grad is not None and torch.isfinite(a.grad).all(), what
+        rel = (a.grad - b_.grad).norm() / b_.grad.norm()
+        assert rel < 3e-2, (what, rel.item())
+
+
+def test_module_fused_depthnet_train_step():
+    cfg, gc, rig, frustum, _ = _setup("c2")
+    torch.manual_seed(0)
+    m = L.compile_model(gc, syn.data_aug_conf(cfg["final_dim"]), 1).to(DEV).eval()
+    m.bev_layout = "nhwc"
+    imgs = syn.make_images(cfg["B"], cfg["N"], cfg["final_dim"]).to(DEV)
+    outs = []
+    for fuse in (True, False):
+        m.fuse_depthnet = fuse
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            bev = m.get_voxels(imgs, **_rig_dev(rig))
+        bev.float().square().mean().backward()
+        outs.append((bev.detach().float(), m.camencode.depthnet.weight.grad.clone()))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-2, atol=2e-2)
+    rel = (outs[0][1] - outs[1][1]).norm() / outs[1][1].norm()
+    assert rel < 3e-2, rel.item()
