@@ -51,9 +51,9 @@ def parse():
     ap.add_argument("--bev-layout", default="nhwc", choices=["nhwc", "nchw"])
     ap.add_argument("--trunk-channels-last", type=int, default=0)
     ap.add_argument("--trunk-fp32", type=int, default=0, help="run CamEncode outside autocast")
-    ap.add_argument("--dw-fp32", type=int, default=0, help="depthwise convs of the trunk in fp32")
+    ap.add_argument("--dw-impl", default="hip", choices=["hip", "miopen", "native", "fp32"],
+                    help="depthwise convs of the trunk: HIP kernels, MIOpen, PyTorch native, MIOpen in fp32")
     ap.add_argument("--miopen-find", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
-    ap.add_argument("--dw-native", type=int, default=0, help="depthwise convs on PyTorch's native kernels")
     ap.add_argument("--bn-native", default="", help="BatchNorm on native kernels: '', 'trunk', 'bev', 'all'")
     ap.add_argument("--inverse", default="host", choices=["host", "device"])
     ap.add_argument("--fuse-depthnet", type=int, default=1, help="depthnet 1x1 conv inside the lift kernel (MFMA)")
@@ -98,18 +98,14 @@ def build_model(args, dev, cfg, gc, dac):
         model.bevencode.to(memory_format=torch.channels_last)
     if args.trunk_channels_last:
         model.camencode.to(memory_format=torch.channels_last)
-    if args.dw_native:
-        from lss_carla_amd.efficientnet import set_depthwise_native
-        set_depthwise_native(model.camencode.trunk, True)
+    from lss_carla_amd.efficientnet import set_depthwise_impl
+    set_depthwise_impl(model.camencode.trunk, args.dw_impl)
     if args.bn_native:
         from lss_carla_amd.efficientnet import set_batchnorm_native
         if args.bn_native in ("trunk", "all"):
             set_batchnorm_native(model.camencode)
         if args.bn_native in ("bev", "all"):
             set_batchnorm_native(model.bevencode)
-    if args.dw_fp32:
-        from lss_carla_amd.efficientnet import set_depthwise_fp32
-        set_depthwise_fp32(model.camencode.trunk, True)
     if args.trunk_fp32:
         ce = model.camencode
         fwd = ce.depthnet_out
@@ -256,7 +252,8 @@ def main():
             "config": {"workload": f"{args.config}: B={B}/GPU x {N} cams x {fd[0]}x{fd[1]}, D={D}, {X}x{Y} BEV, "
                                    "full train step (fwd+loss+bwd+clip+Adam)",
                        "global_batch": world * B, "parallelism": f"dp{world}", "bev_layout": args.bev_layout,
-                       "inverse": args.inverse, "fuse_depthnet": bool(args.fuse_depthnet)},
+                       "inverse": args.inverse, "fuse_depthnet": bool(args.fuse_depthnet),
+                       "depthwise": args.dw_impl},
             "roofline": {"kernel": "lss_splat_fwd", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,

@@ -1,4 +1,4 @@
-"""ctypes binding of ``liblss_hip.so`` (the C ABI of ``include/lss_hip.h``).
+"""ctypes binding of ``liblss_hip.so`` (the C ABI of ``include/lss_hip.h`` and ``include/lss_convs.h``).
 
 The library is built in-tree by ``__graft_entry__.build()`` (or
 ``python -m lss_carla_amd.build``). There is no fallback: if the library is
@@ -52,6 +52,10 @@ SIGNATURES = {
     "lss_bev_rows": (ctypes.c_int, [_p, _i32, _p, _DIMS, _GRID, _p, _p]),
     "lss_splat_bwd": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p, _i32, _DIMS, _GRID, _p, _i32, _p]),
     "lss_splat_bwd_lifted": (ctypes.c_int, [_p, _i32, _i32, _p, _i32, _DIMS, _GRID, _p, _p]),
+    # include/lss_convs.h (conv-stack kernels, same library)
+    "lss_dwconv_fwd": (ctypes.c_int, [_p, _i32, _p] + [_i32] * 10 + [_p, _p]),
+    "lss_dwconv_bwd_data": (ctypes.c_int, [_p, _i32, _p] + [_i32] * 10 + [_p, _p]),
+    "lss_dwconv_bwd_weight": (ctypes.c_int, [_p, _p, _i32] + [_i32] * 11 + [_p, _p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -1,0 +1,336 @@
+// lss_convs.hip -- gfx950 kernels for the conv stack in front of the Lift-Splat hot path: the
+// depthwise convolutions of CamEncode's EfficientNet-B0 trunk (src/models.py:43, 63-84; 16 MBConv
+// blocks, 3x3 / 5x5, stride 1 / 2, TF "same" padding). MIOpen has no bf16 NCHW depthwise solver and
+// falls back to naive kernels (≈5 ms of a 27 ms training step at config 3).
+//
+// NCHW planes, fp32 accumulation, activations fp32 or bf16, weights fp32 (the parameter itself: no
+// per-step cast, and the weight gradient stays fp32).
+//
+// Forward / stride-1 backward-data: a thread owns a strip of TH output rows of one column; lanes run
+// along the row, so every input-row load instruction of a wave is contiguous, and each input row
+// loaded into registers feeds every output of the strip it overlaps. Index math is 32-bit (element
+// counts are checked < 2^31); a wave whose lanes share one channel reads the weights with scalar
+// loads. Stride-1 backward-data is the
+// forward correlation with the kernel flipped and the padding mirrored. Stride-2 backward-data: a
+// thread per 2 x 4 input elements with compile-time tap offsets. Backward-weight: a block per (channel, group
+// of images) accumulates the K*K tap sums of its elements in registers, reduces them over the block
+// in a fixed order and writes one partial per group; the caller sums the groups.
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <limits.h>
+#include <stdint.h>
+
+#include "lss_convs.h"
+
+namespace {
+
+using bf16 = __hip_bfloat16;
+constexpr int kBlock = 256;
+constexpr int kWave = 64;
+// output tile per thread (rows x columns)
+template <int S> struct Tile { static constexpr int TH = S == 1 ? 8 : 4, TW = S == 1 ? 4 : 2; };
+
+__device__ __forceinline__ float ld(const float* p) { return *p; }
+__device__ __forceinline__ float ld(const bf16* p) { return __bfloat162float(*p); }
+__device__ __forceinline__ void st(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st(bf16* p, float v) { *p = __float2bfloat16(v); }
+
+struct DwGeo {
+    int C, Hi, Wi, Ho, Wo, pt, pl, nplanes;  // input (Hi, Wi) -> output (Ho, Wo); nplanes = N * C
+};
+
+// Weights of channel c for a wave: when every lane of the wave works on the same channel (planes
+// of >= 64 outputs per row strip), the channel index is wave-uniform and the weights come in with
+// scalar loads (SGPR operands of the FMAs); otherwise per lane.
+template <int K, typename F>
+__device__ __forceinline__ void with_weights(const float* __restrict__ w, int c, bool flip, F&& body) {
+    const int cu = __builtin_amdgcn_readfirstlane(c);
+    if (__ballot(c != cu) == 0) {
+        const float* wc = w + (size_t)cu * K * K;
+        float wk[K * K];
+#pragma unroll
+        for (int i = 0; i < K * K; ++i) wk[i] = wc[flip ? K * K - 1 - i : i];
+        body(wk);
+    } else {
+        const float* wc = w + (size_t)c * K * K;
+        float wk[K * K];
+#pragma unroll
+        for (int i = 0; i < K * K; ++i) wk[i] = wc[flip ? K * K - 1 - i : i];
+        body(wk);
+    }
+}
+
+// y[p][oh][ow] = sum_{kh, kw} x[p][oh*S - pt + kh][ow*S - pl + kw] * w[c][kh][kw] (zero outside x);
+// flip: w[c][K-1-kh][K-1-kw] (stride-1 backward-data). Thread = (plane, TH x TW output tile): each
+// input row segment it loads ((TW-1)*S + K values) feeds every output of the tile under it.
+template <int K, int S, int TH, int TW, typename T>
+__global__ __launch_bounds__(kBlock) void k_dw_fwd(const T* __restrict__ x, const float* __restrict__ w, DwGeo g,
+                                                   int flip, T* __restrict__ y) {
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    const int ncol = (g.Wo + TW - 1) / TW, nrow = (g.Ho + TH - 1) / TH;
+    const int per_plane = nrow * ncol;
+    const bool live = t < g.nplanes * per_plane;
+    const int plane = live ? t / per_plane : 0;
+    const int rem = t - plane * per_plane;
+    const int tr = rem / ncol, tc = rem - tr * ncol;
+    const int c = plane % g.C;
+    const int oh0 = tr * TH, ow0 = tc * TW;
+    const int ih0 = oh0 * S - g.pt, iw0 = ow0 * S - g.pl;
+    const T* xp = x + (size_t)plane * g.Hi * g.Wi;
+    with_weights<K>(w, c, flip != 0, [&](const float* wk) {
+        if (!live) return;
+        float acc[TH][TW];
+#pragma unroll
+        for (int i = 0; i < TH; ++i)
+#pragma unroll
+            for (int j = 0; j < TW; ++j) acc[i][j] = 0.f;
+        constexpr int R = (TH - 1) * S + K, CW = (TW - 1) * S + K;
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) {
+            const int ih = ih0 + rr;
+            const bool row_ok = ih >= 0 && ih < g.Hi;
+            float v[CW];
+#pragma unroll
+            for (int q = 0; q < CW; ++q) {
+                const int iw = iw0 + q;
+                v[q] = (row_ok && iw >= 0 && iw < g.Wi) ? ld(xp + ih * g.Wi + iw) : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < TH; ++i) {
+                const int kh = rr - i * S;
+                if (kh >= 0 && kh < K) {
+#pragma unroll
+                    for (int j = 0; j < TW; ++j)
+#pragma unroll
+                        for (int kw = 0; kw < K; ++kw) acc[i][j] = fmaf(v[j * S + kw], wk[kh * K + kw], acc[i][j]);
+                }
+            }
+        }
+        T* yp = y + (size_t)plane * g.Ho * g.Wo;
+#pragma unroll
+        for (int i = 0; i < TH; ++i)
+#pragma unroll
+            for (int j = 0; j < TW; ++j)
+                if (oh0 + i < g.Ho && ow0 + j < g.Wo) st(yp + (oh0 + i) * g.Wo + ow0 + j, acc[i][j]);
+    });
+}
+
+// Stride-2 backward-data. Thread = 2 rows x 4 columns of dx: ih = 2m + a, iw = 4j + b. With
+// pt = 2 PT2 + PT1, pl = 2 PL2 + PL1 (PT1, PL1 template parameters) the taps that reach dx[ih][iw]
+// have kh = a + PT1 (mod 2), kw = b + PL1 (mod 2), at dy[m + PT2 + (a + PT1 - kh) / 2]
+// [2j + PL2 + (b + PL1 - kw) / 2]: every offset is a compile-time constant, so the thread loads one
+// small dy window and runs straight-line FMAs. g describes the forward conv.
+template <int K, int PT1, int PL1, typename T>
+__global__ __launch_bounds__(kBlock) void k_dw_bwd_data_s2(const T* __restrict__ dy, const float* __restrict__ w,
+                                                           DwGeo g, T* __restrict__ dx) {
+    constexpr int H0 = -(K - 1) / 2, H1 = 1;      // dy row offsets reached (relative to m + PT2)
+    constexpr int W0 = -(K - 1) / 2, W1 = 2;      // dy column offsets reached (relative to 2j + PL2)
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    const int ncol = (g.Wi + 3) / 4, nrow = (g.Hi + 1) / 2;
+    const int per_plane = nrow * ncol;
+    const bool live = t < g.nplanes * per_plane;
+    const int plane = live ? t / per_plane : 0;
+    const int rem = t - plane * per_plane;
+    const int m = rem / ncol, j = rem - m * ncol;
+    const int c = plane % g.C;
+    const int hb = m + (g.pt >> 1), wb = 2 * j + (g.pl >> 1);
+    const T* dp = dy + (size_t)plane * g.Ho * g.Wo;
+    with_weights<K>(w, c, false, [&](const float* wk) {
+        if (!live) return;
+        float win[H1 - H0 + 1][W1 - W0 + 1];
+#pragma unroll
+        for (int r = H0; r <= H1; ++r) {
+            const int oh = hb + r;
+#pragma unroll
+            for (int q = W0; q <= W1; ++q) {
+                const int ow = wb + q;
+                win[r - H0][q - W0] = (oh >= 0 && oh < g.Ho && ow >= 0 && ow < g.Wo) ? ld(dp + oh * g.Wo + ow) : 0.f;
+            }
+        }
+        T* xp = dx + (size_t)plane * g.Hi * g.Wi;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                float acc = 0.f;
+#pragma unroll
+                for (int kh = (a + PT1) & 1; kh < K; kh += 2)
+#pragma unroll
+                    for (int kw = (b + PL1) & 1; kw < K; kw += 2)
+                        acc = fmaf(win[(a + PT1 - kh) / 2 - H0][(b + PL1 - kw) / 2 - W0], wk[kh * K + kw], acc);
+                const int ih = 2 * m + a, iw = 4 * j + b;
+                if (ih < g.Hi && iw < g.Wi) st(xp + ih * g.Wi + iw, acc);
+            }
+        }
+    });
+}
+
+// Backward-weight partials: block (group q, channel c) sums, over images n in its group and every
+// output element, dy[n][c][oh][ow] * x[n][c][oh*S - pt + kh][ow*S - pl + kw] for each tap; a thread
+// takes TH x TW output tiles of the group's flat (image, tile) space.
+// partial[(c * ngroups + q) * K*K + tap]; fixed reduction order (wave shuffles, then waves in order).
+template <int K, int S, int TH, int TW, typename T>
+__global__ __launch_bounds__(kBlock) void k_dw_bwd_weight(const T* __restrict__ x, const T* __restrict__ dy, DwGeo g,
+                                                          int nimg, int ngroups, float* __restrict__ partial) {
+    __shared__ float s_red[kBlock / kWave][K * K];
+    const int c = blockIdx.x % g.C, q = blockIdx.x / g.C;
+    const int n0 = (int)((long)nimg * q / ngroups), n1 = (int)((long)nimg * (q + 1) / ngroups);
+    const int ncol = (g.Wo + TW - 1) / TW, nrow = (g.Ho + TH - 1) / TH;
+    const int per_img = nrow * ncol;
+    const int count = per_img * (n1 - n0);
+    float acc[K * K];
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
+    constexpr int R = (TH - 1) * S + K, CW = (TW - 1) * S + K;
+    for (int e = threadIdx.x; e < count; e += kBlock) {
+        const int nl = e / per_img;
+        const int rem = e - nl * per_img;
+        const int tr = rem / ncol, tc = rem - tr * ncol;
+        const int plane = (n0 + nl) * g.C + c;
+        const T* xp = x + (size_t)plane * g.Hi * g.Wi;
+        const T* dp = dy + (size_t)plane * g.Ho * g.Wo;
+        const int oh0 = tr * TH, ow0 = tc * TW;
+        float d[TH][TW];
+#pragma unroll
+        for (int i = 0; i < TH; ++i)
+#pragma unroll
+            for (int j = 0; j < TW; ++j)
+                d[i][j] = (oh0 + i < g.Ho && ow0 + j < g.Wo) ? ld(dp + (oh0 + i) * g.Wo + ow0 + j) : 0.f;
+        const int ih0 = oh0 * S - g.pt, iw0 = ow0 * S - g.pl;
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) {
+            const int ih = ih0 + rr;
+            const bool row_ok = ih >= 0 && ih < g.Hi;
+            float v[CW];
+#pragma unroll
+            for (int qq = 0; qq < CW; ++qq) {
+                const int iw = iw0 + qq;
+                v[qq] = (row_ok && iw >= 0 && iw < g.Wi) ? ld(xp + ih * g.Wi + iw) : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < TH; ++i) {
+                const int kh = rr - i * S;
+                if (kh >= 0 && kh < K) {
+#pragma unroll
+                    for (int j = 0; j < TW; ++j)
+#pragma unroll
+                        for (int kw = 0; kw < K; ++kw)
+                            acc[kh * K + kw] = fmaf(d[i][j], v[j * S + kw], acc[kh * K + kw]);
+                }
+            }
+        }
+    }
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) {
+        float v = acc[i];
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+        if (lane == 0) s_red[wave][i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < K * K) {
+        float s = 0.f;
+#pragma unroll
+        for (int jw = 0; jw < kBlock / kWave; ++jw) s += s_red[jw][threadIdx.x];
+        partial[((size_t)c * ngroups + q) * K * K + threadIdx.x] = s;
+    }
+}
+
+inline int blocks_for(long n) { return (int)((n + kBlock - 1) / kBlock); }
+
+inline int launch_status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+inline bool geo_ok(int N, int C, int Hi, int Wi, int K, int S, int Ho, int Wo) {
+    return N > 0 && C > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && (K == 3 || K == 5) && (S == 1 || S == 2) &&
+           (long)N * C * Hi * Wi < INT_MAX && (long)N * C * Ho * Wo < INT_MAX;
+}
+
+// dispatch over (K, S, T)
+template <template <int, int, typename> class F, typename... A>
+int dispatch_kst(int K, int S, int dtype, A... a) {
+    if (dtype == LSS_CONV_F32) {
+        if (K == 3 && S == 1) return F<3, 1, float>::run(a...);
+        if (K == 3 && S == 2) return F<3, 2, float>::run(a...);
+        if (K == 5 && S == 1) return F<5, 1, float>::run(a...);
+        if (K == 5 && S == 2) return F<5, 2, float>::run(a...);
+    } else if (dtype == LSS_CONV_BF16) {
+        if (K == 3 && S == 1) return F<3, 1, bf16>::run(a...);
+        if (K == 3 && S == 2) return F<3, 2, bf16>::run(a...);
+        if (K == 5 && S == 1) return F<5, 1, bf16>::run(a...);
+        if (K == 5 && S == 2) return F<5, 2, bf16>::run(a...);
+    }
+    return LSS_CONV_EINVAL;
+}
+
+template <int K, int S, typename T>
+struct Fwd {
+    static int run(const void* x, const float* w, DwGeo g, int flip, void* y, hipStream_t s) {
+        constexpr int TH = Tile<S>::TH, TW = Tile<S>::TW;
+        const long n = (long)g.nplanes * ((g.Ho + TH - 1) / TH) * ((g.Wo + TW - 1) / TW);
+        hipLaunchKernelGGL((k_dw_fwd<K, S, TH, TW, T>), dim3(blocks_for(n)), dim3(kBlock), 0, s, (const T*)x, w, g,
+                           flip, (T*)y);
+        return launch_status();
+    }
+};
+
+template <int K, int S, typename T>
+struct BwdData {
+    static int run(const void* dy, const float* w, DwGeo g, void* dx, hipStream_t s) {
+        if (S == 1) {  // the forward correlation with the kernel flipped, padding mirrored
+            DwGeo t{g.C, g.Ho, g.Wo, g.Hi, g.Wi, K - 1 - g.pt, K - 1 - g.pl, g.nplanes};
+            return Fwd<K, 1, T>::run(dy, w, t, 1, dx, s);
+        }
+        const dim3 gr(blocks_for((long)g.nplanes * ((g.Hi + 1) / 2) * ((g.Wi + 3) / 4))), bl(kBlock);
+        const int par = ((g.pt & 1) << 1) | (g.pl & 1);
+        if (par == 0) hipLaunchKernelGGL((k_dw_bwd_data_s2<K, 0, 0, T>), gr, bl, 0, s, (const T*)dy, w, g, (T*)dx);
+        else if (par == 1) hipLaunchKernelGGL((k_dw_bwd_data_s2<K, 0, 1, T>), gr, bl, 0, s, (const T*)dy, w, g, (T*)dx);
+        else if (par == 2) hipLaunchKernelGGL((k_dw_bwd_data_s2<K, 1, 0, T>), gr, bl, 0, s, (const T*)dy, w, g, (T*)dx);
+        else hipLaunchKernelGGL((k_dw_bwd_data_s2<K, 1, 1, T>), gr, bl, 0, s, (const T*)dy, w, g, (T*)dx);
+        return launch_status();
+    }
+};
+
+template <int K, int S, typename T>
+struct BwdWeight {
+    static int run(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, hipStream_t s) {
+        hipLaunchKernelGGL((k_dw_bwd_weight<K, S, 4, S == 1 ? 4 : 2, T>), dim3(g.C * ngroups), dim3(kBlock), 0, s,
+                           (const T*)x, (const T*)dy, g, nimg, ngroups, partial);
+        return launch_status();
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int lss_dwconv_fwd(const void* x, int32_t dtype, const float* w, int32_t N, int32_t C, int32_t Hi, int32_t Wi,
+                   int32_t K, int32_t stride, int32_t pad_top, int32_t pad_left, int32_t Ho, int32_t Wo, void* y,
+                   void* stream) {
+    if (!x || !w || !y || !geo_ok(N, C, Hi, Wi, K, stride, Ho, Wo)) return LSS_CONV_EINVAL;
+    const DwGeo g{C, Hi, Wi, Ho, Wo, pad_top, pad_left, N * C};
+    return dispatch_kst<Fwd>(K, stride, dtype, x, w, g, 0, y, (hipStream_t)stream);
+}
+
+int lss_dwconv_bwd_data(const void* dy, int32_t dtype, const float* w, int32_t N, int32_t C, int32_t Hi, int32_t Wi,
+                        int32_t K, int32_t stride, int32_t pad_top, int32_t pad_left, int32_t Ho, int32_t Wo, void* dx,
+                        void* stream) {
+    if (!dy || !w || !dx || !geo_ok(N, C, Hi, Wi, K, stride, Ho, Wo)) return LSS_CONV_EINVAL;
+    const DwGeo g{C, Hi, Wi, Ho, Wo, pad_top, pad_left, N * C};
+    return dispatch_kst<BwdData>(K, stride, dtype, dy, w, g, dx, (hipStream_t)stream);
+}
+
+int lss_dwconv_bwd_weight(const void* x, const void* dy, int32_t dtype, int32_t N, int32_t C, int32_t Hi, int32_t Wi,
+                          int32_t K, int32_t stride, int32_t pad_top, int32_t pad_left, int32_t Ho, int32_t Wo,
+                          int32_t ngroups, float* partial, void* stream) {
+    if (!x || !dy || !partial || ngroups <= 0 || ngroups > N || !geo_ok(N, C, Hi, Wi, K, stride, Ho, Wo))
+        return LSS_CONV_EINVAL;
+    const DwGeo g{C, Hi, Wi, Ho, Wo, pad_top, pad_left, N * C};
+    return dispatch_kst<BwdWeight>(K, stride, dtype, x, dy, g, (int)N, (int)ngroups, partial, (hipStream_t)stream);
+}
+
+}  // extern "C"

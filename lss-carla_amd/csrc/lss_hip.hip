@@ -482,7 +482,6 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
     const int o = wave * 32 + r;
     const bf16* wrow = weight + (size_t)min(o, O - 1) * K + 8 * h;
     f32x16 acc = {};
-#pragma unroll 4
     for (int k0 = 0; k0 < K; k0 += 16) {
         // A[row o][k = k0 + 8h + j] (weight row), B[k = k0 + 8h + j][col p = r] (staged pixel r)
         bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + k0);
@@ -1099,7 +1098,7 @@ __global__ __launch_bounds__(kBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const 
         const int zb = zgi * 8 + x;
         if (zb >= nzero_blocks) return;
         const int u = (zb * (kBlock / kWave) + wave) * kZeroUnits;
-        const int zslot = nchunk_blocks * (kBlock / kWave) + zb * (kBlock / kWave) + wave;
+        [[maybe_unused]] const int zslot = nchunk_blocks * (kBlock / kWave) + zb * (kBlock / kWave) + wave;
         LSS_STAMP(zslot, 0);
         if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, g, out, lane);
         LSS_STAMP(zslot, 3);

@@ -13,7 +13,8 @@ checkpoint of the reference loads into it. Weights are randomly initialised
 Architecture facts restated from the published B0 definition: width = depth =
 1.0, image_size 224, batch-norm momentum 0.01 / eps 1e-3, drop-connect 0.2,
 SE ratio 0.25, TF "static same" padding computed for 224x224 inputs, swish.
-Runs as stock PyTorch-ROCm convolutions (MIOpen) -- MFMA via the library.
+Runs as stock PyTorch-ROCm convolutions (MIOpen, MFMA via the library), except the depthwise
+convolutions, which run on this package's HIP kernels (include/lss_convs.h) on the GPU.
 """
 from __future__ import annotations
 
@@ -101,6 +102,68 @@ class _NativeConv2d(torch.autograd.Function):
         return gx, gw, None, None, None, None
 
 
+class _HipDepthwise(torch.autograd.Function):
+    """Depthwise conv (groups = C) on the lss_dwconv_* kernels of include/lss_convs.h.
+
+    Activations in the autocast dtype (as the reference's ``nn.Conv2d`` under autocast), the fp32
+    weight parameter read as is, fp32 accumulation; the weight gradient is fp32 (summed per image
+    group on the device, then over the groups in a fixed order).
+    """
+
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, pads: Tuple[int, int, int, int]):
+        from . import _lib
+        lib = _lib.load()
+        if torch.is_autocast_enabled("cuda"):
+            x = x.to(torch.get_autocast_dtype("cuda"))
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        x = x.contiguous()
+        N, C, Hi, Wi = x.shape
+        K = weight.shape[-1]
+        pl, pr, pt, pb = pads
+        Ho, Wo = (Hi + pt + pb - K) // stride + 1, (Wi + pl + pr - K) // stride + 1
+        w = weight.detach().float().reshape(C, K * K).contiguous()
+        y = torch.empty(N, C, Ho, Wo, device=x.device, dtype=x.dtype)
+        _lib.check(lib.lss_dwconv_fwd(_lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(w), N, C, Hi, Wi, K, stride,
+                                      pt, pl, Ho, Wo, _lib.ptr(y), _lib.stream_handle(x.device)), "lss_dwconv_fwd")
+        ctx.save_for_backward(x, w)
+        ctx.conf = (stride, pt, pl, Ho, Wo, weight.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+        lib = _lib.load()
+        x, w = ctx.saved_tensors
+        stride, pt, pl, Ho, Wo, wdtype = ctx.conf
+        N, C, Hi, Wi = x.shape
+        K = int(round((w.shape[1]) ** 0.5))
+        dy = dy.to(x.dtype).contiguous()
+        st = _lib.stream_handle(x.device)
+        code = _lib.dtype_code(x.dtype)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _lib.check(lib.lss_dwconv_bwd_data(_lib.ptr(dy), code, _lib.ptr(w), N, C, Hi, Wi, K, stride, pt, pl, Ho,
+                                               Wo, _lib.ptr(dx), st), "lss_dwconv_bwd_data")
+        if ctx.needs_input_grad[1]:
+            groups = max(1, min(N, (N * Ho * Wo) // 8192))
+            part = torch.empty(C, groups, K * K, device=x.device, dtype=torch.float32)
+            _lib.check(lib.lss_dwconv_bwd_weight(_lib.ptr(x), _lib.ptr(dy), code, N, C, Hi, Wi, K, stride, pt, pl,
+                                                 Ho, Wo, groups, _lib.ptr(part), st), "lss_dwconv_bwd_weight")
+            dw = part.sum(1).view(C, 1, K, K).to(wdtype)
+        return dx, dw, None, None
+
+
+def depthwise_same_pads(conv: "Conv2dStaticSamePadding") -> Tuple[int, int, int, int]:
+    """(left, right, top, bottom) padding of a static-same conv, whether it pads itself or via ZeroPad2d."""
+    if isinstance(conv.static_padding, nn.ZeroPad2d):
+        return tuple(conv.static_padding.padding)
+    ph, pw = conv.padding
+    return (pw, pw, ph, ph)
+
+
 def drop_connect(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
     """Per-sample stochastic depth (efficientnet_pytorch ``drop_connect``)."""
     if not training or not p:
@@ -127,17 +190,20 @@ class MBConvBlock(nn.Module):
         self._se_expand = Conv2dStaticSamePadding(sq, mid, 1, image_size=(1, 1))
         self._project_conv = Conv2dStaticSamePadding(mid, out_f, 1, bias=False, image_size=image_size)
         self._bn2 = nn.BatchNorm2d(out_f, momentum=BN_MOMENTUM, eps=BN_EPS)
-        self.depthwise_fp32 = False  # run the depthwise conv outside autocast (MIOpen solver choice)
-        self.depthwise_native = False  # run the depthwise conv on PyTorch's native kernels (not MIOpen)
+        # depthwise conv backend on the GPU: 'hip' (lss_dwconv_* kernels), 'miopen', 'native' (PyTorch's
+        # own kernels), 'fp32' (MIOpen outside autocast)
+        self.depthwise_impl = "hip"
 
     def forward(self, inputs: torch.Tensor, drop_connect_rate=None) -> torch.Tensor:
         x = inputs
         if self.expand != 1:
             x = F.silu(self._bn0(self._expand_conv(x)))
-        if self.depthwise_native and x.is_cuda:
-            dw = self._depthwise_conv
+        dw = self._depthwise_conv
+        if self.depthwise_impl == "hip" and x.is_cuda:
+            x = _HipDepthwise.apply(x, dw.weight, dw.stride[0], depthwise_same_pads(dw))
+        elif self.depthwise_impl == "native" and x.is_cuda:
             x = _NativeConv2d.apply(dw.static_padding(x), dw.weight, dw.stride, dw.padding, dw.dilation, dw.groups)
-        elif self.depthwise_fp32 and x.is_cuda and torch.is_autocast_enabled("cuda"):
+        elif self.depthwise_impl == "fp32" and x.is_cuda and torch.is_autocast_enabled("cuda"):
             with torch.autocast("cuda", enabled=False):
                 x = self._depthwise_conv(x.float())
         else:
@@ -154,16 +220,13 @@ class MBConvBlock(nn.Module):
         return x
 
 
-def set_depthwise_fp32(module: nn.Module, flag: bool = True) -> None:
+def set_depthwise_impl(module: nn.Module, impl: str) -> None:
+    """Depthwise-conv backend of every MBConv block under `module`: 'hip', 'miopen', 'native' or 'fp32'."""
+    if impl not in ("hip", "miopen", "native", "fp32"):
+        raise ValueError(f"unknown depthwise implementation {impl!r}")
     for m in module.modules():
         if isinstance(m, MBConvBlock):
-            m.depthwise_fp32 = flag
-
-
-def set_depthwise_native(module: nn.Module, flag: bool = True) -> None:
-    for m in module.modules():
-        if isinstance(m, MBConvBlock):
-            m.depthwise_native = flag
+            m.depthwise_impl = impl
 
 
 class _NativeBatchNorm2d(nn.BatchNorm2d):

@@ -12,11 +12,11 @@ import lss_carla_amd as L
 from lss_carla_amd import _lib, ops
 from lss_carla_amd import synthetic as syn
 
-HEADER = os.path.join(REPO, "include", "lss_hip.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("lss_hip.h", "lss_convs.h")]
 
 
 def _declared():
-    text = open(HEADER).read()
+    text = "".join(open(h).read() for h in HEADERS)
     return set(re.findall(r"^\s*(?:int|int32_t|size_t|const char\*)\s+(lss_\w+)\s*\(", text, re.M))
 
 
