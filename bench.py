@@ -3,8 +3,10 @@
 Workload (config 3 of BASELINE.json): B=8 samples x 6 cameras x 128x352 per GPU,
 D=41, 200x200 BEV, bf16 autocast, full training step of train_simbev.py:229-248
 (forward, SimpleLoss, backward, clip_grad_norm_(5.0), Adam step). Synthetic
-SimBEV-shaped inputs, random-init weights. For N>1: torchrun,
-one rank per GPU, DDP gradient all-reduce over RCCL, B=8 per rank (weak scaling).
+SimBEV-shaped inputs, random-init weights. The step is replayed as
+two HIP graphs (train_step.TrainStep: fwd+loss+bwd | clip+Adam) with one RCCL
+all-reduce of the flat fp32 gradient between them; --graph 0 runs it eagerly (DDP).
+For N>1: torchrun, one rank per GPU, B=8 per rank (weak scaling).
 
 Also reported on the same JSON line:
   roofline      the fused lift+splat forward kernel (lss_splat_fwd): algorithmic
@@ -54,9 +56,16 @@ def parse():
     ap.add_argument("--dw-impl", default="hip", choices=["hip", "miopen", "native", "fp32"],
                     help="depthwise convs of the trunk: HIP kernels, MIOpen, PyTorch native, MIOpen in fp32")
     ap.add_argument("--miopen-find", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
-    ap.add_argument("--bn-native", default="", help="BatchNorm on native kernels: '', 'trunk', 'bev', 'all'")
+    ap.add_argument("--hip-bn", type=int, default=1, help="BatchNorm + activation on the lss_bn_* kernels")
+    ap.add_argument("--bn-native", default="", help="with --hip-bn 0: BatchNorm on PyTorch's native kernels: "
+                                                    "'', 'trunk', 'bev', 'all'")
     ap.add_argument("--inverse", default="host", choices=["host", "device"])
     ap.add_argument("--fuse-depthnet", type=int, default=1, help="depthnet 1x1 conv inside the lift kernel (MFMA)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="replay the step as two HIP graphs (fwd+bwd, clip+Adam) with the gradient all-reduce "
+                         "between them; 0 = eager (DDP for N>1)")
+    ap.add_argument("--profile-steps", type=int, default=5,
+                    help="with --graph 1: eager steps after the timed region on which the splat kernel is timed")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "splat_fwd_traffic.json"))
@@ -98,6 +107,8 @@ def build_model(args, dev, cfg, gc, dac):
         model.bevencode.to(memory_format=torch.channels_last)
     if args.trunk_channels_last:
         model.camencode.to(memory_format=torch.channels_last)
+    from lss_carla_amd import norm
+    norm.USE_HIP_BN = bool(args.hip_bn)
     from lss_carla_amd.efficientnet import set_depthwise_impl
     set_depthwise_impl(model.camencode.trunk, args.dw_impl)
     if args.bn_native:
@@ -169,16 +180,25 @@ def main():
     world, rank, dev = setup_dist()
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     from lss_carla_amd import ops, parallel, synthetic as syn
+    from lss_carla_amd.train_step import TrainStep
     import lss_carla_amd as L
 
     cfg, gc, dac = syn.config_confs(args.config)
     B, N, fd = args.batch, cfg["N"], cfg["final_dim"]
     torch.manual_seed(1234 + rank)
+    if args.graph:
+        args.inverse = "device"  # inverse='host' is a device->host round trip: not capturable
     model = build_model(args, dev, cfg, gc, dac)
-    ddp = parallel.make_data_parallel(model, dev) if world > 1 else model
+    grads = None
+    if args.graph:
+        parallel.broadcast_state(model)  # identical replicas, as DDP's constructor ensures
+        grads = parallel.FlatGradients(model, dev)
+        ddp = model
+    else:
+        ddp = parallel.make_data_parallel(model, dev) if world > 1 else model
+    params = [p for p in model.parameters() if p.requires_grad]
     loss_fn = L.SimpleLoss(2.13).to(dev)
-    opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-7,
-                           fused=True)
+    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-7, fused=True, capturable=bool(args.graph))
     rig = {k: v.to(dev) for k, v in syn.make_rig(B, N, fd, seed=rank).items()}
     imgs = syn.make_images(B, N, fd, seed=rank).to(dev)
     if args.trunk_channels_last:
@@ -187,36 +207,46 @@ def main():
     labels = syn.make_labels(B, X, Y, seed=rank).to(dev)
     amp_dtype = torch.bfloat16 if args.dtype == "bf16" else None
 
-    def step():
-        opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp_dtype is not None):
-            preds = ddp(imgs, rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"])
-        loss = loss_fn(preds.float(), labels)
-        loss.backward()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 5.0)
-        opt.step()
-        return loss
-
+    train = TrainStep(ddp, (imgs, rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"]),
+                      labels, loss_fn, opt, params, grads=grads, amp_dtype=amp_dtype, max_grad_norm=5.0)
     t_w = time.perf_counter()
-    for i in range(args.warmup):
-        step()
+
+    def first(i):
         if i == 0:
             torch.cuda.synchronize()
             log(f"[rank {rank}] first step done in {time.perf_counter() - t_w:.1f} s")
-    torch.cuda.synchronize()
-    log(f"[rank {rank}] warmup {args.warmup} steps in {time.perf_counter() - t_w:.1f} s")
 
-    ops.SPLAT_PROFILE.reset(True)
+    if args.graph:
+        # eager warm-up on a side stream (MIOpen find, optimizer state), capture, 2 untimed replays
+        train.capture(warmup=max(args.warmup, 2), on_warmup=first)
+        for _ in range(2):
+            train()
+    else:
+        for i in range(args.warmup):
+            train()
+            first(i)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] warmup {args.warmup} steps in {time.perf_counter() - t_w:.1f} s"
+        + (" (incl. graph capture)" if args.graph else ""))
+
+    ops.SPLAT_PROFILE.reset(not args.graph)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = train()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if args.graph:
+        # a captured launch cannot carry kernel-stamped events: time lss_splat_fwd on eager steps
+        # (same inputs, same kernel) right after the timed replays
+        ops.SPLAT_PROFILE.reset(True)
+        for _ in range(args.profile_steps):
+            train.eager()
+        torch.cuda.synchronize()
     ops.SPLAT_PROFILE.enabled = False
     splat_ms = ops.SPLAT_PROFILE.avg_ms()
     ops.SPLAT_PROFILE.release()
@@ -253,7 +283,8 @@ def main():
                                    "full train step (fwd+loss+bwd+clip+Adam)",
                        "global_batch": world * B, "parallelism": f"dp{world}", "bev_layout": args.bev_layout,
                        "inverse": args.inverse, "fuse_depthnet": bool(args.fuse_depthnet),
-                       "depthwise": args.dw_impl},
+                       "depthwise": args.dw_impl, "batchnorm": "hip" if args.hip_bn else "miopen",
+                       "step": "hipgraph" if args.graph else "eager"},
             "roofline": {"kernel": "lss_splat_fwd", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,

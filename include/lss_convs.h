@@ -21,6 +21,8 @@ extern "C" {
 #endif
 
 enum { LSS_CONV_F32 = 0, LSS_CONV_BF16 = 1 };
+enum { LSS_CONV_NCHW = 0, LSS_CONV_NHWC = 1 };
+enum { LSS_ACT_NONE = 0, LSS_ACT_RELU = 1, LSS_ACT_SWISH = 2 };
 enum { LSS_CONV_EINVAL = -1 };
 
 /* y (N, C, Ho, Wo) = depthwise_conv(x (N, C, Hi, Wi), w) */
@@ -38,6 +40,46 @@ int lss_dwconv_bwd_data(const void* dy, int32_t dtype, const float* w, int32_t N
 int lss_dwconv_bwd_weight(const void* x, const void* dy, int32_t dtype, int32_t N, int32_t C, int32_t Hi, int32_t Wi,
                           int32_t K, int32_t stride, int32_t pad_top, int32_t pad_left, int32_t Ho, int32_t Wo,
                           int32_t ngroups, float* partial, void* stream);
+
+/* Training-mode batch norm fused with an activation (and, for ReLU, a residual add), for
+ * nn.BatchNorm2d followed by swish (EfficientNet-B0, src/models.py:68 and the MBConv blocks) or
+ * ReLU (CamEncode.up1, BevEncode, src/models.py:15-34, 92-130):
+ *   y = act(x * scale_c + shift_c [+ residual]),  scale_c = gamma_c / sqrt(var_c + eps),
+ *   shift_c = beta_c - mean_c * scale_c, mean / biased var over (N, H, W); running_mean / running_var
+ *   (nullable) updated with `momentum` and the unbiased variance, as nn.BatchNorm2d does.
+ * x, residual, y: (N, C, H, W) with HW = H*W, NCHW or channels-last (LSS_CONV_NHWC: C a multiple
+ * of 8 with 256 % (C / 8) == 0), element type dtype; gamma, beta and every statistic fp32.
+ * partial: (C, ngroups, 2) fp32 scratch, ngroups from lss_bn_groups. save_mean, save_rstd, scale,
+ * shift are the four rows of one (4, C) fp32 array (outputs kept for lss_bn_bwd). */
+int lss_bn_groups(int32_t N, int32_t C, int32_t HW, int32_t layout);
+int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layout, int32_t N, int32_t C, int32_t HW,
+               const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
+               float* running_var, int32_t act, int32_t ngroups, float* partial, float* save_mean, float* save_rstd,
+               float* scale, float* shift, void* y, void* stream);
+
+/* Backward of lss_bn_fwd: dx (and dresidual = the gradient of the residual, nullable) of element
+ * type dtype; dgamma, dbeta fp32 (nullable). y is the forward output (needed for ReLU). coef:
+ * (C, 2) fp32 scratch. */
+int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int32_t layout, int32_t N, int32_t C,
+               int32_t HW, const float* scale, const float* shift, const float* save_mean, const float* save_rstd,
+               int32_t act, int32_t ngroups, float* partial, float* coef, float* dgamma, float* dbeta, void* dx,
+               void* dresidual, void* stream);
+
+/* Bilinear upsampling with align_corners=True (nn.Upsample(mode="bilinear", align_corners=True),
+ * src/models.py:19, 109) fused with Up's channel concatenation (torch.cat([x2, x1], 1),
+ * src/models.py:33). All tensors channels-last bf16, 16-byte aligned, C1 and C2 multiples of 8,
+ * upsampling only (Ho >= Hi > 1, Wo >= Wi > 1):
+ *   y (N, Ho, Wo, C2 + C1) = cat([skip (N, Ho, Wo, C2), up(x (N, Hi, Wi, C1))]) -- skip may be NULL
+ *   when C2 == 0; the blend is fp32 in PyTorch's order, rounded to bf16 once (the value the bf16
+ *   autocast cast of the reference's fp32 upsample + cat produces). */
+int lss_upsample_cat_fwd(const void* x, const void* skip, int32_t N, int32_t Hi, int32_t Wi, int32_t C1, int32_t C2,
+                         int32_t Ho, int32_t Wo, void* y, void* stream);
+
+/* dx (N, Hi, Wi, C1) bf16 = the upsample's backward applied to channels [C2, C2 + C1) of dy
+ * (N, Ho, Wo, C2 + C1) bf16: a gather (each input element sums its weighted output gradients in
+ * fp32, fixed order), no atomics. The skip's gradient is dy's first C2 channels (a view). */
+int lss_upsample_bwd(const void* dy, int32_t N, int32_t Hi, int32_t Wi, int32_t C1, int32_t C2, int32_t Ho,
+                     int32_t Wo, void* dx, void* stream);
 
 #ifdef __cplusplus
 }

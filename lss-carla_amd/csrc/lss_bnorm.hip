@@ -1,0 +1,660 @@
+// lss_bnorm.hip -- gfx950 training-mode batch norm (+ activation, + residual) for the conv stacks
+// around the Lift-Splat hot path: the EfficientNet-B0 trunk's BN + swish (src/models.py:68 and the
+// MBConv blocks), CamEncode.up1 / BevEncode's BN + ReLU (src/models.py:15-34, 92-130).
+//
+// Activations fp32 or bf16, NCHW or channels-last (NHWC); statistics, affine parameters and all
+// arithmetic fp32. Two launches per direction:
+//   forward  1. per-group shifted sums of x - K_c and (x - K_c)^2 (K_c = the channel's first
+//               element, so the one-pass variance does not cancel);
+//            2. every block folds the group sums of its channel(s) in a fixed order (all blocks
+//               get identical statistics; the first block of a channel also writes the running
+//               statistics and the saved mean / rstd / scale / shift) and writes
+//               y = act(x * scale_c + shift_c [+ residual]).
+//   backward 1. per-group sums of g and g * xhat, g = dy * act'(.) (ReLU from y; swish from the
+//               pre-activation recomputed from x);
+//            2. fold as above (first block writes dgamma, dbeta), dx = scale_c (g - mean g -
+//               xhat mean(g xhat)), d residual = g.
+// NCHW: block = (channel, group of images), the channel is block-uniform (scalar loads / SGPR
+// operands), V consecutive elements per thread. NHWC: block = group of pixels x all channels,
+// 8 consecutive channels per thread, per-channel coefficients staged in LDS.
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <limits.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "lss_convs.h"
+
+namespace {
+
+using bf16 = __hip_bfloat16;
+constexpr int kBlock = 256;
+constexpr int kWave = 64;
+constexpr int kMaxGroupsNhwc = 4096;
+
+__device__ __forceinline__ float ld(const float* p) { return *p; }
+__device__ __forceinline__ float ld(const bf16* p) { return __bfloat162float(*p); }
+
+// V consecutive elements <-> fp32 (V in {1, 4, 8})
+template <int V> __device__ __forceinline__ void ldv(const float* p, float* o) {
+    if constexpr (V == 1) {
+        o[0] = *p;
+    } else {
+#pragma unroll
+        for (int i = 0; i < V; i += 4) {
+            const float4 a = *reinterpret_cast<const float4*>(p + i);
+            o[i] = a.x; o[i + 1] = a.y; o[i + 2] = a.z; o[i + 3] = a.w;
+        }
+    }
+}
+template <int V> __device__ __forceinline__ void ldv(const bf16* p, float* o) {
+    if constexpr (V == 1) {
+        o[0] = __bfloat162float(*p);
+    } else {
+        unsigned w[V / 2];
+        if constexpr (V == 8) {
+            const uint4 u = *reinterpret_cast<const uint4*>(p);
+            w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
+        } else {
+            const uint2 u = *reinterpret_cast<const uint2*>(p);
+            w[0] = u.x; w[1] = u.y;
+        }
+#pragma unroll
+        for (int i = 0; i < V / 2; ++i) {
+            o[2 * i] = __uint_as_float(w[i] << 16);
+            o[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+        }
+    }
+}
+template <int V> __device__ __forceinline__ void stv(float* p, const float* v) {
+    if constexpr (V == 1) {
+        *p = v[0];
+    } else {
+#pragma unroll
+        for (int i = 0; i < V; i += 4) *reinterpret_cast<float4*>(p + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+    }
+}
+template <int V> __device__ __forceinline__ void stv(bf16* p, const float* v) {
+    if constexpr (V == 1) {
+        *p = __float2bfloat16(v[0]);
+    } else {
+        bf16 b[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) b[i] = __float2bfloat16(v[i]);
+        if constexpr (V == 8) *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(b);
+        else *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(b);
+    }
+}
+
+__device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + __expf(-z)); }
+
+__device__ __forceinline__ float act_fwd(float z, int act) {
+    if (act == LSS_ACT_RELU) return fmaxf(z, 0.f);
+    if (act == LSS_ACT_SWISH) return z * sigmoidf(z);
+    return z;
+}
+
+// dy -> g = dy * act'(pre-activation z); ReLU: from the output (y > 0), swish: from z
+__device__ __forceinline__ float grad_pre(float dy, float y, float z, int act) {
+    if (act == LSS_ACT_RELU) return y > 0.f ? dy : 0.f;
+    if (act == LSS_ACT_SWISH) {
+        const float s = sigmoidf(z);
+        return dy * s * (1.f + z * (1.f - s));
+    }
+    return dy;
+}
+
+struct BnGeo {
+    int N, C, HW;
+};
+
+template <typename T>
+__device__ __forceinline__ float first_nchw(const T* x, int c, const BnGeo& g) { return ld(x + (size_t)c * g.HW); }
+
+// sum of a pair over a block, fixed order (wave shuffles, then waves in order); result valid in thread 0
+__device__ __forceinline__ void block_pair_sum(float& a, float& b, float (*s_red)[kBlock / kWave]) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, kWave);
+        b += __shfl_xor(b, o, kWave);
+    }
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    if (lane == 0) {
+        s_red[0][wave] = a;
+        s_red[1][wave] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a = 0.f;
+        b = 0.f;
+#pragma unroll
+        for (int j = 0; j < kBlock / kWave; ++j) {
+            a += s_red[0][j];
+            b += s_red[1][j];
+        }
+    }
+}
+
+// fold G pairs partial[(c * G + q) * 2 + k] (NCHW layout of the partials) with one wave, lanes over
+// groups, fixed order; returns the sums in every lane of wave 0 (others: undefined)
+__device__ __forceinline__ void fold_groups(const float* __restrict__ partial, int c, int G, float& a, float& b) {
+    a = 0.f;
+    b = 0.f;
+    for (int q = threadIdx.x; q < G; q += kWave) {
+        a += partial[((size_t)c * G + q) * 2];
+        b += partial[((size_t)c * G + q) * 2 + 1];
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, kWave);
+        b += __shfl_xor(b, o, kWave);
+    }
+}
+
+// ============================================================================= NCHW
+// block (c, q): images [N q / G, N (q+1) / G) of channel c; V elements per thread (HW % V == 0)
+template <int V, typename T, typename F>
+__device__ __forceinline__ void for_chunk_nchw(const BnGeo& g, int G, int c, int q, F&& f) {
+    const int n0 = (int)((long)g.N * q / G), n1 = (int)((long)g.N * (q + 1) / G);
+    const int per = g.HW / V;
+    const int count = per * (n1 - n0);
+    for (int e = threadIdx.x; e < count; e += kBlock) {
+        const int nl = e / per, p = (e - nl * per) * V;
+        f(((size_t)(n0 + nl) * g.C + c) * g.HW + p);
+    }
+}
+
+template <int V, typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_stats_nchw(const T* __restrict__ x, BnGeo g, int G,
+                                                          float* __restrict__ partial) {
+    __shared__ float s_red[2][kBlock / kWave];
+    const int c = blockIdx.x % g.C, q = blockIdx.x / g.C;
+    const float k = first_nchw(x, c, g);
+    float s1 = 0.f, s2 = 0.f;
+    for_chunk_nchw<V, T>(g, G, c, q, [&](size_t i) {
+        float v[V];
+        ldv<V>(x + i, v);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const float d = v[j] - k;
+            s1 += d;
+            s2 = fmaf(d, d, s2);
+        }
+    });
+    block_pair_sum(s1, s2, s_red);
+    if (threadIdx.x == 0) {
+        partial[((size_t)c * G + q) * 2] = s1;
+        partial[((size_t)c * G + q) * 2 + 1] = s2;
+    }
+}
+
+struct BnParams {
+    const float* gamma;
+    const float* beta;
+    float eps, momentum;
+    float* run_mean;
+    float* run_var;
+    float* stats;  // (4, C): save_mean, save_rstd, scale, shift
+};
+
+// statistics of channel c from its folded sums; the writer block stores running / saved values
+__device__ __forceinline__ void finalize_channel(float s1, float s2, float k, float n, int c, int C,
+                                                 const BnParams& P, bool writer, float& scale, float& shift) {
+    const float d = s1 / n;
+    const float mean = k + d;
+    const float var = fmaxf(s2 / n - d * d, 0.f);  // biased, used to normalise
+    const float rstd = rsqrtf(var + P.eps);
+    scale = (P.gamma ? P.gamma[c] : 1.f) * rstd;
+    shift = (P.beta ? P.beta[c] : 0.f) - mean * scale;
+    if (writer) {
+        if (P.run_mean) P.run_mean[c] = (1.f - P.momentum) * P.run_mean[c] + P.momentum * mean;
+        if (P.run_var)
+            P.run_var[c] = (1.f - P.momentum) * P.run_var[c] + P.momentum * (n > 1.f ? var * n / (n - 1.f) : var);
+        P.stats[c] = mean;
+        P.stats[C + c] = rstd;
+        P.stats[2 * C + c] = scale;
+        P.stats[3 * C + c] = shift;
+    }
+}
+
+template <int V, typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_apply_nchw(const T* __restrict__ x, const T* __restrict__ res, BnGeo g,
+                                                          int G, const float* __restrict__ partial, BnParams P, int act,
+                                                          T* __restrict__ y) {
+    __shared__ float s_coef[2];
+    const int c = blockIdx.x % g.C, q = blockIdx.x / g.C;
+    if (threadIdx.x < kWave) {
+        float s1, s2;
+        fold_groups(partial, c, G, s1, s2);
+        float sc, sh;
+        finalize_channel(s1, s2, first_nchw(x, c, g), (float)g.N * (float)g.HW, c, g.C, P, q == 0 && threadIdx.x == 0,
+                         sc, sh);
+        if (threadIdx.x == 0) {
+            s_coef[0] = sc;
+            s_coef[1] = sh;
+        }
+    }
+    __syncthreads();
+    const float sc = s_coef[0], sh = s_coef[1];
+    for_chunk_nchw<V, T>(g, G, c, q, [&](size_t i) {
+        float v[V], r[V];
+        ldv<V>(x + i, v);
+        if (res) ldv<V>(res + i, r);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            float z = fmaf(v[j], sc, sh);
+            if (res) z += r[j];
+            v[j] = act_fwd(z, act);
+        }
+        stv<V>(y + i, v);
+    });
+}
+
+template <int V, typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_bwd_stats_nchw(const T* __restrict__ dy, const T* __restrict__ x,
+                                                              const T* __restrict__ y, BnGeo g, int G,
+                                                              const float* __restrict__ stats, int act,
+                                                              float* __restrict__ partial) {
+    __shared__ float s_red[2][kBlock / kWave];
+    const int c = blockIdx.x % g.C, q = blockIdx.x / g.C;
+    const float mean = stats[c], rstd = stats[g.C + c], sc = stats[2 * g.C + c], sh = stats[3 * g.C + c];
+    float sg = 0.f, sgx = 0.f;
+    for_chunk_nchw<V, T>(g, G, c, q, [&](size_t i) {
+        float d[V], xv[V], yv[V];
+        ldv<V>(dy + i, d);
+        ldv<V>(x + i, xv);
+        if (act == LSS_ACT_RELU) ldv<V>(y + i, yv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const float gr = grad_pre(d[j], act == LSS_ACT_RELU ? yv[j] : 0.f, fmaf(xv[j], sc, sh), act);
+            sg += gr;
+            sgx = fmaf(gr, (xv[j] - mean) * rstd, sgx);
+        }
+    });
+    block_pair_sum(sg, sgx, s_red);
+    if (threadIdx.x == 0) {
+        partial[((size_t)c * G + q) * 2] = sg;
+        partial[((size_t)c * G + q) * 2 + 1] = sgx;
+    }
+}
+
+template <int V, typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_bwd_apply_nchw(const T* __restrict__ dy, const T* __restrict__ x,
+                                                              const T* __restrict__ y, BnGeo g, int G,
+                                                              const float* __restrict__ stats,
+                                                              const float* __restrict__ partial, int act,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                              T* __restrict__ dx, T* __restrict__ dres) {
+    __shared__ float s_coef[2];
+    const int c = blockIdx.x % g.C, q = blockIdx.x / g.C;
+    if (threadIdx.x < kWave) {
+        float sg, sgx;
+        fold_groups(partial, c, G, sg, sgx);
+        if (threadIdx.x == 0) {
+            if (q == 0) {
+                if (dgamma) dgamma[c] = sgx;
+                if (dbeta) dbeta[c] = sg;
+            }
+            const float n = (float)g.N * (float)g.HW;
+            s_coef[0] = sg / n;
+            s_coef[1] = sgx / n;
+        }
+    }
+    __syncthreads();
+    const float mg = s_coef[0], mgx = s_coef[1];
+    const float mean = stats[c], rstd = stats[g.C + c], sc = stats[2 * g.C + c], sh = stats[3 * g.C + c];
+    for_chunk_nchw<V, T>(g, G, c, q, [&](size_t i) {
+        float d[V], xv[V], yv[V], o[V], gr[V];
+        ldv<V>(dy + i, d);
+        ldv<V>(x + i, xv);
+        if (act == LSS_ACT_RELU) ldv<V>(y + i, yv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            gr[j] = grad_pre(d[j], act == LSS_ACT_RELU ? yv[j] : 0.f, fmaf(xv[j], sc, sh), act);
+            o[j] = sc * (gr[j] - mg - (xv[j] - mean) * rstd * mgx);
+        }
+        stv<V>(dx + i, o);
+        if (dres) stv<V>(dres + i, gr);
+    });
+}
+
+// ============================================================================= NHWC (channels-last)
+// block q: pixels [M q / G, M (q+1) / G) x all C channels; thread = 8 consecutive channels of a pixel.
+// Partials (C, G, 2) as in NCHW; a separate fold kernel (one wave per channel) turns them into the
+// per-channel coefficients the apply passes read.
+template <typename T, typename F>
+__device__ __forceinline__ void for_chunk_nhwc(const BnGeo& g, int G, int q, F&& f) {
+    const long M = (long)g.N * g.HW;
+    const long r0 = M * q / G, r1 = M * (q + 1) / G;
+    const int cg = g.C / 8;
+    const long count = (r1 - r0) * cg;
+    for (long e = threadIdx.x; e < count; e += kBlock) {
+        const long r = r0 + e / cg;
+        const int c0 = (int)(e % cg) * 8;
+        f((size_t)r * g.C + c0, c0);
+    }
+}
+
+// per-thread 8-channel sums -> per-channel block sums in LDS [C][2] -> partial[q][c][2]
+__device__ __forceinline__ void nhwc_block_sums(const BnGeo& g, int G, int q, const float* a, const float* b, int c0,
+                                                bool active, float* s_acc, float* __restrict__ partial) {
+    for (int i = threadIdx.x; i < 2 * g.C; i += kBlock) s_acc[i] = 0.f;
+    __syncthreads();
+    // fixed order: threads holding the same channels add in thread order, one thread group at a time
+    const int cg = g.C / 8;
+    const int rounds = kBlock / cg;  // threads sharing a channel group (the grid stride keeps each on one group)
+    for (int rd = 0; rd < rounds; ++rd) {
+        if (active && (int)threadIdx.x / cg == rd) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                s_acc[2 * (c0 + j)] += a[j];
+                s_acc[2 * (c0 + j) + 1] += b[j];
+            }
+        }
+        __syncthreads();
+    }
+    for (int c = threadIdx.x; c < g.C; c += kBlock) {
+        partial[((size_t)c * G + q) * 2] = s_acc[2 * c];
+        partial[((size_t)c * G + q) * 2 + 1] = s_acc[2 * c + 1];
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_stats_nhwc(const T* __restrict__ x, BnGeo g, int G,
+                                                          float* __restrict__ partial) {
+    extern __shared__ float s_dyn[];  // [C][2]
+    const int cg = g.C / 8;
+    const int c0 = ((int)threadIdx.x % cg) * 8;  // a thread's channel group is fixed (kBlock % cg == 0)
+    float k[8];
+    ldv<8>(x + c0, k);  // first pixel: the shifts
+    float a[8] = {}, b[8] = {};
+    for_chunk_nhwc<T>(g, G, blockIdx.x, [&](size_t i, int) {
+        float v[8];
+        ldv<8>(x + i, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float d = v[j] - k[j];
+            a[j] += d;
+            b[j] = fmaf(d, d, b[j]);
+        }
+    });
+    nhwc_block_sums(g, G, blockIdx.x, a, b, c0, (int)threadIdx.x < (kBlock / cg) * cg, s_dyn, partial);
+}
+
+// fold kernels (NHWC): one wave per channel, lanes over groups, fixed order
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_fold_nhwc(const float* __restrict__ partial, int G, const T* __restrict__ x,
+                                                         BnGeo g, BnParams P) {
+    const int c = blockIdx.x * (kBlock / kWave) + (int)threadIdx.x / kWave;
+    if (c >= g.C) return;
+    float s1 = 0.f, s2 = 0.f;
+    for (int q = threadIdx.x & (kWave - 1); q < G; q += kWave) {
+        s1 += partial[((size_t)c * G + q) * 2];
+        s2 += partial[((size_t)c * G + q) * 2 + 1];
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o, kWave);
+        s2 += __shfl_xor(s2, o, kWave);
+    }
+    float sc, sh;
+    finalize_channel(s1, s2, ld(x + c), (float)g.N * (float)g.HW, c, g.C, P, (threadIdx.x & (kWave - 1)) == 0, sc, sh);
+}
+
+__global__ __launch_bounds__(kBlock) void k_bn_bwd_fold_nhwc(const float* __restrict__ partial, int G, BnGeo g,
+                                                             float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                             float* __restrict__ coef) {
+    const int c = blockIdx.x * (kBlock / kWave) + (int)threadIdx.x / kWave;
+    if (c >= g.C) return;
+    float sg = 0.f, sgx = 0.f;
+    for (int q = threadIdx.x & (kWave - 1); q < G; q += kWave) {
+        sg += partial[((size_t)c * G + q) * 2];
+        sgx += partial[((size_t)c * G + q) * 2 + 1];
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        sg += __shfl_xor(sg, o, kWave);
+        sgx += __shfl_xor(sgx, o, kWave);
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        if (dgamma) dgamma[c] = sgx;
+        if (dbeta) dbeta[c] = sg;
+        const float n = (float)g.N * (float)g.HW;
+        coef[2 * c] = sg / n;
+        coef[2 * c + 1] = sgx / n;
+    }
+}
+
+// y = act(x * scale_c + shift_c [+ residual]), grid-stride over 8-channel vectors
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_apply_nhwc(const T* __restrict__ x, const T* __restrict__ res, BnGeo g,
+                                                          const float* __restrict__ stats, int act, T* __restrict__ y) {
+    extern __shared__ float s_dyn[];  // scale[C], shift[C]
+    for (int c = threadIdx.x; c < g.C; c += kBlock) {
+        s_dyn[c] = stats[2 * g.C + c];
+        s_dyn[g.C + c] = stats[3 * g.C + c];
+    }
+    __syncthreads();
+    const long nv = (long)g.N * g.HW * g.C / 8;
+    for (long e = (long)blockIdx.x * kBlock + threadIdx.x; e < nv; e += (long)gridDim.x * kBlock) {
+        const size_t i = (size_t)e * 8;
+        const int c0 = (int)(i % g.C);
+        float v[8], r[8];
+        ldv<8>(x + i, v);
+        if (res) ldv<8>(res + i, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float z = fmaf(v[j], s_dyn[c0 + j], s_dyn[g.C + c0 + j]);
+            if (res) z += r[j];
+            v[j] = act_fwd(z, act);
+        }
+        stv<8>(y + i, v);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_bwd_stats_nhwc(const T* __restrict__ dy, const T* __restrict__ x,
+                                                              const T* __restrict__ y, BnGeo g, int G,
+                                                              const float* __restrict__ stats, int act,
+                                                              float* __restrict__ partial) {
+    extern __shared__ float s_dyn[];  // [C][2]
+    const int cg = g.C / 8;
+    const int c0 = ((int)threadIdx.x % cg) * 8;
+    float mean[8], rstd[8], sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        mean[j] = stats[c0 + j];
+        rstd[j] = stats[g.C + c0 + j];
+        sc[j] = stats[2 * g.C + c0 + j];
+        sh[j] = stats[3 * g.C + c0 + j];
+    }
+    float a[8] = {}, b[8] = {};
+    for_chunk_nhwc<T>(g, G, blockIdx.x, [&](size_t i, int) {
+        float d[8], xv[8], yv[8];
+        ldv<8>(dy + i, d);
+        ldv<8>(x + i, xv);
+        if (act == LSS_ACT_RELU) ldv<8>(y + i, yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float gr = grad_pre(d[j], act == LSS_ACT_RELU ? yv[j] : 0.f, fmaf(xv[j], sc[j], sh[j]), act);
+            a[j] += gr;
+            b[j] = fmaf(gr, (xv[j] - mean[j]) * rstd[j], b[j]);
+        }
+    });
+    nhwc_block_sums(g, G, blockIdx.x, a, b, c0, (int)threadIdx.x < (kBlock / cg) * cg, s_dyn, partial);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_bwd_apply_nhwc(const T* __restrict__ dy, const T* __restrict__ x,
+                                                              const T* __restrict__ y, BnGeo g,
+                                                              const float* __restrict__ stats,
+                                                              const float* __restrict__ coef, int act,
+                                                              T* __restrict__ dx, T* __restrict__ dres) {
+    extern __shared__ float s_dyn[];  // mean, rstd, scale, shift, mean(g), mean(g xhat): [6][C]
+    for (int c = threadIdx.x; c < g.C; c += kBlock) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s_dyn[k * g.C + c] = stats[k * g.C + c];
+        s_dyn[4 * g.C + c] = coef[2 * c];
+        s_dyn[5 * g.C + c] = coef[2 * c + 1];
+    }
+    __syncthreads();
+    const long nv = (long)g.N * g.HW * g.C / 8;
+    for (long e = (long)blockIdx.x * kBlock + threadIdx.x; e < nv; e += (long)gridDim.x * kBlock) {
+        const size_t i = (size_t)e * 8;
+        const int c0 = (int)(i % g.C);
+        float d[8], xv[8], yv[8], o[8], gr[8];
+        ldv<8>(dy + i, d);
+        ldv<8>(x + i, xv);
+        if (act == LSS_ACT_RELU) ldv<8>(y + i, yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = c0 + j;
+            const float sc = s_dyn[2 * g.C + c];
+            gr[j] = grad_pre(d[j], act == LSS_ACT_RELU ? yv[j] : 0.f, fmaf(xv[j], sc, s_dyn[3 * g.C + c]), act);
+            o[j] = sc * (gr[j] - s_dyn[4 * g.C + c] - (xv[j] - s_dyn[c]) * s_dyn[g.C + c] * s_dyn[5 * g.C + c]);
+        }
+        stv<8>(dx + i, o);
+        if (dres) stv<8>(dres + i, gr);
+    }
+}
+
+// ============================================================================= host side
+inline int launch_status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+inline bool bn_ok(const BnGeo& g, int layout) {
+    if (g.N <= 0 || g.C <= 0 || g.HW <= 0 || (long)g.N * g.C * g.HW >= INT_MAX) return false;
+    if (layout == LSS_CONV_NHWC) return g.C % 8 == 0 && g.C / 8 <= kBlock && kBlock % (g.C / 8) == 0;
+    return layout == LSS_CONV_NCHW;
+}
+
+inline int vec_nchw(int HW) { return HW % 8 == 0 ? 8 : (HW % 4 == 0 ? 4 : 1); }
+
+inline int apply_blocks(const BnGeo& g) {  // grid-stride elementwise passes: up to 8 blocks per CU
+    const long nv = (long)g.N * g.HW * g.C / 8;
+    const long b = (nv + kBlock - 1) / kBlock;
+    return (int)(b < 2048 ? b : 2048);
+}
+
+}  // namespace
+
+extern "C" {
+
+int lss_bn_groups(int32_t N, int32_t C, int32_t HW, int32_t layout) {
+    const long per_chan = (long)N * HW;
+    if (layout == LSS_CONV_NHWC) {  // ~32 K elements per block
+        const long g = per_chan * C / 32768;
+        return (int)(g < 1 ? 1 : (g > kMaxGroupsNhwc ? kMaxGroupsNhwc : g));
+    }
+    const long g = per_chan / 8192;  // ~8 K elements of one channel per block
+    return (int)(g < 1 ? 1 : (g > N ? N : g));
+}
+
+int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layout, int32_t N, int32_t C, int32_t HW,
+               const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
+               float* running_var, int32_t act, int32_t ngroups, float* partial, float* save_mean, float* save_rstd,
+               float* scale, float* shift, void* y, void* stream) {
+    const BnGeo g{N, C, HW};
+    if (!x || !y || !partial || !save_mean || !save_rstd || !scale || !shift || ngroups <= 0 || !bn_ok(g, layout))
+        return LSS_CONV_EINVAL;
+    if (act != LSS_ACT_NONE && act != LSS_ACT_RELU && act != LSS_ACT_SWISH) return LSS_CONV_EINVAL;
+    // the saved statistics are one (4, C) array: mean, rstd, scale, shift
+    if (save_rstd != save_mean + C || scale != save_mean + 2 * C || shift != save_mean + 3 * C) return LSS_CONV_EINVAL;
+    if (layout == LSS_CONV_NHWC && ngroups > kMaxGroupsNhwc) return LSS_CONV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const BnParams P{gamma, beta, eps, momentum, running_mean, running_var, save_mean};
+    const int G = ngroups;
+#define LSS_BN_FWD(T)                                                                                              \
+    do {                                                                                                           \
+        const T* xx = (const T*)x;                                                                                 \
+        const T* rr = (const T*)residual;                                                                          \
+        T* yy = (T*)y;                                                                                             \
+        if (layout == LSS_CONV_NHWC) {                                                                             \
+            const size_t lds = 2 * C * sizeof(float);                                                              \
+            hipLaunchKernelGGL(k_bn_stats_nhwc<T>, dim3(G), dim3(kBlock), lds, s, xx, g, G, partial);              \
+            hipLaunchKernelGGL(k_bn_fold_nhwc<T>, dim3((C + 3) / 4), dim3(kBlock), 0, s, partial, G, xx, g, P);   \
+            hipLaunchKernelGGL(k_bn_apply_nhwc<T>, dim3(apply_blocks(g)), dim3(kBlock), lds, s, xx, rr, g,        \
+                               save_mean, (int)act, yy);                                                           \
+        } else {                                                                                                   \
+            const int V = vec_nchw(HW);                                                                            \
+            const dim3 gr(C * G), bl(kBlock);                                                                      \
+            if (V == 8) {                                                                                          \
+                hipLaunchKernelGGL((k_bn_stats_nchw<8, T>), gr, bl, 0, s, xx, g, G, partial);                     \
+                hipLaunchKernelGGL((k_bn_apply_nchw<8, T>), gr, bl, 0, s, xx, rr, g, G, partial, P, (int)act, yy); \
+            } else if (V == 4) {                                                                                   \
+                hipLaunchKernelGGL((k_bn_stats_nchw<4, T>), gr, bl, 0, s, xx, g, G, partial);                     \
+                hipLaunchKernelGGL((k_bn_apply_nchw<4, T>), gr, bl, 0, s, xx, rr, g, G, partial, P, (int)act, yy); \
+            } else {                                                                                               \
+                hipLaunchKernelGGL((k_bn_stats_nchw<1, T>), gr, bl, 0, s, xx, g, G, partial);                     \
+                hipLaunchKernelGGL((k_bn_apply_nchw<1, T>), gr, bl, 0, s, xx, rr, g, G, partial, P, (int)act, yy); \
+            }                                                                                                      \
+        }                                                                                                          \
+    } while (0)
+    if (dtype == LSS_CONV_F32) LSS_BN_FWD(float);
+    else if (dtype == LSS_CONV_BF16) LSS_BN_FWD(bf16);
+    else return LSS_CONV_EINVAL;
+#undef LSS_BN_FWD
+    return launch_status();
+}
+
+int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int32_t layout, int32_t N, int32_t C,
+               int32_t HW, const float* scale, const float* shift, const float* save_mean, const float* save_rstd,
+               int32_t act, int32_t ngroups, float* partial, float* coef, float* dgamma, float* dbeta, void* dx,
+               void* dresidual, void* stream) {
+    const BnGeo g{N, C, HW};
+    if (!dy || !x || !scale || !shift || !save_mean || !save_rstd || !partial || !coef || !dx || ngroups <= 0 ||
+        !bn_ok(g, layout))
+        return LSS_CONV_EINVAL;
+    if (save_rstd != save_mean + C || scale != save_mean + 2 * C || shift != save_mean + 3 * C) return LSS_CONV_EINVAL;
+    if (act == LSS_ACT_RELU && !y) return LSS_CONV_EINVAL;
+    if (act != LSS_ACT_NONE && act != LSS_ACT_RELU && act != LSS_ACT_SWISH) return LSS_CONV_EINVAL;
+    if (layout == LSS_CONV_NHWC && ngroups > kMaxGroupsNhwc) return LSS_CONV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const int G = ngroups;
+    const float* stats = save_mean;
+#define LSS_BN_BWD(T)                                                                                              \
+    do {                                                                                                           \
+        const T* d = (const T*)dy;                                                                                 \
+        const T* xx = (const T*)x;                                                                                 \
+        const T* yy = (const T*)y;                                                                                 \
+        T* o = (T*)dx;                                                                                             \
+        T* orr = (T*)dresidual;                                                                                    \
+        if (layout == LSS_CONV_NHWC) {                                                                             \
+            hipLaunchKernelGGL(k_bn_bwd_stats_nhwc<T>, dim3(G), dim3(kBlock), 2 * C * sizeof(float), s, d, xx, yy, \
+                               g, G, stats, (int)act, partial);                                                    \
+            hipLaunchKernelGGL(k_bn_bwd_fold_nhwc, dim3((C + 3) / 4), dim3(kBlock), 0, s, partial, G, g, dgamma,  \
+                               dbeta, coef);                                                                       \
+            hipLaunchKernelGGL(k_bn_bwd_apply_nhwc<T>, dim3(apply_blocks(g)), dim3(kBlock), 6 * C * sizeof(float), \
+                               s, d, xx, yy, g, stats, coef, (int)act, o, orr);                                    \
+        } else {                                                                                                   \
+            const int V = vec_nchw(HW);                                                                            \
+            const dim3 gr(C * G), bl(kBlock);                                                                      \
+            if (V == 8) {                                                                                          \
+                hipLaunchKernelGGL((k_bn_bwd_stats_nchw<8, T>), gr, bl, 0, s, d, xx, yy, g, G, stats, (int)act,    \
+                                   partial);                                                                       \
+                hipLaunchKernelGGL((k_bn_bwd_apply_nchw<8, T>), gr, bl, 0, s, d, xx, yy, g, G, stats, partial,    \
+                                   (int)act, dgamma, dbeta, o, orr);                                               \
+            } else if (V == 4) {                                                                                   \
+                hipLaunchKernelGGL((k_bn_bwd_stats_nchw<4, T>), gr, bl, 0, s, d, xx, yy, g, G, stats, (int)act,    \
+                                   partial);                                                                       \
+                hipLaunchKernelGGL((k_bn_bwd_apply_nchw<4, T>), gr, bl, 0, s, d, xx, yy, g, G, stats, partial,    \
+                                   (int)act, dgamma, dbeta, o, orr);                                               \
+            } else {                                                                                               \
+                hipLaunchKernelGGL((k_bn_bwd_stats_nchw<1, T>), gr, bl, 0, s, d, xx, yy, g, G, stats, (int)act,    \
+                                   partial);                                                                       \
+                hipLaunchKernelGGL((k_bn_bwd_apply_nchw<1, T>), gr, bl, 0, s, d, xx, yy, g, G, stats, partial,    \
+                                   (int)act, dgamma, dbeta, o, orr);                                               \
+            }                                                                                                      \
+        }                                                                                                          \
+    } while (0)
+    if (dtype == LSS_CONV_F32) LSS_BN_BWD(float);
+    else if (dtype == LSS_CONV_BF16) LSS_BN_BWD(bf16);
+    else return LSS_CONV_EINVAL;
+#undef LSS_BN_BWD
+    return launch_status();
+}
+
+}  // extern "C"

@@ -1438,9 +1438,17 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), wpb);
         const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), wpb);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kBlock);
+// kernel-stamped events only when asked for: a plain launch is what a hipGraph capture records
 #define LSS_NHWC_FWD(F, RT, T)                                                                                     \
-    hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, (const RT*)rows,           \
-                          cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, (T*)out)
+    do {                                                                                                           \
+        if (e0 || e1)                                                                                              \
+            hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, (const RT*)rows,   \
+                                  cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks,      \
+                                  (T*)out);                                                                        \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, depth, (const RT*)rows, cell_start,     \
+                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, (T*)out);           \
+    } while (0)
         if (out_dtype == LSS_F32) {
             if (!fused) LSS_NHWC_FWD(false, float, float);
             else if (ctx_bf16) LSS_NHWC_FWD(true, bf16, float);
@@ -1457,8 +1465,15 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
     const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
     const size_t lds = (size_t)kC * (sg.YT + 4) * sizeof(float);
 #define LSS_SPLAT(F, RT, T)                                                                                       \
-    hipExtLaunchKernelGGL((k_splat_fwd<F, RT, T, false>), dim3(nblocks), dim3(kFwdBlock), (uint32_t)lds, s, e0, e1, \
-                          0, depth, (const RT*)rows, cell_start, sorted_key, sorted_row, sg, nprime, (T*)out)
+    do {                                                                                                          \
+        if (e0 || e1)                                                                                             \
+            hipExtLaunchKernelGGL((k_splat_fwd<F, RT, T, false>), dim3(nblocks), dim3(kFwdBlock), (uint32_t)lds, \
+                                  s, e0, e1, 0, depth, (const RT*)rows, cell_start, sorted_key, sorted_row, sg,   \
+                                  nprime, (T*)out);                                                               \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_splat_fwd<F, RT, T, false>), dim3(nblocks), dim3(kFwdBlock), lds, s, depth,     \
+                               (const RT*)rows, cell_start, sorted_key, sorted_row, sg, nprime, (T*)out);         \
+    } while (0)
     if (out_dtype == LSS_F32) {
         if (!fused) LSS_SPLAT(false, float, float);
         else if (ctx_bf16) LSS_SPLAT(true, bf16, float);

@@ -26,6 +26,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .norm import bn_act
+
 # (repeats, kernel, stride, expand, in, out) for the 7 stages of B0, SE ratio 0.25.
 B0_STAGES = (
     (1, 3, 1, 1, 32, 16),
@@ -197,7 +199,7 @@ class MBConvBlock(nn.Module):
     def forward(self, inputs: torch.Tensor, drop_connect_rate=None) -> torch.Tensor:
         x = inputs
         if self.expand != 1:
-            x = F.silu(self._bn0(self._expand_conv(x)))
+            x = bn_act(self._bn0, self._expand_conv(x), "swish")
         dw = self._depthwise_conv
         if self.depthwise_impl == "hip" and x.is_cuda:
             x = _HipDepthwise.apply(x, dw.weight, dw.stride[0], depthwise_same_pads(dw))
@@ -208,11 +210,11 @@ class MBConvBlock(nn.Module):
                 x = self._depthwise_conv(x.float())
         else:
             x = self._depthwise_conv(x)
-        x = F.silu(self._bn1(x))
+        x = bn_act(self._bn1, x, "swish")
         s = F.adaptive_avg_pool2d(x, 1)
         s = self._se_expand(F.silu(self._se_reduce(s)))
         x = torch.sigmoid(s) * x
-        x = self._bn2(self._project_conv(x))
+        x = bn_act(self._bn2, self._project_conv(x))
         if self.stride == 1 and self.in_f == self.out_f:
             if drop_connect_rate:
                 x = drop_connect(x, drop_connect_rate, self.training)
@@ -277,7 +279,7 @@ class EfficientNetB0(nn.Module):
         return F.silu(x)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:  # classification head (unused by LSS)
-        x = self._swish(self._bn0(self._conv_stem(x)))
+        x = bn_act(self._bn0, self._conv_stem(x), "swish")
         for idx, block in enumerate(self._blocks):
             x = block(x, self._global_params.drop_connect_rate * idx / len(self._blocks))
         x = self._swish(self._bn1(self._conv_head(x)))

@@ -33,6 +33,8 @@ from torch import nn
 
 from . import _lib, ops
 from .efficientnet import EfficientNetB0
+from . import resample
+from .norm import bn_act
 from .tools import gen_dx_bx
 
 
@@ -52,13 +54,20 @@ class Up(nn.Module):
         )
 
     def forward(self, x1, x2):
+        c = self.conv  # conv-BN-ReLU twice; BN + ReLU fused (lss_bn_*)
+        if resample.USE_HIP_UPSAMPLE and resample._eligible(x1) and resample._eligible(x2):
+            # channels-last bf16 (BevEncode under autocast): upsample + cat in one kernel
+            x = resample.upsample_cat(x1, x2, int(self.up.scale_factor))
+            x = bn_act(c[1], c[0](x), "relu")
+            return bn_act(c[4], c[3](x), "relu")
         if x1.is_cuda and not x1.is_contiguous(memory_format=torch.channels_last):
             # PyTorch's NCHW bilinear kernel parallelises over output pixels only (a 8x22 map:
             # 176 threads, each looping over N*C); the channels-last kernel covers every element.
             x1 = self.up(x1.contiguous(memory_format=torch.channels_last)).contiguous()
         else:
             x1 = self.up(x1)
-        return self.conv(torch.cat([x2, x1], dim=1))
+        x = bn_act(c[1], c[0](torch.cat([x2, x1], dim=1)), "relu")
+        return bn_act(c[4], c[3](x), "relu")
 
 
 class CamEncode(nn.Module):
@@ -75,7 +84,7 @@ class CamEncode(nn.Module):
     def get_eff_depth(self, x):
         """Endpoints reduction_4 / reduction_5 of the trunk, fused by ``up1`` (src/models.py:63-84)."""
         t = self.trunk
-        x = t._swish(t._bn0(t._conv_stem(x)))
+        x = bn_act(t._bn0, t._conv_stem(x), "swish")
         endpoints = []
         prev = x
         nblk = len(t._blocks)
@@ -127,10 +136,12 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + identity)
+        if self.downsample is None:
+            identity = x
+        else:
+            identity = bn_act(self.downsample[1], self.downsample[0](x))
+        out = bn_act(self.bn1, self.conv1(x), "relu")
+        return bn_act(self.bn2, self.conv2(out), "relu", residual=identity)
 
 
 def _resnet_layer(inplanes, planes, blocks, stride):
@@ -181,11 +192,16 @@ class BevEncode(nn.Module):
         )
 
     def forward(self, x):
-        x = self.relu(self.bn1(self.conv1(x)))
+        x = bn_act(self.bn1, self.conv1(x), "relu")
         x1 = self.layer1(x)
         x = self.layer3(self.layer2(x1))
         x = self.dropout(self.up1(x, x1))
-        return self.up2(x)
+        u = self.up2  # Upsample, conv, BN, ReLU, conv
+        if resample.USE_HIP_UPSAMPLE and resample._eligible(x):
+            x = resample.upsample_cat(x, None, int(u[0].scale_factor))
+        else:
+            x = u[0](x)
+        return u[4](bn_act(u[2], u[1](x), "relu"))
 
 
 class LiftSplatShoot(nn.Module):

@@ -1,0 +1,102 @@
+"""The training step of train_simbev.py:229-248 -- forward, SimpleLoss, backward,
+clip_grad_norm_(max_grad_norm), Adam -- eager, or replayed as two HIP graphs.
+
+A B=8 step launches ~1000 kernels (conv stacks, BN, the lift/splat path, fused Adam); eager, the
+host's Python + launch cost per kernel is longer than many of the kernels, so the GPU idles.
+Captured (``torch.cuda.CUDAGraph``, i.e. hipGraph), the step is two graph launches:
+
+  graph A  zero the flat gradient buffer, forward under bf16 autocast, loss, backward
+  (eager)  all-reduce of the flat gradient buffer over RCCL (world size > 1)
+  graph B  divide by the world size, clip_grad_norm_, fused Adam (capturable)
+
+The collective stays outside the graphs: one ~50 MB ring all-reduce over xGMI per step, the
+same averaged gradients as DDP (parallel.FlatGradients). Every op of the LSS path is capturable:
+its kernels only take device pointers, and the plan's sizes come from the static shapes; the one
+host round trip of the reference (torch.inverse on the CPU, src/models.py:180,186) is replaced by
+the device inverse (ops.camera_inverses(mode='device')).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Sequence
+
+import torch
+
+from .parallel import FlatGradients
+
+
+class TrainStep:
+    def __init__(self, forward: Callable[..., torch.Tensor], inputs: Sequence[torch.Tensor], labels: torch.Tensor,
+                 loss_fn: Callable, opt: torch.optim.Optimizer, params: Sequence[torch.nn.Parameter],
+                 grads: Optional[FlatGradients] = None, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
+                 max_grad_norm: float = 5.0):
+        self.forward, self.inputs, self.labels = forward, tuple(inputs), labels
+        self.loss_fn, self.opt, self.params, self.grads = loss_fn, opt, list(params), grads
+        self.amp_dtype, self.max_grad_norm = amp_dtype, max_grad_norm
+        self.graphs = None
+        self.static_loss = None
+
+    @property
+    def captured(self) -> bool:
+        return self.graphs is not None
+
+    def forward_backward(self) -> torch.Tensor:
+        if self.grads is not None:
+            self.grads.zero()
+        else:
+            self.opt.zero_grad(set_to_none=True)
+        dev_type = self.labels.device.type
+        # autocast's cast cache must be off while capturing (its entries would outlive the capture)
+        capturing = dev_type == "cuda" and torch.cuda.is_current_stream_capturing()
+        with torch.autocast(dev_type, dtype=self.amp_dtype or torch.bfloat16, enabled=self.amp_dtype is not None,
+                            cache_enabled=not capturing):
+            preds = self.forward(*self.inputs)
+        loss = self.loss_fn(preds.float(), self.labels)
+        loss.backward()
+        return loss
+
+    def update(self) -> None:
+        if self.grads is not None:
+            self.grads.average()
+        torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)
+        self.opt.step()
+
+    def eager(self) -> torch.Tensor:
+        loss = self.forward_backward()
+        if self.grads is not None:
+            self.grads.all_reduce()
+        self.update()
+        return loss
+
+    def capture(self, warmup: int = 2, on_warmup: Optional[Callable[[int], None]] = None) -> None:
+        """`warmup` eager steps on a side stream (MIOpen find, optimizer state, allocator), then
+        capture. Needs FlatGradients (gradient addresses fixed across replays) and an optimizer
+        built with capturable=True."""
+        if self.grads is None:
+            raise RuntimeError("TrainStep.capture needs FlatGradients")
+        dev = self.labels.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for i in range(max(warmup, 1)):
+                self.eager()
+                if on_warmup is not None:
+                    on_warmup(i)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        g_fb, g_up = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
+            # detached: holding the captured autograd graph would keep its AccumulateGrad nodes
+            # (bound to the capture stream) alive into later eager steps
+            self.static_loss = self.forward_backward().detach()
+        with torch.cuda.graph(g_up, pool=g_fb.pool()):
+            self.update()
+        self.graphs = (g_fb, g_up)
+
+    def __call__(self) -> torch.Tensor:
+        if self.graphs is None:
+            return self.eager()
+        g_fb, g_up = self.graphs
+        g_fb.replay()
+        self.grads.all_reduce()
+        g_up.replay()
+        return self.static_loss

@@ -73,6 +73,23 @@ def _worker(rank, world, port, outdir):
     if rank == 0:
         torch.save({n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None},
                    os.path.join(outdir, "ddp.pt"))
+    # the captured-step path: broadcast replicas, gradients in one flat buffer, one all-reduce
+    m2 = _model()
+    if rank == 1:
+        with torch.no_grad():
+            for p in m2.parameters():
+                if p.is_floating_point():
+                    p.add_(1.0)
+    parallel.broadcast_state(m2)
+    flat = parallel.FlatGradients(m2, dev)
+    flat.zero()
+    _grads(_CpuLSS(m2), seed=10 + rank)
+    flat.all_reduce()
+    flat.average()
+    assert all(p.grad.data_ptr() >= flat.flat.data_ptr() for p in flat.params)  # still the views
+    if rank == 0:
+        torch.save({n: p.grad.clone().contiguous() for n, p in m2.named_parameters() if p.requires_grad},
+                   os.path.join(outdir, "flat.pt"))
     t = parallel.max_over_ranks(float(rank), dev)
     assert t == world - 1
     dist.destroy_process_group()
@@ -90,6 +107,7 @@ def test_ddp_gradients_equal_mean_of_replicas():
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
         ddp = torch.load(os.path.join(d, "ddp.pt"), weights_only=True)
+        flat = torch.load(os.path.join(d, "flat.pt"), weights_only=True)
     ref = {}
     nthreads = torch.get_num_threads()
     torch.set_num_threads(2)  # the workers' thread count: same conv algorithms and reduction order
@@ -107,6 +125,12 @@ def test_ddp_gradients_equal_mean_of_replicas():
         err = (ddp[n] - ref[n]).abs().max() / scale
         assert err < 1e-3, (n, float(err), float(scale))
     assert not any(n.startswith(parallel.UNUSED_PREFIXES) for n in ddp)
+    # FlatGradients (bench.py --graph): same averaged gradients, frozen head excluded
+    assert set(flat) == set(ref)
+    for n in ref:
+        scale = ref[n].abs().max().clamp_min(1e-12)
+        err = (flat[n] - ref[n]).abs().max() / scale
+        assert err < 1e-3, (n, float(err), float(scale))
 
 
 def test_freeze_unused_through_wrapper():
@@ -119,3 +143,26 @@ def test_freeze_unused_counts_head_params():
     frozen = parallel.freeze_unused(m)
     assert frozen == 320 * 1280 + 2 * 1280 + 1280 * 1000 + 1000
     assert all(not p.requires_grad for n, p in m.named_parameters() if n.startswith(parallel.UNUSED_PREFIXES))
+
+
+def test_flat_gradients_single_process_channels_last():
+    """World size 1: the views keep each parameter's strides (channels-last convs) and receive the
+    same gradients as freshly allocated .grad tensors; average() / all_reduce() are no-ops."""
+    torch.manual_seed(3)
+    net = torch.nn.Sequential(torch.nn.Conv2d(8, 16, 3, padding=1), torch.nn.BatchNorm2d(16), torch.nn.ReLU(),
+                              torch.nn.Conv2d(16, 4, 1)).to(memory_format=torch.channels_last)
+    x = torch.randn(2, 8, 10, 12).contiguous(memory_format=torch.channels_last)
+    net(x).square().mean().backward()
+    want = {n: p.grad.clone() for n, p in net.named_parameters()}
+    flat = parallel.FlatGradients(net, torch.device("cpu"))
+    assert flat.numel == sum(p.numel() for p in net.parameters())
+    for p in net.parameters():
+        assert p.grad.stride() == p.stride()
+    flat.zero()
+    net(x).square().mean().backward()
+    flat.all_reduce()
+    flat.average()
+    base, end = flat.flat.data_ptr(), flat.flat.data_ptr() + 4 * flat.numel
+    for n, p in net.named_parameters():
+        assert base <= p.grad.data_ptr() < end, n
+        torch.testing.assert_close(p.grad, want[n], rtol=1e-6, atol=1e-7)

@@ -73,3 +73,136 @@ def test_trunk_hip_vs_miopen_depthwise():
         outs.append((h.detach(), trunk._blocks[3]._depthwise_conv.weight.grad.clone()))
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-3, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- batch norm + activation
+from lss_carla_amd import norm as Nm  # noqa: E402
+
+BN_CASES = [  # (N, C, H, W, layout)
+    (3, 32, 64, 176, "nchw"),
+    (4, 96, 8, 22, "nchw"),
+    (5, 40, 4, 11, "nchw"),
+    (2, 64, 100, 100, "nhwc"),
+    (2, 256, 25, 25, "nhwc"),
+    (3, 24, 7, 9, "nhwc"),
+]
+
+
+def _bn_reference(x, w, b, rm, rv, eps, mom, act, res, dy):
+    xr = x.detach().cpu().double().requires_grad_(True)
+    wr = w.detach().cpu().double().requires_grad_(True)
+    br = b.detach().cpu().double().requires_grad_(True)
+    rr = res.detach().cpu().double().requires_grad_(True) if res is not None else None
+    rm, rv = rm.cpu().double(), rv.cpu().double()
+    y = F.batch_norm(xr, rm, rv, wr, br, training=True, momentum=mom, eps=eps)
+    if rr is not None:
+        y = y + rr
+    y = {"none": y, "relu": F.relu(y), "swish": F.silu(y)}[act]
+    y.backward(dy.detach().cpu().double())
+    return y.detach(), xr.grad, wr.grad, br.grad, (rr.grad if rr is not None else None), rm, rv
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act,with_res", [("none", False), ("swish", False), ("relu", False), ("relu", True)])
+@pytest.mark.parametrize("N,C,H,W,layout", BN_CASES)
+def test_bn_act_vs_fp64(N, C, H, W, layout, act, with_res, dtype):
+    g = torch.Generator().manual_seed(N * 1000 + C + H)
+    x = (torch.randn(N, C, H, W, generator=g) * 2 + 3).to(dtype)  # offset mean: exercises the shifted sums
+    res = torch.randn(N, C, H, W, generator=g).to(dtype) if with_res else None
+    bn = torch.nn.BatchNorm2d(C, eps=1e-3, momentum=0.01).to(DEV).train()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, generator=g) * 0.1)
+        bn.running_mean.copy_(torch.randn(C, generator=g))
+        bn.running_var.copy_(torch.rand(C, generator=g) + 0.5)
+    rm0, rv0 = bn.running_mean.clone(), bn.running_var.clone()
+    mf = torch.channels_last if layout == "nhwc" else torch.contiguous_format
+    xd = x.to(DEV).contiguous(memory_format=mf).requires_grad_(True)
+    rd = res.to(DEV).contiguous(memory_format=mf).requires_grad_(True) if with_res else None
+    y = Nm.bn_act(bn, xd, act, rd)
+    assert y.dtype == dtype and y.is_contiguous(memory_format=mf)
+    dy = torch.randn(y.shape, generator=g).to(dtype)
+    y.backward(dy.to(DEV).contiguous(memory_format=mf))
+    ref = _bn_reference(x, bn.weight, bn.bias, rm0, rv0, bn.eps, bn.momentum, act, res, dy)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(y.detach().cpu().double(), ref[0], **tol)
+    torch.testing.assert_close(xd.grad.cpu().double(), ref[1], **tol)
+    gtol = dict(rtol=1e-3, atol=1e-2) if dtype == torch.float32 else dict(rtol=3e-2, atol=1.0)
+    torch.testing.assert_close(bn.weight.grad.cpu().double(), ref[2], **gtol)
+    torch.testing.assert_close(bn.bias.grad.cpu().double(), ref[3], **gtol)
+    if with_res:
+        torch.testing.assert_close(rd.grad.cpu().double(), ref[4], **tol)
+    torch.testing.assert_close(bn.running_mean.cpu().double(), ref[5], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_var.cpu().double(), ref[6], rtol=1e-3, atol=1e-4)
+    assert int(bn.num_batches_tracked) == 1
+
+
+# ----------------------------------------------------------------------------- bilinear upsample + cat
+from lss_carla_amd import resample as R  # noqa: E402
+
+UP_CASES = [  # (N, C1, Hi, Wi, C2, scale): BevEncode.up1 / up2, CamEncode.up1 (channels-last), odd sizes
+    (2, 256, 25, 25, 64, 4),
+    (2, 256, 100, 100, 0, 2),
+    (3, 320, 4, 11, 112, 2),
+    (1, 16, 5, 7, 8, 3),
+]
+
+
+@pytest.mark.parametrize("N,C1,H,W,C2,s", UP_CASES)
+def test_upsample_cat_vs_fp64(N, C1, H, W, C2, s):
+    g = torch.Generator().manual_seed(N * 7 + C1 + H)
+    cl = torch.channels_last
+    x = torch.randn(N, C1, H, W, generator=g).bfloat16()
+    skip = torch.randn(N, C2, H * s, W * s, generator=g).bfloat16() if C2 else None
+    xd = x.to(DEV).contiguous(memory_format=cl).requires_grad_(True)
+    sd = skip.to(DEV).contiguous(memory_format=cl).requires_grad_(True) if C2 else None
+    y = R.upsample_cat(xd, sd, s)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=cl) and y.shape == (N, C1 + C2, H * s, W * s)
+    # reference: the fp64 upsample of the same bf16 values, concatenated as src/models.py:33 does
+    xr = x.double().requires_grad_(True)
+    up = F.interpolate(xr, scale_factor=s, mode="bilinear", align_corners=True)
+    ref = torch.cat([skip.double(), up], 1) if C2 else up
+    torch.testing.assert_close(y.detach().cpu().double(), ref.detach(), rtol=8e-3, atol=8e-3)  # one bf16 rounding
+    if C2:
+        assert torch.equal(y[:, :C2].detach().cpu(), skip)
+    # the autocast reference: PyTorch's fp32 kernel, cast to bf16 -- equal but for FMA-contraction ulps
+    with torch.no_grad():
+        t32 = F.interpolate(xd.float(), scale_factor=s, mode="bilinear", align_corners=True).bfloat16()
+    assert (y[:, C2:].detach() == t32).float().mean().item() > 0.99
+    dy = torch.randn(y.shape, generator=g).bfloat16()
+    y.backward(dy.to(DEV).contiguous(memory_format=cl))
+    ref.backward(dy.double())
+    assert xd.grad.dtype == torch.bfloat16
+    torch.testing.assert_close(xd.grad.cpu().double(), xr.grad, rtol=1e-2, atol=2e-2)
+    if C2:
+        assert torch.equal(sd.grad.cpu(), dy[:, :C2])
+    # deterministic backward (gather, no atomics)
+    g1 = xd.grad.clone()
+    xd.grad = None
+    R.upsample_cat(xd, sd, s).backward(dy.to(DEV).contiguous(memory_format=cl))
+    assert torch.equal(xd.grad, g1)
+
+
+def test_bevencode_hip_upsample_vs_torch():
+    """BevEncode under bf16 autocast: fused upsample+cat kernels vs PyTorch's fp32 upsample + cat."""
+    from lss_carla_amd.models import BevEncode
+    torch.manual_seed(5)
+    m = BevEncode(64, 1).to(DEV).to(memory_format=torch.channels_last).train()
+    m.dropout.p = 0.0
+    x = torch.randn(2, 64, 200, 200, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for use in (True, False):
+        R.USE_HIP_UPSAMPLE = use
+        try:
+            m.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = m(xi)
+            y.float().square().mean().backward()
+            outs.append((y.detach().float(), xi.grad.float(), m.up1.conv[0].weight.grad.clone(),
+                         m.layer3[0].conv1.weight.grad.clone()))
+        finally:
+            R.USE_HIP_UPSAMPLE = True
+    for a, b in zip(outs[0], outs[1]):
+        err = (a - b).abs().max() / b.abs().max().clamp_min(1e-6)
+        assert err < 3e-2, float(err)
