@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--graph", type=int, default=1,
                     help="replay the step as two HIP graphs (fwd+bwd, clip+Adam) with the gradient all-reduce "
                          "between them; 0 = eager (DDP for N>1)")
+    ap.add_argument("--flat-params", type=int, default=1,
+                    help="trainable parameters as one fp32 master tensor with one bf16 working copy per step")
     ap.add_argument("--profile-steps", type=int, default=5,
                     help="with --graph 1: eager steps after the timed region on which the splat kernel is timed")
     ap.add_argument("--cpu-baseline", type=int, default=1)
@@ -180,6 +182,7 @@ def main():
     world, rank, dev = setup_dist()
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     from lss_carla_amd import ops, parallel, synthetic as syn
+    from lss_carla_amd.flat_params import FlatParams
     from lss_carla_amd.train_step import TrainStep
     import lss_carla_amd as L
 
@@ -189,14 +192,18 @@ def main():
     if args.graph:
         args.inverse = "device"  # inverse='host' is a device->host round trip: not capturable
     model = build_model(args, dev, cfg, gc, dac)
-    grads = None
-    if args.graph:
-        parallel.broadcast_state(model)  # identical replicas, as DDP's constructor ensures
-        grads = parallel.FlatGradients(model, dev)
-        ddp = model
+    amp_dtype = torch.bfloat16 if args.dtype == "bf16" else None
+    flat = None
+    if args.graph or args.flat_params:
+        # one process per GPU without DDP: identical replicas, one flat gradient all-reduce
+        parallel.broadcast_state(model)
+        parallel.freeze_unused(model)
+        flat = FlatParams(model, cast_dtype=amp_dtype) if args.flat_params else None
+    if flat is not None:
+        fwd, params = flat.bind(model), [flat.master]
     else:
-        ddp = parallel.make_data_parallel(model, dev) if world > 1 else model
-    params = [p for p in model.parameters() if p.requires_grad]
+        fwd = model if (args.graph or world == 1) else parallel.make_data_parallel(model, dev)
+        params = [p for p in model.parameters() if p.requires_grad]
     loss_fn = L.SimpleLoss(2.13).to(dev)
     opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-7, fused=True, capturable=bool(args.graph))
     rig = {k: v.to(dev) for k, v in syn.make_rig(B, N, fd, seed=rank).items()}
@@ -205,10 +212,10 @@ def main():
         imgs = imgs.contiguous()
     X, Y, Z = ops.GridSpec.from_conf(gc).nx
     labels = syn.make_labels(B, X, Y, seed=rank).to(dev)
-    amp_dtype = torch.bfloat16 if args.dtype == "bf16" else None
 
-    train = TrainStep(ddp, (imgs, rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"]),
-                      labels, loss_fn, opt, params, grads=grads, amp_dtype=amp_dtype, max_grad_norm=5.0)
+    train = TrainStep(fwd, (imgs, rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"]),
+                      labels, loss_fn, opt, params, all_reduce=bool(args.graph or args.flat_params),
+                      amp_dtype=amp_dtype, max_grad_norm=5.0)
     t_w = time.perf_counter()
 
     def first(i):
@@ -284,7 +291,7 @@ def main():
                        "global_batch": world * B, "parallelism": f"dp{world}", "bev_layout": args.bev_layout,
                        "inverse": args.inverse, "fuse_depthnet": bool(args.fuse_depthnet),
                        "depthwise": args.dw_impl, "batchnorm": "hip" if args.hip_bn else "miopen",
-                       "step": "hipgraph" if args.graph else "eager"},
+                       "step": "hipgraph" if args.graph else "eager", "flat_params": bool(args.flat_params)},
             "roofline": {"kernel": "lss_splat_fwd", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,

@@ -50,12 +50,14 @@ int lss_dwconv_bwd_weight(const void* x, const void* dy, int32_t dtype, int32_t 
  * x, residual, y: (N, C, H, W) with HW = H*W, NCHW or channels-last (LSS_CONV_NHWC: C a multiple
  * of 8 with 256 % (C / 8) == 0), element type dtype; gamma, beta and every statistic fp32.
  * partial: (C, ngroups, 2) fp32 scratch, ngroups from lss_bn_groups. save_mean, save_rstd, scale,
- * shift are the four rows of one (4, C) fp32 array (outputs kept for lss_bn_bwd). */
+ * shift are the four rows of one (4, C) fp32 array (outputs kept for lss_bn_bwd).
+ * num_batches_tracked (nullable): the module's int64 counter, incremented on the device (no
+ * separate launch per BN layer). */
 int lss_bn_groups(int32_t N, int32_t C, int32_t HW, int32_t layout);
 int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layout, int32_t N, int32_t C, int32_t HW,
                const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
-               float* running_var, int32_t act, int32_t ngroups, float* partial, float* save_mean, float* save_rstd,
-               float* scale, float* shift, void* y, void* stream);
+               float* running_var, long long* num_batches_tracked, int32_t act, int32_t ngroups, float* partial,
+               float* save_mean, float* save_rstd, float* scale, float* shift, void* y, void* stream);
 
 /* Backward of lss_bn_fwd: dx (and dresidual = the gradient of the residual, nullable) of element
  * type dtype; dgamma, dbeta fp32 (nullable). y is the forward output (needed for ReLU). coef:

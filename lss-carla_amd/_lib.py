@@ -58,7 +58,7 @@ SIGNATURES = {
     "lss_dwconv_bwd_weight": (ctypes.c_int, [_p, _p, _i32] + [_i32] * 11 + [_p, _p]),
     "lss_bn_groups": (ctypes.c_int, [_i32, _i32, _i32, _i32]),
     "lss_bn_fwd": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, ctypes.c_float, ctypes.c_float,
-                                  _p, _p, _i32, _i32, _p, _p, _p, _p, _p, _p, _p]),
+                                  _p, _p, _p, _i32, _i32, _p, _p, _p, _p, _p, _p, _p]),
     "lss_bn_bwd": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p,
                                   _p, _p, _p, _p, _p]),
     "lss_upsample_cat_fwd": (ctypes.c_int, [_p, _p] + [_i32] * 7 + [_p, _p]),

@@ -196,6 +196,7 @@ struct BnParams {
     float* run_mean;
     float* run_var;
     float* stats;  // (4, C): save_mean, save_rstd, scale, shift
+    long long* batches;  // nn.BatchNorm2d.num_batches_tracked (nullable), +1 per forward
 };
 
 // statistics of channel c from its folded sums; the writer block stores running / saved values
@@ -208,6 +209,7 @@ __device__ __forceinline__ void finalize_channel(float s1, float s2, float k, fl
     scale = (P.gamma ? P.gamma[c] : 1.f) * rstd;
     shift = (P.beta ? P.beta[c] : 0.f) - mean * scale;
     if (writer) {
+        if (c == 0 && P.batches) *P.batches += 1;
         if (P.run_mean) P.run_mean[c] = (1.f - P.momentum) * P.run_mean[c] + P.momentum * mean;
         if (P.run_var)
             P.run_var[c] = (1.f - P.momentum) * P.run_var[c] + P.momentum * (n > 1.f ? var * n / (n - 1.f) : var);
@@ -555,8 +557,8 @@ int lss_bn_groups(int32_t N, int32_t C, int32_t HW, int32_t layout) {
 
 int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layout, int32_t N, int32_t C, int32_t HW,
                const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
-               float* running_var, int32_t act, int32_t ngroups, float* partial, float* save_mean, float* save_rstd,
-               float* scale, float* shift, void* y, void* stream) {
+               float* running_var, long long* num_batches_tracked, int32_t act, int32_t ngroups, float* partial,
+               float* save_mean, float* save_rstd, float* scale, float* shift, void* y, void* stream) {
     const BnGeo g{N, C, HW};
     if (!x || !y || !partial || !save_mean || !save_rstd || !scale || !shift || ngroups <= 0 || !bn_ok(g, layout))
         return LSS_CONV_EINVAL;
@@ -565,7 +567,7 @@ int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layou
     if (save_rstd != save_mean + C || scale != save_mean + 2 * C || shift != save_mean + 3 * C) return LSS_CONV_EINVAL;
     if (layout == LSS_CONV_NHWC && ngroups > kMaxGroupsNhwc) return LSS_CONV_EINVAL;
     hipStream_t s = (hipStream_t)stream;
-    const BnParams P{gamma, beta, eps, momentum, running_mean, running_var, save_mean};
+    const BnParams P{gamma, beta, eps, momentum, running_mean, running_var, save_mean, num_batches_tracked};
     const int G = ngroups;
 #define LSS_BN_FWD(T)                                                                                              \
     do {                                                                                                           \

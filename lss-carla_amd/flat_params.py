@@ -1,0 +1,126 @@
+"""Flat fp32 master parameters with per-step bf16 working copies (mixed precision in two kernels).
+
+Under bf16 autocast every conv casts its fp32 weight (and bias) to bf16 on each call and the
+backward casts each bf16 weight gradient back to fp32: ~250 small copy kernels per step at config
+3, each a few microseconds, plus one gradient-accumulation, Adam and clip pass per parameter tensor.
+``FlatParams`` keeps the trainable parameters of a module in ONE fp32 buffer (``master``, the only
+tensor the optimizer and the all-reduce see; the module's nn.Parameters become views of it, so
+state_dict and in-place updates stay coherent) and materialises, once per forward:
+
+  * the weights/biases autocast would cast (nn.Conv2d with groups == 1, nn.Linear) as bf16 views of
+    one buffer -- ``master[:n16].to(bf16)``, one kernel, the same round-to-nearest-even values the
+    autocast cast produces;
+  * the rest (BatchNorm affine parameters, depthwise weights consumed in fp32 by the lss_dwconv_*
+    kernels) as fp32 views of one copy.
+
+``forward(*args)`` runs the module with these tensors swapped in (torch.func.functional_call).
+Backward gathers the per-view gradients into one flat bf16 and one flat fp32 buffer with
+multi-tensor copies and returns ``master``'s fp32 gradient in one piece (it lands in
+``master.grad`` without an accumulation kernel). Numerics are those of autocast: identical bf16
+operands and fp32 gradients; only the summation order of clip_grad_norm_'s norm changes.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import torch
+from torch import nn
+
+
+def autocast_cast_names(model: nn.Module) -> set:
+    """Names of parameters a bf16 autocast region would cast on use: weights and biases of
+    non-grouped nn.Conv2d and of nn.Linear (depthwise convs stay fp32: lss_dwconv_* reads fp32)."""
+    names = set()
+    for mname, m in model.named_modules():
+        if (isinstance(m, nn.Conv2d) and m.groups == 1) or isinstance(m, nn.Linear):
+            for pname, _ in m.named_parameters(recurse=False):
+                names.add(f"{mname}.{pname}" if mname else pname)
+    return names
+
+
+def _dense(p: torch.Tensor) -> bool:
+    return p.is_contiguous() or (p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last))
+
+
+def _views(buf: torch.Tensor, like: List[torch.Tensor]) -> List[torch.Tensor]:
+    out, off = [], buf.storage_offset()  # as_strided offsets are absolute in the storage
+    for p in like:
+        out.append(buf.as_strided(p.shape, p.stride(), off))
+        off += p.numel()
+    return out
+
+
+class _Materialize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, master: torch.Tensor, fp: "FlatParams"):
+        n16 = fp.n16
+        if n16:
+            fp.work16.copy_(master[:n16])
+        fp.work32.copy_(master[n16:])
+        ctx.fp = fp
+        # fresh view objects per call (each carries this call's autograd history)
+        return tuple(_views(fp.work16, fp.like16) + _views(fp.work32, fp.like32))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        fp: FlatParams = ctx.fp
+        n16, k16 = fp.n16, len(fp.like16)
+        dev = fp.master.device
+        d_master = torch.empty(fp.numel, device=dev, dtype=torch.float32)
+        if n16:
+            g16 = torch.empty(n16, device=dev, dtype=fp.cast_dtype)
+            _gather(_views(g16, fp.like16), grads[:k16], g16)
+            d_master[:n16].copy_(g16)
+        _gather(_views(d_master[n16:], fp.like32), grads[k16:], d_master[n16:])
+        return d_master, None
+
+
+def _gather(dst_views, grads, buf) -> None:
+    """Copy the per-parameter gradients into their views of buf (unused parameters: zero)."""
+    if any(g is None for g in grads):
+        buf.zero_()
+    pairs = [(d, g) for d, g in zip(dst_views, grads) if g is not None]
+    if pairs:
+        torch._foreach_copy_([d for d, _ in pairs], [g.to(d.dtype) for d, g in pairs])
+
+
+class FlatParams:
+    def __init__(self, model: nn.Module, cast_dtype=torch.bfloat16):
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        if not named:
+            raise ValueError("FlatParams: no trainable parameters")
+        for n, p in named:
+            if p.dtype != torch.float32 or not _dense(p):
+                raise ValueError(f"FlatParams: {n} must be a dense fp32 tensor")
+        cast = autocast_cast_names(model) if cast_dtype is not None else set()
+        self.names16 = [n for n, _ in named if n in cast]
+        self.names32 = [n for n, _ in named if n not in cast]
+        byname = dict(named)
+        self.like16 = [byname[n] for n in self.names16]
+        self.like32 = [byname[n] for n in self.names32]
+        self.cast_dtype = cast_dtype
+        self.n16 = sum(p.numel() for p in self.like16)
+        self.numel = self.n16 + sum(p.numel() for p in self.like32)
+        dev = named[0][1].device
+        master = torch.empty(self.numel, device=dev, dtype=torch.float32)
+        with torch.no_grad():
+            for v, p in zip(_views(master, self.like16 + self.like32), self.like16 + self.like32):
+                v.copy_(p)
+                p.data = v  # the module's Parameters now alias the master buffer
+        self.master = nn.Parameter(master)
+        self.work16 = torch.empty(self.n16, device=dev, dtype=cast_dtype or torch.float32)
+        self.work32 = torch.empty(self.numel - self.n16, device=dev, dtype=torch.float32)
+
+    def tensors(self) -> Dict[str, torch.Tensor]:
+        outs = _Materialize.apply(self.master, self)
+        return dict(zip(self.names16 + self.names32, outs))
+
+    def bind(self, model: nn.Module):
+        """A callable running `model` on the materialised working parameters."""
+        def run(*args, **kwargs):
+            return torch.func.functional_call(model, self.tensors(), args, kwargs, strict=False)
+        return run
+
+    def views_of(self, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """Per-parameter views (the original shapes/strides) of a flat tensor laid out like master."""
+        return dict(zip(self.names16 + self.names32, _views(flat, self.like16 + self.like32)))

@@ -47,15 +47,18 @@ class _BnAct(torch.autograd.Function):
         partial = torch.empty(C, groups, 2, **f32)
         stats = torch.empty(4, C, **f32)  # save_mean, save_rstd, scale, shift
         momentum = bn.momentum if bn.momentum is not None else 0.0
+        counter = None  # num_batches_tracked: incremented by the kernel
         if bn.track_running_stats and bn.num_batches_tracked is not None:
-            bn.num_batches_tracked.add_(1)
-            if bn.momentum is None:  # cumulative moving average
+            if bn.momentum is None:  # cumulative moving average: the factor needs the count on the host
+                bn.num_batches_tracked.add_(1)
                 momentum = 1.0 / float(bn.num_batches_tracked.item())
+            else:
+                counter = bn.num_batches_tracked
         rm = bn.running_mean if bn.track_running_stats else None
         rv = bn.running_var if bn.track_running_stats else None
         _lib.check(lib.lss_bn_fwd(_lib.ptr(x), _lib.ptr(residual), _lib.dtype_code(x.dtype), layout, N, C, HW,
                                   _lib.ptr(weight), _lib.ptr(bias), float(bn.eps), float(momentum), _lib.ptr(rm),
-                                  _lib.ptr(rv), act, groups, _lib.ptr(partial), _lib.ptr(stats[0]),
+                                  _lib.ptr(rv), _lib.ptr(counter), act, groups, _lib.ptr(partial), _lib.ptr(stats[0]),
                                   _lib.ptr(stats[1]), _lib.ptr(stats[2]), _lib.ptr(stats[3]), _lib.ptr(y), st),
                    "lss_bn_fwd")
         ctx.save_for_backward(x, y if act == ACT["relu"] else None, stats)

@@ -71,47 +71,6 @@ def broadcast_state(model: torch.nn.Module, src: int = 0) -> None:
             dist.broadcast(t.data, src)
 
 
-class FlatGradients:
-    """The gradients of every trainable parameter as views of ONE flat fp32 buffer.
-
-    For the captured training step (bench.py --graph): backward accumulates into the views (the
-    graph replays write the same addresses every step), one all_reduce of the flat buffer runs
-    between the forward/backward graph and the optimizer graph, and ``average()`` divides by the
-    world size. Same averaged gradients as DDP (``make_data_parallel``), one collective of the whole
-    ~50 MB gradient instead of DDP's bucketed overlap -- on xGMI one large ring all-reduce is
-    link-bandwidth bound either way. Each view keeps its parameter's strides (channels-last
-    weights), so fused optimizers see matching parameter / gradient layouts.
-    """
-
-    def __init__(self, model: torch.nn.Module, device: torch.device):
-        freeze_unused(model)
-        self.params = [p for p in model.parameters() if p.requires_grad]
-        for p in self.params:
-            if p.dtype != torch.float32:
-                raise TypeError(f"FlatGradients: fp32 parameters only, got {p.dtype}")
-            if not (p.is_contiguous() or (p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last))):
-                raise ValueError("FlatGradients: parameters must be dense (contiguous or channels-last)")
-        self.numel = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(self.numel, device=device, dtype=torch.float32)
-        off = 0
-        for p in self.params:
-            p.grad = self.flat.as_strided(p.shape, p.stride(), off)
-            off += p.numel()
-        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
-
-    def zero(self) -> None:
-        self.flat.zero_()
-
-    def all_reduce(self) -> None:
-        """Sum over ranks (eager: call it outside any graph capture)."""
-        if self.world > 1:
-            dist.all_reduce(self.flat)
-
-    def average(self) -> None:
-        if self.world > 1:
-            self.flat.mul_(1.0 / self.world)
-
-
 def max_over_ranks(value: float, device: torch.device) -> float:
     if not (dist.is_available() and dist.is_initialized()):
         return value

@@ -1,38 +1,43 @@
 """The training step of train_simbev.py:229-248 -- forward, SimpleLoss, backward,
 clip_grad_norm_(max_grad_norm), Adam -- eager, or replayed as two HIP graphs.
 
-A B=8 step launches ~1000 kernels (conv stacks, BN, the lift/splat path, fused Adam); eager, the
+A B=8 step launches ~2000 kernels (conv stacks, BN, the lift/splat path, optimizer); eager, the
 host's Python + launch cost per kernel is longer than many of the kernels, so the GPU idles.
 Captured (``torch.cuda.CUDAGraph``, i.e. hipGraph), the step is two graph launches:
 
-  graph A  zero the flat gradient buffer, forward under bf16 autocast, loss, backward
-  (eager)  all-reduce of the flat gradient buffer over RCCL (world size > 1)
+  graph A  forward under bf16 autocast, loss, backward
+  (eager)  all-reduce of the gradients over RCCL (world size > 1)
   graph B  divide by the world size, clip_grad_norm_, fused Adam (capturable)
 
-The collective stays outside the graphs: one ~50 MB ring all-reduce over xGMI per step, the
-same averaged gradients as DDP (parallel.FlatGradients). Every op of the LSS path is capturable:
-its kernels only take device pointers, and the plan's sizes come from the static shapes; the one
-host round trip of the reference (torch.inverse on the CPU, src/models.py:180,186) is replaced by
-the device inverse (ops.camera_inverses(mode='device')).
+With ``flat_params.FlatParams`` the trainable parameters are one fp32 tensor, so the gradient is one
+tensor too: one ~50 MB ring all-reduce over xGMI per step (the same averaged gradient as DDP), a
+single-tensor Adam and norm. Every op of the LSS path is capturable: its kernels take device
+pointers only and the plan's sizes come from the static shapes; the one host round trip of the
+reference (torch.inverse on the CPU, src/models.py:180,186) is replaced by the device inverse
+(ops.camera_inverses(mode='device')).
 """
 from __future__ import annotations
 
 from typing import Callable, Optional, Sequence
 
 import torch
-
-from .parallel import FlatGradients
+import torch.distributed as dist
 
 
 class TrainStep:
+    """forward(*inputs) -> preds; params: what the optimizer updates (e.g. [FlatParams.master]);
+    all_reduce: average params' gradients over the process group here (False under DDP)."""
+
     def __init__(self, forward: Callable[..., torch.Tensor], inputs: Sequence[torch.Tensor], labels: torch.Tensor,
-                 loss_fn: Callable, opt: torch.optim.Optimizer, params: Sequence[torch.nn.Parameter],
-                 grads: Optional[FlatGradients] = None, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
+                 loss_fn: Callable, opt: torch.optim.Optimizer, params: Sequence[torch.Tensor],
+                 all_reduce: bool = False, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
                  max_grad_norm: float = 5.0):
         self.forward, self.inputs, self.labels = forward, tuple(inputs), labels
-        self.loss_fn, self.opt, self.params, self.grads = loss_fn, opt, list(params), grads
+        self.loss_fn, self.opt, self.params = loss_fn, opt, list(params)
         self.amp_dtype, self.max_grad_norm = amp_dtype, max_grad_norm
+        self.world = dist.get_world_size() if (all_reduce and dist.is_available() and dist.is_initialized()) else 1
         self.graphs = None
+        self.graph_grads = None
         self.static_loss = None
 
     @property
@@ -40,10 +45,7 @@ class TrainStep:
         return self.graphs is not None
 
     def forward_backward(self) -> torch.Tensor:
-        if self.grads is not None:
-            self.grads.zero()
-        else:
-            self.opt.zero_grad(set_to_none=True)
+        self.opt.zero_grad(set_to_none=True)  # backward's gradient is stolen, not accumulated
         dev_type = self.labels.device.type
         # autocast's cast cache must be off while capturing (its entries would outlive the capture)
         capturing = dev_type == "cuda" and torch.cuda.is_current_stream_capturing()
@@ -54,25 +56,30 @@ class TrainStep:
         loss.backward()
         return loss
 
+    def all_reduce(self, grads=None) -> None:
+        """Sum the gradients over ranks (eager: outside any capture)."""
+        if self.world > 1:
+            for g in (grads if grads is not None else [p.grad for p in self.params]):
+                if g is not None:
+                    dist.all_reduce(g)
+
     def update(self) -> None:
-        if self.grads is not None:
-            self.grads.average()
+        if self.world > 1:
+            for p in self.params:
+                if p.grad is not None:
+                    p.grad.mul_(1.0 / self.world)
         torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)
         self.opt.step()
 
     def eager(self) -> torch.Tensor:
         loss = self.forward_backward()
-        if self.grads is not None:
-            self.grads.all_reduce()
+        self.all_reduce()
         self.update()
         return loss
 
     def capture(self, warmup: int = 2, on_warmup: Optional[Callable[[int], None]] = None) -> None:
         """`warmup` eager steps on a side stream (MIOpen find, optimizer state, allocator), then
-        capture. Needs FlatGradients (gradient addresses fixed across replays) and an optimizer
-        built with capturable=True."""
-        if self.grads is None:
-            raise RuntimeError("TrainStep.capture needs FlatGradients")
+        capture (the optimizer must be built with capturable=True)."""
         dev = self.labels.device
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
@@ -86,8 +93,10 @@ class TrainStep:
         g_fb, g_up = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_fb):
             # detached: holding the captured autograd graph would keep its AccumulateGrad nodes
-            # (bound to the capture stream) alive into later eager steps
+            # (bound to the capture stream) alive into later eager steps. The gradients allocated
+            # here (graph pool) are what graph B and the all-reduce read on every replay.
             self.static_loss = self.forward_backward().detach()
+        self.graph_grads = [p.grad for p in self.params]
         with torch.cuda.graph(g_up, pool=g_fb.pool()):
             self.update()
         self.graphs = (g_fb, g_up)
@@ -97,6 +106,6 @@ class TrainStep:
             return self.eager()
         g_fb, g_up = self.graphs
         g_fb.replay()
-        self.grads.all_reduce()
+        self.all_reduce(self.graph_grads)
         g_up.replay()
         return self.static_loss

@@ -15,6 +15,7 @@ import torch.multiprocessing as mp
 
 import lss_carla_amd as L
 from lss_carla_amd import parallel
+from lss_carla_amd.flat_params import FlatParams
 from lss_carla_amd import synthetic as syn
 
 FD = (64, 192)
@@ -73,7 +74,7 @@ def _worker(rank, world, port, outdir):
     if rank == 0:
         torch.save({n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None},
                    os.path.join(outdir, "ddp.pt"))
-    # the captured-step path: broadcast replicas, gradients in one flat buffer, one all-reduce
+    # the captured-step path: broadcast replicas, flat master parameters, one all-reduce
     m2 = _model()
     if rank == 1:
         with torch.no_grad():
@@ -81,15 +82,15 @@ def _worker(rank, world, port, outdir):
                 if p.is_floating_point():
                     p.add_(1.0)
     parallel.broadcast_state(m2)
-    flat = parallel.FlatGradients(m2, dev)
-    flat.zero()
-    _grads(_CpuLSS(m2), seed=10 + rank)
-    flat.all_reduce()
-    flat.average()
-    assert all(p.grad.data_ptr() >= flat.flat.data_ptr() for p in flat.params)  # still the views
+    parallel.freeze_unused(m2)
+    wrapped = _CpuLSS(m2)
+    flat = FlatParams(wrapped, cast_dtype=None)
+    _grads(flat.bind(wrapped), seed=10 + rank)
+    dist.all_reduce(flat.master.grad)
+    flat.master.grad.mul_(1.0 / world)
     if rank == 0:
-        torch.save({n: p.grad.clone().contiguous() for n, p in m2.named_parameters() if p.requires_grad},
-                   os.path.join(outdir, "flat.pt"))
+        g = {n.removeprefix("model."): v.clone().contiguous() for n, v in flat.views_of(flat.master.grad).items()}
+        torch.save(g, os.path.join(outdir, "flat.pt"))
     t = parallel.max_over_ranks(float(rank), dev)
     assert t == world - 1
     dist.destroy_process_group()
@@ -125,7 +126,7 @@ def test_ddp_gradients_equal_mean_of_replicas():
         err = (ddp[n] - ref[n]).abs().max() / scale
         assert err < 1e-3, (n, float(err), float(scale))
     assert not any(n.startswith(parallel.UNUSED_PREFIXES) for n in ddp)
-    # FlatGradients (bench.py --graph): same averaged gradients, frozen head excluded
+    # FlatParams + one all-reduce (bench.py --graph): same averaged gradients, frozen head excluded
     assert set(flat) == set(ref)
     for n in ref:
         scale = ref[n].abs().max().clamp_min(1e-12)
@@ -145,24 +146,32 @@ def test_freeze_unused_counts_head_params():
     assert all(not p.requires_grad for n, p in m.named_parameters() if n.startswith(parallel.UNUSED_PREFIXES))
 
 
-def test_flat_gradients_single_process_channels_last():
-    """World size 1: the views keep each parameter's strides (channels-last convs) and receive the
-    same gradients as freshly allocated .grad tensors; average() / all_reduce() are no-ops."""
+def test_flat_params_match_autocast_gradients():
+    """FlatParams under CPU bf16 autocast: same forward and parameter gradients as the module run
+    with its own Parameters (autocast casting each weight), channels-last weights included."""
     torch.manual_seed(3)
     net = torch.nn.Sequential(torch.nn.Conv2d(8, 16, 3, padding=1), torch.nn.BatchNorm2d(16), torch.nn.ReLU(),
+                              torch.nn.Conv2d(16, 16, 3, padding=1, groups=16, bias=False),
                               torch.nn.Conv2d(16, 4, 1)).to(memory_format=torch.channels_last)
     x = torch.randn(2, 8, 10, 12).contiguous(memory_format=torch.channels_last)
-    net(x).square().mean().backward()
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        y0 = net(x)
+    y0.float().square().mean().backward()
     want = {n: p.grad.clone() for n, p in net.named_parameters()}
-    flat = parallel.FlatGradients(net, torch.device("cpu"))
+    flat = FlatParams(net, cast_dtype=torch.bfloat16)
+    assert set(flat.names16) == {"0.weight", "0.bias", "4.weight", "4.bias"}  # depthwise + BN stay fp32
     assert flat.numel == sum(p.numel() for p in net.parameters())
-    for p in net.parameters():
-        assert p.grad.stride() == p.stride()
-    flat.zero()
-    net(x).square().mean().backward()
-    flat.all_reduce()
-    flat.average()
-    base, end = flat.flat.data_ptr(), flat.flat.data_ptr() + 4 * flat.numel
-    for n, p in net.named_parameters():
-        assert base <= p.grad.data_ptr() < end, n
-        torch.testing.assert_close(p.grad, want[n], rtol=1e-6, atol=1e-7)
+    for p in net.parameters():  # the module's Parameters alias the master buffer
+        base, end = flat.master.data_ptr(), flat.master.data_ptr() + 4 * flat.numel
+        assert base <= p.data_ptr() < end
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        y1 = flat.bind(net)(x)
+    assert torch.equal(y0, y1)
+    y1.float().square().mean().backward()
+    got = flat.views_of(flat.master.grad)
+    for n in want:
+        torch.testing.assert_close(got[n], want[n], rtol=0, atol=0)
+    # an optimizer step on master is seen by the module
+    with torch.no_grad():
+        flat.master.add_(1.0)
+    assert torch.equal(net[0].bias.detach(), flat.views_of(flat.master.detach())["0.bias"])
