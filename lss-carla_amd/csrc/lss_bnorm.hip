@@ -325,17 +325,21 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_apply_nchw(const T* __restric
 // block q: pixels [M q / G, M (q+1) / G) x all C channels; thread = 8 consecutive channels of a pixel.
 // Partials (C, G, 2) as in NCHW; a separate fold kernel (one wave per channel) turns them into the
 // per-channel coefficients the apply passes read.
+// A thread keeps one channel octet (kBlock % (C/8) == 0) and walks the block's pixels with a stride
+// of kBlock / (C/8) rows, four rows per iteration so four 16-byte loads are in flight; 32-bit
+// offsets (the host checks N*HW*C < 2^31).
 template <typename T, typename F>
 __device__ __forceinline__ void for_chunk_nhwc(const BnGeo& g, int G, int q, F&& f) {
-    const long M = (long)g.N * g.HW;
-    const long r0 = M * q / G, r1 = M * (q + 1) / G;
-    const int cg = g.C / 8;
-    const long count = (r1 - r0) * cg;
-    for (long e = threadIdx.x; e < count; e += kBlock) {
-        const long r = r0 + e / cg;
-        const int c0 = (int)(e % cg) * 8;
-        f((size_t)r * g.C + c0, c0);
+    const int M = g.N * g.HW;
+    const int r0 = (int)((long)M * q / G), r1 = (int)((long)M * (q + 1) / G);
+    const int cg = g.C >> 3;
+    const int step = kBlock / cg;
+    const int c0 = ((int)threadIdx.x % cg) * 8;
+    int r = r0 + (int)threadIdx.x / cg;
+    for (; r + 3 * step < r1; r += 4 * step) {
+        f(r * g.C + c0, (r + step) * g.C + c0, (r + 2 * step) * g.C + c0, (r + 3 * step) * g.C + c0);
     }
+    for (; r < r1; r += step) f(r * g.C + c0, -1, -1, -1);
 }
 
 // per-thread 8-channel sums -> per-channel block sums in LDS [C][2] -> partial[q][c][2]
@@ -371,14 +375,21 @@ __global__ __launch_bounds__(kBlock) void k_bn_stats_nhwc(const T* __restrict__ 
     float k[8];
     ldv<8>(x + c0, k);  // first pixel: the shifts
     float a[8] = {}, b[8] = {};
-    for_chunk_nhwc<T>(g, G, blockIdx.x, [&](size_t i, int) {
-        float v[8];
-        ldv<8>(x + i, v);
+    for_chunk_nhwc<T>(g, G, blockIdx.x, [&](int i0, int i1, int i2, int i3) {
+        const int idx[4] = {i0, i1, i2, i3};
+        float v[4][8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float d = v[j] - k[j];
-            a[j] += d;
-            b[j] = fmaf(d, d, b[j]);
+        for (int u = 0; u < 4; ++u)
+            if (idx[u] >= 0) ldv<8>(x + idx[u], v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (idx[u] < 0) continue;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float d = v[u][j] - k[j];
+                a[j] += d;
+                b[j] = fmaf(d, d, b[j]);
+            }
         }
     });
     nhwc_block_sums(g, G, blockIdx.x, a, b, c0, (int)threadIdx.x < (kBlock / cg) * cg, s_dyn, partial);
@@ -472,16 +483,26 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_stats_nhwc(const T* __restric
         sh[j] = stats[3 * g.C + c0 + j];
     }
     float a[8] = {}, b[8] = {};
-    for_chunk_nhwc<T>(g, G, blockIdx.x, [&](size_t i, int) {
-        float d[8], xv[8], yv[8];
-        ldv<8>(dy + i, d);
-        ldv<8>(x + i, xv);
-        if (act == LSS_ACT_RELU) ldv<8>(y + i, yv);
+    const bool relu = act == LSS_ACT_RELU;
+    for_chunk_nhwc<T>(g, G, blockIdx.x, [&](int i0, int i1, int i2, int i3) {
+        const int idx[4] = {i0, i1, i2, i3};
+        float d[4][8], xv[4][8], yv[4][8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float gr = grad_pre(d[j], act == LSS_ACT_RELU ? yv[j] : 0.f, fmaf(xv[j], sc[j], sh[j]), act);
-            a[j] += gr;
-            b[j] = fmaf(gr, (xv[j] - mean[j]) * rstd[j], b[j]);
+        for (int u = 0; u < 4; ++u) {
+            if (idx[u] < 0) continue;
+            ldv<8>(dy + idx[u], d[u]);
+            ldv<8>(x + idx[u], xv[u]);
+            if (relu) ldv<8>(y + idx[u], yv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (idx[u] < 0) continue;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float gr = grad_pre(d[u][j], relu ? yv[u][j] : 0.f, fmaf(xv[u][j], sc[j], sh[j]), act);
+                a[j] += gr;
+                b[j] = fmaf(gr, (xv[u][j] - mean[j]) * rstd[j], b[j]);
+            }
         }
     });
     nhwc_block_sums(g, G, blockIdx.x, a, b, c0, (int)threadIdx.x < (kBlock / cg) * cg, s_dyn, partial);
@@ -547,8 +568,8 @@ extern "C" {
 
 int lss_bn_groups(int32_t N, int32_t C, int32_t HW, int32_t layout) {
     const long per_chan = (long)N * HW;
-    if (layout == LSS_CONV_NHWC) {  // ~32 K elements per block
-        const long g = per_chan * C / 32768;
+    if (layout == LSS_CONV_NHWC) {
+        const long g = per_chan * C / 8192;  // ~8 K elements (32 per thread) per block
         return (int)(g < 1 ? 1 : (g > kMaxGroupsNhwc ? kMaxGroupsNhwc : g));
     }
     const long g = per_chan / 8192;  // ~8 K elements of one channel per block
