@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 8
+#define LSS_ABI_VERSION 9
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -88,20 +88,26 @@ int lss_cells_from_geom(const float* geom, int32_t nprime, int32_t points_per_ba
  * (cell << 32) | p, followed by the sentinel key -1 in every slot from cell_start[ncells] to
  * Nprime; sorted_row (Nprime capacity) = the row each entry's features are read from: the pixel
  * q(p) when dims is given (fused lift), p itself when dims is NULL (per-point rows); defined for
- * the first cell_start[ncells] entries. scratch: lss_csr_scratch_bytes bytes. */
+ * the first cell_start[ncells] entries. pos_of (Nprime, nullable) = the inverse permutation: the
+ * sorted position of point p, -1 for a dropped point (lets the lift write its depth weights in CSR
+ * order, see lss_lift_prep). scratch: lss_csr_scratch_bytes bytes. */
 size_t lss_csr_scratch_bytes(int32_t ncells, int32_t nprime);
 int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime,
                   const int32_t* cell_count, int32_t ncells, const lss_dims_t* dims,
-                  int32_t* cell_start, long long* sorted_key, int32_t* sorted_row, void* scratch,
-                  lss_stream_t stream);
+                  int32_t* cell_start, long long* sorted_key, int32_t* sorted_row, int32_t* pos_of,
+                  void* scratch, lss_stream_t stream);
 
 /* Lift, part 1 (CamEncode.get_depth_dist + layout, src/models.py:49-59, 192-202):
  * depth (B*N, D, H, W) fp32 = softmax over D of depthnet_out[:, :D];
  * ctx_t (B*N*H*W, C), element type ctx_dtype = depthnet_out[:, D:D+C] moved to pixel-major rows
  * (bf16 rows are exact when depthnet_out is bf16, as under autocast).
- * depthnet_out is (B*N, D+C, H, W) contiguous, element type in_dtype. */
+ * depthnet_out is (B*N, D+C, H, W) contiguous, element type in_dtype. With pos_of (from
+ * lss_csr_build; nullable) every kept point's weight is also written to sorted_depth[pos_of[p]]
+ * (Nprime fp32): the splat then reads its weights contiguously, in CSR order, instead of
+ * gathering depth[p] per entry. */
 int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims,
-                  float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream);
+                  float* depth, void* ctx_t, int32_t ctx_dtype, const int32_t* pos_of,
+                  float* sorted_depth, lss_stream_t stream);
 
 /* Depthnet + lift, part 1, fused (CamEncode.depthnet 1x1 conv + get_depth_dist + layout,
  * src/models.py:47, 55-59, 192-202): logits = weight . feat + bias on MFMA (bf16 in, fp32
@@ -110,10 +116,11 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
  * depthnet output (B*N, D+C, H, W) is never written. feat (B*N, K, H, W) contiguous, weight
  * (D+C, K) row-major, bias (D+C); dtype and ctx_dtype must be LSS_BF16; K % 16 == 0, K <= 512,
  * D + C <= 128 (else LSS_EUNSUPPORTED). The backward stays the conv's: d(logits) from
- * lss_splat_bwd feeds the 1x1 conv's weight / input gradients. */
+ * lss_splat_bwd feeds the 1x1 conv's weight / input gradients. pos_of / sorted_depth as in
+ * lss_lift_prep. */
 int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
                       const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype,
-                      lss_stream_t stream);
+                      const int32_t* pos_of, float* sorted_depth, lss_stream_t stream);
 
 /* Splat forward: segmented per-cell sum written as the dense (B, Z*C, X, Y) BEV
  * (voxel_pooling + QuickCumsum.forward + griddify, src/models.py:233-246,
@@ -126,12 +133,14 @@ int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, in
  * 64-entry chunk of the CSR (one gather round trip, LDS-staged ordered sums, rows stored
  * directly) plus zero-fill waves; LSS_NCHW: a BEV-row tile kernel (<= 128 cells per tile along Y)
  * with an LDS transpose. sorted_key / sorted_row as lss_csr_build wrote them (sorted_row is
- * unused in lifted mode, where the rows are the point ids).
+ * unused in lifted mode, where the rows are the point ids). sorted_depth (nullable, fused mode):
+ * the depth weights in CSR order as lss_lift_prep / lss_depthnet_lift wrote them; LSS_NHWC then
+ * reads them with the keys instead of gathering depth[p] (the same values: identical results).
  * ev_start / ev_stop (nullable) are stamped with the kernel's own start / end
  * (hipExtLaunchKernel), so their elapsed time is the kernel alone, never launch latency. */
 int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
                   const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
-                  const lss_dims_t* dims, const lss_grid_t* grid,
+                  const float* sorted_depth, const lss_dims_t* dims, const lss_grid_t* grid,
                   void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream,
                   lss_event_t ev_start, lss_event_t ev_stop);
 

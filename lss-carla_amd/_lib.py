@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(_HERE, "liblss_hip.so")
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class Dims(ctypes.Structure):
@@ -45,10 +45,10 @@ SIGNATURES = {
     "lss_geometry_cells": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _p, _p, _p, _p]),
     "lss_cells_from_geom": (ctypes.c_int, [_p, _i32, _i32, _GRID, _p, _p, _p, _p]),
     "lss_csr_scratch_bytes": (ctypes.c_size_t, [_i32, _i32]),
-    "lss_csr_build": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p]),
-    "lss_lift_prep": (ctypes.c_int, [_p, _i32, _DIMS, _p, _p, _i32, _p]),
-    "lss_depthnet_lift": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p]),
-    "lss_splat_fwd": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _p, _p, _p]),
+    "lss_csr_build": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p, _p]),
+    "lss_lift_prep": (ctypes.c_int, [_p, _i32, _DIMS, _p, _p, _i32, _p, _p, _p]),
+    "lss_depthnet_lift": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p, _p, _p]),
+    "lss_splat_fwd": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _p, _p, _p]),
     "lss_bev_rows": (ctypes.c_int, [_p, _i32, _p, _DIMS, _GRID, _p, _p]),
     "lss_splat_bwd": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p, _i32, _DIMS, _GRID, _p, _i32, _p]),
     "lss_splat_bwd_lifted": (ctypes.c_int, [_p, _i32, _i32, _p, _i32, _DIMS, _GRID, _p, _p]),

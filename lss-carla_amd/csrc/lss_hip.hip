@@ -310,7 +310,9 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
                                                       const int32_t* __restrict__ total_ptr, int nchunks, int nprime,
                                                       int DHW,
                                                       int HW, long long* __restrict__ key_out,
-                                                      int32_t* __restrict__ row_out) {
+                                                      int32_t* __restrict__ row_out,
+                                                      const int32_t* __restrict__ cell_of,
+                                                      int32_t* __restrict__ pos_out) {
     const int lane = threadIdx.x & 63;
     const int w = blockIdx.x * (kBlock / kWave) + uniform(threadIdx.x >> 6);
     if (w >= nchunks) return;
@@ -319,6 +321,8 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
     const int e0 = base + lane, e1 = base + kWave + lane;
     // sentinel tail: entries [total, nprime) hold key -1 (cell -1), so a reader needs no entry count
     if (e0 >= total && e0 < nprime) key_out[e0] = -1ll;
+    // sorted position of every point (pos_out[p], -1 = dropped): dropped points here, kept ones below
+    if (pos_out && e0 < nprime && cell_of[e0] < 0) pos_out[e0] = -1;
     if (base >= total) return;
     const long long k0 = e0 < total ? key_in[e0] : -1ll;
     const long long k1 = e1 < total ? key_in[e1] : -1ll;
@@ -346,10 +350,12 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
     if (e0 >= cc.s && e0 < cc.end) {
         key_out[cs0 + r0] = k0;
         row_out[cs0 + r0] = point_row(p0, DHW, HW);
+        if (pos_out) pos_out[p0] = cs0 + r0;
     }
     if (e1 >= cc.s && e1 < cc.end) {
         key_out[cs1 + r1] = k1;
         row_out[cs1 + r1] = point_row(p1, DHW, HW);
+        if (pos_out) pos_out[p1] = cs1 + r1;
     }
     if (cc.big_start >= 0) {
         // one cell with more than 64 entries: ordered selection straight from memory (rare)
@@ -367,6 +373,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
             if (lane == 0) {
                 key_out[cc.big_start + k] = ((long long)cell << 32) | (unsigned)best;
                 row_out[cc.big_start + k] = point_row(best, DHW, HW);
+                if (pos_out) pos_out[best] = cc.big_start + k;
             }
             last = best;
         }
@@ -381,7 +388,9 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
 // pixel-major rows ctx_t[q*64 + c] (coalesced 256-B rows).
 template <typename InT, typename CT>
 __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn, int D, int HW, int npix,
-                                                      float* __restrict__ depth, CT* __restrict__ ctx_t) {
+                                                      float* __restrict__ depth, CT* __restrict__ ctx_t,
+                                                      const int32_t* __restrict__ pos_of,
+                                                      float* __restrict__ sorted_depth) {
     __shared__ float s_ctx[kC][65];
     __shared__ float s_red[2][4][64];
     const int q0 = blockIdx.x * 64;
@@ -419,7 +428,14 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int d = part + 4 * i;
-            if (d < D) dst[(size_t)d * HW] = e[i] / sum;
+            if (d < D) {
+                const float v = e[i] / sum;
+                dst[(size_t)d * HW] = v;
+                if (pos_of) {  // the same weight at the point's CSR position (contiguous reads in the splat)
+                    const int at = pos_of[(bn * D + d) * HW + hw];
+                    if (at >= 0) sorted_depth[at] = v;
+                }
+            }
         }
     }
     for (int i = threadIdx.x; i < 64 * kC; i += kBlock) {
@@ -443,7 +459,9 @@ constexpr int kDnMaxO = 128;  // D + C <= 4 waves x 32 output channels
 
 __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict__ feat, const bf16* __restrict__ weight,
                                                           const bf16* __restrict__ bias, int K, int D, int HW,
-                                                          int npix, float* __restrict__ depth, bf16* __restrict__ ctx_t) {
+                                                          int npix, float* __restrict__ depth, bf16* __restrict__ ctx_t,
+                                                          const int32_t* __restrict__ pos_of,
+                                                          float* __restrict__ sorted_depth) {
     using bf16x8 = __attribute__((ext_vector_type(8))) short;
     using f32x16 = __attribute__((ext_vector_type(16))) float;
     __shared__ __attribute__((aligned(16))) bf16 s_x[kDnPix][kDnMaxK + 8];  // [pixel][k]; +8: spread the banks
@@ -517,7 +535,14 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
     if (q < npix) {
         const int bn = q / HW, hw = q - bn * HW;
         float* dst = depth + (size_t)bn * D * HW + hw;
-        for (int d = part; d < D; d += kParts) dst[(size_t)d * HW] = expf(s_lg[d][p] - m) / sum;
+        for (int d = part; d < D; d += kParts) {
+            const float v = expf(s_lg[d][p] - m) / sum;
+            dst[(size_t)d * HW] = v;
+            if (pos_of) {
+                const int at = pos_of[(bn * D + d) * HW + hw];
+                if (at >= 0) sorted_depth[at] = v;
+            }
+        }
     }
     // context rows: 64 consecutive channels of a pixel = one 128-B row
     for (int i = threadIdx.x; i < kDnPix * kC; i += kBlock) {
@@ -916,12 +941,13 @@ __device__ __forceinline__ void store_slice(bf16* dst, const float* a) {
 constexpr int kUnroll = LSS_UNROLL;
 
 // Entry metadata of a chunk's 128-entry window, staged once in LDS: (row, point, cell).
-struct EntryMeta {
-    int row, p, cell, pad;
+struct alignas(16) EntryMeta {
+    int row, p, cell, wbits;  // wbits: the depth weight (float bits) when the CSR-ordered copy is given
 };
 
 template <bool FUSED, typename RT, typename OutT>
 __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __restrict__ depth,
+                                            const float* __restrict__ sorted_depth,
                                             const RT* __restrict__ rows_base,
                                             const long long* __restrict__ sorted_key,
                                             const int32_t* __restrict__ sorted_row, const BevGeo& g,
@@ -939,6 +965,13 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
         rs1 = e1 < nprime ? sorted_row[e1] : 0;
     }
     const int prevcell = base > 0 ? (int)(sorted_key[base - 1] >> 32) : -2;
+    // depth weights in CSR order (coalesced, same round trip) when the lift wrote them
+    const bool sorted_w = FUSED && sorted_depth != nullptr;
+    float sw0 = 0.f, sw1 = 0.f;
+    if (sorted_w) {
+        sw0 = e0 < nprime ? sorted_depth[e0] : 0.f;
+        sw1 = e1 < nprime ? sorted_depth[e1] : 0.f;
+    }
     const int c0 = (int)(k0 >> 32), c1 = (int)(k1 >> 32);
     const int p0 = (int)(k0 & 0xFFFFFFFF), p1 = (int)(k1 & 0xFFFFFFFF);
     if (!FUSED) {
@@ -953,8 +986,8 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
         return;
     }
     if (end > 0) {
-        meta[lane] = EntryMeta{rs0, p0, c0, 0};
-        meta[kWave + lane] = EntryMeta{rs1, p1, c1, 0};
+        meta[lane] = EntryMeta{rs0, p0, c0, __float_as_int(sw0)};
+        meta[kWave + lane] = EntryMeta{rs1, p1, c1, __float_as_int(sw1)};
         __builtin_amdgcn_wave_barrier();
         const int up = __shfl(c0, (lane + 63) & 63, kWave);
         const unsigned long long starts = __ballot(c0 != (lane == 0 ? prevcell : up)) &
@@ -993,9 +1026,9 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
             float wt[kUnroll];
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
-                const int2 m = *reinterpret_cast<const int2*>(&meta[min(e + u, ge - 1)]);  // (row, p)
+                const int4 m = *reinterpret_cast<const int4*>(&meta[min(e + u, ge - 1)]);  // (row, p, cell, w)
                 v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)m.x * kC + col);
-                wt[u] = (FUSED && !LSS_NO_DEPTH) ? depth[m.y] : 1.f;
+                wt[u] = (FUSED && !LSS_NO_DEPTH) ? (sorted_w ? __int_as_float(m.w) : depth[m.y]) : 1.f;
             }
             if (LSS_CHUNK_STOP == 2) {
                 unsigned x = 0;
@@ -1052,6 +1085,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 
 template <bool FUSED, typename RT, typename OutT>
 __global__ __launch_bounds__(kBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const float* __restrict__ depth,
+                                                           const float* __restrict__ sorted_depth,
                                                            const RT* __restrict__ rows_base,
                                                            const int32_t* __restrict__ cell_start,
                                                            const long long* __restrict__ sorted_key,
@@ -1086,7 +1120,7 @@ __global__ __launch_bounds__(kBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const 
         if (cb >= nchunk_blocks) return;
         const int w = cb * (kBlock / kWave) + wave;
         LSS_STAMP(w, 0);
-        splat_chunk<FUSED, RT, OutT>(w, nprime, depth, rows_base, sorted_key, sorted_row, g, out, s_meta[wave],
+        splat_chunk<FUSED, RT, OutT>(w, nprime, depth, sorted_depth, rows_base, sorted_key, sorted_row, g, out, s_meta[wave],
                                      s_part[wave], lane);
         LSS_STAMP(w, 3);
 #if LSS_TRACE
@@ -1353,7 +1387,7 @@ size_t lss_csr_scratch_bytes(int32_t ncells, int32_t nprime) {
 
 int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, const int32_t* cell_count,
                   int32_t ncells, const lss_dims_t* dims, int32_t* cell_start, long long* sorted_key,
-                  int32_t* sorted_row, void* scratch, lss_stream_t stream) {
+                  int32_t* sorted_row, int32_t* pos_of, void* scratch, lss_stream_t stream) {
     if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !sorted_row || !scratch || nprime <= 0 ||
         ncells <= 0)
         return LSS_EINVAL;
@@ -1375,20 +1409,21 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
                        cell_start, tmp_key);
     const int nchunks = (nprime + kWave - 1) / kWave;
     hipLaunchKernelGGL(k_csr_canon, dim3(grid_blocks(nchunks, kBlock / kWave)), dim3(kBlock), 0, s, tmp_key,
-                       cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row);
+                       cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row, cell_of, pos_of);
     return launch_status();
 }
 
 int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims, float* depth, void* ctx_t,
-                  int32_t ctx_dtype, lss_stream_t stream) {
-    if (!dims_ok(dims) || !depthnet_out || !depth || !ctx_t) return LSS_EINVAL;
+                  int32_t ctx_dtype, const int32_t* pos_of, float* sorted_depth, lss_stream_t stream) {
+    if (!dims_ok(dims) || !depthnet_out || !depth || !ctx_t || (pos_of && !sorted_depth)) return LSS_EINVAL;
     if (dims->D > 64) return LSS_EUNSUPPORTED;
     const int HW = dims->H * dims->W;
     const int npix = dims->B * dims->N * HW;
     const dim3 grid(grid_blocks(npix, 64)), block(kBlock);
     hipStream_t s = (hipStream_t)stream;
 #define LSS_PREP(IT, CT) \
-    hipLaunchKernelGGL((k_lift_prep<IT, CT>), grid, block, 0, s, (const IT*)depthnet_out, dims->D, HW, npix, depth, (CT*)ctx_t)
+    hipLaunchKernelGGL((k_lift_prep<IT, CT>), grid, block, 0, s, (const IT*)depthnet_out, dims->D, HW, npix, depth, \
+                       (CT*)ctx_t, pos_of, sorted_depth)
     if (in_dtype == LSS_F32 && ctx_dtype == LSS_F32) LSS_PREP(float, float);
     else if (in_dtype == LSS_F32 && ctx_dtype == LSS_BF16) LSS_PREP(float, bf16);
     else if (in_dtype == LSS_BF16 && ctx_dtype == LSS_F32) LSS_PREP(bf16, float);
@@ -1399,8 +1434,9 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
 }
 
 int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
-                      const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream) {
-    if (!dims_ok(dims) || !feat || !weight || !bias || !depth || !ctx_t) return LSS_EINVAL;
+                      const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, const int32_t* pos_of,
+                      float* sorted_depth, lss_stream_t stream) {
+    if (!dims_ok(dims) || !feat || !weight || !bias || !depth || !ctx_t || (pos_of && !sorted_depth)) return LSS_EINVAL;
     if (dtype != LSS_BF16 || ctx_dtype != LSS_BF16) return LSS_EUNSUPPORTED;
     if (K <= 0 || K % 16 != 0 || K > kDnMaxK || dims->D + kC > kDnMaxO) return LSS_EUNSUPPORTED;
     const int HW = dims->H * dims->W;
@@ -1408,12 +1444,13 @@ int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, in
     if (npix >= INT_MAX) return LSS_EUNSUPPORTED;
     hipLaunchKernelGGL(k_depthnet_lift, dim3(grid_blocks(npix, kDnPix)), dim3(kBlock), 0, (hipStream_t)stream,
                        (const bf16*)feat, (const bf16*)weight, (const bf16*)bias, K, dims->D, HW, (int)npix, depth,
-                       (bf16*)ctx_t);
+                       (bf16*)ctx_t, pos_of, sorted_depth);
     return launch_status();
 }
 
 int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
                   const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
+                  const float* sorted_depth,
                   const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout,
                   lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop) {
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
@@ -1442,11 +1479,13 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
 #define LSS_NHWC_FWD(F, RT, T)                                                                                     \
     do {                                                                                                           \
         if (e0 || e1)                                                                                              \
-            hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, (const RT*)rows,   \
+            hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, sorted_depth,      \
+                                  (const RT*)rows,                                                                 \
                                   cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks,      \
                                   (T*)out);                                                                        \
         else                                                                                                       \
-            hipLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, depth, (const RT*)rows, cell_start,     \
+            hipLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, depth, sorted_depth, (const RT*)rows,   \
+                               cell_start,                                                                         \
                                sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, (T*)out);           \
     } while (0)
         if (out_dtype == LSS_F32) {

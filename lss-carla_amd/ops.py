@@ -112,6 +112,7 @@ class SplatPlan:
                                # only the first cell_start[-1] entries are meaningful
     sorted_row: torch.Tensor   # (Nprime,) int32 context row (pixel) of each sorted entry
     geom: Optional[torch.Tensor] = None
+    pos_of: Optional[torch.Tensor] = None  # (Nprime,) int32 sorted position of each point, -1 = dropped
 
     @property
     def c_dims(self) -> _lib.Dims:
@@ -131,11 +132,12 @@ def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev):
     cell_start = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
     sorted_key = torch.empty(nprime, device=dev, dtype=torch.int64)
     sorted_row = torch.empty(nprime, device=dev, dtype=torch.int32)
+    pos_of = torch.empty(nprime, device=dev, dtype=torch.int32) if SORTED_DEPTH else None
     scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
     _lib.check(lib.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
                                  make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key), _lib.ptr(sorted_row),
-                                 _lib.ptr(scratch), _lib.stream_handle(dev)), "lss_csr_build")
-    return cell_start, sorted_key, sorted_row
+                                 _lib.ptr(pos_of), _lib.ptr(scratch), _lib.stream_handle(dev)), "lss_csr_build")
+    return cell_start, sorted_key, sorted_row, pos_of
 
 
 def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, post_trans, grid: GridSpec,
@@ -165,10 +167,11 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
     _lib.check(lib.lss_geometry_cells(_lib.ptr(fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv),
                                       _lib.ptr(pt), dims, g, _lib.ptr(geom), _lib.ptr(cell_of), _lib.ptr(counts),
                                       _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
-    cell_start = sorted_key = sorted_row = None
+    cell_start = sorted_key = sorted_row = pos_of = None
     if want_csr:
-        cell_start, sorted_key, sorted_row = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev)
-    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom)
+        cell_start, sorted_key, sorted_row, pos_of = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells,
+                                                                dev)
+    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom, pos_of)
 
 
 def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
@@ -185,8 +188,8 @@ def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
     _lib.check(lib.lss_cells_from_geom(_lib.ptr(gm), nprime, nprime // B, grid.c_struct(), _lib.ptr(cell_of),
                                        _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)),
                "lss_cells_from_geom")
-    cell_start, sorted_key, sorted_row = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev)
-    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, None)
+    cell_start, sorted_key, sorted_row, pos_of = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev)
+    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, None, pos_of)
 
 
 # ----------------------------------------------------------------------------- profiling hook
@@ -242,14 +245,30 @@ def _new_bev(B, Z, X, Y, dtype, layout, dev) -> torch.Tensor:
     return torch.empty(B, Z * C_CAM, X, Y, device=dev, dtype=dtype)
 
 
-def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, layout: int):
+# Option: the CSR build also writes each point's sorted position (plan.pos_of) and the lift writes
+# the depth weights in CSR order, so the channels-last splat reads them with the keys instead of
+# gathering depth[p] per entry. Measured at c3 (scripts/kbench.py, training-step cache state): the
+# splat drops 12.35 -> 11.89 us but the lift's scattered writes cost +2.6 us (lss_lift_prep) /
+# +3.4 us (lss_depthnet_lift), so it is off by default.
+SORTED_DEPTH = False
+
+
+def _sorted_depth_buffers(plan: SplatPlan, layout: int, dev):
+    """(pos_of, sorted_depth) for the lift kernels, or (None, None)."""
+    if SORTED_DEPTH and layout == _lib.NHWC and plan.pos_of is not None:
+        return plan.pos_of, torch.empty(plan.nprime, device=dev, dtype=torch.float32)
+    return None, None
+
+
+def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, layout: int, sorted_depth=None):
     lib = _lib.load()
     dev = out.device
     e0, e1 = SPLAT_PROFILE.new_pair() if SPLAT_PROFILE.enabled else (None, None)
     ctx_code = _lib.dtype_code(ctx_t.dtype) if ctx_t is not None else _lib.F32
     _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), ctx_code, _lib.ptr(x_rows),
                                  _lib.ptr(plan.cell_start),
-                                 _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), plan.c_dims,
+                                 _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), _lib.ptr(sorted_depth),
+                                 plan.c_dims,
                                  plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype), layout,
                                  _lib.stream_handle(dev), e0, e1), "lss_splat_fwd")
 
@@ -295,12 +314,14 @@ class LiftSplat(torch.autograd.Function):
         # context rows keep the input's element type: bf16 rows are exact for a bf16 depthnet output
         # and halve the splat's gathered bytes
         ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=dn.dtype)
+        pos_of, sorted_depth = _sorted_depth_buffers(plan, layout, dev)
         _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.dtype_code(dn.dtype), plan.c_dims, _lib.ptr(depth),
-                                     _lib.ptr(ctx_t), _lib.dtype_code(ctx_t.dtype), _lib.stream_handle(dev)),
+                                     _lib.ptr(ctx_t), _lib.dtype_code(ctx_t.dtype), _lib.ptr(pos_of),
+                                     _lib.ptr(sorted_depth), _lib.stream_handle(dev)),
                    "lss_lift_prep")
         X, Y, Z = plan.grid.nx
         out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
-        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout)
+        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout, sorted_depth)
         ctx.save_for_backward(depth, ctx_t)
         ctx.plan = plan
         ctx.dn_dtype = depthnet_out.dtype
@@ -356,12 +377,14 @@ class DepthnetLiftSplat(torch.autograd.Function):
         b = bias.detach().contiguous()
         depth = torch.empty(B * N, D, H, W, device=dev, dtype=torch.float32)
         ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=torch.bfloat16)
+        pos_of, sorted_depth = _sorted_depth_buffers(plan, layout, dev)
         _lib.check(lib.lss_depthnet_lift(_lib.ptr(f), _lib.ptr(w), _lib.ptr(b), _lib.BF16, K, plan.c_dims,
-                                         _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, _lib.stream_handle(dev)),
+                                         _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(pos_of),
+                                         _lib.ptr(sorted_depth), _lib.stream_handle(dev)),
                    "lss_depthnet_lift")
         X, Y, Z = plan.grid.nx
         out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
-        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout)
+        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout, sorted_depth)
         ctx.save_for_backward(f, weight, depth, ctx_t)
         ctx.plan = plan
         return out

@@ -10,7 +10,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 echo "trace=$rc"; tail -1 $OUT/trace_bench.log | cut -c1-200; [ $rc -ne 0 ] && exit $rc
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $c --kernel-include-regex k_splat_fwd --output-format csv -d $OUT/pmc_$c -o run -- \
-      python3 bench.py --steps 10 --warmup 3 --cpu-baseline 0 > $OUT/pmc_$c.log 2>&1; rc=$?
+      python3 bench.py --steps 10 --warmup 3 --cpu-baseline 0 --graph 0 > $OUT/pmc_$c.log 2>&1; rc=$?
   echo "pmc $c=$rc"; [ $rc -ne 0 ] && { tail -3 $OUT/pmc_$c.log; exit $rc; }
 done
 exit 0

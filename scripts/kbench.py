@@ -24,6 +24,13 @@ sys.path.insert(0, REPO)
 VARIANTS = {
     "skip_chunks": ["LSS_FWD_SKIP=1"],  # zero units only (timing decomposition; wrong output)
     "skip_zero": ["LSS_FWD_SKIP=2"],    # chunks only (timing decomposition; wrong output)
+    "zero_plain": ["LSS_ZERO_STORE=0"],  # zero fill with plain stores (may stay in the Infinity Cache)
+    "row_nt": ["LSS_ROW_NT=1"],
+    "zero_units2": ["LSS_ZERO_UNITS=2"],
+    "interleave": ["LSS_INTERLEAVE=1"],
+    "zero_first": ["LSS_INTERLEAVE=2"],
+    "minwaves4": ["LSS_MIN_WAVES=4"],
+    "unroll4": ["LSS_UNROLL=4"],
 }
 
 
@@ -93,15 +100,16 @@ def main():
                                         _lib.ptr(pinv), _lib.ptr(pt), dims, g, None, _lib.ptr(cell_of),
                                         _lib.ptr(counts), _lib.ptr(slot), st()), "geom")
         if into is not None:
-            cs, sk, sr = into
+            cs, sk, sr, po = into
         else:
             cs = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
             sk = torch.empty(nprime, device=dev, dtype=torch.int64)
             sr = torch.empty(nprime, device=dev, dtype=torch.int32)
+            po = torch.empty(nprime, device=dev, dtype=torch.int32)
         scr = torch.empty(int(l.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
         _lib.check(l.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot), nprime, _lib.ptr(counts), ncells, dims,
-                                   _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), _lib.ptr(scr), st()), "csr")
-        return cs, sk, sr
+                                   _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), _lib.ptr(po), _lib.ptr(scr), st()), "csr")
+        return cs, sk, sr, po
 
     def named(name, fn, *a):
         timeit.name = name
@@ -116,8 +124,12 @@ def main():
     res["copy_bev_f32_82MB"] = named("copy_bev_f32_82MB", lambda: bev_f.copy_(bev_bf))
     res["plan_total(device inv)"] = named("plan_total(device inv)",
                                           lambda: ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device"))
+    sdepth = torch.empty(nprime, device=dev)  # depth weights in CSR order (lift with pos_of)
     res["lift_prep"] = named("lift_prep", lambda: _lib.check(lib.lss_lift_prep(
-        _lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, st()), "lift"))
+        _lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, None, None, st()), "lift"))
+    res["lift_prep (+sorted depth)"] = named("lift_prep (+sorted depth)", lambda: _lib.check(lib.lss_lift_prep(
+        _lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(plan.pos_of),
+        _lib.ptr(sdepth), st()), "lift"))
     feat = torch.randn(B * N, 512, H, W, device=dev).to(torch.bfloat16)
     wdn = (torch.randn(D + 64, 512, 1, 1, device=dev) * 0.05).to(torch.bfloat16)
     bdn = torch.zeros(D + 64, device=dev, dtype=torch.bfloat16)
@@ -125,24 +137,29 @@ def main():
                                                 lambda: torch.nn.functional.conv2d(feat, wdn, bdn))
     res["depthnet_lift (fused, MFMA)"] = named("depthnet_lift (fused, MFMA)", lambda: _lib.check(lib.lss_depthnet_lift(
         _lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
-        st()), "depthnet_lift"))
+        None, None, st()), "depthnet_lift"))
+    res["depthnet_lift (+sorted depth)"] = named("depthnet_lift (+sorted depth)", lambda: _lib.check(
+        lib.lss_depthnet_lift(_lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims, _lib.ptr(depth),
+                              _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(plan.pos_of), _lib.ptr(sdepth), st()),
+        "depthnet_lift"))
     ctx_f = torch.empty(B * N * H * W, 64, device=dev)
-    _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_f), _lib.F32, st()),
-               "lift")
+    _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_f), _lib.F32,
+                                 _lib.ptr(plan.pos_of), _lib.ptr(sdepth), st()), "lift")
 
-    pcsr = (plan.cell_start, plan.sorted_key, plan.sorted_row)
+    pcsr = (plan.cell_start, plan.sorted_key, plan.sorted_row, plan.pos_of)
 
-    def fwd(l, out, layout, csr=pcsr, ctx=None):
-        cs, sk, its = csr
+    def fwd(l, out, layout, csr=pcsr, ctx=None, sd=None):
+        cs, sk, its, _ = csr
         ctx = ctx_t if ctx is None else ctx
         return lambda: _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx), _lib.dtype_code(ctx.dtype), None,
-                                                  _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(its), dims, g, _lib.ptr(out),
-                                                  _lib.dtype_code(out.dtype), layout, st(), None, None), "fwd")
+                                                  _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(its), _lib.ptr(sd), dims, g,
+                                                  _lib.ptr(out), _lib.dtype_code(out.dtype), layout, st(), None, None),
+                                  "fwd")
 
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
 
-    def stamped(l, out, layout, csr=pcsr, ctx=None, mode="warm", iters=20):
-        cs, sk, its = csr
+    def stamped(l, out, layout, csr=pcsr, ctx=None, mode="warm", iters=20, sd=None):
+        cs, sk, its, po = csr
         ctx = ctx_t if ctx is None else ctx
         tot = 0.0
         for i in range(iters + 3):
@@ -151,12 +168,13 @@ def main():
             if mode == "step":
                 lib_plan(l, csr)
                 _lib.check(l.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx),
-                                           _lib.dtype_code(ctx.dtype), st()), "lift")
+                                           _lib.dtype_code(ctx.dtype), _lib.ptr(po if sd is not None else None),
+                                           _lib.ptr(sd), st()), "lift")
             a, b = ct.c_void_p(), ct.c_void_p()
             l.lss_event_create(ct.byref(a))
             l.lss_event_create(ct.byref(b))
             _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx), _lib.dtype_code(ctx.dtype), None, _lib.ptr(cs),
-                                       _lib.ptr(sk), _lib.ptr(its), dims, g, _lib.ptr(out),
+                                       _lib.ptr(sk), _lib.ptr(its), _lib.ptr(sd), dims, g, _lib.ptr(out),
                                        _lib.dtype_code(out.dtype), layout, st(), a, b), "fwd")
             ms = ct.c_float()
             l.lss_event_elapsed_ms(a, b, ct.byref(ms))
@@ -171,8 +189,12 @@ def main():
     ref_out = bev_bf.clone()
     if not args.only or "splat_fwd" in args.only:
         res["launch-to-launch splat_fwd nhwc bf16"] = named("splat_fwd nhwc bf16", fwd(lib, bev_bf, _lib.NHWC))
+        fwd(lib, bev_bf, _lib.NHWC, sd=sdepth)()
+        if not torch.equal(bev_bf, ref_out):
+            print("WARNING: sorted-depth splat differs from the gather splat", flush=True)
         for m in modes:
             res[f"{m} splat_fwd nhwc bf16"] = stamped(lib, bev_bf, _lib.NHWC, mode=m)
+            res[f"{m} splat_fwd nhwc bf16 (sorted depth)"] = stamped(lib, bev_bf, _lib.NHWC, mode=m, sd=sdepth)
             res[f"{m} splat_fwd nhwc bf16 (f32 ctx)"] = stamped(lib, bev_bf, _lib.NHWC, ctx=ctx_f, mode=m)
         res["warm splat_fwd nchw f32"] = stamped(lib, bev_f, _lib.NCHW)
     for path in sorted(glob.glob(os.path.join(REPO, "lss-carla_amd", "variants", "*.so"))) if args.variants else []:
@@ -182,8 +204,11 @@ def main():
         fwd(vl, bev_bf, _lib.NHWC, vcsr)()
         if not torch.equal(bev_bf, ref_out):
             print(f"WARNING variant {name}: output differs from the product kernel", flush=True)
+        vsd = torch.empty(nprime, device=dev)
+        _lib.check(vl.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
+                                    _lib.ptr(vcsr[3]), _lib.ptr(vsd), st()), "lift")
         for m in modes:
-            res[f"{m} splat_fwd nhwc bf16 [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m)
+            res[f"{m} splat_fwd nhwc bf16 [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m, sd=vsd)
             res[f"{m} splat_fwd nhwc bf16 (f32 ctx) [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, ctx=ctx_f,
                                                                           mode=m)
     g_bf = torch.randn(B, Z * 64, X, Y, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)

@@ -42,6 +42,7 @@ def main():
     plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device")  # product library's CSR
     dims, g = plan.c_dims, grid.c_struct()
     depth = torch.empty(B * N, D, H, W, device=dev)
+    sdepth = torch.empty(B * N * D * H * W, device=dev)  # depth weights in CSR order
     ctx = torch.empty(B * N * H * W, 64, device=dev, dtype=torch.bfloat16)
     out = torch.empty(B, Z * 64, X, Y, device=dev, dtype=torch.bfloat16, memory_format=torch.channels_last)
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
@@ -49,12 +50,14 @@ def main():
         if a.mode == "step":
             flush.zero_()
             plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device")
-        _lib.check(l.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, st), "lift")
+        _lib.check(l.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16,
+                                   _lib.ptr(plan.pos_of), _lib.ptr(sdepth), st), "lift")
         e0, e1 = ct.c_void_p(), ct.c_void_p()
         l.lss_event_create(ct.byref(e0))
         l.lss_event_create(ct.byref(e1))
         _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, None, _lib.ptr(plan.cell_start),
-                                   _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), dims, g, _lib.ptr(out),
+                                   _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), _lib.ptr(sdepth), dims, g,
+                                   _lib.ptr(out),
                                    _lib.BF16, _lib.NHWC, st, e0, e1), "fwd")
         ms = ct.c_float()
         l.lss_event_elapsed_ms(e0, e1, ct.byref(ms))

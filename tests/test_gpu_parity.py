@@ -372,7 +372,7 @@ def test_depthnet_lift_kernel_vs_conv_then_lift_prep(name):
     ctx_t = torch.empty(B * N * H * W, 64, device=DEV, dtype=torch.bfloat16)
     _lib.check(lib.lss_depthnet_lift(_lib.ptr(f), _lib.ptr(w.reshape(D + 64, -1).contiguous()), _lib.ptr(b),
                                      _lib.BF16, 512, plan.c_dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
-                                     _lib.stream_handle(DEV)), "depthnet_lift")
+                                     None, None, _lib.stream_handle(DEV)), "depthnet_lift")
     # reference: the conv in fp64 from the same bf16 operands, rounded to bf16 like the autocast conv output
     logits = torch.einsum("nkhw,ok->nohw", feat.double(), weight.double().flatten(1)) + bias.double().view(1, -1, 1, 1)
     dn = logits.to(torch.bfloat16)
@@ -423,3 +423,42 @@ def test_module_fused_depthnet_train_step():
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-2, atol=2e-2)
     rel = (outs[0][1] - outs[1][1]).norm() / outs[1][1].norm()
     assert rel < 3e-2, rel.item()
+
+
+@pytest.mark.parametrize("cfg_name", ["c1", "c3"])
+def test_sorted_depth_positions_and_splat(cfg_name):
+    """pos_of is the inverse of the canonical CSR permutation (-1 for dropped points); the lift's
+    CSR-ordered depth copy equals depth[p] entry by entry; the channels-last splat reading it gives
+    the same bits as the splat gathering depth[p]."""
+    cfg, gc, _ = syn.config_confs(cfg_name)
+    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
+    rig = {k: v.to(DEV) for k, v in syn.make_rig(B, N, fd, seed=3).items()}
+    frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
+    D, H, W = frustum.shape[:3]
+    grid = ops.GridSpec.from_conf(gc)
+    ops.SORTED_DEPTH = True
+    try:
+        plan = ops.plan_from_cameras(frustum, **rig, grid=grid)
+    finally:
+        ops.SORTED_DEPTH = False
+    kept = int(plan.cell_start[-1])
+    pts = (plan.sorted_key[:kept] & 0xFFFFFFFF).long()
+    want = torch.full((plan.nprime,), -1, dtype=torch.int32, device=DEV)
+    want[pts] = torch.arange(kept, dtype=torch.int32, device=DEV)
+    assert torch.equal(plan.pos_of, want)
+    dn = syn.make_depthnet_out(B, N, D, H, W, seed=4).to(DEV, torch.bfloat16)
+    outs = []
+    for sorted_depth in (False, True):
+        ops.SORTED_DEPTH = sorted_depth
+        try:
+            outs.append(ops.lift_splat(dn, plan, torch.bfloat16, _lib.NHWC))
+        finally:
+            ops.SORTED_DEPTH = False
+    assert torch.equal(outs[0], outs[1])
+    lib = _lib.load()
+    depth = torch.empty(B * N, D, H, W, device=DEV)
+    ctx_t = torch.empty(B * N * H * W, 64, device=DEV, dtype=torch.bfloat16)
+    sdepth = torch.zeros(plan.nprime, device=DEV)
+    _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, plan.c_dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
+                                 _lib.ptr(plan.pos_of), _lib.ptr(sdepth), _lib.stream_handle(DEV)), "lift")
+    assert torch.equal(sdepth[:kept], depth.reshape(-1)[pts])
