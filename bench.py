@@ -66,7 +66,7 @@ def parse():
                          "between them; 0 = eager (DDP for N>1)")
     ap.add_argument("--flat-params", type=int, default=1,
                     help="trainable parameters as one fp32 master tensor with one bf16 working copy per step")
-    ap.add_argument("--profile-steps", type=int, default=5,
+    ap.add_argument("--profile-steps", type=int, default=8,
                     help="with --graph 1: eager steps after the timed region on which the splat kernel is timed")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -250,6 +250,8 @@ def main():
     if args.graph:
         # a captured launch cannot carry kernel-stamped events: time lss_splat_fwd on eager steps
         # (same inputs, same kernel) right after the timed replays
+        train.eager()  # the first eager step after the replays runs cold: not timed
+        torch.cuda.synchronize()
         ops.SPLAT_PROFILE.reset(True)
         for _ in range(args.profile_steps):
             train.eager()

@@ -83,6 +83,23 @@ int lss_upsample_cat_fwd(const void* x, const void* skip, int32_t N, int32_t Hi,
 int lss_upsample_bwd(const void* dy, int32_t N, int32_t Hi, int32_t Wi, int32_t C1, int32_t C2, int32_t Ho,
                      int32_t Wo, void* dx, void* stream);
 
+/* Squeeze-and-excitation of an MBConv block (efficientnet_pytorch MBConvBlock, used by CamEncode's
+ * trunk, src/models.py:43): y = x * sigmoid(W2 swish(W1 mean_hw(x) + b1) + b2), x / y (N, C, HW)
+ * NCHW bf16 (HW % 4 == 0, C <= 2048, sq <= 64), W1 (sq, C), b1 (sq), W2 (C, sq), b2 (C) fp32
+ * masters. Weights and values are rounded to bf16 where bf16 autocast rounds them (conv operands,
+ * pooled map, both conv outputs, swish, sigmoid). Saved for the backward: m (N, C) pooled means, r / h (N, sq) reduce-conv output and
+ * its swish, sig (N, C); all fp32 buffers. */
+int lss_se_fwd(const void* x, int32_t N, int32_t C, int32_t HW, const float* w1, const float* b1, const float* w2,
+               const float* b2, int32_t sq, float* m, float* r, float* h, float* sig, void* y, void* stream);
+
+/* Backward: dx (bf16) = dy * sig + dm / HW (the excitation and the pooling paths), and the
+ * per-image gradients the caller turns into parameter gradients with small GEMMs: de (N, C) =
+ * d(expand-conv output), dr (N, sq) = d(reduce-conv output), dm (N, C) = d(pooled means).
+ * Scratch: t (N, C) fp32 (sum over HW of dy * x), dh_part (N, ceil(C / 64), sq) fp32. */
+int lss_se_bwd(const void* dy, const void* x, int32_t N, int32_t C, int32_t HW, const float* w1, const float* w2,
+               int32_t sq, const float* r, const float* sig, float* t, float* dh_part, float* de, float* dr, float* dm,
+               void* dx, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

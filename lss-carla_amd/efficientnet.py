@@ -190,6 +190,8 @@ class MBConvBlock(nn.Module):
         sq = max(1, int(in_f * se_ratio))
         self._se_reduce = Conv2dStaticSamePadding(mid, sq, 1, image_size=(1, 1))
         self._se_expand = Conv2dStaticSamePadding(sq, mid, 1, image_size=(1, 1))
+        # the lss_se_* kernels read these fp32 masters and round them to bf16 themselves
+        self._se_reduce.lss_fp32_params = self._se_expand.lss_fp32_params = True
         self._project_conv = Conv2dStaticSamePadding(mid, out_f, 1, bias=False, image_size=image_size)
         self._bn2 = nn.BatchNorm2d(out_f, momentum=BN_MOMENTUM, eps=BN_EPS)
         # depthwise conv backend on the GPU: 'hip' (lss_dwconv_* kernels), 'miopen', 'native' (PyTorch's
@@ -211,15 +213,75 @@ class MBConvBlock(nn.Module):
         else:
             x = self._depthwise_conv(x)
         x = bn_act(self._bn1, x, "swish")
-        s = F.adaptive_avg_pool2d(x, 1)
-        s = self._se_expand(F.silu(self._se_reduce(s)))
-        x = torch.sigmoid(s) * x
+        x = squeeze_excite(x, self._se_reduce, self._se_expand)
         x = bn_act(self._bn2, self._project_conv(x))
         if self.stride == 1 and self.in_f == self.out_f:
             if drop_connect_rate:
                 x = drop_connect(x, drop_connect_rate, self.training)
             x = x + inputs
         return x
+
+
+USE_HIP_SE = True
+
+
+class _HipSqueezeExcite(torch.autograd.Function):
+    """x * sigmoid(W2 swish(W1 avg_pool(x) + b1) + b2) on the lss_se_* kernels (NCHW bf16 x, fp32
+    weights rounded to bf16 in-kernel as autocast's conv would). Backward: two streaming kernels
+    (sum_hw dy*x, then dx = dy*sig + dm/HW) around a per-image MLP backward; the weight / bias
+    gradients are four small fp32 GEMMs / sums."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        from . import _lib
+        lib = _lib.load()
+        N, C, H, W = x.shape
+        sq = w1.shape[0]
+        f32 = dict(device=x.device, dtype=torch.float32)
+        W1 = w1.detach().reshape(sq, C).float().contiguous()
+        W2 = w2.detach().reshape(C, sq).float().contiguous()
+        B1, B2 = b1.detach().float().contiguous(), b2.detach().float().contiguous()
+        m, sig = torch.empty(N, C, **f32), torch.empty(N, C, **f32)
+        r, h = torch.empty(N, sq, **f32), torch.empty(N, sq, **f32)
+        y = torch.empty_like(x)
+        _lib.check(lib.lss_se_fwd(_lib.ptr(x), N, C, H * W, _lib.ptr(W1), _lib.ptr(B1), _lib.ptr(W2), _lib.ptr(B2), sq,
+                                  _lib.ptr(m), _lib.ptr(r), _lib.ptr(h), _lib.ptr(sig), _lib.ptr(y),
+                                  _lib.stream_handle(x.device)), "lss_se_fwd")
+        ctx.save_for_backward(x, W1, W2, m, r, h, sig)
+        ctx.shapes = (w1.shape, w1.dtype, b1.dtype, w2.shape, w2.dtype, b2.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+        lib = _lib.load()
+        x, W1, W2, m, r, h, sig = ctx.saved_tensors
+        w1s, w1t, b1t, w2s, w2t, b2t = ctx.shapes
+        N, C, H, W = x.shape
+        sq = W1.shape[0]
+        dy = dy.to(torch.bfloat16).contiguous()
+        f32 = dict(device=x.device, dtype=torch.float32)
+        t, de, dm = torch.empty(N, C, **f32), torch.empty(N, C, **f32), torch.empty(N, C, **f32)
+        dr = torch.empty(N, sq, **f32)
+        dh_part = torch.empty(N, (C + 63) // 64, sq, **f32)
+        dx = torch.empty_like(x)
+        _lib.check(lib.lss_se_bwd(_lib.ptr(dy), _lib.ptr(x), N, C, H * W, _lib.ptr(W1), _lib.ptr(W2), sq, _lib.ptr(r),
+                                  _lib.ptr(sig), _lib.ptr(t), _lib.ptr(dh_part), _lib.ptr(de), _lib.ptr(dr),
+                                  _lib.ptr(dm), _lib.ptr(dx), _lib.stream_handle(x.device)), "lss_se_bwd")
+        dw2 = (de.t() @ h).reshape(w2s).to(w2t)
+        dw1 = (dr.t() @ m).reshape(w1s).to(w1t)
+        return dx, dw1, dr.sum(0).to(b1t), dw2, de.sum(0).to(b2t)
+
+
+def squeeze_excite(x: torch.Tensor, se_reduce: nn.Conv2d, se_expand: nn.Conv2d) -> torch.Tensor:
+    """x * sigmoid(se_expand(swish(se_reduce(avg_pool(x))))) (efficientnet_pytorch MBConvBlock)."""
+    if (USE_HIP_SE and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous()
+            and (x.shape[2] * x.shape[3]) % 4 == 0 and x.shape[1] <= 2048 and se_reduce.weight.shape[0] <= 64
+            and se_reduce.bias is not None and se_expand.bias is not None):
+        return _HipSqueezeExcite.apply(x, se_reduce.weight, se_reduce.bias, se_expand.weight, se_expand.bias)
+    s = F.adaptive_avg_pool2d(x, 1)
+    s = se_expand(F.silu(se_reduce(s)))
+    return torch.sigmoid(s) * x
 
 
 def set_depthwise_impl(module: nn.Module, impl: str) -> None:

@@ -32,6 +32,8 @@ def autocast_cast_names(model: nn.Module) -> set:
     non-grouped nn.Conv2d and of nn.Linear (depthwise convs stay fp32: lss_dwconv_* reads fp32)."""
     names = set()
     for mname, m in model.named_modules():
+        if getattr(m, "lss_fp32_params", False):  # consumed in fp32 by a HIP kernel (rounds them itself)
+            continue
         if (isinstance(m, nn.Conv2d) and m.groups == 1) or isinstance(m, nn.Linear):
             for pname, _ in m.named_parameters(recurse=False):
                 names.add(f"{mname}.{pname}" if mname else pname)

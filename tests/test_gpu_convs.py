@@ -206,3 +206,64 @@ def test_bevencode_hip_upsample_vs_torch():
     for a, b in zip(outs[0], outs[1]):
         err = (a - b).abs().max() / b.abs().max().clamp_min(1e-6)
         assert err < 3e-2, float(err)
+
+
+# ----------------------------------------------------------------------------- squeeze-and-excitation
+SE_CASES = [  # (N, C, H, W, sq): MBConv blocks of the trunk at config-3 resolutions (fewer images)
+    (4, 32, 64, 176, 8),
+    (3, 96, 32, 88, 4),
+    (6, 240, 16, 44, 10),
+    (5, 1152, 4, 11, 48),
+]
+
+
+def _rel(a, b):
+    return float((a.double().cpu() - b.double().cpu()).abs().max() / b.double().abs().max().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("N,C,H,W,sq", SE_CASES)
+def test_squeeze_excite_vs_fp64(N, C, H, W, sq):
+    g = torch.Generator().manual_seed(C + H)
+    torch.manual_seed(C)
+    x = (torch.randn(N, C, H, W, generator=g) * 2).bfloat16()
+    red = torch.nn.Conv2d(C, sq, 1).to(DEV)
+    exp = torch.nn.Conv2d(sq, C, 1).to(DEV)
+    xd = x.to(DEV).requires_grad_(True)
+    y = E.squeeze_excite(xd, red, exp)
+    assert y.dtype == torch.bfloat16 and y.shape == x.shape
+    dy = torch.randn(y.shape, generator=g).bfloat16()
+    y.backward(dy.to(DEV))
+    # fp64 reference on the bf16-rounded weights (what the autocast convs multiply with)
+    ps = [t.detach().cpu().bfloat16().double().requires_grad_(True)
+          for t in (red.weight, red.bias, exp.weight, exp.bias)]
+    xr = x.double().requires_grad_(True)
+    s = F.conv2d(F.silu(F.conv2d(xr.mean((2, 3), keepdim=True), ps[0], ps[1])), ps[2], ps[3])
+    yr = torch.sigmoid(s) * xr
+    yr.backward(dy.double())
+    torch.testing.assert_close(y.detach().cpu().double(), yr.detach(), rtol=2e-2, atol=3e-2)
+    assert _rel(xd.grad, xr.grad) < 2e-2
+    for got, ref_p in zip((red.weight.grad, red.bias.grad, exp.weight.grad, exp.bias.grad), ps):
+        assert got.dtype == torch.float32
+        assert _rel(got, ref_p.grad) < 5e-2, _rel(got, ref_p.grad)
+
+
+def test_mbconv_hip_se_vs_torch_autocast():
+    """An MBConv block under bf16 autocast: lss_se_* vs PyTorch's SE ops (same block, same input)."""
+    torch.manual_seed(11)
+    blk = E.MBConvBlock(5, 1, 6, 40, 40, image_size=(16, 44)).to(DEV).train()
+    x = torch.randn(6, 40, 16, 44, device=DEV).bfloat16()
+    outs = []
+    for use in (True, False):
+        E.USE_HIP_SE = use
+        try:
+            blk.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = blk(xi)
+            y.float().square().mean().backward()
+            outs.append((y.detach(), xi.grad, blk._se_reduce.weight.grad.clone(), blk._se_expand.bias.grad.clone(),
+                         blk._expand_conv.weight.grad.clone()))
+        finally:
+            E.USE_HIP_SE = True
+    for a, b in zip(*outs):
+        assert _rel(a, b) < 5e-2, _rel(a, b)
