@@ -55,6 +55,9 @@ const char* lss_error_string(int code);
 int lss_event_create(lss_event_t* ev);
 int lss_event_destroy(lss_event_t ev);
 int lss_event_elapsed_ms(lss_event_t start, lss_event_t stop, float* ms); /* synchronises on stop */
+/* Record ev on stream. While the stream is being captured into a hipGraph this adds an explicit
+ * event-record node to the graph (so every replay stamps the event), not a capture dependency. */
+int lss_event_record(lss_event_t ev, lss_stream_t stream);
 
 /* Device 3x3 inverses of post_rots and intrins (fp64 adjugate, rounded to fp32).
  * Replaces torch.inverse(post_rots.cpu()) / torch.inverse(intrins.cpu())

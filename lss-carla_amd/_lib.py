@@ -41,6 +41,7 @@ SIGNATURES = {
     "lss_event_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "lss_event_destroy": (ctypes.c_int, [_p]),
     "lss_event_elapsed_ms": (ctypes.c_int, [_p, _p, ctypes.POINTER(ctypes.c_float)]),
+    "lss_event_record": (ctypes.c_int, [_p, _p]),
     "lss_camera_inverse": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p]),
     "lss_geometry_cells": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _p, _p, _p, _p]),
     "lss_cells_from_geom": (ctypes.c_int, [_p, _i32, _i32, _GRID, _p, _p, _p, _p]),

@@ -1339,6 +1339,23 @@ int lss_event_elapsed_ms(lss_event_t start, lss_event_t stop, float* ms) {
     return (int)hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop);
 }
 
+int lss_event_record(lss_event_t ev, lss_stream_t stream) {
+    if (!ev) return LSS_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t graph = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t ndeps = 0;
+    hipError_t r = hipStreamGetCaptureInfo_v2(s, &st, &id, &graph, &deps, &ndeps);
+    if (r != hipSuccess) return (int)r;
+    if (st != hipStreamCaptureStatusActive) return (int)hipEventRecord((hipEvent_t)ev, s);
+    hipGraphNode_t node;
+    r = hipGraphAddEventRecordNode(&node, graph, deps, ndeps, (hipEvent_t)ev);
+    if (r != hipSuccess) return (int)r;
+    return (int)hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
+}
+
 const char* lss_error_string(int code) {
     if (code == 0) return "success";
     if (code == LSS_EINVAL) return "lss: invalid argument";

@@ -203,6 +203,12 @@ class _SplatProfile:
     def __init__(self):
         self.enabled = False
         self.pairs = []
+        # Captured mode: while a hipGraph is being captured, bracket the launch with timing
+        # hipEvents on the capture stream (event-record nodes of the graph: a captured launch cannot
+        # carry kernel-stamped events). After each replay, graph_avg_ms() reads the pairs.
+        self.capture = False
+        self.graph_pairs = []
+        self.empty_pairs = []
 
     def reset(self, enabled: bool = True):
         self.release()
@@ -226,6 +232,31 @@ class _SplatProfile:
             _lib.check(lib.lss_event_elapsed_ms(a, b, ctypes.byref(ms)), "lss_event_elapsed_ms")
             tot += ms.value
         return tot / len(self.pairs)
+
+    def new_graph_pair(self, empty: bool = False):
+        lib = _lib.load()
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(lib.lss_event_create(ctypes.byref(a)), "lss_event_create")
+        _lib.check(lib.lss_event_create(ctypes.byref(b)), "lss_event_create")
+        (self.empty_pairs if empty else self.graph_pairs).append((a, b))
+        return a, b
+
+    @staticmethod
+    def _mean_ms(pairs) -> float:
+        lib = _lib.load()
+        tot = 0.0
+        for a, b in pairs:
+            ms = ctypes.c_float()
+            _lib.check(lib.lss_event_elapsed_ms(a, b, ctypes.byref(ms)), "lss_event_elapsed_ms")
+            tot += ms.value
+        return tot / len(pairs)
+
+    def graph_ms(self) -> Optional[Tuple[float, float]]:
+        """(bracketed ms, empty-pair ms) averaged over the captured pairs of the last replay: the
+        splat's duration is the first minus the second (one event-record node's own cost)."""
+        if not self.graph_pairs:
+            return None
+        return self._mean_ms(self.graph_pairs), self._mean_ms(self.empty_pairs)
 
     def release(self):
         if self.pairs:
@@ -264,6 +295,12 @@ def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, 
     lib = _lib.load()
     dev = out.device
     e0, e1 = SPLAT_PROFILE.new_pair() if SPLAT_PROFILE.enabled else (None, None)
+    gpair = None
+    if SPLAT_PROFILE.capture and dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        # explicit event-record nodes in the captured graph (lss_event_record)
+        gpair = SPLAT_PROFILE.new_graph_pair()
+        _lib.check(lib.lss_event_record(gpair[0], _lib.stream_handle(dev)), "lss_event_record")
+        e0 = e1 = None
     ctx_code = _lib.dtype_code(ctx_t.dtype) if ctx_t is not None else _lib.F32
     _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), ctx_code, _lib.ptr(x_rows),
                                  _lib.ptr(plan.cell_start),
@@ -271,6 +308,12 @@ def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, 
                                  plan.c_dims,
                                  plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype), layout,
                                  _lib.stream_handle(dev), e0, e1), "lss_splat_fwd")
+    if gpair is not None:
+        _lib.check(lib.lss_event_record(gpair[1], _lib.stream_handle(dev)), "lss_event_record")
+        # an empty pair right after: the cost of one event-record node, subtracted by graph_ms()
+        epair = SPLAT_PROFILE.new_graph_pair(empty=True)
+        _lib.check(lib.lss_event_record(epair[0], _lib.stream_handle(dev)), "lss_event_record")
+        _lib.check(lib.lss_event_record(epair[1], _lib.stream_handle(dev)), "lss_event_record")
 
 
 def _grad_rows(plan: SplatPlan, dbev: torch.Tensor) -> Tuple[torch.Tensor, int]:

@@ -1,7 +1,7 @@
 # Round measurement: GPU parity tests, default bench (+CPU baseline), kernel trace, splat PMC passes.
 set -o pipefail
 OUT=gpurun_out/round; mkdir -p $OUT
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/gpu_tests.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1; rc=$?
 echo "tests=$rc"; tail -3 $OUT/gpu_tests.log; [ $rc -gt 1 ] && exit $rc
 timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1; rc=$?; echo "bench=$rc"; tail -1 $OUT/bench.log; [ $rc -ne 0 ] && exit $rc
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
