@@ -31,6 +31,8 @@ VARIANTS = {
     "zero_first": ["LSS_INTERLEAVE=2"],
     "minwaves4": ["LSS_MIN_WAVES=4"],
     "unroll4": ["LSS_UNROLL=4"],
+    "zu8": ["LSS_ZERO_UNITS=8"],    # few heavy zero waves, so all chunk + zero waves are resident at once
+    "zu16": ["LSS_ZERO_UNITS=16"],
 }
 
 
@@ -84,7 +86,9 @@ def main():
         return e0.elapsed_time(e1) / iters * 1e3  # us
 
     res = {}
+    ops.SORTED_DEPTH = True  # the plan carries pos_of, so the "(sorted depth)" rows get real weights
     plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device")
+    assert plan.pos_of is not None
     kept = int(plan.cell_start[-1])
     dims, g = plan.c_dims, grid.c_struct()
     ncells, nprime = grid.ncells(B), plan.nprime
@@ -197,6 +201,9 @@ def main():
             res[f"{m} splat_fwd nhwc bf16 (sorted depth)"] = stamped(lib, bev_bf, _lib.NHWC, mode=m, sd=sdepth)
             res[f"{m} splat_fwd nhwc bf16 (f32 ctx)"] = stamped(lib, bev_bf, _lib.NHWC, ctx=ctx_f, mode=m)
         res["warm splat_fwd nchw f32"] = stamped(lib, bev_f, _lib.NCHW)
+    # the timing modes above rewrote ctx_t (the "step" mode reruns the lift): fresh reference output
+    fwd(lib, bev_bf, _lib.NHWC)()
+    ref_out = bev_bf.clone()
     for path in sorted(glob.glob(os.path.join(REPO, "lss-carla_amd", "variants", "*.so"))) if args.variants else []:
         vl = _lib.open_library(path)
         name = os.path.basename(path)[:-3]
