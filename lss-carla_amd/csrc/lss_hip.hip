@@ -844,17 +844,40 @@ __device__ __forceinline__ OutT* cell_row(OutT* out, int cell, const BevGeo& g) 
 #define LSS_ZERO_UNITS 1  // 64-cell zero-fill units per wave (their cell_start loads in flight together)
 #endif
 constexpr int kZeroUnits = LSS_ZERO_UNITS;
+#ifndef LSS_CHUNK_GAP
+#define LSS_CHUNK_GAP 0  // >0: each chunk wave also zeroes the first G empty cells after each cell it owns
+#endif
+constexpr int kChunkGap = LSS_CHUNK_GAP;
+
+// Empty cells [lo, hi) written as zero rows (non-temporal 16-B stores), RPS rows per instruction.
+template <typename OutT>
+__device__ __forceinline__ void zero_gap_rows(int lo, int hi, const BevGeo& g, OutT* __restrict__ out, int lane) {
+    constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
+    for (int r0 = lo; r0 < hi; r0 += RPS) {
+        const int r = r0 + lane / LPR;
+        if (r < hi)
+            __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u},
+                                        reinterpret_cast<u32x4*>(cell_row(out, r, g) + (lane % LPR) * EPL));
+    }
+}
 
 // Zero-fill units [u0, u0 + kZeroUnits): cells [64u, 64u + 64) each; empty cells' rows written as zeros.
+// With kChunkGap > 0, an empty cell k at most kChunkGap cells past the previous occupied cell (the
+// cell of entry cell_start[k] - 1) is left to that cell's chunk wave.
 template <typename OutT>
-__device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start, const BevGeo& g,
+__device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start,
+                                const long long* __restrict__ sorted_key, const BevGeo& g,
                                 OutT* __restrict__ out, int lane) {
     unsigned long long emask[kZeroUnits];
 #pragma unroll
     for (int i = 0; i < kZeroUnits; ++i) {
         const int k = (u0 + i) * kWave + lane;
         bool empty = false;
-        if (k < g.ncells) empty = cell_start[k] == cell_start[k + 1];
+        if (k < g.ncells) {
+            const int a = cell_start[k];
+            empty = a == cell_start[k + 1];
+            if (kChunkGap > 0 && empty && a > 0 && k - (int)(sorted_key[a - 1] >> 32) <= kChunkGap) empty = false;
+        }
         emask[i] = __ballot(empty);
     }
     constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
@@ -950,7 +973,8 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                                             const float* __restrict__ sorted_depth,
                                             const RT* __restrict__ rows_base,
                                             const long long* __restrict__ sorted_key,
-                                            const int32_t* __restrict__ sorted_row, const BevGeo& g,
+                                            const int32_t* __restrict__ sorted_row,
+                                            const int32_t* __restrict__ cell_start, const BevGeo& g,
                                             OutT* __restrict__ out, EntryMeta* __restrict__ meta,
                                             float* __restrict__ part, int lane) {
     using RS = RowSlice<RT>;
@@ -1074,12 +1098,33 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
             }
             store_slice<RS::EPL>(cell_row(out, first_cell, g) + col, sum);
         }
+        if (kChunkGap > 0) {
+            // empty cells after each owned cell, up to kChunkGap of them (the next occupied cell is
+            // the cell of the next start, or of entry `end`: the big cell, the next chunk's, or -1)
+            unsigned long long m = starts;
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1;
+                const int c = __builtin_amdgcn_readlane(c0, j);
+                const int np = m ? (int)__builtin_ctzll(m) : end;
+                int nc = np < kWave ? __builtin_amdgcn_readlane(c0, np) : __builtin_amdgcn_readlane(c1, np - kWave);
+                if (nc < 0) nc = g.ncells;
+                zero_gap_rows<OutT>(c + 1, min(nc, c + 1 + kChunkGap), g, out, lane);
+            }
+        }
     }
     if (big >= 0) {
         int cell;
         const float a2 = reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base,
                                                     lane, &cell);
         cell_row(out, cell, g)[lane] = from_f32<OutT>(a2);
+        if (kChunkGap > 0) {
+            const int nx = uniform(cell_start[cell + 1]);
+            int nc = nx < nprime ? (int)(sorted_key[nx] >> 32) : -1;
+            nc = uniform(nc);
+            if (nc < 0) nc = g.ncells;
+            zero_gap_rows<OutT>(cell + 1, min(nc, cell + 1 + kChunkGap), g, out, lane);
+        }
     }
 }
 
@@ -1120,7 +1165,7 @@ __global__ __launch_bounds__(kBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const 
         if (cb >= nchunk_blocks) return;
         const int w = cb * (kBlock / kWave) + wave;
         LSS_STAMP(w, 0);
-        splat_chunk<FUSED, RT, OutT>(w, nprime, depth, sorted_depth, rows_base, sorted_key, sorted_row, g, out, s_meta[wave],
+        splat_chunk<FUSED, RT, OutT>(w, nprime, depth, sorted_depth, rows_base, sorted_key, sorted_row, cell_start, g, out, s_meta[wave],
                                      s_part[wave], lane);
         LSS_STAMP(w, 3);
 #if LSS_TRACE
@@ -1134,7 +1179,7 @@ __global__ __launch_bounds__(kBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const 
         const int u = (zb * (kBlock / kWave) + wave) * kZeroUnits;
         [[maybe_unused]] const int zslot = nchunk_blocks * (kBlock / kWave) + zb * (kBlock / kWave) + wave;
         LSS_STAMP(zslot, 0);
-        if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, g, out, lane);
+        if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, sorted_key, g, out, lane);
         LSS_STAMP(zslot, 3);
 #if LSS_TRACE
         if (lane == 0 && zslot < 16384) g_lss_trace[zslot][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |

@@ -33,6 +33,8 @@ VARIANTS = {
     "unroll4": ["LSS_UNROLL=4"],
     "zu8": ["LSS_ZERO_UNITS=8"],    # few heavy zero waves, so all chunk + zero waves are resident at once
     "zu16": ["LSS_ZERO_UNITS=16"],
+    "gap8": ["LSS_CHUNK_GAP=8"],    # chunk waves zero the first 8 empty cells after each owned cell
+    "gap32": ["LSS_CHUNK_GAP=32"],
 }
 
 
