@@ -114,13 +114,43 @@ __device__ __forceinline__ int quantize_cell(float ex, float ey, float ez, const
     return ((b * g.nx[2] + iz) * g.nx[0] + ix) * g.nx[1] + iy;
 }
 
-__device__ __forceinline__ void emit_cell(int p, int cell, int32_t* cell_of, int32_t* cell_count, int32_t* slot_of) {
-    cell_of[p] = cell;
-    if (cell_count != nullptr) {
+#ifndef LSS_GEOM_AGG
+#define LSS_GEOM_AGG 1  // 1: one atomic per distinct cell of a wave (lanes of a cell share it), 0: one per point
+#endif
+
+// Slot of point p inside its cell (arrival order; k_csr_canon fixes the order later). Atomics on
+// the counts execute at the memory side, so a wave first groups its lanes by cell (a ballot per
+// distinct cell, no memory traffic), then ONE atomic instruction adds each group's size from its
+// leader lane; a lane's slot is its leader's old count plus its rank in the group.
+// Must be called by every lane of the wave (cell = -1 for dropped / out-of-range points).
+__device__ __forceinline__ void emit_cell(int p, int cell, int32_t* cell_of, int32_t* cell_count, int32_t* slot_of,
+                                          bool live = true) {
+    if (live) cell_of[p] = cell;
+    if (cell_count == nullptr) return;
+    if (!LSS_GEOM_AGG) {
         int slot = -1;
-        if (cell >= 0) slot = atomicAdd(cell_count + cell, 1);
-        slot_of[p] = slot;
+        if (live && cell >= 0) slot = atomicAdd(cell_count + cell, 1);
+        if (live) slot_of[p] = slot;
+        return;
     }
+    const int lane = threadIdx.x & 63;
+    unsigned long long rem = __ballot(live && cell >= 0);
+    int leader = -1, rank = 0, size = 0;
+    while (rem) {
+        const int l0 = __builtin_ctzll(rem);
+        const int c = __builtin_amdgcn_readlane(cell, l0);
+        const unsigned long long peers = __ballot(cell == c) & rem;
+        rem &= ~peers;
+        if ((peers >> lane) & 1ull) {
+            leader = l0;
+            rank = __builtin_popcountll(peers & ((1ull << lane) - 1));
+            size = __builtin_popcountll(peers);
+        }
+    }
+    int base = 0;
+    if (leader == lane) base = atomicAdd(cell_count + cell, size);
+    base = __shfl(base, leader < 0 ? lane : leader, kWave);
+    if (live) slot_of[p] = leader < 0 ? -1 : base + rank;
 }
 
 __global__ __launch_bounds__(kBlock) void k_geometry_cells(
@@ -128,8 +158,9 @@ __global__ __launch_bounds__(kBlock) void k_geometry_cells(
     const float* __restrict__ kinv, const float* __restrict__ pinv, const float* __restrict__ post_trans,
     int N, int DHW, int nprime, lss_grid_t g, float* __restrict__ out_geom, int32_t* __restrict__ cell_of,
     int32_t* __restrict__ cell_count, int32_t* __restrict__ slot_of) {
-    const int p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= nprime) return;
+    const int p0 = blockIdx.x * kBlock + threadIdx.x;
+    const bool live = p0 < nprime;
+    const int p = live ? p0 : nprime - 1;  // dead lanes recompute the last point, then write nothing
     const int cam = p / DHW;
     const int f = p - cam * DHW;
     const int b = cam / N;
@@ -155,12 +186,12 @@ __global__ __launch_bounds__(kBlock) void k_geometry_cells(
         const float c2 = dot3_seq(R[3 * i + 0], R[3 * i + 1], R[3 * i + 2], K[2], K[5], K[8]);
         e[i] = __fadd_rn(dot3_seq(c0, c1, c2, r0, r1, r2), trans[3 * cam + i]);
     }
-    if (out_geom != nullptr) {
+    if (out_geom != nullptr && live) {
         out_geom[3 * (size_t)p + 0] = e[0];
         out_geom[3 * (size_t)p + 1] = e[1];
         out_geom[3 * (size_t)p + 2] = e[2];
     }
-    emit_cell(p, quantize_cell(e[0], e[1], e[2], g, b), cell_of, cell_count, slot_of);
+    emit_cell(p, live ? quantize_cell(e[0], e[1], e[2], g, b) : -1, cell_of, cell_count, slot_of, live);
 }
 
 __global__ __launch_bounds__(kBlock) void k_cells_from_geom(const float* __restrict__ geom, int nprime, int ppb,
@@ -168,9 +199,10 @@ __global__ __launch_bounds__(kBlock) void k_cells_from_geom(const float* __restr
                                                             int32_t* __restrict__ cell_count,
                                                             int32_t* __restrict__ slot_of) {
     const int p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= nprime) return;
-    const int cell = quantize_cell(geom[3 * (size_t)p], geom[3 * (size_t)p + 1], geom[3 * (size_t)p + 2], g, p / ppb);
-    emit_cell(p, cell, cell_of, cell_count, slot_of);
+    const bool live = p < nprime;
+    const int cell =
+        live ? quantize_cell(geom[3 * (size_t)p], geom[3 * (size_t)p + 1], geom[3 * (size_t)p + 2], g, p / ppb) : -1;
+    emit_cell(p, cell, cell_of, cell_count, slot_of, live);
 }
 
 // ----------------------------------------------------------------------------- CSR (counting sort)
