@@ -1354,6 +1354,90 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd(const GT* __restrict__ g, 
     dst[(size_t)(D + lane) * HW] = from_f32<DT>(dctx);
 }
 
+// Register-only form of k_splat_bwd (no LDS, so occupancy is not capped by a 10.9 KB-per-wave
+// staging buffer): lane (sub, j) holds rows r = k*RPI + sub, channels [EPL*j, EPL*j + EPL) of the
+// pixel's D gradient rows. d_ctx: per-lane sums over its rows, then a butterfly over the RPI row
+// groups; d_depth: per-row dot over the lane's channels, then a butterfly over the LPR lanes of the
+// row. Fixed association order (deterministic); the sums are fp32 like the LDS form.
+template <typename GT, typename DT, typename CT, bool NHWC>
+__global__ __launch_bounds__(kBlock) void k_splat_bwd_reg(const GT* __restrict__ g, const int32_t* __restrict__ cell_of,
+                                                          const float* __restrict__ depth,
+                                                          const CT* __restrict__ ctx_t, int D, int HW, int npix,
+                                                          SplatGeo sg, DT* __restrict__ d_dn) {
+    constexpr int EPL = 16 / sizeof(GT);    // row elements per 16-B lane load
+    constexpr int LPR = kC / EPL;           // lanes per row
+    constexpr int RPI = kWave / LPR;        // rows per wave-instruction
+    constexpr int NI = kWave / RPI;         // instructions for 64 rows
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * (kBlock / kWave) + uniform(threadIdx.x >> 6);
+    if (q >= npix) return;  // wave-uniform
+    const int bn = q / HW, hw = q - bn * HW;
+    const size_t pbase = (size_t)bn * D * HW + hw;  // point (bn, d = 0, hw)
+    float my_depth = 0.f;
+    int my_cell = -1;
+    if (lane < D) {
+        my_depth = depth[pbase + (size_t)lane * HW];
+        my_cell = cell_of[pbase + (size_t)lane * HW];
+    }
+    const int sub = lane / LPR, col = (lane % LPR) * EPL;
+    float cx[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) cx[e] = to_f32(ctx_t[(size_t)q * kC + col + e]);
+    uint4 raw[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int cell = __shfl(my_cell, (k * RPI + sub) & 63, kWave);  // -1 beyond D
+        raw[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (k * RPI < D && cell >= 0) raw[k] = *reinterpret_cast<const uint4*>(g + row_offset<NHWC>(cell, sg) + col);
+    }
+    float dc[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) dc[e] = 0.f;
+    float part[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const float w = __shfl(my_depth, (k * RPI + sub) & 63, kWave);  // 0 beyond D
+        float f[EPL];
+        unpack16(raw[k], (const GT*)nullptr, f);
+        float t = 0.f;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+            dc[e] = fmaf(f[e], w, dc[e]);
+            t = fmaf(f[e], cx[e], t);
+        }
+        part[k] = t;
+    }
+    // d_ctx: sum over the RPI row groups (lanes j, j + LPR, j + 2 LPR, ...)
+#pragma unroll
+    for (int o = LPR; o < kWave; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) dc[e] += __shfl_xor(dc[e], o, kWave);
+    // d_depth of row k*RPI + sub: sum over the LPR lanes of the row
+#pragma unroll
+    for (int k = 0; k < NI; ++k)
+#pragma unroll
+        for (int o = 1; o < LPR; o <<= 1) part[k] += __shfl_xor(part[k], o, kWave);
+    // lane d takes row d: instruction d / RPI, held by the lanes of row group d % RPI
+    float dd = 0.f;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const float v = __shfl(part[k], (lane % RPI) * LPR, kWave);
+        if (lane / RPI == k) dd = v;
+    }
+    if (lane >= D) dd = 0.f;
+    const float s = wave_sum(my_depth * dd);
+    const float dl = my_depth * (dd - s);
+    DT* dst = d_dn + (size_t)bn * (D + kC) * HW + hw;
+    if (lane < D) dst[(size_t)lane * HW] = from_f32<DT>(dl);
+    if (sub == 0)
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) dst[(size_t)(D + col + e) * HW] = from_f32<DT>(dc[e]);
+}
+
+#ifndef LSS_BWD_REG
+#define LSS_BWD_REG 1  // 1: k_splat_bwd_reg (registers + shuffles), 0: k_splat_bwd (LDS staging)
+#endif
+
 template <typename GT, bool NHWC>
 __global__ __launch_bounds__(kBlock) void k_splat_bwd_lifted(const GT* __restrict__ g, const int32_t* __restrict__ cell_of,
                                                              int nprime, SplatGeo sg, float* __restrict__ dx) {
@@ -1677,7 +1761,13 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
     const bool nhwc = rows_layout == LSS_NHWC;
 #define LSS_BWD(GT, DT, CT)                                                                                       \
     do {                                                                                                          \
-        if (nhwc)                                                                                                 \
+        if (LSS_BWD_REG && nhwc)                                                                                  \
+            hipLaunchKernelGGL((k_splat_bwd_reg<GT, DT, CT, true>), gr, bl, 0, s, (const GT*)g, cell_of, depth,   \
+                               (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
+        else if (LSS_BWD_REG)                                                                                     \
+            hipLaunchKernelGGL((k_splat_bwd_reg<GT, DT, CT, false>), gr, bl, 0, s, (const GT*)g, cell_of, depth,  \
+                               (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
+        else if (nhwc)                                                                                            \
             hipLaunchKernelGGL((k_splat_bwd<GT, DT, CT, true>), gr, bl, lds, s, (const GT*)g, cell_of, depth,     \
                                (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
         else                                                                                                      \
