@@ -528,16 +528,28 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
     // stage: element (k, p), pixels fastest. With HW % 8 == 0 an aligned run of 8 pixels never
     // crosses an image, so each thread moves 16 B (8 pixels of one channel) per load.
     if ((HW & 7) == 0) {
-        for (int i = threadIdx.x; i < K * (kDnPix / 8); i += kBlock) {
-            const int k = i / (kDnPix / 8), p8 = (i - k * (kDnPix / 8)) * 8, q = q0 + p8;
-            uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if (q < npix) {
-                const int bn = q / HW, hw = q - bn * HW;
-                v = *reinterpret_cast<const uint4*>(feat + ((size_t)bn * K + k) * HW + hw);
-            }
-            const unsigned short* e = reinterpret_cast<const unsigned short*>(&v);
+        // every load of the thread first (one memory round trip), then the LDS writes
+        constexpr int kIt = kDnMaxK * (kDnPix / 8) / kBlock;
+        uint4 v[kIt];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) reinterpret_cast<unsigned short*>(&s_x[p8 + j][0])[k] = e[j];
+        for (int t = 0; t < kIt; ++t) {
+            const int i = threadIdx.x + t * kBlock;
+            const int k = i / (kDnPix / 8), p8 = (i - k * (kDnPix / 8)) * 8, q = q0 + p8;
+            v[t] = make_uint4(0u, 0u, 0u, 0u);
+            if (k < K && q < npix) {
+                const int bn = q / HW, hw = q - bn * HW;
+                v[t] = *reinterpret_cast<const uint4*>(feat + ((size_t)bn * K + k) * HW + hw);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < kIt; ++t) {
+            const int i = threadIdx.x + t * kBlock;
+            const int k = i / (kDnPix / 8), p8 = (i - k * (kDnPix / 8)) * 8;
+            if (k < K) {
+                const unsigned short* e = reinterpret_cast<const unsigned short*>(&v[t]);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) reinterpret_cast<unsigned short*>(&s_x[p8 + j][0])[k] = e[j];
+            }
         }
     } else {
         for (int i = threadIdx.x; i < K * kDnPix; i += kBlock) {
@@ -556,12 +568,19 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
     const int o = wave * 32 + r;
     const bf16* wrow = weight + (size_t)min(o, O - 1) * K + 8 * h;
     f32x16 acc = {};
-    for (int k0 = 0; k0 < K; k0 += 16) {
-        // A[row o][k = k0 + 8h + j] (weight row), B[k = k0 + 8h + j][col p = r] (staged pixel r)
-        bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + k0);
-        if (o >= O) a = bf16x8{};
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&s_x[r][k0 + 8 * h]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+    // four weight fragments (L2 reads) in flight ahead of their MFMAs
+    for (int k0 = 0; k0 < K; k0 += 64) {
+        bf16x8 a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int kk = min(k0 + 16 * u, K - 16);  // K % 16 == 0; a clamped step is skipped below
+            a[u] = *reinterpret_cast<const bf16x8*>(wrow + kk);
+            if (o >= O) a[u] = bf16x8{};
+            b[u] = *reinterpret_cast<const bf16x8*>(&s_x[r][kk + 8 * h]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k0 + 16 * u < K) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], b[u], acc, 0, 0, 0);
     }
     // D/C layout: column (pixel) = lane & 31, row (output channel) = (i & 3) + 8 (i >> 2) + 4 (lane >> 5)
 #pragma unroll
