@@ -1,26 +1,40 @@
 """LSS fwd+bwd frames/sec (BASELINE.json metric) on 1..8 MI355X, one process per GPU.
 
-Workload (config 3 of BASELINE.json): B=8 samples x 6 cameras x 128x352 per GPU,
-D=41, 200x200 BEV, bf16 autocast, full training step of train_simbev.py:229-248
-(forward, SimpleLoss, backward, clip_grad_norm_(5.0), Adam step). Synthetic
-SimBEV-shaped inputs, random-init weights. The step is replayed as
-two HIP graphs (train_step.TrainStep: fwd+loss+bwd | clip+Adam) with one RCCL
-all-reduce of the flat fp32 gradient between them; --graph 0 runs it eagerly (DDP).
-For N>1: torchrun, one rank per GPU, B=8 per rank (weak scaling).
+Workload (default: config 3 of BASELINE.json): B=8 samples x 6 cameras x 128x352 per GPU, D=41,
+200x200 BEV, bf16 autocast, the full training step of train_simbev.py:229-248 (forward, SimpleLoss,
+backward, clip_grad_norm_(5.0), Adam step). Synthetic SimBEV-shaped inputs,
+random-init weights. The step is replayed as two HIP graphs (train_step.TrainStep: fwd+loss+bwd |
+clip+Adam) with one RCCL all-reduce of the flat fp32 gradient between them; the camera inverses are
+the host's torch.inverse (src/models.py:180,186), staged into the graph's static inputs before each
+replay (ops.HostInverses). --graph 0 runs the step eagerly (DDP for N>1).
+
+  python bench.py                          # N=1, config 3
+  python bench.py --gpus 8                 # launches 8 ranks (torchrun) itself, B=8 per rank
+  python bench.py --config c2              # config 2: B=4, fp32, forward only (NCHW BEV)
+  python bench.py --config c5              # config 5 per-GPU shard: B=4, 256x704, D=60, 400x400
 
 Also reported on the same JSON line:
-  roofline      the fused lift+splat forward kernel (lss_splat_fwd): algorithmic
-                bytes per launch / its average launch time (HIP events on the
-                launch stream, over the timed steps) vs 8 TB/s HBM peak
-  cpu_baseline  the CPU oracle (restatement of the reference's path, fp32 eager,
-                conv stacks on the CPU) timed on this host, rank 0, N=1 only
+  roofline      the splat forward kernel (lss_splat_fwd): algorithmic bytes per launch / its average
+                launch time (kernel-stamped hipEvents on its own stream) vs 8 TB/s HBM peak; `traffic`
+                = HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the
+                same kernel and shapes, run by this script (scripts/splat_pmc.py, before the GPU is
+                touched here), FETCH_SIZE doubled per the gfx950 correction of MI355X_MICROARCH.md
+  cpu_baseline  the CPU oracle (restatement of the reference's path, fp32 eager, same conv stacks)
+                timed on this host, rank 0, N=1 only: full-model training steps and the hot path
+                alone, at the config 3 shape and at config 1; `value` = full model at config 3
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -47,39 +61,67 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=8, help="samples per GPU")
-    ap.add_argument("--config", default="c3")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--bev-layout", default="nhwc", choices=["nhwc", "nchw"])
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--batch", type=int, default=0, help="samples per GPU (0: the config's)")
+    ap.add_argument("--mode", default="auto", choices=["auto", "train", "fwd"],
+                    help="auto: forward only for config 2 (fp32), the full training step otherwise")
+    ap.add_argument("--dtype", default="", choices=["", "bf16", "fp32"])
+    ap.add_argument("--bev-layout", default="", choices=["", "nhwc", "nchw"])
     ap.add_argument("--trunk-channels-last", type=int, default=0)
-    ap.add_argument("--trunk-fp32", type=int, default=0, help="run CamEncode outside autocast")
     ap.add_argument("--dw-impl", default="hip", choices=["hip", "miopen", "native", "fp32"],
                     help="depthwise convs of the trunk: HIP kernels, MIOpen, PyTorch native, MIOpen in fp32")
     ap.add_argument("--miopen-find", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
     ap.add_argument("--hip-bn", type=int, default=1, help="BatchNorm + activation on the lss_bn_* kernels")
-    ap.add_argument("--bn-native", default="", help="with --hip-bn 0: BatchNorm on PyTorch's native kernels: "
-                                                    "'', 'trunk', 'bev', 'all'")
-    ap.add_argument("--inverse", default="host", choices=["host", "device"])
+    ap.add_argument("--inverse", default="host", choices=["host", "device"],
+                    help="host: torch.inverse on the CPU (the reference's; bit-exact ids), device: fp64 kernel")
     ap.add_argument("--fuse-depthnet", type=int, default=1, help="depthnet 1x1 conv inside the lift kernel (MFMA)")
     ap.add_argument("--graph", type=int, default=1,
-                    help="replay the step as two HIP graphs (fwd+bwd, clip+Adam) with the gradient all-reduce "
+                    help="replay the step as HIP graphs (fwd+bwd, clip+Adam) with the gradient all-reduce "
                          "between them; 0 = eager (DDP for N>1)")
     ap.add_argument("--flat-params", type=int, default=1,
                     help="trainable parameters as one fp32 master tensor with one bf16 working copy per step")
-    ap.add_argument("--graph-splat-timing", type=int, default=0,
-                    help="also bracket the captured splat launch with event-record nodes (upper bound)")
     ap.add_argument("--profile-steps", type=int, default=8,
-                    help="steps after the timed region on which the splat kernel is timed (graph replays, then eager)")
+                    help="eager steps after the timed region on which the splat kernel is timed")
+    ap.add_argument("--pmc-traffic", type=int, default=1, help="rocprofv3 FETCH_SIZE/WRITE_SIZE passes (rank 0, N=1)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "splat_fwd_traffic.json"))
-    return ap.parse_args()
+    ap.add_argument("--cpu-runs", type=int, default=3, help="timed CPU runs per case (median; 1 warm-up before)")
+    args = ap.parse_args()
+    cfg_b = {"c1": 1, "c2": 4, "c3": 8, "c4": 8, "c5": 4}[args.config]
+    args.batch = args.batch or cfg_b
+    if args.mode == "auto":
+        args.mode = "fwd" if args.config == "c2" else "train"
+    if not args.dtype:
+        args.dtype = "fp32" if args.mode == "fwd" else "bf16"
+    if not args.bev_layout:
+        args.bev_layout = "nhwc" if args.dtype == "bf16" else "nchw"
+    return args
 
 
-def setup_dist():
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def maybe_launch_ranks(args) -> None:
+    """`--gpus N` without a torchrun environment: launch N ranks (one process per GPU) through
+    torch.distributed.run as a child process -- before this process touches the GPU -- and exit with
+    its status. Rank 0 of the child job prints the JSON line."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    log(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[rank {rank}] note: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the job's {world} ranks")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -90,17 +132,148 @@ def setup_dist():
 
 
 def splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes, ctx_bytes) -> int:
-    """Algorithmic bytes of one lss_splat_fwd launch."""
+    """Algorithmic bytes of one lss_splat_fwd launch (Roofline)."""
     nprime = B * N * D * H * W
     ncells = B * Z * X * Y
-    return (nprime * 4                    # depth (fp32)
+    return (nprime * 4                    # depth weights (fp32), one per point
             + B * N * H * W * 64 * ctx_bytes  # context rows (the depthnet output's type: bf16 under autocast)
             + kept * 4                    # sorted point ids
             + (ncells + 1) * 4            # cell_start
             + ncells * 64 * out_bytes)    # dense BEV, every element written once
 
 
-def build_model(args, dev, cfg, gc, dac):
+# ----------------------------------------------------------------------------- HBM traffic (PMC)
+def measure_traffic(args, B) -> dict | None:
+    """FETCH_SIZE and WRITE_SIZE of lss_splat_fwd per launch (rocprofv3, one pass per counter group),
+    on scripts/splat_pmc.py with this run's config / batch / dtype / layout. Runs child processes
+    before this process initialises the GPU; returns None if rocprofv3 is unavailable or fails."""
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="lss_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(tmp, ctr)
+        cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", ctr, "--kernel-include-regex", "k_splat_fwd",
+               "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable,
+               os.path.join(REPO, "scripts", "splat_pmc.py"), "--config", args.config, "--batch", str(B),
+               "--dtype", args.dtype, "--layout", args.bev_layout]
+        try:
+            r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=170)
+        except subprocess.TimeoutExpired:
+            log(f"[bench] rocprofv3 {ctr} pass timed out")
+            return None
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            log(f"[bench] rocprofv3 {ctr} pass failed (rc={r.returncode}): {r.stderr[-400:]}")
+            return None
+        vals = []
+        for f in files:
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if "k_splat_fwd" in row["Kernel_Name"] and row["Counter_Name"] == ctr:
+                        vals.append(float(row["Counter_Value"]))
+        if not vals:
+            return None
+        vals = vals[2:] if len(vals) > 4 else vals  # first launches: cold caches, one-time page mapping
+        out[ctr] = sum(vals) / len(vals) * 1024.0  # counters are in KiB
+    shutil.rmtree(tmp, ignore_errors=True)
+    return {"fetch_bytes_raw": round(out["FETCH_SIZE"]), "write_bytes": round(out["WRITE_SIZE"]),
+            "hbm_bytes_per_launch": round(2 * out["FETCH_SIZE"] + out["WRITE_SIZE"])}
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_threads() -> tuple:
+    """Threads for the CPU baseline: the CPUs this process may run on, capped by the cgroup quota."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    n = min(aff, quota) if quota else aff
+    return n, {"os_cpu_count": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota}
+
+
+def cpu_baseline(model, args) -> dict:
+    """The reference path on the host (fp32 eager): the oracle's geometry/lift/splat (a restatement of
+    src/models.py:170-246, src/tools.py:182-219) plus the same conv stacks. Full-model training steps
+    (fwd + SimpleLoss + bwd + clip + Adam) and the hot path alone (depthnet output -> geometry, lift,
+    splat -> sum().backward()), at the config 3 shape (B=8 x 6 cams) and at config 1; 1 warm-up, then
+    the median of `cpu_runs` runs."""
+    import copy
+    import statistics
+
+    from oracle import lss_ref as ref
+    from lss_carla_amd import synthetic as syn
+    import lss_carla_amd as L
+
+    threads, tinfo = cpu_threads()
+    torch.set_num_threads(threads)
+    cpu_model = copy.deepcopy(model).to("cpu").float()
+    cpu_model.static_inverses = None
+    cpu_model.bevencode.to(memory_format=torch.contiguous_format)
+    cpu_model.camencode.to(memory_format=torch.contiguous_format)
+    cpu_model.train()
+    loss_fn = L.SimpleLoss(2.13)
+    opt = torch.optim.Adam(cpu_model.parameters(), lr=1e-3, weight_decay=1e-7)
+    frustum = cpu_model.frustum.detach()
+
+    def median_time(fn):
+        fn()  # warm-up
+        ts = []
+        for _ in range(args.cpu_runs):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts)
+
+    res = {}
+    for name in ("c3", "c1"):
+        cfg, gc, _ = syn.config_confs(name)
+        B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
+        dx, bx, nx = ref.gen_dx_bx(gc["xbound"], gc["ybound"], gc["zbound"])
+        rig = syn.make_rig(B, N, fd, seed=0)
+        imgs = syn.make_images(B, N, fd)
+        labels = syn.make_labels(B, int(nx[0]), int(nx[1]))
+        fr = ref.create_frustum(fd, gc["dbound"]) if name != args.config else frustum
+        D, H, W = fr.shape[:3]
+        dn = syn.make_depthnet_out(B, N, D, H, W, seed=0).requires_grad_(True)
+
+        def full_step():
+            opt.zero_grad()
+            out = ref.full_forward(cpu_model.camencode.depthnet_out, cpu_model.bevencode, fr, imgs, rig["rots"],
+                                   rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"], dx, bx, nx, D)
+            loss_fn(out, labels).backward()
+            torch.nn.utils.clip_grad_norm_(cpu_model.parameters(), 5.0)
+            opt.step()
+
+        def hot_path():
+            dn.grad = None
+            ref.get_voxels(fr, dn, rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"],
+                           dx, bx, nx, D).sum().backward()
+
+        t_hot = median_time(hot_path)
+        t_full = median_time(full_step)
+        res[name] = {"B": B, "N": N, "full_model_frames_per_s": round(B / t_full, 4),
+                     "hot_path_frames_per_s": round(B / t_hot, 3),
+                     "full_step_s": round(t_full, 4), "hot_path_s": round(t_hot, 5)}
+    return {"value": res["c3"]["full_model_frames_per_s"], "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": (f"full training steps (fwd+loss+bwd+clip+Adam) at the config 3 shape, B=8 x 6 cams x "
+                       f"128x352, fp32 eager, oracle lift/splat + the same conv stacks; {threads} threads "
+                       f"({tinfo}); 1 warm-up + median of {args.cpu_runs}"),
+            "detail": res}
+
+
+# ----------------------------------------------------------------------------- model / steps
+def build_model(args, dev, gc, dac):
     import lss_carla_amd as L
 
     model = L.compile_model(gc, dac, outC=1).to(dev)
@@ -115,109 +288,106 @@ def build_model(args, dev, cfg, gc, dac):
     norm.USE_HIP_BN = bool(args.hip_bn)
     from lss_carla_amd.efficientnet import set_depthwise_impl
     set_depthwise_impl(model.camencode.trunk, args.dw_impl)
-    if args.bn_native:
-        from lss_carla_amd.efficientnet import set_batchnorm_native
-        if args.bn_native in ("trunk", "all"):
-            set_batchnorm_native(model.camencode)
-        if args.bn_native in ("bev", "all"):
-            set_batchnorm_native(model.bevencode)
-    if args.trunk_fp32:
-        ce = model.camencode
-        fwd = ce.depthnet_out
-
-        def depthnet_out_fp32(x):
-            with torch.autocast("cuda", enabled=False):
-                return fwd(x.float())
-        ce.depthnet_out = depthnet_out_fp32
-    model.train()
+    model.train() if args.mode == "train" else model.eval()
     return model
 
 
-def cpu_baseline(model, cfg, gc, seconds: float):
-    """Reference path on the host: oracle geometry/lift/splat + the same conv stacks, fp32, eager."""
-    import copy
+class FwdStep:
+    """Forward only (config 2): the model's forward under no_grad, eager or replayed as one HIP graph."""
 
-    from oracle import lss_ref as ref
-    from lss_carla_amd import synthetic as syn
-    import lss_carla_amd as L
+    def __init__(self, model, inputs, pre_step=None):
+        self.model, self.inputs, self.pre_step = model, inputs, pre_step
+        self.graph = None
+        self.out = None
 
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    torch.set_num_threads(threads)
-    cpu_model = copy.deepcopy(model).to("cpu").float()
-    cpu_model.bevencode.to(memory_format=torch.contiguous_format)
-    cpu_model.camencode.to(memory_format=torch.contiguous_format)
-    cpu_model.train()
-    B = 1
-    rig = syn.make_rig(B, cfg["N"], cfg["final_dim"], seed=0)
-    imgs = syn.make_images(B, cfg["N"], cfg["final_dim"])
-    labels = syn.make_labels(B, 200, 200)
-    frustum = cpu_model.frustum.detach()
-    dx, bx, nx = ref.gen_dx_bx(gc["xbound"], gc["ybound"], gc["zbound"])
-    loss_fn = L.SimpleLoss(2.13)
-    opt = torch.optim.Adam(cpu_model.parameters(), lr=1e-3, weight_decay=1e-7)
+    def eager(self):
+        if self.pre_step is not None:
+            self.pre_step()
+        with torch.no_grad():
+            self.out = self.model(*self.inputs)
+        return self.out
 
-    def step():
-        opt.zero_grad()
-        out = ref.full_forward(cpu_model.camencode.depthnet_out, cpu_model.bevencode, frustum, imgs, rig["rots"],
-                               rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"], dx, bx, nx,
-                               cpu_model.D)
-        loss = loss_fn(out, labels)
-        loss.backward()
-        torch.nn.utils.clip_grad_norm_(cpu_model.parameters(), 5.0)
-        opt.step()
+    def capture(self, warmup, on_warmup=None):
+        dev = self.inputs[0].device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for i in range(max(warmup, 1)):
+                self.eager()
+                if on_warmup is not None:
+                    on_warmup(i)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph), torch.no_grad():
+            self.out = self.model(*self.inputs)
 
-    step()  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        step()
-        n += 1
-        el = time.perf_counter() - t0
-        if (el >= seconds and n >= 2) or el >= 2 * seconds:
-            break
-    return {"value": round(B * n / el, 4), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"B=1 x {cfg['N']} cams x {cfg['final_dim'][0]}x{cfg['final_dim'][1]}, {n} full training "
-                      f"steps (fwd+bwd+clip+Adam) in {el:.1f} s, fp32 eager, oracle lift/splat + same conv stacks"}
+    def __call__(self):
+        if self.graph is None:
+            return self.eager()
+        if self.pre_step is not None:
+            self.pre_step()
+        self.graph.replay()
+        return self.out
 
 
 def main():
     args = parse()
-    world, rank, dev = setup_dist()
+    maybe_launch_ranks(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    from lss_carla_amd import synthetic as syn
+    cfg, gc, dac = syn.config_confs(args.config)
+    B, N, fd = args.batch, cfg["N"], cfg["final_dim"]
+    traffic = None
+    if args.pmc_traffic and world == 1 and rank == 0:
+        t_p = time.perf_counter()
+        traffic = measure_traffic(args, B)  # child processes, before this process touches the GPU
+        log(f"[rank 0] splat PMC traffic {traffic} ({time.perf_counter() - t_p:.1f} s)")
+
+    world, rank, dev = setup_dist(args)
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
-    from lss_carla_amd import ops, parallel, synthetic as syn
+    from lss_carla_amd import ops, parallel
     from lss_carla_amd.flat_params import FlatParams
     from lss_carla_amd.train_step import TrainStep
     import lss_carla_amd as L
 
-    cfg, gc, dac = syn.config_confs(args.config)
-    B, N, fd = args.batch, cfg["N"], cfg["final_dim"]
     torch.manual_seed(1234 + rank)
-    if args.graph:
-        args.inverse = "device"  # inverse='host' is a device->host round trip: not capturable
-    model = build_model(args, dev, cfg, gc, dac)
+    model = build_model(args, dev, gc, dac)
     amp_dtype = torch.bfloat16 if args.dtype == "bf16" else None
-    flat = None
-    if args.graph or args.flat_params:
-        # one process per GPU without DDP: identical replicas, one flat gradient all-reduce
-        parallel.broadcast_state(model)
-        parallel.freeze_unused(model)
-        flat = FlatParams(model, cast_dtype=amp_dtype) if args.flat_params else None
-    if flat is not None:
-        fwd, params = flat.bind(model), [flat.master]
-    else:
-        fwd = model if (args.graph or world == 1) else parallel.make_data_parallel(model, dev)
-        params = [p for p in model.parameters() if p.requires_grad]
-    loss_fn = L.SimpleLoss(2.13).to(dev)
-    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-7, fused=True, capturable=bool(args.graph))
-    rig = {k: v.to(dev) for k, v in syn.make_rig(B, N, fd, seed=rank).items()}
+    rig_host = syn.make_rig(B, N, fd, seed=rank)
+    rig = {k: v.to(dev) for k, v in rig_host.items()}
     imgs = syn.make_images(B, N, fd, seed=rank).to(dev)
-    if args.trunk_channels_last:
-        imgs = imgs.contiguous()
     X, Y, Z = ops.GridSpec.from_conf(gc).nx
     labels = syn.make_labels(B, X, Y, seed=rank).to(dev)
+    inputs = (imgs, rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"])
 
-    train = TrainStep(fwd, (imgs, rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"]),
-                      labels, loss_fn, opt, params, all_reduce=bool(args.graph or args.flat_params),
-                      amp_dtype=amp_dtype, max_grad_norm=5.0)
+    pre_step = None
+    if args.graph and args.inverse == "host":
+        # host torch.inverse of the (host) rig before every step, staged into the graph's static inputs
+        hinv = ops.HostInverses(B * N, dev)
+        model.static_inverses = (hinv.pinv, hinv.kinv)
+        pinned = {k: rig_host[k].pin_memory() for k in ("post_rots", "intrins")}
+        pre_step = lambda: hinv.update(pinned["post_rots"], pinned["intrins"])  # noqa: E731
+
+    if args.mode == "train":
+        flat = None
+        if args.graph or args.flat_params:
+            # one process per GPU without DDP: identical replicas, one flat gradient all-reduce
+            parallel.broadcast_state(model)
+            parallel.freeze_unused(model)
+            flat = FlatParams(model, cast_dtype=amp_dtype) if args.flat_params else None
+        if flat is not None:
+            fwd, params = flat.bind(model), [flat.master]
+        else:
+            fwd = model if (args.graph or world == 1) else parallel.make_data_parallel(model, dev)
+            params = [p for p in model.parameters() if p.requires_grad]
+        loss_fn = L.SimpleLoss(2.13).to(dev)
+        opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-7, fused=True, capturable=bool(args.graph))
+        step = TrainStep(fwd, inputs, labels, loss_fn, opt, params, all_reduce=bool(args.graph or args.flat_params),
+                         amp_dtype=amp_dtype, max_grad_norm=5.0, pre_step=pre_step)
+    else:
+        step = FwdStep(model, inputs, pre_step)
     t_w = time.perf_counter()
 
     def first(i):
@@ -227,63 +397,44 @@ def main():
 
     if args.graph:
         # eager warm-up on a side stream (MIOpen find, optimizer state), capture, 2 untimed replays
-        # opt-in: event-record nodes around the captured splat launch (an upper bound: each node
-        # adds a marker packet to the interval; measured 14.6 us bracket vs ~12 us kernel in rocprof)
-        ops.SPLAT_PROFILE.capture = bool(args.graph_splat_timing)
-        train.capture(warmup=max(args.warmup, 2), on_warmup=first)
-        ops.SPLAT_PROFILE.capture = False
+        step.capture(warmup=max(args.warmup, 2), on_warmup=first)
         for _ in range(2):
-            train()
+            step()
     else:
         for i in range(args.warmup):
-            train()
+            step()
             first(i)
     torch.cuda.synchronize()
     log(f"[rank {rank}] warmup {args.warmup} steps in {time.perf_counter() - t_w:.1f} s"
         + (" (incl. graph capture)" if args.graph else ""))
 
-    ops.SPLAT_PROFILE.reset(not args.graph)
+    ops.SPLAT_PROFILE.reset(False)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = train()
+        out = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    graph_bracket_ms = graph_marker_ms = None
-    if args.graph:
-        # Primary: the captured splat launch, bracketed by hipEvent-record nodes in the graph,
-        # read after each of `profile_steps` further replays (same cache state as the timed steps).
-        if ops.SPLAT_PROFILE.graph_pairs:
-            gms = []
-            try:
-                for _ in range(args.profile_steps):
-                    train()
-                    torch.cuda.synchronize()
-                    gms.append(ops.SPLAT_PROFILE.graph_ms())
-                graph_bracket_ms = sum(g[0] for g in gms) / len(gms)
-                graph_marker_ms = sum(g[1] for g in gms) / len(gms)
-            except RuntimeError as e:  # event-record nodes unsupported: fall back to the eager timing
-                log(f"[rank {rank}] captured splat timing unavailable ({e}); timing eager steps")
-        # Secondary: kernel-stamped events (hipExtLaunchKernel) on eager steps, same inputs
-        train.eager()  # the first eager step after the replays runs cold: not timed
-        torch.cuda.synchronize()
-        ops.SPLAT_PROFILE.reset(True)
-        for _ in range(args.profile_steps):
-            train.eager()
-        torch.cuda.synchronize()
+    # the splat kernel, timed with kernel-stamped events (hipExtLaunchKernel) on eager steps after the
+    # timed region, same inputs (a captured launch cannot carry kernel-stamped events)
+    step.eager()  # the first eager step after the replays runs cold: not timed
+    torch.cuda.synchronize()
+    ops.SPLAT_PROFILE.reset(True)
+    for _ in range(args.profile_steps):
+        step.eager()
+    torch.cuda.synchronize()
     ops.SPLAT_PROFILE.enabled = False
-    splat_eager_ms = ops.SPLAT_PROFILE.avg_ms()
+    splat_ms = ops.SPLAT_PROFILE.avg_ms()
     ops.SPLAT_PROFILE.release()
-    splat_ms = splat_eager_ms
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f} s, loss {loss.item():.4f}")
+    log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f} s, out {float(out.float().mean()):.4f}")
 
     if rank == 0:
         D, H, W = model.frustum.shape[:3]
@@ -293,38 +444,32 @@ def main():
         out_bytes = 2 if amp_dtype is not None else 4
         nbytes = splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes, ctx_bytes=out_bytes)
         achieved = nbytes / (splat_ms * 1e-3) / 1e9 if splat_ms else None
-        traffic = None
-        if os.path.exists(args.traffic_json):
-            try:
-                with open(args.traffic_json) as f:
-                    tj = json.load(f)
-                if tj.get("config") == args.config and tj.get("out_bytes") == out_bytes:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
         frames = world * B * args.steps
+        what = "full train step (fwd+loss+bwd+clip+Adam)" if args.mode == "train" else "forward only"
         res = {
             "metric": METRIC, "value": round(frames / elapsed, 3), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (SimBEV-shaped rig, random-init weights)",
             "config": {"workload": f"{args.config}: B={B}/GPU x {N} cams x {fd[0]}x{fd[1]}, D={D}, {X}x{Y} BEV, "
-                                   "full train step (fwd+loss+bwd+clip+Adam)",
+                                   + what,
                        "global_batch": world * B, "parallelism": f"dp{world}", "bev_layout": args.bev_layout,
                        "inverse": args.inverse, "fuse_depthnet": bool(args.fuse_depthnet),
                        "depthwise": args.dw_impl, "batchnorm": "hip" if args.hip_bn else "miopen",
                        "step": "hipgraph" if args.graph else "eager", "flat_params": bool(args.flat_params)},
             "roofline": {"kernel": "lss_splat_fwd", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,
-                         "algorithmic_bytes": nbytes, "avg_launch_us": round(splat_ms * 1e3, 2) if splat_ms else None,
-                         "timed_in": "eager steps after the timed replays, kernel-stamped hipEvents",
-                         **({"graph_bracket_us": round(graph_bracket_ms * 1e3, 2),
-                             "graph_empty_pair_us": round(graph_marker_ms * 1e3, 2)} if graph_bracket_ms else {})},
+                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                         "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
+                         "traffic_detail": traffic, "algorithmic_bytes": nbytes,
+                         "avg_launch_us": round(splat_ms * 1e3, 2) if splat_ms else None,
+                         "timed_in": "eager steps after the timed replays, kernel-stamped hipEvents"},
         }
-        if args.cpu_baseline and world == 1:
+        if args.cpu_baseline and world == 1 and args.config == "c3":
             log("[rank 0] timing the CPU baseline ...")
-            res["cpu_baseline"] = cpu_baseline(model, cfg, gc, args.cpu_seconds)
+            t_c = time.perf_counter()
+            res["cpu_baseline"] = cpu_baseline(model, args)
+            log(f"[rank 0] CPU baseline in {time.perf_counter() - t_c:.1f} s")
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)

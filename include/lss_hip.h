@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 9
+#define LSS_ABI_VERSION 10
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -165,6 +165,26 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
 int lss_splat_bwd_lifted(const void* g, int32_t g_dtype, int32_t rows_layout, const int32_t* cell_of,
                          int32_t nprime, const lss_dims_t* dims, const lss_grid_t* grid,
                          float* dx, lss_stream_t stream);
+
+/* ---- The reference's op-level boundary: QuickCumsum / cumsum_trick (src/tools.py:182-219).
+ * Rows x (n, C) fp32 sorted by an int64 rank (src/models.py:226-231); one output row per run of
+ * equal ranks.
+ * lss_segment_build: seg_of[i] (n) = run index of row i; seg_start (n + 1 capacity) = first row of
+ *   each run, seg_start[nseg] = n; nseg (1 int, device) = number of runs. Replaces
+ *   `kept[:-1] = ranks[1:] != ranks[:-1]` and QuickCumsum.backward's `cumsum(kept) - 1`
+ *   (src/tools.py:197-198, 214-215). scratch: lss_segment_scratch_bytes(n) bytes. n > 0.
+ * lss_segment_sum: out[j] (nseg, C) = sum of the rows of run j in row order (fp32);
+ *   key_out[j] (nseg, key_width) = keys row of the run's last row -- geom_feats[kept]
+ *   (src/tools.py:200); keys may be NULL. Replaces QuickCumsum.forward / cumsum_trick
+ *   (src/tools.py:182-209).
+ * lss_segment_gather: dx[i] = g[seg_of[i]] (n, C) -- QuickCumsum.backward (src/tools.py:212-219). */
+size_t lss_segment_scratch_bytes(int32_t n);
+int lss_segment_build(const long long* ranks, int32_t n, int32_t* seg_of, int32_t* seg_start, int32_t* nseg,
+                      void* scratch, lss_stream_t stream);
+int lss_segment_sum(const float* x, int32_t C, const int32_t* seg_start, int32_t nseg, const long long* keys,
+                    int32_t key_width, long long* key_out, float* out, lss_stream_t stream);
+int lss_segment_gather(const float* g, int32_t C, const int32_t* seg_of, int32_t n, float* dx,
+                       lss_stream_t stream);
 
 #ifdef __cplusplus
 }

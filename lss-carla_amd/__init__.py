@@ -14,8 +14,8 @@ __version__ = "0.1.0"
 _LAZY = {
     "compile_model": "models", "LiftSplatShoot": "models", "CamEncode": "models",
     "BevEncode": "models", "Up": "models",
-    "gen_dx_bx": "tools", "SimpleLoss": "tools", "get_batch_iou": "tools",
-    "QuickCumsum": "tools", "cumsum_trick": "tools",
+    "gen_dx_bx": "tools", "SimpleLoss": "tools", "get_batch_iou": "tools", "get_batch_iou_device": "tools",
+    "get_val_info": "tools", "QuickCumsum": "tools", "cumsum_trick": "tools",
 }
 
 

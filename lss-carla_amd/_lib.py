@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(_HERE, "liblss_hip.so")
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class Dims(ctypes.Structure):
@@ -53,6 +53,10 @@ SIGNATURES = {
     "lss_bev_rows": (ctypes.c_int, [_p, _i32, _p, _DIMS, _GRID, _p, _p]),
     "lss_splat_bwd": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p, _i32, _DIMS, _GRID, _p, _i32, _p]),
     "lss_splat_bwd_lifted": (ctypes.c_int, [_p, _i32, _i32, _p, _i32, _DIMS, _GRID, _p, _p]),
+    "lss_segment_scratch_bytes": (ctypes.c_size_t, [_i32]),
+    "lss_segment_build": (ctypes.c_int, [_p, _i32, _p, _p, _p, _p, _p]),
+    "lss_segment_sum": (ctypes.c_int, [_p, _i32, _p, _i32, _p, _i32, _p, _p, _p]),
+    "lss_segment_gather": (ctypes.c_int, [_p, _i32, _p, _i32, _p, _p]),
     # include/lss_convs.h (conv-stack kernels, same library)
     "lss_dwconv_fwd": (ctypes.c_int, [_p, _i32, _p] + [_i32] * 10 + [_p, _p]),
     "lss_dwconv_bwd_data": (ctypes.c_int, [_p, _i32, _p] + [_i32] * 10 + [_p, _p]),

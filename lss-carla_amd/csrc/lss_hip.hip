@@ -919,6 +919,11 @@ __device__ __forceinline__ OutT* cell_row(OutT* out, int cell, const BevGeo& g) 
 #define LSS_ZERO_UNITS 1  // 64-cell zero-fill units per wave (their cell_start loads in flight together)
 #endif
 constexpr int kZeroUnits = LSS_ZERO_UNITS;
+#ifndef LSS_SPLAT_WAVES
+#define LSS_SPLAT_WAVES 4  // waves per block of the channels-last splat kernels (waves are independent)
+#endif
+constexpr int kSplatWaves = LSS_SPLAT_WAVES;
+constexpr int kSplatBlock = kSplatWaves * kWave;
 #ifndef LSS_CHUNK_GAP
 #define LSS_CHUNK_GAP 0  // >0: each chunk wave also zeroes the first G empty cells after each cell it owns
 #endif
@@ -1204,7 +1209,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 }
 
 template <bool FUSED, typename RT, typename OutT>
-__global__ __launch_bounds__(kBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const float* __restrict__ depth,
+__global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const float* __restrict__ depth,
                                                            const float* __restrict__ sorted_depth,
                                                            const RT* __restrict__ rows_base,
                                                            const int32_t* __restrict__ cell_start,
@@ -1212,8 +1217,8 @@ __global__ __launch_bounds__(kBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const 
                                                            const int32_t* __restrict__ sorted_row, BevGeo g,
                                                            int nprime, int nchunk_blocks, int nzero_blocks,
                                                            OutT* __restrict__ out) {
-    __shared__ EntryMeta s_meta[kBlock / kWave][2 * kWave];
-    __shared__ __attribute__((aligned(16))) float s_part[kBlock / kWave][2 * RowSlice<RT>::NG * kC];
+    __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
+    __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][2 * RowSlice<RT>::NG * kC];
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     // Blocks come in groups of 8, one per XCD (blocks are dealt round-robin over the 8 XCDs). Chunk
@@ -1238,7 +1243,7 @@ __global__ __launch_bounds__(kBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const 
         if (LSS_FWD_SKIP & 1) return;
         const int cb = LSS_XCD_MAP ? x * ncg + cgi : cgi * 8 + x;
         if (cb >= nchunk_blocks) return;
-        const int w = cb * (kBlock / kWave) + wave;
+        const int w = cb * (kSplatWaves) + wave;
         LSS_STAMP(w, 0);
         splat_chunk<FUSED, RT, OutT>(w, nprime, depth, sorted_depth, rows_base, sorted_key, sorted_row, cell_start, g, out, s_meta[wave],
                                      s_part[wave], lane);
@@ -1251,8 +1256,8 @@ __global__ __launch_bounds__(kBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const 
         if (LSS_FWD_SKIP & 2) return;
         const int zb = zgi * 8 + x;
         if (zb >= nzero_blocks) return;
-        const int u = (zb * (kBlock / kWave) + wave) * kZeroUnits;
-        [[maybe_unused]] const int zslot = nchunk_blocks * (kBlock / kWave) + zb * (kBlock / kWave) + wave;
+        const int u = (zb * (kSplatWaves) + wave) * kZeroUnits;
+        [[maybe_unused]] const int zslot = nchunk_blocks * (kSplatWaves) + zb * (kSplatWaves) + wave;
         LSS_STAMP(zslot, 0);
         if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, sorted_key, g, out, lane);
         LSS_STAMP(zslot, 3);
@@ -1260,6 +1265,205 @@ __global__ __launch_bounds__(kBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const 
         if (lane == 0 && zslot < 16384) g_lss_trace[zslot][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
                                                         (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
 #endif
+    }
+}
+
+// ----------------------------------------------------------------------------- splat forward, channels-last, merged roles
+// Every wave owns one chunk (64 canonical CSR entries, cells owned as in splat_chunk) AND one zero
+// unit (64 consecutive cells), so the grid is max(chunks, units) waves -- all resident at once at
+// c3 -- instead of chunks + units waves in two generations. Order inside a wave:
+//   round trip 1   the chunk's keys / context rows / previous cell and the unit's cell starts, one batch;
+//   gathers        every owned entry's context-row slice and depth weight (lane groups as splat_chunk);
+//   zero stores    the unit's empty rows, issued while the gathers are in flight (a load issued AFTER a
+//                  store would wait for it: vmcnt counts both in issue order, so stores go after loads);
+//   sums           cell by cell in canonical order; rows of cells inside one lane group stored at once;
+//   split cells    a cell cut by lane-group boundaries: the groups' pieces are combined by a segmented
+//                  scan over the groups with cross-lane shuffles (fixed association, no LDS, no barrier).
+#ifndef LSS_SPLAT_IMPL
+#define LSS_SPLAT_IMPL 0  // channels-last splat: 0 two block roles (k_splat_fwd_nhwc), 1 merged roles
+#endif
+#ifndef LSS_MIN_WAVES_M
+#define LSS_MIN_WAVES_M 6  // occupancy floor of the merged kernel (waves per SIMD)
+#endif
+#ifndef LSS_UNROLL_M
+#define LSS_UNROLL_M 8     // entries per lane group gathered in the first batch
+#endif
+constexpr int kUnrollM = LSS_UNROLL_M;
+
+template <typename OutT>
+__device__ __forceinline__ void zero_unit_rows(int k0, unsigned long long emask, const BevGeo& g,
+                                               OutT* __restrict__ out, int lane) {
+    constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
+    constexpr unsigned long long kRowMask = (RPS == 64) ? ~0ull : ((1ull << RPS) - 1);
+#pragma unroll
+    for (int r0 = 0; r0 < kWave; r0 += RPS) {
+        if (((emask >> r0) & kRowMask) == 0) continue;  // wave-uniform
+        const int r = r0 + lane / LPR;
+        if ((emask >> r) & 1ull) {
+            OutT* dst = cell_row(out, k0 + r, g) + (lane % LPR) * EPL;
+            if (LSS_ZERO_STORE == 1) __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, reinterpret_cast<u32x4*>(dst));
+            else store_zero_vec(dst);
+        }
+    }
+}
+
+template <bool FUSED, typename RT, typename OutT>
+__global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES_M) void k_splat_fwd_nhwc_m(
+    const float* __restrict__ depth, const float* __restrict__ sorted_depth, const RT* __restrict__ rows_base,
+    const int32_t* __restrict__ cell_start, const long long* __restrict__ sorted_key,
+    const int32_t* __restrict__ sorted_row, BevGeo g, int nprime, int nchunks, int nunits, OutT* __restrict__ out) {
+    using RS = RowSlice<RT>;
+    constexpr int EPL = RS::EPL, LPR = RS::LPR, NG = RS::NG;
+    __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
+    __shared__ __attribute__((aligned(16))) float s_head[kSplatWaves][NG * kC];  // head pieces, lane-private
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    EntryMeta* meta = s_meta[wave];
+    // blocks are dealt round-robin over the 8 XCDs: the chunk blocks of one XCD are a contiguous run of
+    // chunks (about one sample's cameras, whose context rows then stay in that L2); gridDim.x % 8 == 0
+    const int per_xcd = gridDim.x >> 3;
+    const int w = ((blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3)) * (kSplatWaves) + wave;  // chunk
+    const int zu = blockIdx.x * (kSplatWaves) + wave;                                        // zero unit
+
+    // ---- round trip 1
+    const bool has_chunk = w < nchunks;  // wave-uniform
+    const int base = w * kWave;
+    const int e0 = base + lane, e1 = base + kWave + lane;
+    long long k0 = -1ll, k1 = -1ll;
+    int rs0 = 0, rs1 = 0, prevcell = -2;
+    float sw0 = 0.f, sw1 = 0.f;
+    const bool sorted_w = FUSED && sorted_depth != nullptr;
+    if (has_chunk) {
+        k0 = e0 < nprime ? sorted_key[e0] : -1ll;
+        k1 = e1 < nprime ? sorted_key[e1] : -1ll;
+        if (FUSED) {
+            rs0 = e0 < nprime ? sorted_row[e0] : 0;
+            rs1 = e1 < nprime ? sorted_row[e1] : 0;
+        }
+        if (sorted_w) {
+            sw0 = e0 < nprime ? sorted_depth[e0] : 0.f;
+            sw1 = e1 < nprime ? sorted_depth[e1] : 0.f;
+        }
+        prevcell = base > 0 ? (int)(sorted_key[base - 1] >> 32) : -2;
+    }
+    const int kz = zu * kWave + lane;
+    int za = 0, zb = 0;
+    if (zu < nunits && kz < g.ncells) {
+        za = cell_start[kz];
+        zb = cell_start[kz + 1];
+    }
+    const unsigned long long emask = __ballot(zu < nunits && kz < g.ncells && za == zb);
+    const int c0 = (int)(k0 >> 32), c1 = (int)(k1 >> 32);
+    const int p0 = (int)(k0 & 0xFFFFFFFF), p1 = (int)(k1 & 0xFFFFFFFF);
+    if (!FUSED) {
+        rs0 = p0;
+        rs1 = p1;
+    }
+    Span sp{0, 0, -1};
+    if (has_chunk) sp = chunk_span(c0, c1, prevcell, lane);
+    const int s = uniform(sp.s), end = uniform(sp.end), big = uniform(sp.big);
+
+    if (end > 0) {
+        meta[lane] = EntryMeta{rs0, p0, c0, __float_as_int(sw0)};
+        meta[kWave + lane] = EntryMeta{rs1, p1, c1, __float_as_int(sw1)};
+        __builtin_amdgcn_wave_barrier();
+        const int n = end - s;
+        const int grp = lane / LPR, col = (lane % LPR) * EPL;
+        const int gs = s + (n * grp) / NG, ge = s + (n * (grp + 1)) / NG;
+        const int first_cell = gs < ge ? meta[gs].cell : -1;
+        const int last_cell = gs < ge ? meta[ge - 1].cell : -1;
+        const bool head_split = gs < ge && gs > s && meta[gs - 1].cell == first_cell;
+        const bool tail_split = gs < ge && ge < end && meta[ge].cell == last_cell;
+        const bool middle = head_split && tail_split && first_cell == last_cell;  // one cell across both cuts
+        // gathers of the first batch: row slices and depth weights, all in flight together
+        uint4 v[kUnrollM];
+        float wt[kUnrollM];
+#pragma unroll
+        for (int u = 0; u < kUnrollM; ++u) {
+            const int4 m = *reinterpret_cast<const int4*>(&meta[gs < ge ? min(gs + u, ge - 1) : s]);
+            v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)m.x * kC + col);
+            wt[u] = FUSED ? (sorted_w ? __int_as_float(m.w) : depth[m.y]) : 1.f;
+        }
+        // the zero unit's rows go out while the gathers are in flight
+        zero_unit_rows<OutT>(zu * kWave, emask, g, out, lane);
+        float acc[EPL];
+#pragma unroll
+        for (int i = 0; i < EPL; ++i) acc[i] = 0.f;
+        float* hsum = &s_head[wave][grp * kC + col];  // this lane's slice of its group's head piece
+        int cur = -1;
+        auto finish = [&](bool last) {  // the cell `cur` ends at this point of the group
+            if (cur == first_cell && head_split) {
+#pragma unroll
+                for (int i = 0; i < EPL; i += 4)  // head piece: combined after the scan
+                    *reinterpret_cast<float4*>(hsum + i) = make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
+            } else if (!(last && tail_split)) {
+                store_slice<EPL>(cell_row(out, cur, g) + col, acc);
+            }  // tail piece: stays in acc
+        };
+        auto consume = [&](const uint4& raw, float w_, int cl) {
+            if (cl != cur) {
+                if (cur >= 0) finish(false);
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) acc[i] = 0.f;
+                cur = cl;
+            }
+            float x[EPL];
+            unpack16(raw, (const RT*)nullptr, x);
+#pragma unroll
+            for (int i = 0; i < EPL; ++i) acc[i] = FUSED ? fmaf(w_, x[i], acc[i]) : __fadd_rn(acc[i], x[i]);
+        };
+#pragma unroll
+        for (int u = 0; u < kUnrollM; ++u)
+            if (gs + u < ge) consume(v[u], wt[u], meta[gs + u].cell);
+        // further batches (a group holds more than kUnrollM entries only when the chunk owns > 64)
+        for (int e = gs + kUnrollM; e < ge; e += kUnrollM) {
+#pragma unroll
+            for (int u = 0; u < kUnrollM; ++u) {
+                const int4 m = *reinterpret_cast<const int4*>(&meta[min(e + u, ge - 1)]);
+                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)m.x * kC + col);
+                wt[u] = FUSED ? (sorted_w ? __int_as_float(m.w) : depth[m.y]) : 1.f;
+            }
+#pragma unroll
+            for (int u = 0; u < kUnrollM; ++u)
+                if (e + u < ge) consume(v[u], wt[u], meta[e + u].cell);
+        }
+        if (cur >= 0) finish(true);
+        // split cells: inclusive segmented scan over the groups of (restart flag, exported piece)
+        if (__ballot(head_split)) {
+            float c[EPL];
+            bool f = !tail_split || !middle;  // restart unless the group continues its predecessor's cell
+#pragma unroll
+            for (int i = 0; i < EPL; ++i) c[i] = tail_split ? acc[i] : 0.f;
+#pragma unroll
+            for (int d = 1; d < NG; d <<= 1) {
+                const bool fu = __shfl_up((int)f, d * LPR, kWave) != 0;
+                float up[EPL];
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) up[i] = __shfl_up(c[i], d * LPR, kWave);
+                if (grp >= d && !f) {
+#pragma unroll
+                    for (int i = 0; i < EPL; ++i) c[i] = __fadd_rn(up[i], c[i]);
+                    f = fu;
+                }
+            }
+            float carry[EPL];
+#pragma unroll
+            for (int i = 0; i < EPL; ++i) carry[i] = __shfl_up(c[i], LPR, kWave);
+            if (head_split && !middle) {
+                // the head cell ends in this group: predecessors' pieces (in group order) + this group's
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) carry[i] = __fadd_rn(carry[i], hsum[i]);
+                store_slice<EPL>(cell_row(out, first_cell, g) + col, carry);
+            }
+        }
+    } else {
+        zero_unit_rows<OutT>(zu * kWave, emask, g, out, lane);
+    }
+    if (big >= 0) {
+        int cell;
+        const float a2 = reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base, lane,
+                                                    &cell);
+        cell_row(out, cell, g)[lane] = from_f32<OutT>(a2);
     }
 }
 
@@ -1471,6 +1675,81 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd_lifted(const GT* __restric
         v = make_float4(to_f32(r[0]), to_f32(r[1]), to_f32(r[2]), to_f32(r[3]));
     }
     *reinterpret_cast<float4*>(dx + (size_t)p * kC + j) = v;
+}
+
+// ----------------------------------------------------------------------------- QuickCumsum operator boundary
+// The reference's op-level interface (QuickCumsum / cumsum_trick, src/tools.py:182-219): rows x
+// (n, C) already sorted by rank; one output row per run of equal ranks. The reference sums a run as
+// the difference of two fp32-rounded prefix sums; here each run is summed directly, in row order, in
+// fp32 (closer to the exact sum; the backward gather is identical).
+__global__ __launch_bounds__(kBlock) void k_seg_flags(const long long* __restrict__ ranks, int n,
+                                                      int32_t* __restrict__ flag) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) flag[i] = (i == 0 || ranks[i] != ranks[i - 1]) ? 1 : 0;
+}
+
+// excl = exclusive scan of flag (excl[n] = number of runs): run id of row i and first row of each run.
+__global__ __launch_bounds__(kBlock) void k_seg_finish(const int32_t* __restrict__ flag,
+                                                       const int32_t* __restrict__ excl, int n,
+                                                       int32_t* __restrict__ seg_of, int32_t* __restrict__ seg_start,
+                                                       int32_t* __restrict__ nseg) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) {
+        const int f = flag[i], e = excl[i];
+        seg_of[i] = e + f - 1;
+        if (f) seg_start[e] = i;
+    }
+    if (i == 0) {
+        const int t = excl[n];
+        seg_start[t] = n;
+        *nseg = t;
+    }
+}
+
+// One wave per run: lane = channel (C in slices of 64), rows summed in order; key_out[j] = the
+// keys (geom_feats) row of the run's LAST row, as geom_feats[kept] (src/tools.py:200).
+__global__ __launch_bounds__(kBlock) void k_seg_sum(const float* __restrict__ x, int C,
+                                                    const int32_t* __restrict__ seg_start, int nseg,
+                                                    const long long* __restrict__ keys, int kw,
+                                                    long long* __restrict__ key_out, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * (kBlock / kWave) + uniform(threadIdx.x >> 6);
+    if (w >= nseg) return;
+    const int s = seg_start[w], e = seg_start[w + 1];
+    for (int c0 = 0; c0 < C; c0 += kWave) {
+        const int c = c0 + lane;
+        if (c < C) {
+            float acc = 0.f;
+            int r = s;
+            for (; r + 4 <= e; r += 4) {  // four independent loads in flight, summed in order
+                const float a = x[(size_t)r * C + c], b = x[(size_t)(r + 1) * C + c];
+                const float d = x[(size_t)(r + 2) * C + c], f = x[(size_t)(r + 3) * C + c];
+                acc = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(acc, a), b), d), f);
+            }
+            for (; r < e; ++r) acc = __fadd_rn(acc, x[(size_t)r * C + c]);
+            out[(size_t)w * C + c] = acc;
+        }
+    }
+    if (keys != nullptr)
+        for (int k = lane; k < kw; k += kWave) key_out[(size_t)w * kw + k] = keys[(size_t)(e - 1) * kw + k];
+}
+
+// QuickCumsum.backward (src/tools.py:212-219): dx[i] = g[run of row i] -- a pure gather.
+__global__ __launch_bounds__(kBlock) void k_seg_gather(const float* __restrict__ g, int C,
+                                                       const int32_t* __restrict__ seg_of, long n_elems,
+                                                       float* __restrict__ dx) {
+    const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+    if ((C & 3) == 0) {
+        const long e = i * 4;
+        if (e >= n_elems) return;
+        const long r = e / C;
+        const int c = (int)(e - r * C);
+        *reinterpret_cast<float4*>(dx + e) = *reinterpret_cast<const float4*>(g + (size_t)seg_of[r] * C + c);
+    } else {
+        if (i >= n_elems) return;
+        const long r = i / C;
+        dx[i] = g[(size_t)seg_of[r] * C + (int)(i - r * C)];
+    }
 }
 
 // ----------------------------------------------------------------------------- host helpers
@@ -1692,10 +1971,36 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         BevGeo g;
         g.X = sg.X; g.Y = sg.Y; g.Z = sg.Z;
         g.ncells = dims->B * sg.Z * sg.X * sg.Y;
-        const int wpb = kBlock / kWave;
+        const int wpb = kSplatWaves;
+        if (LSS_SPLAT_IMPL == 1) {
+            const int nchunks = grid_blocks(nprime, kWave), nunits = grid_blocks(g.ncells, kWave);
+            const dim3 grm(8 * grid_blocks(grid_blocks(std::max(nchunks, nunits), wpb), 8)), blm(kSplatBlock);
+#define LSS_NHWC_FWD_M(F, RT, T)                                                                                   \
+    do {                                                                                                           \
+        if (e0 || e1)                                                                                              \
+            hipExtLaunchKernelGGL((k_splat_fwd_nhwc_m<F, RT, T>), grm, blm, 0, s, e0, e1, 0, depth, sorted_depth,  \
+                                  (const RT*)rows, cell_start, sorted_key, sorted_row, g, nprime, nchunks, nunits, \
+                                  (T*)out);                                                                        \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_splat_fwd_nhwc_m<F, RT, T>), grm, blm, 0, s, depth, sorted_depth,                \
+                               (const RT*)rows, cell_start, sorted_key, sorted_row, g, nprime, nchunks, nunits,    \
+                               (T*)out);                                                                           \
+    } while (0)
+            if (out_dtype == LSS_F32) {
+                if (!fused) LSS_NHWC_FWD_M(false, float, float);
+                else if (ctx_bf16) LSS_NHWC_FWD_M(true, bf16, float);
+                else LSS_NHWC_FWD_M(true, float, float);
+            } else {
+                if (!fused) LSS_NHWC_FWD_M(false, float, bf16);
+                else if (ctx_bf16) LSS_NHWC_FWD_M(true, bf16, bf16);
+                else LSS_NHWC_FWD_M(true, float, bf16);
+            }
+#undef LSS_NHWC_FWD_M
+            return launch_status();
+        }
         const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), wpb);
         const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), wpb);
-        const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kBlock);
+        const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);
 // kernel-stamped events only when asked for: a plain launch is what a hipGraph capture records
 #define LSS_NHWC_FWD(F, RT, T)                                                                                     \
     do {                                                                                                           \
@@ -1822,6 +2127,51 @@ int lss_splat_bwd_lifted(const void* g, int32_t g_dtype, int32_t rows_layout, co
     } else {
         return LSS_EINVAL;
     }
+    return launch_status();
+}
+
+size_t lss_segment_scratch_bytes(int32_t n) {
+    if (n < 0) return 0;
+    const size_t partial = sizeof(int32_t) * (size_t)((n + kScanItems - 1) / kScanItems + 1);
+    const size_t a = (partial + 255) & ~(size_t)255;
+    const size_t f = ((sizeof(int32_t) * (size_t)n) + 255) & ~(size_t)255;
+    return a + f + sizeof(int32_t) * ((size_t)n + 1);
+}
+
+int lss_segment_build(const long long* ranks, int32_t n, int32_t* seg_of, int32_t* seg_start, int32_t* nseg,
+                      void* scratch, lss_stream_t stream) {
+    if (!ranks || !seg_of || !seg_start || !nseg || !scratch || n <= 0 || n >= INT_MAX - kBlock) return LSS_EINVAL;
+    const int nb = (n + kScanItems - 1) / kScanItems;
+    char* base = static_cast<char*>(scratch);
+    int32_t* partial = reinterpret_cast<int32_t*>(base);
+    const size_t a = ((sizeof(int32_t) * (size_t)(nb + 1)) + 255) & ~(size_t)255;
+    int32_t* flag = reinterpret_cast<int32_t*>(base + a);
+    int32_t* excl = reinterpret_cast<int32_t*>(base + a + (((sizeof(int32_t) * (size_t)n) + 255) & ~(size_t)255));
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_seg_flags, dim3(grid_blocks(n, kBlock)), dim3(kBlock), 0, s, ranks, n, flag);
+    hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(1024), 0, s, flag, n, partial);
+    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(1024), 0, s, flag, n, partial, excl);
+    hipLaunchKernelGGL(k_seg_finish, dim3(grid_blocks(n, kBlock)), dim3(kBlock), 0, s, flag, excl, n, seg_of,
+                       seg_start, nseg);
+    return launch_status();
+}
+
+int lss_segment_sum(const float* x, int32_t C, const int32_t* seg_start, int32_t nseg, const long long* keys,
+                    int32_t key_width, long long* key_out, float* out, lss_stream_t stream) {
+    if (!x || !seg_start || !out || C <= 0 || nseg < 0 || (keys && (!key_out || key_width <= 0))) return LSS_EINVAL;
+    if (nseg == 0) return 0;
+    hipLaunchKernelGGL(k_seg_sum, dim3(grid_blocks(nseg, kBlock / kWave)), dim3(kBlock), 0, (hipStream_t)stream, x,
+                       C, seg_start, nseg, keys, key_width, key_out, out);
+    return launch_status();
+}
+
+int lss_segment_gather(const float* g, int32_t C, const int32_t* seg_of, int32_t n, float* dx, lss_stream_t stream) {
+    if (!g || !seg_of || !dx || C <= 0 || n < 0) return LSS_EINVAL;
+    if (n == 0) return 0;
+    const long elems = (long)n * C;
+    const long threads = (C & 3) == 0 ? elems / 4 : elems;
+    hipLaunchKernelGGL(k_seg_gather, dim3(grid_blocks(threads, kBlock)), dim3(kBlock), 0, (hipStream_t)stream, g, C,
+                       seg_of, elems, dx);
     return launch_status();
 }
 

@@ -224,6 +224,9 @@ class LiftSplatShoot(nn.Module):
         self.bev_layout = "nchw"
         self.inverse = "host"
         self.fuse_depthnet = True  # bf16 autocast: depthnet conv fused into the lift kernel
+        # (pinv, kinv) device buffers filled from host torch.inverse by ops.HostInverses before the
+        # step (captured training step); None: get_voxels computes them per `inverse`
+        self.static_inverses = None
         self._grid = ops.GridSpec.from_conf(grid_conf)
 
     def create_frustum(self):
@@ -277,7 +280,9 @@ class LiftSplatShoot(nn.Module):
         so the splat reads the CSR from the caches instead of HBM.
         """
         B, N, C, imH, imW = x.shape
-        inv = ops.camera_inverses(post_rots, intrins, self.inverse)
+        inv = self.static_inverses
+        if inv is None:
+            inv = ops.camera_inverses(post_rots, intrins, self.inverse)
         ce = self.camencode
         feat = ce.dropout(ce.get_eff_depth(x.view(B * N, C, imH, imW)))
         plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,

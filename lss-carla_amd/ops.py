@@ -100,6 +100,44 @@ def camera_inverses(post_rots: torch.Tensor, intrins: torch.Tensor, mode: str = 
     return pinv, kinv
 
 
+class HostInverses:
+    """Host ``torch.inverse`` results (src/models.py:180,186, bit for bit) in static device buffers.
+
+    ``inverse='host'`` is a device->host->device round trip inside the forward, which a captured
+    (hipGraph) step cannot contain. In training the rig arrives on the host anyway (the loader
+    builds it there), so ``update(post_rots, intrins)`` inverts the host copy with the reference's
+    own call and stages the result through pinned memory into ``pinv`` / ``kinv``, on the current
+    stream, before the step is launched; ``LiftSplatShoot.static_inverses = (pinv, kinv)`` makes
+    the forward read them. Two pinned staging buffers alternate; a buffer is rewritten only after
+    the copy that last read it has executed (the host never runs more than two steps ahead).
+    """
+
+    def __init__(self, n_cams: int, device: torch.device):
+        self.pinv = torch.empty(n_cams, 9, device=device, dtype=torch.float32)
+        self.kinv = torch.empty(n_cams, 9, device=device, dtype=torch.float32)
+        self._host = [torch.empty(2, n_cams, 9, dtype=torch.float32).pin_memory() for _ in range(2)]
+        self._done = [None, None]
+        self._i = 0
+        self.n_cams = n_cams
+
+    def update(self, post_rots: torch.Tensor, intrins: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        if post_rots.is_cuda or intrins.is_cuda:
+            raise RuntimeError("HostInverses.update takes the host copies of post_rots / intrins")
+        i = self._i
+        self._i ^= 1
+        if self._done[i] is not None:
+            self._done[i].synchronize()
+        h = self._host[i]
+        h[0].copy_(torch.inverse(post_rots.float()).reshape(self.n_cams, 9))
+        h[1].copy_(torch.inverse(intrins.float()).reshape(self.n_cams, 9))
+        self.pinv.copy_(h[0], non_blocking=True)
+        self.kinv.copy_(h[1], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.pinv.device))
+        self._done[i] = ev
+        return self.pinv, self.kinv
+
+
 # ----------------------------------------------------------------------------- plan
 @dataclass
 class SplatPlan:
@@ -486,3 +524,67 @@ class VoxelPool(torch.autograd.Function):
 
 def voxel_pool_rows(x_rows: torch.Tensor, plan: SplatPlan, layout: int = _lib.NCHW) -> torch.Tensor:
     return VoxelPool.apply(x_rows, plan, layout)
+
+
+# ----------------------------------------------------------------------------- op-level boundary: runs of ranks
+def _f32_rows(t: torch.Tensor) -> torch.Tensor:
+    """Contiguous fp32 copy/view with a 16-B aligned base (the gather's vector loads need it)."""
+    t = t.detach().to(torch.float32).contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+def segment_runs(ranks: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, int]:
+    """(seg_of, seg_start, nseg) of a sorted int64 rank vector (lss_segment_build).
+
+    The number of runs sizes the outputs of QuickCumsum, so it is read back to the host -- the same
+    synchronisation as the reference's boolean-mask indexing ``x[kept]`` (src/tools.py:200).
+    """
+    dev = _require_cuda(ranks)
+    lib = _lib.load()
+    r = ranks.detach()
+    if r.dtype != torch.int64:
+        r = r.to(torch.int64)
+    r = r.contiguous()
+    n = r.numel()
+    seg_of = torch.empty(n, device=dev, dtype=torch.int32)
+    seg_start = torch.empty(n + 1, device=dev, dtype=torch.int32)
+    nseg = torch.empty(1, device=dev, dtype=torch.int32)
+    scratch = torch.empty(int(lib.lss_segment_scratch_bytes(n)), device=dev, dtype=torch.uint8)
+    _lib.check(lib.lss_segment_build(_lib.ptr(r), n, _lib.ptr(seg_of), _lib.ptr(seg_start), _lib.ptr(nseg),
+                                     _lib.ptr(scratch), _lib.stream_handle(dev)), "lss_segment_build")
+    return seg_of, seg_start, int(nseg.item())
+
+
+def segment_sum(x: torch.Tensor, seg_start: torch.Tensor, nseg: int,
+                keys: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Per-run row sums (nseg, C) fp32 and the keys row of each run's last row (lss_segment_sum)."""
+    dev = _require_cuda(x, seg_start, keys)
+    lib = _lib.load()
+    xr = _f32_rows(x)
+    C = xr.shape[1]
+    out = torch.empty(nseg, C, device=dev, dtype=torch.float32)
+    key_out = None
+    kp = None
+    kw = 0
+    if keys is not None:
+        if keys.dtype != torch.int64 or keys.dim() != 2:
+            raise RuntimeError(f"lss_carla_amd: keys (geom_feats) must be a 2-D int64 tensor, got {keys.dtype} "
+                               f"{tuple(keys.shape)}")
+        kp = keys.detach().contiguous()
+        kw = kp.shape[1]
+        key_out = torch.empty(nseg, kw, device=dev, dtype=torch.int64)
+    _lib.check(lib.lss_segment_sum(_lib.ptr(xr), C, _lib.ptr(seg_start), nseg, _lib.ptr(kp), kw, _lib.ptr(key_out),
+                                   _lib.ptr(out), _lib.stream_handle(dev)), "lss_segment_sum")
+    return out, key_out
+
+
+def segment_gather(g: torch.Tensor, seg_of: torch.Tensor) -> torch.Tensor:
+    """dx[i] = g[seg_of[i]] (lss_segment_gather): QuickCumsum's backward."""
+    dev = _require_cuda(g, seg_of)
+    lib = _lib.load()
+    gr = _f32_rows(g)
+    n, C = seg_of.numel(), gr.shape[1]
+    dx = torch.empty(n, C, device=dev, dtype=torch.float32)
+    _lib.check(lib.lss_segment_gather(_lib.ptr(gr), C, _lib.ptr(seg_of), n, _lib.ptr(dx), _lib.stream_handle(dev)),
+               "lss_segment_gather")
+    return dx

@@ -1,8 +1,9 @@
 """Training-side helpers with the reference's names (src/tools.py).
 
-Only what the LiftSplatShoot training step needs: the grid helper, the loss
-and the IoU metric. The reference's nuScenes/visualisation helpers are out of
-scope.
+What the LiftSplatShoot training step and its callers use: the grid helper, the op-level
+segmented sum (``QuickCumsum`` / ``cumsum_trick``, HIP-backed), the loss and the IoU metric. The
+reference's nuScenes/visualisation helpers are out of scope; its
+image/label helpers live in ``simbev.py``.
 """
 from __future__ import annotations
 
@@ -18,6 +19,55 @@ def gen_dx_bx(xbound, ybound, zbound):
     return dx, bx, nx
 
 
+# ----------------------------------------------------------------------------- op-level segmented sum
+class QuickCumsum(torch.autograd.Function):
+    """``QuickCumsum.apply(x, geom_feats, ranks)`` of src/tools.py:193-219 on HIP kernels.
+
+    x (n, C) rows sorted by ``ranks`` (n,) int64; geom_feats (n, k) int64. Returns one row per run
+    of equal ranks: (x_seg (nseg, C), geom_seg (nseg, k)) with geom_seg = the geom_feats row of the
+    run's last row, as the reference's ``geom_feats[kept]``. Forward: lss_segment_build +
+    lss_segment_sum (each run summed in row order in fp32 -- the reference differences two
+    fp32-rounded prefix sums, which is off the exact sum by ~ulp(prefix); this is not). Backward:
+    lss_segment_gather, the reference's ``gradx[back]`` (identical values). The number of runs is
+    read back once, as the reference's boolean indexing does. Device tensors only.
+    """
+
+    @staticmethod
+    def forward(ctx, x, geom_feats, ranks):
+        from . import ops
+        if x.dim() != 2 or ranks.dim() != 1 or ranks.shape[0] != x.shape[0] or geom_feats.shape[0] != x.shape[0]:
+            raise RuntimeError(f"QuickCumsum: x {tuple(x.shape)}, geom_feats {tuple(geom_feats.shape)} and ranks "
+                               f"{tuple(ranks.shape)} do not describe the same rows")
+        ops._require_cuda(x, geom_feats, ranks)
+        n, C = x.shape
+        if n == 0:
+            seg_of = torch.empty(0, device=x.device, dtype=torch.int32)
+            out, gout = x.new_empty(0, C), geom_feats.new_empty((0,) + tuple(geom_feats.shape[1:]))
+        else:
+            seg_of, seg_start, nseg = ops.segment_runs(ranks)
+            out, gout = ops.segment_sum(x, seg_start, nseg, geom_feats)
+            out = out.to(x.dtype)
+        ctx.save_for_backward(seg_of)
+        ctx.x_dtype = x.dtype
+        ctx.mark_non_differentiable(gout)
+        return out, gout
+
+    @staticmethod
+    def backward(ctx, gradx, gradgeom):
+        from . import ops
+        seg_of, = ctx.saved_tensors
+        if seg_of.numel() == 0:
+            return gradx.new_empty(0, gradx.shape[1]), None, None
+        return ops.segment_gather(gradx, seg_of).to(ctx.x_dtype), None, None
+
+
+def cumsum_trick(x, geom_feats, ranks):
+    """src/tools.py:182-190: the same segmented sum, differentiable in x (the reference reaches the
+    same gradient through autograd of cumsum / indexing / cat; here it is the gather directly)."""
+    return QuickCumsum.apply(x, geom_feats, ranks)
+
+
+# ----------------------------------------------------------------------------- loss / metrics
 class SimpleLoss(torch.nn.Module):
     """BCE-with-logits with a positive-class weight (src/tools.py:222-230)."""
 
@@ -33,7 +83,7 @@ def get_batch_iou(preds: torch.Tensor, binimgs: torch.Tensor):
     """Intersection, union and IoU of (logit > 0) vs the labels, as Python floats (src/tools.py:232-240)."""
     intersect, union = get_batch_iou_device(preds, binimgs)
     intersect, union = intersect.item(), union.item()
-    return intersect, union, intersect / union if union > 0 else 1.0
+    return intersect, union, intersect / union if (union > 0) else 1.0
 
 
 def get_batch_iou_device(preds: torch.Tensor, binimgs: torch.Tensor):
@@ -44,23 +94,35 @@ def get_batch_iou_device(preds: torch.Tensor, binimgs: torch.Tensor):
         return (pred & tgt).sum().float(), (pred | tgt).sum().float()
 
 
-def get_val_info(model, valloader, loss_fn, device, use_tqdm: bool = False):
-    """Validation loss / IoU over a loader (src/tools.py:243-270); one host sync per epoch, not per batch."""
+def get_val_info(model, valloader, loss_fn, device, use_tqdm=True):
+    """Validation loss / IoU over a loader (src/tools.py:243-270).
+
+    Same results and the same return dict as the reference, but the per-batch ``.item()`` syncs
+    are gone: loss (x batch size) and the intersection / union counts accumulate on the device in
+    float64 and are read once at the end. As in the reference, the loss is divided by
+    ``len(valloader.dataset)`` and an empty union raises ZeroDivisionError.
+    """
     model.eval()
-    total_loss = torch.zeros((), device=device)
-    inter = torch.zeros((), device=device)
-    union = torch.zeros((), device=device)
-    n = 0
+    total_loss = torch.zeros((), device=device, dtype=torch.float64)
+    total_intersect = torch.zeros((), device=device, dtype=torch.float64)
+    total_union = torch.zeros((), device=device, dtype=torch.float64)
+    print("running eval...")
+    loader = valloader
+    if use_tqdm:
+        from tqdm import tqdm
+        loader = tqdm(valloader, desc="Validation")
     with torch.no_grad():
-        for allimgs, rots, trans, intrins, post_rots, post_trans, binimgs in valloader:
+        for batch in loader:
+            allimgs, rots, trans, intrins, post_rots, post_trans, binimgs = batch
             preds = model(allimgs.to(device), rots.to(device), trans.to(device), intrins.to(device),
                           post_rots.to(device), post_trans.to(device))
             binimgs = binimgs.to(device)
-            total_loss += loss_fn(preds, binimgs) * preds.shape[0]
+            total_loss += loss_fn(preds, binimgs).double() * preds.shape[0]
             i, u = get_batch_iou_device(preds, binimgs)
-            inter += i
-            union += u
-            n += preds.shape[0]
+            total_intersect += i.double()
+            total_union += u.double()
     model.train()
-    return {"loss": total_loss.item() / max(len(getattr(valloader, "dataset", [])) or n, 1),
-            "iou": inter.item() / union.item() if union.item() > 0 else 1.0}
+    return {
+        "loss": total_loss.item() / len(valloader.dataset),
+        "iou": total_intersect.item() / total_union.item(),
+    }

@@ -13,8 +13,10 @@ With ``flat_params.FlatParams`` the trainable parameters are one fp32 tensor, so
 tensor too: one ~50 MB ring all-reduce over xGMI per step (the same averaged gradient as DDP), a
 single-tensor Adam and norm. Every op of the LSS path is capturable: its kernels take device
 pointers only and the plan's sizes come from the static shapes; the one host round trip of the
-reference (torch.inverse on the CPU, src/models.py:180,186) is replaced by the device inverse
-(ops.camera_inverses(mode='device')).
+reference (torch.inverse on the CPU, src/models.py:180,186) moves out of the captured region:
+``pre_step`` inverts the host copy of the rig with the same call and stages the results into static
+device buffers (ops.HostInverses) before each replay, so the captured step reads bit-identical
+inverses (``inverse='device'`` -- an fp64 adjugate kernel, not bit-exact -- remains an option).
 """
 from __future__ import annotations
 
@@ -31,8 +33,11 @@ class TrainStep:
     def __init__(self, forward: Callable[..., torch.Tensor], inputs: Sequence[torch.Tensor], labels: torch.Tensor,
                  loss_fn: Callable, opt: torch.optim.Optimizer, params: Sequence[torch.Tensor],
                  all_reduce: bool = False, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
-                 max_grad_norm: float = 5.0):
+                 max_grad_norm: float = 5.0, pre_step: Optional[Callable[[], None]] = None):
         self.forward, self.inputs, self.labels = forward, tuple(inputs), labels
+        # host work staged into the step's static device inputs before each step is launched
+        # (e.g. ops.HostInverses.update: the reference's host torch.inverse of the rig)
+        self.pre_step = pre_step
         self.loss_fn, self.opt, self.params = loss_fn, opt, list(params)
         self.amp_dtype, self.max_grad_norm = amp_dtype, max_grad_norm
         self.world = dist.get_world_size() if (all_reduce and dist.is_available() and dist.is_initialized()) else 1
@@ -72,6 +77,8 @@ class TrainStep:
         self.opt.step()
 
     def eager(self) -> torch.Tensor:
+        if self.pre_step is not None:
+            self.pre_step()
         loss = self.forward_backward()
         self.all_reduce()
         self.update()
@@ -105,6 +112,8 @@ class TrainStep:
         if self.graphs is None:
             return self.eager()
         g_fb, g_up = self.graphs
+        if self.pre_step is not None:
+            self.pre_step()
         g_fb.replay()
         self.all_reduce(self.graph_grads)
         g_up.replay()

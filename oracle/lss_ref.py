@@ -187,10 +187,13 @@ class QuickCumsum(torch.autograd.Function):
 
 
 # ----------------------------------------------------------------------------- a7-a12
-def voxel_pooling(geom: np.ndarray, x: torch.Tensor, dx, bx, nx, use_quickcumsum: bool = True) -> torch.Tensor:
+def voxel_pooling(geom: np.ndarray, x: torch.Tensor, dx, bx, nx, use_quickcumsum: bool = True,
+                  segment_fn: Optional[Callable] = None) -> torch.Tensor:
     """Reference splat: (B, N, D, fH, fW, C) features -> (B, Z*C, X, Y) (``src/models.py:204-246``).
 
     Differentiable in ``x``. ``geom`` is the float32 geometry from :func:`get_geometry`.
+    ``segment_fn(x, geom_feats, ranks)``, if given, replaces the cumsum step (``src/models.py:233-237``):
+    the op-level parity tests plug the product's HIP ``QuickCumsum`` in here.
     """
     B, N, D, H, W, C = x.shape
     nprime = B * N * D * H * W
@@ -202,7 +205,9 @@ def voxel_pooling(geom: np.ndarray, x: torch.Tensor, dx, bx, nx, use_quickcumsum
     ranks = torch.from_numpy(ranks_of(ids[kept], nx, B))
     order = ranks.argsort()
     xf, ids_t, ranks = xf[order], ids_t[order], ranks[order]
-    if use_quickcumsum:
+    if segment_fn is not None:
+        xf, ids_t = segment_fn(xf, ids_t, ranks)
+    elif use_quickcumsum:
         xf, ids_t = QuickCumsum.apply(xf, ids_t, ranks)
     else:
         xf, ids_t = cumsum_trick(xf, ids_t, ranks)
@@ -254,14 +259,15 @@ def lift_splat_backward_fp64(depthnet_out: np.ndarray, geom: np.ndarray, dbev: n
 
 # ----------------------------------------------------------------------------- a13
 def get_voxels(frustum, depthnet_out: torch.Tensor, rots, trans, intrins, post_rots, post_trans,
-               dx, bx, nx, D: int, C: int = 64, use_quickcumsum: bool = True) -> torch.Tensor:
+               dx, bx, nx, D: int, C: int = 64, use_quickcumsum: bool = True,
+               segment_fn: Optional[Callable] = None) -> torch.Tensor:
     """geometry -> lift -> splat, i.e. ``get_voxels`` with the trunk already applied
     (``src/models.py:248-254``); ``depthnet_out`` is (B*N, D+C, fH, fW)."""
     B, N = trans.shape[:2]
     geom = get_geometry(frustum, rots, trans, intrins, post_rots, post_trans)
     _, new_x = lift(depthnet_out, D, C)
     x = cam_feats_layout(new_x, B, N)
-    return voxel_pooling(geom, x, dx, bx, nx, use_quickcumsum)
+    return voxel_pooling(geom, x, dx, bx, nx, use_quickcumsum, segment_fn)
 
 
 def full_forward(trunk: Callable[[torch.Tensor], torch.Tensor], bevencode: Callable[[torch.Tensor], torch.Tensor],

@@ -22,31 +22,37 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
-    "skip_chunks": ["LSS_FWD_SKIP=1"],  # zero units only (timing decomposition; wrong output)
-    "skip_zero": ["LSS_FWD_SKIP=2"],    # chunks only (timing decomposition; wrong output)
-    "zero_plain": ["LSS_ZERO_STORE=0"],  # zero fill with plain stores (may stay in the Infinity Cache)
-    "row_nt": ["LSS_ROW_NT=1"],
-    "zero_units2": ["LSS_ZERO_UNITS=2"],
-    "interleave": ["LSS_INTERLEAVE=1"],
-    "zero_first": ["LSS_INTERLEAVE=2"],
-    "minwaves4": ["LSS_MIN_WAVES=4"],
-    "unroll4": ["LSS_UNROLL=4"],
-    "zu8": ["LSS_ZERO_UNITS=8"],    # few heavy zero waves, so all chunk + zero waves are resident at once
-    "zu16": ["LSS_ZERO_UNITS=16"],
-    "gap8": ["LSS_CHUNK_GAP=8"],    # chunk waves zero the first 8 empty cells after each owned cell
-    "gap32": ["LSS_CHUNK_GAP=32"],
+    # two block roles (product default, LSS_SPLAT_IMPL=0): knobs
+    "r2_u16": ["LSS_UNROLL=16"],            # every lane group issues all its gathers before any store
+    "r2_w8": ["LSS_SPLAT_WAVES=8"],         # 512-thread blocks: half as many blocks to dispatch
+    "r2_w16": ["LSS_SPLAT_WAVES=16"],
+    "r2_mw6": ["LSS_MIN_WAVES=6"],
+    # merged roles (LSS_SPLAT_IMPL=1)
+    "merged": ["LSS_SPLAT_IMPL=1"],
+    "m_u16": ["LSS_SPLAT_IMPL=1", "LSS_UNROLL_M=16", "LSS_MIN_WAVES_M=4"],
+    "m_w8": ["LSS_SPLAT_IMPL=1", "LSS_SPLAT_WAVES=8"],
+}
+VARIANTS_R1 = {  # round-1 knobs of the two-role kernel (kept for reference; pass --r1-variants)
+    "skip_chunks": ["LSS_SPLAT_IMPL=0", "LSS_FWD_SKIP=1"],  # zero units only (timing decomposition; wrong output)
+    "skip_zero": ["LSS_SPLAT_IMPL=0", "LSS_FWD_SKIP=2"],    # chunks only (timing decomposition; wrong output)
+    "interleave": ["LSS_SPLAT_IMPL=0", "LSS_INTERLEAVE=1"],
+    "gap8": ["LSS_SPLAT_IMPL=0", "LSS_CHUNK_GAP=8"],
 }
 
 
-def build_variants():
+def build_variants(r1=False):
     from lss_carla_amd import build
-    for name, defs in VARIANTS.items():
+    import shutil
+    vdir = os.path.join(REPO, "lss-carla_amd", "variants")
+    shutil.rmtree(vdir, ignore_errors=True)  # stale variants of older ABIs would fail to load
+    for name, defs in (VARIANTS_R1 if r1 else VARIANTS).items():
         print(name, build.build_variant(name, defs), flush=True)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build-variants", action="store_true")
+    ap.add_argument("--r1-variants", action="store_true", help="with --build-variants: the round-1 knob set")
     ap.add_argument("--config", default="c3")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", default="", help="run only ops whose name contains this (for rocprofv3 --pmc)")
@@ -54,7 +60,7 @@ def main():
     ap.add_argument("--cold", type=int, default=1, help="also time splat_fwd in the cold and step cache states")
     args = ap.parse_args()
     if args.build_variants:
-        build_variants()
+        build_variants(args.r1_variants)
         return
     import torch
     from lss_carla_amd import _lib, ops, synthetic as syn
@@ -217,9 +223,9 @@ def main():
         _lib.check(vl.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
                                     _lib.ptr(vcsr[3]), _lib.ptr(vsd), st()), "lift")
         for m in modes:
-            res[f"{m} splat_fwd nhwc bf16 [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m, sd=vsd)
-            res[f"{m} splat_fwd nhwc bf16 (f32 ctx) [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, ctx=ctx_f,
-                                                                          mode=m)
+            res[f"{m} splat_fwd nhwc bf16 [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m)
+            res[f"{m} splat_fwd nhwc bf16 (sorted depth) [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m,
+                                                                               sd=vsd)
     g_bf = torch.randn(B, Z * 64, X, Y, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     d_dn = torch.empty_like(dn)
     res["splat_bwd nhwc bf16"] = named("splat_bwd nhwc bf16", lambda: _lib.check(lib.lss_splat_bwd(
