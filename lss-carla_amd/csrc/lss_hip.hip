@@ -69,6 +69,19 @@ __device__ __forceinline__ int wave_min(int v) {
     return v;
 }
 
+// Blocks are dealt round-robin over the 8 XCDs (observed placement: speed only, never correctness).
+// xcd_block gives each XCD one contiguous run of ceil(nb / 8) logical blocks, so kernels that follow
+// each other with the same mapping hand data over through the same XCD's L2: the lift writes a
+// sample's context rows / depth weights, the CSR build its keys, the scan its cell starts, from the
+// XCD whose splat blocks read them. The grid must be xcd_grid(nb) blocks; logical ids >= nb idle.
+#ifndef LSS_XCD_MAP
+#define LSS_XCD_MAP 1  // 0: plain block order everywhere (timing comparisons)
+#endif
+__device__ __forceinline__ int xcd_block() {
+    return LSS_XCD_MAP ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+}
+inline int xcd_grid(long nb) { return (int)(8 * ((nb + 7) / 8)); }
+
 // acc = 0; for k: acc = acc + m[k] * v[k]   -- fp32, each op rounded (CPU torch.matmul order).
 __device__ __forceinline__ float dot3_seq(float m0, float m1, float m2, float v0, float v1, float v2) {
     float acc = __fmul_rn(m0, v0);
@@ -250,9 +263,12 @@ __global__ __launch_bounds__(1024) void k_scan_apply(const int32_t* __restrict__
     __shared__ int s_wave[32];
     __shared__ int s_total;
     __shared__ int s_red[16];
+    const int lb = xcd_block();
+    const int nb = (ncells + kScanItems - 1) / kScanItems;
+    if (lb >= nb) return;  // block-uniform
     // prefix = sum of the preceding blocks' totals
     int pre = 0;
-    for (int i = threadIdx.x; i < (int)blockIdx.x; i += 1024) pre += partial[i];
+    for (int i = threadIdx.x; i < lb; i += 1024) pre += partial[i];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, kWave);
     if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = pre;
@@ -260,7 +276,7 @@ __global__ __launch_bounds__(1024) void k_scan_apply(const int32_t* __restrict__
     int prefix = 0;
 #pragma unroll
     for (int w = 0; w < 16; ++w) prefix += s_red[w];
-    const int base = blockIdx.x * kScanItems + threadIdx.x * 4;
+    const int base = lb * kScanItems + threadIdx.x * 4;
     int c[4];
     int v = 0;
 #pragma unroll
@@ -274,7 +290,7 @@ __global__ __launch_bounds__(1024) void k_scan_apply(const int32_t* __restrict__
         if (base + i < ncells) cell_start[base + i] = run;
         run += c[i];
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) cell_start[ncells] = prefix + s_total;
+    if (lb == nb - 1 && threadIdx.x == 0) cell_start[ncells] = prefix + s_total;
 }
 
 // Counting-sort scatter: point p lands at cell_start[cell] + slot as the key (cell << 32) | p
@@ -350,7 +366,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
                                                       const int32_t* __restrict__ cell_of,
                                                       int32_t* __restrict__ pos_out) {
     const int lane = threadIdx.x & 63;
-    const int w = blockIdx.x * (kBlock / kWave) + uniform(threadIdx.x >> 6);
+    const int w = xcd_block() * (kBlock / kWave) + uniform(threadIdx.x >> 6);
     if (w >= nchunks) return;
     const int total = *total_ptr;
     const int base = w * kWave;
@@ -449,7 +465,8 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
                                                       float* __restrict__ sorted_depth) {
     __shared__ float s_ctx[kC][65];
     __shared__ float s_red[2][4][64];
-    const int q0 = blockIdx.x * 64;
+    const int q0 = xcd_block() * 64;
+    if (q0 >= npix) return;  // block-uniform
     const int px = threadIdx.x & 63, part = threadIdx.x >> 6;
     const int q = q0 + px;
     const bool live = q < npix;
@@ -523,7 +540,8 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
     __shared__ __attribute__((aligned(16))) bf16 s_x[kDnPix][kDnMaxK + 8];  // [pixel][k]; +8: spread the banks
     __shared__ float s_lg[kDnMaxO][kDnPix + 1];                               // bf16-rounded logits [o][pixel]
     __shared__ float s_red[2][kBlock / kDnPix][kDnPix];
-    const int q0 = blockIdx.x * kDnPix;
+    const int q0 = xcd_block() * kDnPix;
+    if (q0 >= npix) return;  // block-uniform
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // stage: element (k, p), pixels fastest. With HW % 8 == 0 an aligned run of 8 pixels never
     // crosses an image, so each thread moves 16 B (8 pixels of one channel) per load.
@@ -655,9 +673,6 @@ struct SplatGeo {
 #endif
 #ifndef LSS_INTERLEAVE
 #define LSS_INTERLEAVE 0  // dispatch order of the block groups: 0 chunks first, 1 interleaved, 2 zero fill first
-#endif
-#ifndef LSS_XCD_MAP
-#define LSS_XCD_MAP 1     // 1: chunk blocks of one XCD take a contiguous run of chunks (L2 holds ~1/8 of the rows)
 #endif
 #ifndef LSS_CHUNK_STOP
 #define LSS_CHUNK_STOP 0  // timing experiments only: chunk waves stop after round trip 1 (1) or 2 (2)
@@ -1048,6 +1063,25 @@ struct alignas(16) EntryMeta {
     int row, p, cell, wbits;  // wbits: the depth weight (float bits) when the CSR-ordered copy is given
 };
 
+// Depth weights of a lane group's next entries [e, e + KU): lane j of the group loads the weight of
+// entry e + j, so ONE wave-wide gather serves all groups (the group's lanes used to load one shared
+// address per entry: KU gathers, each a full texture-unit pass over 64 lanes for 8 useful values),
+// then each weight is broadcast inside the group through the LDS crossbar (ds_bpermute).
+#ifndef LSS_DEPTH_BCAST
+#define LSS_DEPTH_BCAST 1
+#endif
+template <int LPR, int KU>
+__device__ __forceinline__ float group_weight_load(const EntryMeta* __restrict__ meta,
+                                                   const float* __restrict__ depth, int e, int last, int lane) {
+    static_assert(LPR >= KU, "one lane per entry of the batch");
+    return depth[meta[min(e + lane % LPR, last)].p];
+}
+// weight of entry e + u of the group (broadcast from the group's lane u; one VGPR held across the wait)
+template <int LPR>
+__device__ __forceinline__ float group_weight(float wd, int u, int lane) {
+    return __shfl(wd, lane - lane % LPR + u, kWave);
+}
+
 template <bool FUSED, typename RT, typename OutT>
 __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __restrict__ depth,
                                             const float* __restrict__ sorted_depth,
@@ -1125,19 +1159,25 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
             else store_slice<RS::EPL>(cell_row(out, cur, g) + col, acc);
         };
         // round trip 2 (one per kUnroll entries of a group): row slices and depth weights in flight together
-        for (int e = gs; e < ge; e += kUnroll) {
+#ifndef LSS_TRAP_EXP
+#define LSS_TRAP_EXP 0  // timing experiments only: 1 drops every entry past the first batch (wrong output)
+#endif
+        for (int e = gs; e < (LSS_TRAP_EXP ? min(ge, gs + kUnroll) : ge); e += kUnroll) {
             uint4 v[kUnroll];
-            float wt[kUnroll];
+            float wt[LSS_DEPTH_BCAST ? 1 : kUnroll];  // per-entry weight gathers (LSS_DEPTH_BCAST=0 only)
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
                 const int4 m = *reinterpret_cast<const int4*>(&meta[min(e + u, ge - 1)]);  // (row, p, cell, w)
                 v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)m.x * kC + col);
-                wt[u] = (FUSED && !LSS_NO_DEPTH) ? (sorted_w ? __int_as_float(m.w) : depth[m.y]) : 1.f;
+                if (!LSS_DEPTH_BCAST) wt[u] = (FUSED && !LSS_NO_DEPTH && !sorted_w) ? depth[m.y] : 1.f;
             }
+            // depth weights: CSR-ordered copy (staged in meta), or one wave-wide gather + group broadcast
+            const bool bcast = FUSED && !LSS_NO_DEPTH && !sorted_w && LSS_DEPTH_BCAST;
+            const float wd = bcast ? group_weight_load<RS::LPR, kUnroll>(meta, depth, e, ge - 1, lane) : 0.f;
             if (LSS_CHUNK_STOP == 2) {
                 unsigned x = 0;
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) x ^= v[u].x ^ v[u].w ^ __float_as_uint(wt[u]);
+                for (int u = 0; u < kUnroll; ++u) x ^= v[u].x ^ v[u].w ^ __float_as_uint(wd);
                 if (x == 0x12345u) out[0] = from_f32<OutT>(1.f);
                 continue;
             }
@@ -1154,8 +1194,11 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                     }
                     float x[RS::EPL];
                     unpack16(v[u], (const RT*)nullptr, x);
+                    const float wu = (!FUSED || LSS_NO_DEPTH) ? 1.f
+                                     : sorted_w ? __int_as_float(meta[e + u].wbits)
+                                     : LSS_DEPTH_BCAST ? group_weight<RS::LPR>(wd, u, lane) : wt[LSS_DEPTH_BCAST ? 0 : u];
 #pragma unroll
-                    for (int i = 0; i < RS::EPL; ++i) acc[i] = FUSED ? fmaf(wt[u], x[i], acc[i]) : __fadd_rn(acc[i], x[i]);
+                    for (int i = 0; i < RS::EPL; ++i) acc[i] = FUSED ? fmaf(wu, x[i], acc[i]) : __fadd_rn(acc[i], x[i]);
                 }
             }
         }
@@ -1254,7 +1297,7 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(c
 #endif
     } else {
         if (LSS_FWD_SKIP & 2) return;
-        const int zb = zgi * 8 + x;
+        const int zb = LSS_XCD_MAP ? x * nzg + zgi : zgi * 8 + x;
         if (zb >= nzero_blocks) return;
         const int u = (zb * (kSplatWaves) + wave) * kZeroUnits;
         [[maybe_unused]] const int zslot = nchunk_blocks * (kSplatWaves) + zb * (kSplatWaves) + wave;
@@ -1377,13 +1420,16 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES_M) void k_splat_fwd_nhwc
         const bool middle = head_split && tail_split && first_cell == last_cell;  // one cell across both cuts
         // gathers of the first batch: row slices and depth weights, all in flight together
         uint4 v[kUnrollM];
-        float wt[kUnrollM];
+        float wt[LSS_DEPTH_BCAST ? 1 : kUnrollM];  // per-entry weight gathers (LSS_DEPTH_BCAST=0 only)
 #pragma unroll
         for (int u = 0; u < kUnrollM; ++u) {
             const int4 m = *reinterpret_cast<const int4*>(&meta[gs < ge ? min(gs + u, ge - 1) : s]);
             v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)m.x * kC + col);
-            wt[u] = FUSED ? (sorted_w ? __int_as_float(m.w) : depth[m.y]) : 1.f;
+            if (!LSS_DEPTH_BCAST) wt[u] = (FUSED && !sorted_w) ? depth[m.y] : 1.f;
         }
+        const bool bcast = FUSED && !sorted_w && LSS_DEPTH_BCAST;
+        const float wd = bcast ? group_weight_load<LPR, kUnrollM>(meta, depth, gs < ge ? gs : s, gs < ge ? ge - 1 : s,
+                                                                  lane) : 0.f;
         // the zero unit's rows go out while the gathers are in flight
         zero_unit_rows<OutT>(zu * kWave, emask, g, out, lane);
         float acc[EPL];
@@ -1414,18 +1460,25 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES_M) void k_splat_fwd_nhwc
         };
 #pragma unroll
         for (int u = 0; u < kUnrollM; ++u)
-            if (gs + u < ge) consume(v[u], wt[u], meta[gs + u].cell);
+            if (gs + u < ge)
+                consume(v[u], !FUSED ? 1.f : sorted_w ? __int_as_float(meta[gs + u].wbits)
+                              : LSS_DEPTH_BCAST ? group_weight<LPR>(wd, u, lane) : wt[LSS_DEPTH_BCAST ? 0 : u],
+                        meta[gs + u].cell);
         // further batches (a group holds more than kUnrollM entries only when the chunk owns > 64)
         for (int e = gs + kUnrollM; e < ge; e += kUnrollM) {
 #pragma unroll
             for (int u = 0; u < kUnrollM; ++u) {
                 const int4 m = *reinterpret_cast<const int4*>(&meta[min(e + u, ge - 1)]);
                 v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)m.x * kC + col);
-                wt[u] = FUSED ? (sorted_w ? __int_as_float(m.w) : depth[m.y]) : 1.f;
+                if (!LSS_DEPTH_BCAST) wt[u] = (FUSED && !sorted_w) ? depth[m.y] : 1.f;
             }
+            const float wd2 = bcast ? group_weight_load<LPR, kUnrollM>(meta, depth, e, ge - 1, lane) : 0.f;
 #pragma unroll
             for (int u = 0; u < kUnrollM; ++u)
-                if (e + u < ge) consume(v[u], wt[u], meta[e + u].cell);
+                if (e + u < ge)
+                    consume(v[u], !FUSED ? 1.f : sorted_w ? __int_as_float(meta[e + u].wbits)
+                                  : LSS_DEPTH_BCAST ? group_weight<LPR>(wd2, u, lane) : wt[LSS_DEPTH_BCAST ? 0 : u],
+                            meta[e + u].cell);
         }
         if (cur >= 0) finish(true);
         // split cells: inclusive segmented scan over the groups of (restart flag, exported piece)
@@ -1904,11 +1957,11 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
     long long* tmp_key = reinterpret_cast<long long*>(static_cast<char*>(scratch) + poff);
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial);
-    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(1024), 0, s, cell_count, ncells, partial, cell_start);
+    hipLaunchKernelGGL(k_scan_apply, dim3(xcd_grid(nb)), dim3(1024), 0, s, cell_count, ncells, partial, cell_start);
     hipLaunchKernelGGL(k_scatter, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0, s, cell_of, slot_of, nprime,
                        cell_start, tmp_key);
     const int nchunks = (nprime + kWave - 1) / kWave;
-    hipLaunchKernelGGL(k_csr_canon, dim3(grid_blocks(nchunks, kBlock / kWave)), dim3(kBlock), 0, s, tmp_key,
+    hipLaunchKernelGGL(k_csr_canon, dim3(xcd_grid(grid_blocks(nchunks, kBlock / kWave))), dim3(kBlock), 0, s, tmp_key,
                        cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row, cell_of, pos_of);
     return launch_status();
 }
@@ -1919,7 +1972,7 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
     if (dims->D > 64) return LSS_EUNSUPPORTED;
     const int HW = dims->H * dims->W;
     const int npix = dims->B * dims->N * HW;
-    const dim3 grid(grid_blocks(npix, 64)), block(kBlock);
+    const dim3 grid(xcd_grid(grid_blocks(npix, 64))), block(kBlock);
     hipStream_t s = (hipStream_t)stream;
 #define LSS_PREP(IT, CT) \
     hipLaunchKernelGGL((k_lift_prep<IT, CT>), grid, block, 0, s, (const IT*)depthnet_out, dims->D, HW, npix, depth, \
@@ -1942,7 +1995,7 @@ int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, in
     const int HW = dims->H * dims->W;
     const long npix = (long)dims->B * dims->N * HW;
     if (npix >= INT_MAX) return LSS_EUNSUPPORTED;
-    hipLaunchKernelGGL(k_depthnet_lift, dim3(grid_blocks(npix, kDnPix)), dim3(kBlock), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_depthnet_lift, dim3(xcd_grid(grid_blocks(npix, kDnPix))), dim3(kBlock), 0, (hipStream_t)stream,
                        (const bf16*)feat, (const bf16*)weight, (const bf16*)bias, K, dims->D, HW, (int)npix, depth,
                        (bf16*)ctx_t, pos_of, sorted_depth);
     return launch_status();
@@ -2150,7 +2203,7 @@ int lss_segment_build(const long long* ranks, int32_t n, int32_t* seg_of, int32_
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(k_seg_flags, dim3(grid_blocks(n, kBlock)), dim3(kBlock), 0, s, ranks, n, flag);
     hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(1024), 0, s, flag, n, partial);
-    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(1024), 0, s, flag, n, partial, excl);
+    hipLaunchKernelGGL(k_scan_apply, dim3(xcd_grid(nb)), dim3(1024), 0, s, flag, n, partial, excl);
     hipLaunchKernelGGL(k_seg_finish, dim3(grid_blocks(n, kBlock)), dim3(kBlock), 0, s, flag, excl, n, seg_of,
                        seg_start, nseg);
     return launch_status();

@@ -22,15 +22,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
-    # two block roles (product default, LSS_SPLAT_IMPL=0): knobs
-    "r2_u16": ["LSS_UNROLL=16"],            # every lane group issues all its gathers before any store
-    "r2_w8": ["LSS_SPLAT_WAVES=8"],         # 512-thread blocks: half as many blocks to dispatch
-    "r2_w16": ["LSS_SPLAT_WAVES=16"],
-    "r2_mw6": ["LSS_MIN_WAVES=6"],
-    # merged roles (LSS_SPLAT_IMPL=1)
+    # two block roles (product default, LSS_SPLAT_IMPL=0)
+    "r2_nobcast": ["LSS_DEPTH_BCAST=0"],    # every lane group gathers its depth weights itself
+    "r2_zu2": ["LSS_ZERO_UNITS=2"],         # 128 cells per zero wave: half as many zero waves to launch
+    "r2_zu2_nobcast": ["LSS_ZERO_UNITS=2", "LSS_DEPTH_BCAST=0"],
     "merged": ["LSS_SPLAT_IMPL=1"],
-    "m_u16": ["LSS_SPLAT_IMPL=1", "LSS_UNROLL_M=16", "LSS_MIN_WAVES_M=4"],
-    "m_w8": ["LSS_SPLAT_IMPL=1", "LSS_SPLAT_WAVES=8"],
 }
 VARIANTS_R1 = {  # round-1 knobs of the two-role kernel (kept for reference; pass --r1-variants)
     "skip_chunks": ["LSS_SPLAT_IMPL=0", "LSS_FWD_SKIP=1"],  # zero units only (timing decomposition; wrong output)
@@ -57,6 +53,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", default="", help="run only ops whose name contains this (for rocprofv3 --pmc)")
     ap.add_argument("--variants", type=int, default=1, help="also time the variants/*.so builds")
+    ap.add_argument("--variant-filter", default="", help="only variants whose name contains this")
     ap.add_argument("--cold", type=int, default=1, help="also time splat_fwd in the cold and step cache states")
     args = ap.parse_args()
     if args.build_variants:
@@ -213,8 +210,10 @@ def main():
     fwd(lib, bev_bf, _lib.NHWC)()
     ref_out = bev_bf.clone()
     for path in sorted(glob.glob(os.path.join(REPO, "lss-carla_amd", "variants", "*.so"))) if args.variants else []:
-        vl = _lib.open_library(path)
         name = os.path.basename(path)[:-3]
+        if args.variant_filter and args.variant_filter not in name:
+            continue
+        vl = _lib.open_library(path)
         vcsr = lib_plan(vl)
         fwd(vl, bev_bf, _lib.NHWC, vcsr)()
         if not torch.equal(bev_bf, ref_out):
