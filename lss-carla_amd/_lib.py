@@ -25,6 +25,14 @@ class Dims(ctypes.Structure):
                 ("H", ctypes.c_int32), ("W", ctypes.c_int32), ("C", ctypes.c_int32)]
 
 
+class ImgAug(ctypes.Structure):
+    """lss_img_aug_t of include/lss_simbev.h."""
+    _fields_ = [("src_h", ctypes.c_int32), ("src_w", ctypes.c_int32), ("rs_w", ctypes.c_int32),
+                ("rs_h", ctypes.c_int32), ("crop", ctypes.c_int32 * 4), ("flip", ctypes.c_int32),
+                ("rot_mode", ctypes.c_int32), ("affine", ctypes.c_int32 * 6), ("h_off", ctypes.c_int32),
+                ("h_ksize", ctypes.c_int32), ("v_off", ctypes.c_int32), ("v_ksize", ctypes.c_int32)]
+
+
 class Grid(ctypes.Structure):
     _fields_ = [("lo", ctypes.c_float * 3), ("dx", ctypes.c_float * 3), ("nx", ctypes.c_int32 * 3)]
 
@@ -57,6 +65,11 @@ SIGNATURES = {
     "lss_segment_build": (ctypes.c_int, [_p, _i32, _p, _p, _p, _p, _p]),
     "lss_segment_sum": (ctypes.c_int, [_p, _i32, _p, _i32, _p, _i32, _p, _p, _p]),
     "lss_segment_gather": (ctypes.c_int, [_p, _i32, _p, _i32, _p, _p]),
+    # include/lss_simbev.h (SimBEV input path, same library)
+    "lss_resample_ksize": (ctypes.c_int, [_i32, _i32]),
+    "lss_resample_coeffs": (ctypes.c_int, [_i32, _i32, _p]),
+    "lss_simbev_images": (ctypes.c_int, [_p, _i32, _i32, _i32, _p, _p, _i32, _i32, _p, _p]),
+    "lss_simbev_vehicle_mask": (ctypes.c_int, [_p, _i32, _i32, _i32, _i32, _p, _p]),
     # include/lss_convs.h (conv-stack kernels, same library)
     "lss_dwconv_fwd": (ctypes.c_int, [_p, _i32, _p] + [_i32] * 10 + [_p, _p]),
     "lss_dwconv_bwd_data": (ctypes.c_int, [_p, _i32, _p] + [_i32] * 10 + [_p, _p]),

@@ -14,8 +14,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("lss_hip.hip", "lss_convs.hip", "lss_bnorm.hip",
-                                                            "lss_resample.hip", "lss_se.hip")]
-HEADERS = [os.path.join(REPO, "include", "lss_hip.h"), os.path.join(REPO, "include", "lss_convs.h")]
+                                                            "lss_resample.hip", "lss_se.hip", "lss_simbev.hip")]
+HEADERS = [os.path.join(REPO, "include", h) for h in ("lss_hip.h", "lss_convs.h", "lss_simbev.h")]
 OUT = os.path.join(HERE, "liblss_hip.so")
 ARCH = os.environ.get("LSS_OFFLOAD_ARCH", "gfx950")
 

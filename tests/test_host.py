@@ -12,7 +12,7 @@ import lss_carla_amd as L
 from lss_carla_amd import _lib, ops
 from lss_carla_amd import synthetic as syn
 
-HEADERS = [os.path.join(REPO, "include", h) for h in ("lss_hip.h", "lss_convs.h")]
+HEADERS = [os.path.join(REPO, "include", h) for h in ("lss_hip.h", "lss_convs.h", "lss_simbev.h")]
 
 
 def _declared():
