@@ -147,6 +147,24 @@ __device__ __forceinline__ void emit_cell(int p, int cell, int32_t* cell_of, int
         return;
     }
     const int lane = threadIdx.x & 63;
+    if (LSS_GEOM_AGG == 2) {
+        // runs of equal cells in adjacent lanes (neighbouring pixels at one depth mostly share a cell):
+        // one atomic per run from its first lane; the bit operations replace the per-cell ballot loop
+        const bool kept = live && cell >= 0;
+        const int up = __shfl(cell, (lane + 63) & 63, kWave);
+        const unsigned long long keptm = __ballot(kept);
+        const unsigned long long starts = __ballot(kept && (lane == 0 || up != cell || !((keptm >> (lane - 1)) & 1ull)));
+        const unsigned long long below = starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+        const int lead = below ? 63 - __builtin_clzll(below) : lane;
+        const unsigned long long after = lead == 63 ? 0ull : (~0ull << (lead + 1));
+        const unsigned long long nxt = (starts | ~keptm) & after;  // next run start or dropped lane
+        const int stop = nxt ? __builtin_ctzll(nxt) : 64;
+        int base = 0;
+        if (kept && lead == lane) base = atomicAdd(cell_count + cell, stop - lane);
+        base = __shfl(base, lead, kWave);
+        if (live) slot_of[p] = kept ? base + (lane - lead) : -1;
+        return;
+    }
     unsigned long long rem = __ballot(live && cell >= 0);
     int leader = -1, rank = 0, size = 0;
     while (rem) {
@@ -639,6 +657,123 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
     }
     // context rows: 64 consecutive channels of a pixel = one 128-B row
     for (int i = threadIdx.x; i < kDnPix * kC; i += kBlock) {
+        const int pp = i / kC, c = i - pp * kC;
+        if (q0 + pp < npix) ctx_t[(size_t)(q0 + pp) * kC + c] = __float2bfloat16(s_lg[D + c][pp]);
+    }
+}
+
+// ---- depthnet + lift, version 2: one block = 32 pixels x 8 waves, v_mfma_f32_16x16x32_bf16.
+// Wave m owns output rows [16m, 16m + 16) (its weight rows: 16 x K bf16, loaded once per lane straight
+// into the A fragments -- K/32 16-B loads, all in flight with the feature loads); the block's feature
+// tile is staged in LDS exactly as it lies in memory ([k][pixel], 8 consecutive pixels of one channel
+// per 16-B load and per ds_write_b128), and the B fragments (8 channels of one pixel per lane) come out
+// of it transposed by ds_read_b64_tr_b16 (gfx950: 4 rows x 16 columns of 16-bit elements, delivered
+// column-major), two per K step. Then logits + bias rounded to bf16 (the autocast conv's output), depth
+// softmax over the first D rows, context rows -- as k_depthnet_lift.
+constexpr int kDn2Pix = 32;                    // pixels per block (two 16-pixel MFMA column tiles)
+constexpr int kDn2Waves = 8;                   // 8 x 16 = 128 output rows >= D + C
+constexpr int kDn2Block = kDn2Waves * kWave;
+constexpr int kDn2Row = kDn2Pix * 2 + 8;       // LDS bytes per channel row (+8: spread the banks, 8-B aligned)
+#ifndef LSS_DN_IMPL
+#define LSS_DN_IMPL 2  // 1: k_depthnet_lift (32x32x16, weights streamed from L2), 2: k_depthnet_lift2
+#endif
+
+__global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __restrict__ feat,
+                                                              const bf16* __restrict__ weight,
+                                                              const bf16* __restrict__ bias, int K, int D, int HW,
+                                                              int npix, float* __restrict__ depth,
+                                                              bf16* __restrict__ ctx_t) {
+    using bf16x8 = __attribute__((ext_vector_type(8))) short;
+    using v4s = __attribute__((ext_vector_type(4))) short;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    __shared__ __attribute__((aligned(16))) unsigned char s_x[kDnMaxK * kDn2Row];  // [k][pixel] bf16
+    __shared__ float s_lg[kDnMaxO][kDn2Pix + 1];                                  // bf16-rounded logits
+    __shared__ float s_red[2][kDn2Block / kDn2Pix][kDn2Pix];
+    const int q0 = xcd_block() * kDn2Pix;
+    if (q0 >= npix) return;  // block-uniform
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int O = D + kC;
+    // ---- loads: this wave's weight rows (A fragments) and the block's feature tile, all in flight
+    const int arow = wave * 16 + (lane & 15);
+    const int kq = 8 * (lane >> 4);  // k offset of the lane's 8 elements inside a 32-wide K step
+    constexpr int kSteps = kDnMaxK / 32;
+    bf16x8 a[kSteps];
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+        a[s] = bf16x8{};
+        if (arow < O && 32 * s < K) a[s] = *reinterpret_cast<const bf16x8*>(weight + (size_t)arow * K + 32 * s + kq);
+    }
+    constexpr int kFeatIt = kDnMaxK * (kDn2Pix / 8) / kDn2Block;  // 16-B feature loads per thread
+    uint4 fv[kFeatIt];
+#pragma unroll
+    for (int t = 0; t < kFeatIt; ++t) {
+        const int i = threadIdx.x + t * kDn2Block;
+        const int k = i / (kDn2Pix / 8), p8 = (i % (kDn2Pix / 8)) * 8, q = q0 + p8;
+        fv[t] = make_uint4(0u, 0u, 0u, 0u);
+        if (k < K && q < npix) {
+            const int bn = q / HW, hw = q - bn * HW;  // HW % 8 == 0: 8 pixels never straddle an image
+            fv[t] = *reinterpret_cast<const uint4*>(feat + ((size_t)bn * K + k) * HW + hw);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < kFeatIt; ++t) {
+        const int i = threadIdx.x + t * kDn2Block;
+        const int k = i / (kDn2Pix / 8), p8 = (i % (kDn2Pix / 8)) * 8;
+        *reinterpret_cast<uint4*>(s_x + k * kDn2Row + p8 * 2) = fv[t];
+    }
+    __syncthreads();
+    // ---- MFMA: two 16-pixel column tiles, K/32 steps; B fragments by transposed LDS reads
+    f32x4 acc[2] = {f32x4{}, f32x4{}};
+    const int g = lane >> 4, c16 = lane & 15, tq = c16 >> 2, tp = c16 & 3;
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+        if (32 * s >= K) break;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            // lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3 of a 4 x 16 block; lane c of
+            // the group receives column c (pixel 16t + c), rows 0..3 (4 consecutive channels)
+            const unsigned char* base = s_x + (32 * s + 8 * g + tq) * kDn2Row + (16 * t + 4 * tp) * 2;
+            const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) v4s*)(base));
+            const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) v4s*)(base + 4 * kDn2Row));
+            const bf16x8 b = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], b, acc[t], 0, 0, 0);
+        }
+    }
+    // C/D: column (pixel) = lane & 15, row (output) = 4 (lane >> 4) + i
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int o = wave * 16 + 4 * g + i;
+            if (o < O) s_lg[o][16 * t + c16] = __bfloat162float(__float2bfloat16(acc[t][i] + __bfloat162float(bias[o])));
+        }
+    __syncthreads();
+    // ---- softmax over the D bins of each pixel: thread (part, p) covers bins part, part + 16, ...
+    constexpr int kParts = kDn2Block / kDn2Pix;
+    const int p = threadIdx.x % kDn2Pix, part = threadIdx.x / kDn2Pix;
+    float m = -INFINITY;
+    for (int d = part; d < D; d += kParts) m = fmaxf(m, s_lg[d][p]);
+    s_red[0][part][p] = m;
+    __syncthreads();
+    m = s_red[0][0][p];
+#pragma unroll
+    for (int j = 1; j < kParts; ++j) m = fmaxf(m, s_red[0][j][p]);
+    float sum = 0.f;
+    for (int d = part; d < D; d += kParts) sum += expf(s_lg[d][p] - m);
+    s_red[1][part][p] = sum;
+    __syncthreads();
+    sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < kParts; ++j) sum += s_red[1][j][p];
+    const int q = q0 + p;
+    if (q < npix) {
+        const int bn = q / HW, hw = q - bn * HW;
+        float* dst = depth + (size_t)bn * D * HW + hw;
+        for (int d = part; d < D; d += kParts) dst[(size_t)d * HW] = expf(s_lg[d][p] - m) / sum;
+    }
+    for (int i = threadIdx.x; i < kDn2Pix * kC; i += kDn2Block) {
         const int pp = i / kC, c = i - pp * kC;
         if (q0 + pp < npix) ctx_t[(size_t)(q0 + pp) * kC + c] = __float2bfloat16(s_lg[D + c][pp]);
     }
@@ -1331,6 +1466,9 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(c
 #ifndef LSS_UNROLL_M
 #define LSS_UNROLL_M 8     // entries per lane group gathered in the first batch
 #endif
+#ifndef LSS_MERGED_ZERO_LATE
+#define LSS_MERGED_ZERO_LATE 0  // 1: the zero unit's stores after the chunk's own (no store before a load)
+#endif
 constexpr int kUnrollM = LSS_UNROLL_M;
 
 template <typename OutT>
@@ -1430,8 +1568,8 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES_M) void k_splat_fwd_nhwc
         const bool bcast = FUSED && !sorted_w && LSS_DEPTH_BCAST;
         const float wd = bcast ? group_weight_load<LPR, kUnrollM>(meta, depth, gs < ge ? gs : s, gs < ge ? ge - 1 : s,
                                                                   lane) : 0.f;
-        // the zero unit's rows go out while the gathers are in flight
-        zero_unit_rows<OutT>(zu * kWave, emask, g, out, lane);
+        // the zero unit's rows go out while the gathers are in flight (LSS_MERGED_ZERO_LATE: at the end)
+        if (!LSS_MERGED_ZERO_LATE) zero_unit_rows<OutT>(zu * kWave, emask, g, out, lane);
         float acc[EPL];
 #pragma unroll
         for (int i = 0; i < EPL; ++i) acc[i] = 0.f;
@@ -1509,9 +1647,10 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES_M) void k_splat_fwd_nhwc
                 store_slice<EPL>(cell_row(out, first_cell, g) + col, carry);
             }
         }
-    } else {
+    } else if (!LSS_MERGED_ZERO_LATE) {
         zero_unit_rows<OutT>(zu * kWave, emask, g, out, lane);
     }
+    if (LSS_MERGED_ZERO_LATE) zero_unit_rows<OutT>(zu * kWave, emask, g, out, lane);
     if (big >= 0) {
         int cell;
         const float a2 = reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base, lane,
@@ -1713,6 +1852,115 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd_reg(const GT* __restrict__
 #ifndef LSS_BWD_REG
 #define LSS_BWD_REG 1  // 1: k_splat_bwd_reg (registers + shuffles), 0: k_splat_bwd (LDS staging)
 #endif
+#ifndef LSS_BWD_TILE
+#define LSS_BWD_TILE 1  // 1: k_splat_bwd_tile (pixel tiles, coalesced loads and stores) where the shape allows
+#endif
+
+// Pixel-tile form of k_splat_bwd_reg. The per-pixel form reads the D depth weights and cells of its
+// pixel at a stride of H*W (one cache line per value) and writes d_depthnet_out one element per
+// channel (D + C lines per pixel, 2 bytes each). Here a block (8 waves) takes PX consecutive pixels
+// of one image: their weights, cells and context rows are read as contiguous runs into LDS; each
+// wave takes PPW pixels, issues ALL their gradient-row gathers before any arithmetic (one round trip),
+// reduces each as k_splat_bwd_reg does (fixed association), and leaves d_logits / d_ctx in an LDS
+// tile that the block writes channel by channel, PX consecutive pixels per run.
+constexpr int kBwdWaves = 8;
+constexpr int kBwdBlock = kBwdWaves * kWave;
+
+template <typename GT, typename DT, typename CT, bool NHWC>
+__global__ __launch_bounds__(kBwdBlock) void k_splat_bwd_tile(const GT* __restrict__ g,
+                                                              const int32_t* __restrict__ cell_of,
+                                                              const float* __restrict__ depth,
+                                                              const CT* __restrict__ ctx_t, int D, int HW, int npix,
+                                                              SplatGeo sg, DT* __restrict__ d_dn) {
+    constexpr int EPL = 16 / sizeof(GT);  // row elements per 16-B lane load
+    constexpr int LPR = kC / EPL;         // lanes per row
+    constexpr int RPI = kWave / LPR;      // rows per wave-instruction
+    constexpr int NI = kWave / RPI;       // instructions for 64 rows
+    constexpr int PPW = sizeof(GT) == 2 ? 2 : 1;  // pixels per wave, all gathers in flight
+    constexpr int PX = kBwdWaves * PPW;           // pixels per block
+    __shared__ float s_dep[64][PX];
+    __shared__ int s_cell[64][PX];
+    __shared__ float s_ctx[PX][kC];
+    __shared__ float s_out[64 + kC][PX + 1];
+    const int q0 = xcd_block() * PX;
+    if (q0 >= npix) return;  // block-uniform
+    const int bn = q0 / HW, hw0 = q0 - bn * HW;  // HW % PX == 0: the tile lies in one image
+    const size_t pb = (size_t)bn * D * HW + hw0;
+    for (int i = threadIdx.x; i < D * PX; i += kBwdBlock) {
+        const int d = i / PX, j = i - d * PX;
+        s_dep[d][j] = depth[pb + (size_t)d * HW + j];
+        s_cell[d][j] = cell_of[pb + (size_t)d * HW + j];
+    }
+    for (int i = threadIdx.x; i < PX * kC; i += kBwdBlock) s_ctx[i / kC][i % kC] = to_f32(ctx_t[(size_t)q0 * kC + i]);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane / LPR, col = (lane % LPR) * EPL;
+    uint4 raw[PPW][NI];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int jj = wave * PPW + i;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const int r = k * RPI + sub;
+            raw[i][k] = make_uint4(0u, 0u, 0u, 0u);
+            if (k * RPI < D && r < D) {
+                const int cell = s_cell[r][jj];
+                if (cell >= 0) raw[i][k] = *reinterpret_cast<const uint4*>(g + row_offset<NHWC>(cell, sg) + col);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int jj = wave * PPW + i;
+        const float my_depth = lane < D ? s_dep[lane][jj] : 0.f;
+        float cx[EPL], dc[EPL], part[NI];
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+            cx[e] = s_ctx[jj][col + e];
+            dc[e] = 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const int r = k * RPI + sub;
+            const float w = r < D ? s_dep[r][jj] : 0.f;
+            float f[EPL];
+            unpack16(raw[i][k], (const GT*)nullptr, f);
+            float t = 0.f;
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                dc[e] = fmaf(f[e], w, dc[e]);
+                t = fmaf(f[e], cx[e], t);
+            }
+            part[k] = t;
+        }
+#pragma unroll
+        for (int o = LPR; o < kWave; o <<= 1)
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) dc[e] += __shfl_xor(dc[e], o, kWave);
+#pragma unroll
+        for (int k = 0; k < NI; ++k)
+#pragma unroll
+            for (int o = 1; o < LPR; o <<= 1) part[k] += __shfl_xor(part[k], o, kWave);
+        float dd = 0.f;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const float v = __shfl(part[k], (lane % RPI) * LPR, kWave);
+            if (lane / RPI == k) dd = v;
+        }
+        if (lane >= D) dd = 0.f;
+        const float s = wave_sum(my_depth * dd);
+        if (lane < D) s_out[lane][jj] = my_depth * (dd - s);
+        if (sub == 0)
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) s_out[D + col + e][jj] = dc[e];
+    }
+    __syncthreads();
+    DT* dst = d_dn + (size_t)bn * (D + kC) * HW + hw0;
+    for (int i = threadIdx.x; i < (D + kC) * PX; i += kBwdBlock) {
+        const int ch = i / PX, j = i - ch * PX;
+        dst[(size_t)ch * HW + j] = from_f32<DT>(s_out[ch][j]);
+    }
+}
 
 template <typename GT, bool NHWC>
 __global__ __launch_bounds__(kBlock) void k_splat_bwd_lifted(const GT* __restrict__ g, const int32_t* __restrict__ cell_of,
@@ -1995,6 +2243,12 @@ int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, in
     const int HW = dims->H * dims->W;
     const long npix = (long)dims->B * dims->N * HW;
     if (npix >= INT_MAX) return LSS_EUNSUPPORTED;
+    if (LSS_DN_IMPL == 2 && K % 32 == 0 && HW % 8 == 0 && pos_of == nullptr) {
+        hipLaunchKernelGGL(k_depthnet_lift2, dim3(xcd_grid(grid_blocks(npix, kDn2Pix))), dim3(kDn2Block), 0,
+                           (hipStream_t)stream, (const bf16*)feat, (const bf16*)weight, (const bf16*)bias, K, dims->D,
+                           HW, (int)npix, depth, (bf16*)ctx_t);
+        return launch_status();
+    }
     hipLaunchKernelGGL(k_depthnet_lift, dim3(xcd_grid(grid_blocks(npix, kDnPix))), dim3(kBlock), 0, (hipStream_t)stream,
                        (const bf16*)feat, (const bf16*)weight, (const bf16*)bias, K, dims->D, HW, (int)npix, depth,
                        (bf16*)ctx_t, pos_of, sorted_depth);
@@ -2138,7 +2392,15 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
     const bool nhwc = rows_layout == LSS_NHWC;
 #define LSS_BWD(GT, DT, CT)                                                                                       \
     do {                                                                                                          \
-        if (LSS_BWD_REG && nhwc)                                                                                  \
+        constexpr int px = kBwdWaves * (sizeof(GT) == 2 ? 2 : 1);                                                 \
+        const dim3 grt(xcd_grid(npix / px)), blt(kBwdBlock);                                                      \
+        if (LSS_BWD_TILE && HW % px == 0 && nhwc)                                                                 \
+            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, true>), grt, blt, 0, s, (const GT*)g, cell_of, depth, \
+                               (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
+        else if (LSS_BWD_TILE && HW % px == 0)                                                                    \
+            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, false>), grt, blt, 0, s, (const GT*)g, cell_of,     \
+                               depth, (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);              \
+        else if (LSS_BWD_REG && nhwc)                                                                             \
             hipLaunchKernelGGL((k_splat_bwd_reg<GT, DT, CT, true>), gr, bl, 0, s, (const GT*)g, cell_of, depth,   \
                                (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
         else if (LSS_BWD_REG)                                                                                     \

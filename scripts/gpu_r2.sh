@@ -10,7 +10,7 @@ for s in $steps; do
       echo "tests=$rc"; tail -15 $OUT/gpu_tests.log; [ $rc -ne 0 ] && exit $rc ;;
     kbench)
       timeout -k 10 400 python -u scripts/kbench.py > $OUT/kbench.log 2>&1; rc=$?
-      echo "kbench=$rc"; grep -v Warn $OUT/kbench.log | tail -60; [ $rc -ne 0 ] && exit $rc ;;
+      echo "kbench=$rc"; grep -v Warn $OUT/kbench.log | tail -100; [ $rc -ne 0 ] && exit $rc ;;
     bench)
       timeout -k 10 600 python -u bench.py > $OUT/bench.log 2>&1; rc=$?
       echo "bench=$rc"; grep "^\[" $OUT/bench.log | tail -8; tail -1 $OUT/bench.log; [ $rc -ne 0 ] && exit $rc ;;

@@ -22,11 +22,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
-    # two block roles (product default, LSS_SPLAT_IMPL=0)
-    "r2_nobcast": ["LSS_DEPTH_BCAST=0"],    # every lane group gathers its depth weights itself
-    "r2_zu2": ["LSS_ZERO_UNITS=2"],         # 128 cells per zero wave: half as many zero waves to launch
-    "r2_zu2_nobcast": ["LSS_ZERO_UNITS=2", "LSS_DEPTH_BCAST=0"],
     "merged": ["LSS_SPLAT_IMPL=1"],
+    "merged_late": ["LSS_SPLAT_IMPL=1", "LSS_MERGED_ZERO_LATE=1"],
+    "dn1": ["LSS_DN_IMPL=1"],               # round-1 depthnet lift
+    "agg2": ["LSS_GEOM_AGG=2"],             # geometry: one atomic per run of equal adjacent cells
+    "bwd0": ["LSS_BWD_TILE=0"],             # round-1 splat bwd
 }
 VARIANTS_R1 = {  # round-1 knobs of the two-role kernel (kept for reference; pass --r1-variants)
     "skip_chunks": ["LSS_SPLAT_IMPL=0", "LSS_FWD_SKIP=1"],  # zero units only (timing decomposition; wrong output)
@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--variants", type=int, default=1, help="also time the variants/*.so builds")
     ap.add_argument("--variant-filter", default="", help="only variants whose name contains this")
     ap.add_argument("--cold", type=int, default=1, help="also time splat_fwd in the cold and step cache states")
+    ap.add_argument("--lib", default="", help="use variants/<name>.so as THE library (ops included), for rocprofv3")
     args = ap.parse_args()
     if args.build_variants:
         build_variants(args.r1_variants)
@@ -63,6 +64,8 @@ def main():
     from lss_carla_amd import _lib, ops, synthetic as syn
     from oracle import lss_ref as ref
 
+    if args.lib:
+        _lib._lib = _lib.open_library(os.path.join(REPO, "lss-carla_amd", "variants", args.lib + ".so"))
     dev = torch.device("cuda:0")
     cfg, gc, _ = syn.config_confs(args.config)
     B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
@@ -123,6 +126,44 @@ def main():
     def named(name, fn, *a):
         timeit.name = name
         return timeit(fn, *a)
+
+    def lib_rows(l, tag):
+        """Launch-to-launch rows of library `l` for the plan pieces, the fused lift and the splat bwd."""
+        counts = torch.zeros(ncells, device=dev, dtype=torch.int32)
+        slot = torch.empty(nprime, device=dev, dtype=torch.int32)
+        cell_of = torch.empty(nprime, device=dev, dtype=torch.int32)
+        cs = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
+        sk = torch.empty(nprime, device=dev, dtype=torch.int64)
+        sr = torch.empty(nprime, device=dev, dtype=torch.int32)
+        po = torch.empty(nprime, device=dev, dtype=torch.int32)
+        scr = torch.empty(int(l.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
+        geom = lambda: _lib.check(l.lss_geometry_cells(  # noqa: E731
+            _lib.ptr(frustum), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv), _lib.ptr(pt), dims, g,
+            None, _lib.ptr(cell_of), _lib.ptr(counts), _lib.ptr(slot), st()), "geom")
+        csr = lambda: _lib.check(l.lss_csr_build(  # noqa: E731
+            _lib.ptr(cell_of), _lib.ptr(slot), nprime, _lib.ptr(counts), ncells, dims, _lib.ptr(cs), _lib.ptr(sk),
+            _lib.ptr(sr), _lib.ptr(po), _lib.ptr(scr), st()), "csr")
+
+        def geom_only():
+            counts.zero_()
+            geom()
+
+        def plan3():
+            counts.zero_()
+            geom()
+            csr()
+        res[f"memset counts{tag}"] = named("memset counts", lambda: counts.zero_())
+        res[f"memset+geometry_cells{tag}"] = named("geometry_cells", geom_only)
+        res[f"memset+geometry+csr_build{tag}"] = named("csr_build", plan3)
+        plan3()
+        if not (torch.equal(cs, plan.cell_start) and torch.equal(sk, plan.sorted_key)):
+            print(f"WARNING {tag}: CSR differs from the product plan", flush=True)
+        res[f"depthnet_lift (fused, MFMA){tag}"] = named("depthnet_lift", lambda: _lib.check(l.lss_depthnet_lift(
+            _lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims, _lib.ptr(depth), _lib.ptr(ctx_t),
+            _lib.BF16, None, None, st()), "depthnet_lift"))
+        res[f"splat_bwd nhwc bf16{tag}"] = named("splat_bwd nhwc bf16", lambda: _lib.check(l.lss_splat_bwd(
+            _lib.ptr(g_bf), _lib.BF16, _lib.NHWC, _lib.ptr(plan.cell_of), _lib.ptr(depth), _lib.ptr(ctx_t),
+            _lib.BF16, dims, g, _lib.ptr(d_dn), _lib.BF16, st()), "bwd"))
 
     depth = torch.empty(B * N, D, H, W, device=dev)
     ctx_t = torch.empty(B * N * H * W, 64, device=dev, dtype=torch.bfloat16)  # as ops.LiftSplat for bf16 input
@@ -209,11 +250,20 @@ def main():
     # the timing modes above rewrote ctx_t (the "step" mode reruns the lift): fresh reference output
     fwd(lib, bev_bf, _lib.NHWC)()
     ref_out = bev_bf.clone()
+    g_bf = torch.randn(B, Z * 64, X, Y, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    d_dn = torch.empty_like(dn)
+    def restore_lift():  # lib_rows rewrites depth / ctx_t through the fused lift
+        _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, None,
+                                     None, st()), "lift")
+    lib_rows(lib, "")
+    restore_lift()
     for path in sorted(glob.glob(os.path.join(REPO, "lss-carla_amd", "variants", "*.so"))) if args.variants else []:
         name = os.path.basename(path)[:-3]
         if args.variant_filter and args.variant_filter not in name:
             continue
         vl = _lib.open_library(path)
+        lib_rows(vl, f" [{name}]")
+        restore_lift()
         vcsr = lib_plan(vl)
         fwd(vl, bev_bf, _lib.NHWC, vcsr)()
         if not torch.equal(bev_bf, ref_out):
@@ -225,11 +275,6 @@ def main():
             res[f"{m} splat_fwd nhwc bf16 [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m)
             res[f"{m} splat_fwd nhwc bf16 (sorted depth) [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m,
                                                                                sd=vsd)
-    g_bf = torch.randn(B, Z * 64, X, Y, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    d_dn = torch.empty_like(dn)
-    res["splat_bwd nhwc bf16"] = named("splat_bwd nhwc bf16", lambda: _lib.check(lib.lss_splat_bwd(
-        _lib.ptr(g_bf), _lib.BF16, _lib.NHWC, _lib.ptr(plan.cell_of), _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
-        dims, g, _lib.ptr(d_dn), _lib.BF16, st()), "bwd"))
     rows = torch.empty(ncells * 64, device=dev)
     g_f = torch.randn(B, Z * 64, X, Y, device=dev)
     res["bev_rows nchw f32"] = named("bev_rows nchw f32", lambda: _lib.check(lib.lss_bev_rows(

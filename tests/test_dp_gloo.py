@@ -16,6 +16,7 @@ import torch.multiprocessing as mp
 import lss_carla_amd as L
 from lss_carla_amd import parallel
 from lss_carla_amd.flat_params import FlatParams
+from lss_carla_amd.train_step import TrainStep
 from lss_carla_amd import synthetic as syn
 
 FD = (64, 192)
@@ -175,3 +176,56 @@ def test_flat_params_match_autocast_gradients():
     with torch.no_grad():
         flat.master.add_(1.0)
     assert torch.equal(net[0].bias.detach(), flat.views_of(flat.master.detach())["0.bias"])
+
+
+def _train_step(model, seed, world_reduce):
+    """One TrainStep (flat fp32 master, SimpleLoss, backward, all-reduce, clip 5.0, Adam) on `model`."""
+    parallel.freeze_unused(model)
+    wrapped = _CpuLSS(model)
+    flat = FlatParams(wrapped, cast_dtype=None)
+    imgs, rig, labels = _batch(seed)
+    opt = torch.optim.Adam([flat.master], lr=1e-3, weight_decay=1e-7)
+    inputs = (imgs, rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"])
+    step = TrainStep(flat.bind(wrapped), inputs, labels, L.SimpleLoss(2.13), opt, [flat.master],
+                     all_reduce=world_reduce, amp_dtype=None, max_grad_norm=5.0)
+    return step, flat
+
+
+def _worker_trainstep(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    parallel.init_from_env("gloo")
+    m = _model()
+    parallel.broadcast_state(m)
+    step, flat = _train_step(m, seed=20 + rank, world_reduce=True)
+    assert step.world == world
+    loss = step.eager()
+    assert torch.isfinite(loss)
+    if rank == 0:
+        torch.save({"master": flat.master.detach().clone()}, os.path.join(outdir, "ts.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_train_step_world2_equals_single_process_average():
+    """TrainStep's world > 1 path (the captured bench step's eager twin): all-reduce sum, / world,
+    clip_grad_norm_(5), Adam -- equals one process applying the mean of the two ranks' gradients."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_trainstep, args=(world, _free_port(), d), nprocs=world, join=True)
+        got = torch.load(os.path.join(d, "ts.pt"), weights_only=True)["master"]
+    nthreads = torch.get_num_threads()
+    torch.set_num_threads(2)
+    grads = []
+    for rank in range(world):
+        step, flat = _train_step(_model(), seed=20 + rank, world_reduce=False)
+        step.forward_backward()
+        grads.append(flat.master.grad.clone())
+    step, flat = _train_step(_model(), seed=20, world_reduce=False)
+    flat.master.grad = (grads[0] + grads[1]) * (1.0 / world)
+    step.update()
+    torch.set_num_threads(nthreads)
+    want = flat.master.detach()
+    assert got.shape == want.shape
+    torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-7)

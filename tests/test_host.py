@@ -101,3 +101,33 @@ def test_synthetic_rig_shapes():
     assert rig["post_trans"][0, 0].tolist() == [0.0, -36.0, 0.0]
     dn = syn.make_depthnet_out(1, 1, 41, 8, 22)
     assert dn.shape == (1, 105, 8, 22)
+
+
+def test_bench_gpus_flag_launches_one_rank_per_gpu(monkeypatch):
+    """`bench.py --gpus N` without a torchrun environment re-launches itself as N ranks (torchrun on
+    127.0.0.1) before touching the GPU, and exits with the job's status."""
+    import importlib.util
+    import sys as _sys
+    spec = importlib.util.spec_from_file_location("_bench", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+
+    monkeypatch.setattr(bench.subprocess, "call", fake_call)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(_sys, "argv", ["bench.py", "--gpus", "8", "--steps", "3"])
+    args = bench.parse()
+    with pytest.raises(SystemExit) as e:
+        bench.maybe_launch_ranks(args)
+    assert e.value.code == 7
+    cmd = seen["cmd"]
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"] and "--nproc-per-node=8" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"] and seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    monkeypatch.setenv("WORLD_SIZE", "8")  # under torchrun: no second launch
+    assert bench.maybe_launch_ranks(args) is None
+    assert args.config == "c3" and args.batch == 8 and args.mode == "train" and args.bev_layout == "nhwc"
