@@ -58,6 +58,20 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
+// "v if c else 0" without a branch: the mask goes through an empty asm, so the compiler cannot turn
+// the AND back into a select and then into a branch around the load that produced v (it sinks such
+// loads into conditional blocks, and the blocks serialise loads that should all be in flight).
+__device__ __forceinline__ unsigned keep_mask(bool c) {
+    unsigned m = c ? 0xFFFFFFFFu : 0u;
+    asm("" : "+v"(m));
+    return m;
+}
+__device__ __forceinline__ uint4 keep_if(bool c, uint4 v) {
+    const unsigned m = keep_mask(c);
+    return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+}
+__device__ __forceinline__ float keep_if(bool c, float v) { return __uint_as_float(__float_as_uint(v) & keep_mask(c)); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
@@ -68,6 +82,21 @@ __device__ __forceinline__ int wave_min(int v) {
     for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, kWave));
     return v;
 }
+
+#ifndef LSS_TRACE
+#define LSS_TRACE 0  // diagnostics build: per-wave s_memrealtime stamps of the channels-last splat
+#endif
+#if LSS_TRACE
+// [wave slot][0: start, 1: after round trip 1, 2: after the first gather batch, 3: end, 4: kind | hw id]
+__device__ unsigned long long g_lss_trace[16384][5];
+#define LSS_STAMP(slot, i)                                                                                     \
+    do {                                                                                                       \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                        \
+        if ((threadIdx.x & 63) == 0 && (slot) < 16384) g_lss_trace[(slot)][(i)] = t_;                          \
+    } while (0)
+#else
+#define LSS_STAMP(slot, i) do { } while (0)
+#endif
 
 // Blocks are dealt round-robin over the 8 XCDs (observed placement: speed only, never correctness).
 // xcd_block gives each XCD one contiguous run of ceil(nb / 8) logical blocks, so kernels that follow
@@ -184,17 +213,12 @@ __device__ __forceinline__ void emit_cell(int p, int cell, int32_t* cell_of, int
     if (live) slot_of[p] = leader < 0 ? -1 : base + rank;
 }
 
-__global__ __launch_bounds__(kBlock) void k_geometry_cells(
-    const float* __restrict__ frustum, const float* __restrict__ rots, const float* __restrict__ trans,
-    const float* __restrict__ kinv, const float* __restrict__ pinv, const float* __restrict__ post_trans,
-    int N, int DHW, int nprime, lss_grid_t g, float* __restrict__ out_geom, int32_t* __restrict__ cell_of,
-    int32_t* __restrict__ cell_count, int32_t* __restrict__ slot_of) {
-    const int p0 = blockIdx.x * kBlock + threadIdx.x;
-    const bool live = p0 < nprime;
-    const int p = live ? p0 : nprime - 1;  // dead lanes recompute the last point, then write nothing
-    const int cam = p / DHW;
-    const int f = p - cam * DHW;
-    const int b = cam / N;
+// One frustum point through one camera (src/models.py:172-190), fp32, each op rounded in the
+// reference's order.
+__device__ __forceinline__ void geometry_point(const float* __restrict__ frustum, const float* __restrict__ rots,
+                                               const float* __restrict__ trans, const float* __restrict__ kinv,
+                                               const float* __restrict__ pinv, const float* __restrict__ post_trans,
+                                               int cam, int f, float e[3]) {
     const float* P = pinv + 9 * cam;
     const float* K = kinv + 9 * cam;
     const float* R = rots + 9 * cam;
@@ -209,7 +233,6 @@ __global__ __launch_bounds__(kBlock) void k_geometry_cells(
     // (x*z, y*z, z)                                         (src/models.py:183-185)
     const float r0 = __fmul_rn(q0, q2), r1 = __fmul_rn(q1, q2), r2 = q2;
     // combine = rots @ inv(intrins); points = combine @ points + trans   (src/models.py:186-188)
-    float e[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const float c0 = dot3_seq(R[3 * i + 0], R[3 * i + 1], R[3 * i + 2], K[0], K[3], K[6]);
@@ -217,12 +240,33 @@ __global__ __launch_bounds__(kBlock) void k_geometry_cells(
         const float c2 = dot3_seq(R[3 * i + 0], R[3 * i + 1], R[3 * i + 2], K[2], K[5], K[8]);
         e[i] = __fadd_rn(dot3_seq(c0, c1, c2, r0, r1, r2), trans[3 * cam + i]);
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_geometry_cells(
+    const float* __restrict__ frustum, const float* __restrict__ rots, const float* __restrict__ trans,
+    const float* __restrict__ kinv, const float* __restrict__ pinv, const float* __restrict__ post_trans,
+    int N, int DHW, int nprime, lss_grid_t g, float* __restrict__ out_geom, int32_t* __restrict__ cell_of,
+    int32_t* __restrict__ cell_count, int32_t* __restrict__ slot_of) {
+    LSS_STAMP(blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6), 0);
+    const int p0 = blockIdx.x * kBlock + threadIdx.x;
+    const bool live = p0 < nprime;
+    const int p = live ? p0 : nprime - 1;  // dead lanes recompute the last point, then write nothing
+    const int cam = p / DHW;
+    const int f = p - cam * DHW;
+    const int b = cam / N;
+    float e[3];
+    geometry_point(frustum, rots, trans, kinv, pinv, post_trans, cam, f, e);
     if (out_geom != nullptr && live) {
         out_geom[3 * (size_t)p + 0] = e[0];
         out_geom[3 * (size_t)p + 1] = e[1];
         out_geom[3 * (size_t)p + 2] = e[2];
     }
-    emit_cell(p, live ? quantize_cell(e[0], e[1], e[2], g, b) : -1, cell_of, cell_count, slot_of, live);
+    [[maybe_unused]] const int tslot = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);  // LSS_TRACE builds
+    LSS_STAMP(tslot, 1);
+    const int cell = live ? quantize_cell(e[0], e[1], e[2], g, b) : -1;
+    LSS_STAMP(tslot, 2);
+    emit_cell(p, cell, cell_of, cell_count, slot_of, live);
+    LSS_STAMP(tslot, 3);
 }
 
 __global__ __launch_bounds__(kBlock) void k_cells_from_geom(const float* __restrict__ geom, int nprime, int ppb,
@@ -488,16 +532,25 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
     const int px = threadIdx.x & 63, part = threadIdx.x >> 6;
     const int q = q0 + px;
     const bool live = q < npix;
-    const int bn = live ? q / HW : 0, hw = live ? q - bn * HW : 0;
+    // clamped, unconditional loads (no branch between them, so all are in flight at once); a dead
+    // lane's values feed nothing that is written
+    const int qc = min(q, npix - 1);
+    const int bn = qc / HW, hw = qc - bn * HW;
     const InT* src = dn + (size_t)bn * (D + kC) * HW + hw;
     float cv[16], l[16];
+    int at[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) cv[i] = live ? to_f32(src[(size_t)(D + part * 16 + i) * HW]) : 0.f;
+    for (int i = 0; i < 16; ++i) cv[i] = to_f32(src[(size_t)(D + part * 16 + i) * HW]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) l[i] = to_f32(src[(size_t)min(part + 4 * i, D - 1) * HW]);
+    if (pos_of) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) at[i] = pos_of[(bn * D + min(part + 4 * i, D - 1)) * HW + hw];
+    }
     float m = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        const int d = part + 4 * i;
-        l[i] = (live && d < D) ? to_f32(src[(size_t)d * HW]) : -INFINITY;
+        if (part + 4 * i >= D) l[i] = -INFINITY;
         m = fmaxf(m, l[i]);
     }
 #pragma unroll
@@ -522,10 +575,7 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
             if (d < D) {
                 const float v = e[i] / sum;
                 dst[(size_t)d * HW] = v;
-                if (pos_of) {  // the same weight at the point's CSR position (contiguous reads in the splat)
-                    const int at = pos_of[(bn * D + d) * HW + hw];
-                    if (at >= 0) sorted_depth[at] = v;
-                }
+                if (pos_of && at[i] >= 0) sorted_depth[at[i]] = v;  // the weight at its CSR position
             }
         }
     }
@@ -603,6 +653,9 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
     const int r = lane & 31, h = lane >> 5;
     const int o = wave * 32 + r;
     const bf16* wrow = weight + (size_t)min(o, O - 1) * K + 8 * h;
+    float bv[16];  // bias of the lane's 16 output rows, loaded ahead (not one round trip per row later)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bv[i] = __bfloat162float(bias[min(wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h, O - 1)]);
     f32x16 acc = {};
     // four weight fragments (L2 reads) in flight ahead of their MFMAs
     for (int k0 = 0; k0 < K; k0 += 64) {
@@ -622,7 +675,7 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int og = wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (og < O) s_lg[og][r] = __bfloat162float(__float2bfloat16(acc[i] + __bfloat162float(bias[og])));
+        if (og < O) s_lg[og][r] = __bfloat162float(__float2bfloat16(acc[i] + bv[i]));
     }
     __syncthreads();
     // softmax over the D bins of each pixel: thread (part, p) covers bins part, part + 8, ...
@@ -670,113 +723,136 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
 // of it transposed by ds_read_b64_tr_b16 (gfx950: 4 rows x 16 columns of 16-bit elements, delivered
 // column-major), two per K step. Then logits + bias rounded to bf16 (the autocast conv's output), depth
 // softmax over the first D rows, context rows -- as k_depthnet_lift.
-constexpr int kDn2Pix = 32;                    // pixels per block (two 16-pixel MFMA column tiles)
+#ifndef LSS_DN_PIX
+#define LSS_DN_PIX 48  // pixels per block: 48 -> 176 blocks at B=8 (32 -> 264 blocks, 8 CUs run two)
+#endif
+constexpr int kDn2Pix = LSS_DN_PIX;             // pixels per block (16-pixel MFMA column tiles)
 constexpr int kDn2Waves = 8;                   // 8 x 16 = 128 output rows >= D + C
 constexpr int kDn2Block = kDn2Waves * kWave;
-constexpr int kDn2Row = kDn2Pix * 2 + 8;       // LDS bytes per channel row (+8: spread the banks, 8-B aligned)
+#ifndef LSS_DN_SKIP
+#define LSS_DN_SKIP 0  // timing experiments only (wrong output): 1 skips the weight loads, 2 the feature loads
+#endif
 #ifndef LSS_DN_IMPL
 #define LSS_DN_IMPL 2  // 1: k_depthnet_lift (32x32x16, weights streamed from L2), 2: k_depthnet_lift2
 #endif
 
+template <int K, int PX>  // input channels (compile-time: straight-line code, every load up front), pixels per block
 __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __restrict__ feat,
                                                               const bf16* __restrict__ weight,
-                                                              const bf16* __restrict__ bias, int K, int D, int HW,
+                                                              const bf16* __restrict__ bias, int D, int HW,
                                                               int npix, float* __restrict__ depth,
                                                               bf16* __restrict__ ctx_t) {
+    static_assert(K % 32 == 0 && K <= kDnMaxK, "K steps of 32 staged in LDS");
+    static_assert(PX % 16 == 0, "16-pixel MFMA column tiles");
+    constexpr int kRow = PX * 2 + 8;  // LDS bytes per channel row (+8: spread the banks, 8-B aligned)
+    constexpr int kTiles = PX / 16;
     using bf16x8 = __attribute__((ext_vector_type(8))) short;
     using v4s = __attribute__((ext_vector_type(4))) short;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    __shared__ __attribute__((aligned(16))) unsigned char s_x[kDnMaxK * kDn2Row];  // [k][pixel] bf16
-    __shared__ float s_lg[kDnMaxO][kDn2Pix + 1];                                  // bf16-rounded logits
-    __shared__ float s_red[2][kDn2Block / kDn2Pix][kDn2Pix];
-    const int q0 = xcd_block() * kDn2Pix;
+    __shared__ __attribute__((aligned(16))) unsigned char s_x[K * kRow];  // [k][pixel] bf16
+    __shared__ float s_lg[kDnMaxO][PX + 1];                                  // bf16-rounded logits
+    __shared__ float s_red[2][kDn2Block / PX][PX];
+    const int q0 = xcd_block() * PX;
     if (q0 >= npix) return;  // block-uniform
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int O = D + kC;
+    [[maybe_unused]] const int tslot = blockIdx.x * kDn2Waves + wave;  // LSS_TRACE builds only
+    LSS_STAMP(tslot, 0);
     // ---- loads: this wave's weight rows (A fragments) and the block's feature tile, all in flight
     const int arow = wave * 16 + (lane & 15);
     const int kq = 8 * (lane >> 4);  // k offset of the lane's 8 elements inside a 32-wide K step
-    constexpr int kSteps = kDnMaxK / 32;
+    constexpr int kSteps = K / 32;
+    // Loads are unconditional (clamped addresses, no branches, so none waits on another): rows past O
+    // only feed logits that are never written, and the pixel columns of a clamped tail only feed their
+    // own discarded outputs.
+    const int g = lane >> 4, c16 = lane & 15;
+    const bf16* wrow = weight + (size_t)min(arow, O - 1) * K + kq;
     bf16x8 a[kSteps];
 #pragma unroll
-    for (int s = 0; s < kSteps; ++s) {
-        a[s] = bf16x8{};
-        if (arow < O && 32 * s < K) a[s] = *reinterpret_cast<const bf16x8*>(weight + (size_t)arow * K + 32 * s + kq);
-    }
-    constexpr int kFeatIt = kDnMaxK * (kDn2Pix / 8) / kDn2Block;  // 16-B feature loads per thread
+    for (int s = 0; s < kSteps; ++s)
+        a[s] = (LSS_DN_SKIP & 1) ? bf16x8{(short)lane, 1, 2, 3, 4, 5, 6, (short)s}
+                                 : *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
+    float bv[4];  // the bias of this lane's 4 output rows, in flight with the rest
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[i] = __bfloat162float(bias[min(wave * 16 + 4 * g + i, O - 1)]);
+    constexpr int kFeatIt = K * (PX / 8) / kDn2Block;  // 16-B feature loads per thread
+    static_assert(K * (PX / 8) % kDn2Block == 0, "whole feature loads per thread");
     uint4 fv[kFeatIt];
 #pragma unroll
     for (int t = 0; t < kFeatIt; ++t) {
         const int i = threadIdx.x + t * kDn2Block;
-        const int k = i / (kDn2Pix / 8), p8 = (i % (kDn2Pix / 8)) * 8, q = q0 + p8;
-        fv[t] = make_uint4(0u, 0u, 0u, 0u);
-        if (k < K && q < npix) {
-            const int bn = q / HW, hw = q - bn * HW;  // HW % 8 == 0: 8 pixels never straddle an image
-            fv[t] = *reinterpret_cast<const uint4*>(feat + ((size_t)bn * K + k) * HW + hw);
-        }
+        const int k = i / (PX / 8), q = min(q0 + (i % (PX / 8)) * 8, npix - 8);
+        const int bn = q / HW, hw = q - bn * HW;  // HW % 8 == 0: 8 pixels never straddle an image
+        fv[t] = (LSS_DN_SKIP & 2) ? make_uint4(k, q, t, 1u)
+                                  : *reinterpret_cast<const uint4*>(feat + ((size_t)bn * K + k) * HW + hw);
     }
 #pragma unroll
     for (int t = 0; t < kFeatIt; ++t) {
         const int i = threadIdx.x + t * kDn2Block;
-        const int k = i / (kDn2Pix / 8), p8 = (i % (kDn2Pix / 8)) * 8;
-        *reinterpret_cast<uint4*>(s_x + k * kDn2Row + p8 * 2) = fv[t];
+        const int k = i / (PX / 8), p8 = (i % (PX / 8)) * 8;
+        *reinterpret_cast<uint4*>(s_x + k * kRow + p8 * 2) = fv[t];
     }
     __syncthreads();
+    LSS_STAMP(tslot, 1);
     // ---- MFMA: two 16-pixel column tiles, K/32 steps; B fragments by transposed LDS reads
-    f32x4 acc[2] = {f32x4{}, f32x4{}};
-    const int g = lane >> 4, c16 = lane & 15, tq = c16 >> 2, tp = c16 & 3;
+    f32x4 acc[kTiles];
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t) acc[t] = f32x4{};
+    const int tq = c16 >> 2, tp = c16 & 3;
 #pragma unroll
     for (int s = 0; s < kSteps; ++s) {
-        if (32 * s >= K) break;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < kTiles; ++t) {
             // lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3 of a 4 x 16 block; lane c of
             // the group receives column c (pixel 16t + c), rows 0..3 (4 consecutive channels)
-            const unsigned char* base = s_x + (32 * s + 8 * g + tq) * kDn2Row + (16 * t + 4 * tp) * 2;
+            const unsigned char* base = s_x + (32 * s + 8 * g + tq) * kRow + (16 * t + 4 * tp) * 2;
             const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                 (__attribute__((address_space(3))) v4s*)(base));
             const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) v4s*)(base + 4 * kDn2Row));
+                (__attribute__((address_space(3))) v4s*)(base + 4 * kRow));
             const bf16x8 b = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], b, acc[t], 0, 0, 0);
         }
     }
     // C/D: column (pixel) = lane & 15, row (output) = 4 (lane >> 4) + i
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < kTiles; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int o = wave * 16 + 4 * g + i;
-            if (o < O) s_lg[o][16 * t + c16] = __bfloat162float(__float2bfloat16(acc[t][i] + __bfloat162float(bias[o])));
+            if (o < O) s_lg[o][16 * t + c16] = __bfloat162float(__float2bfloat16(acc[t][i] + bv[i]));
         }
     __syncthreads();
+    LSS_STAMP(tslot, 2);
     // ---- softmax over the D bins of each pixel: thread (part, p) covers bins part, part + 16, ...
-    constexpr int kParts = kDn2Block / kDn2Pix;
-    const int p = threadIdx.x % kDn2Pix, part = threadIdx.x / kDn2Pix;
+    constexpr int kParts = kDn2Block / PX;  // threads past kParts * PX sit the softmax out
+    const int p = threadIdx.x % PX, part = threadIdx.x / PX;
+    const bool sm = part < kParts;
     float m = -INFINITY;
-    for (int d = part; d < D; d += kParts) m = fmaxf(m, s_lg[d][p]);
-    s_red[0][part][p] = m;
+    for (int d = part; sm && d < D; d += kParts) m = fmaxf(m, s_lg[d][p]);
+    if (sm) s_red[0][part][p] = m;
     __syncthreads();
     m = s_red[0][0][p];
 #pragma unroll
     for (int j = 1; j < kParts; ++j) m = fmaxf(m, s_red[0][j][p]);
     float sum = 0.f;
-    for (int d = part; d < D; d += kParts) sum += expf(s_lg[d][p] - m);
-    s_red[1][part][p] = sum;
+    for (int d = part; sm && d < D; d += kParts) sum += expf(s_lg[d][p] - m);
+    if (sm) s_red[1][part][p] = sum;
     __syncthreads();
     sum = 0.f;
 #pragma unroll
     for (int j = 0; j < kParts; ++j) sum += s_red[1][j][p];
     const int q = q0 + p;
-    if (q < npix) {
+    if (sm && q < npix) {
         const int bn = q / HW, hw = q - bn * HW;
         float* dst = depth + (size_t)bn * D * HW + hw;
         for (int d = part; d < D; d += kParts) dst[(size_t)d * HW] = expf(s_lg[d][p] - m) / sum;
     }
-    for (int i = threadIdx.x; i < kDn2Pix * kC; i += kDn2Block) {
+    for (int i = threadIdx.x; i < PX * kC; i += kDn2Block) {
         const int pp = i / kC, c = i - pp * kC;
         if (q0 + pp < npix) ctx_t[(size_t)(q0 + pp) * kC + c] = __float2bfloat16(s_lg[D + c][pp]);
     }
+    LSS_STAMP(tslot, 3);
 }
 
 // 16 bytes of fp32 or bf16 row elements -> fp32.
@@ -814,20 +890,6 @@ struct SplatGeo {
 #endif
 #ifndef LSS_NO_DEPTH
 #define LSS_NO_DEPTH 0  // timing experiments only: 1 skips the depth-weight gathers (wrong output)
-#endif
-#ifndef LSS_TRACE
-#define LSS_TRACE 0  // diagnostics build: per-wave s_memrealtime stamps of the channels-last splat
-#endif
-#if LSS_TRACE
-// [wave slot][0: start, 1: after round trip 1, 2: after the first gather batch, 3: end, 4: kind | hw id]
-__device__ unsigned long long g_lss_trace[16384][5];
-#define LSS_STAMP(slot, i)                                                                                     \
-    do {                                                                                                       \
-        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                        \
-        if ((threadIdx.x & 63) == 0 && (slot) < 16384) g_lss_trace[(slot)][(i)] = t_;                          \
-    } while (0)
-#else
-#define LSS_STAMP(slot, i) do { } while (0)
 #endif
 #ifndef LSS_FWD_SKIP
 #define LSS_FWD_SKIP 0  // timing experiments only: 1 skips the chunks, 2 the zero fill (wrong output)
@@ -1689,14 +1751,19 @@ __global__ __launch_bounds__(kBlock) void k_bev_rows(const GT* __restrict__ dbev
     }
 }
 
-// Offset of cell k's gradient row: compact rows buffer, or the channels-last dbev itself.
+// Row index of cell k's gradient row: compact rows buffer, or the channels-last dbev itself
+// (-1 stays -1). Integer divisions: computed once per point, before any gather.
 template <bool NHWC>
-__device__ __forceinline__ size_t row_offset(int cell, const SplatGeo& sg) {
-    if (!NHWC) return (size_t)cell * kC;
+__device__ __forceinline__ int grad_row(int cell, const SplatGeo& sg) {
+    if (!NHWC || sg.Z == 1 || cell < 0) return cell;  // Z == 1: (b, xy) order is the cell order
     const int XY = sg.X * sg.Y;
     const int bz = cell / XY, xy = cell - bz * XY;
     const int b = bz / sg.Z, z = bz - b * sg.Z;
-    return (((size_t)b * XY + xy) * sg.Z + z) * kC;
+    return (b * XY + xy) * sg.Z + z;
+}
+template <bool NHWC>
+__device__ __forceinline__ size_t row_offset(int cell, const SplatGeo& sg) {
+    return (size_t)grad_row<NHWC>(cell, sg) * kC;
 }
 
 // One wave per pixel. The D gradient rows of the pixel's points are gathered into LDS with
@@ -1788,12 +1855,10 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd_reg(const GT* __restrict__
     if (q >= npix) return;  // wave-uniform
     const int bn = q / HW, hw = q - bn * HW;
     const size_t pbase = (size_t)bn * D * HW + hw;  // point (bn, d = 0, hw)
-    float my_depth = 0.f;
-    int my_cell = -1;
-    if (lane < D) {
-        my_depth = depth[pbase + (size_t)lane * HW];
-        my_cell = cell_of[pbase + (size_t)lane * HW];
-    }
+    const int dl_ = min(lane, D - 1);  // clamped, unconditional loads (see keep_if)
+    const float my_depth = keep_if(lane < D, depth[pbase + (size_t)dl_ * HW]);
+    int my_cell = cell_of[pbase + (size_t)dl_ * HW];
+    my_cell = lane < D ? grad_row<NHWC>(my_cell, sg) : -1;  // gradient row index (-1 stays -1)
     const int sub = lane / LPR, col = (lane % LPR) * EPL;
     float cx[EPL];
 #pragma unroll
@@ -1802,8 +1867,8 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd_reg(const GT* __restrict__
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const int cell = __shfl(my_cell, (k * RPI + sub) & 63, kWave);  // -1 beyond D
-        raw[k] = make_uint4(0u, 0u, 0u, 0u);
-        if (k * RPI < D && cell >= 0) raw[k] = *reinterpret_cast<const uint4*>(g + row_offset<NHWC>(cell, sg) + col);
+        // rows past D (cell -1) read row 0 (one line for the whole instruction) and are zeroed
+        raw[k] = keep_if(cell >= 0, *reinterpret_cast<const uint4*>(g + (size_t)max(cell, 0) * kC + col));
     }
     float dc[EPL];
 #pragma unroll
@@ -1852,6 +1917,13 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd_reg(const GT* __restrict__
 #ifndef LSS_BWD_REG
 #define LSS_BWD_REG 1  // 1: k_splat_bwd_reg (registers + shuffles), 0: k_splat_bwd (LDS staging)
 #endif
+#ifndef LSS_BWD_PPW
+#define LSS_BWD_PPW 1  // pixels per wave of k_splat_bwd_tile for bf16 gradients (2: twice the gathers in flight per
+                       // wave but 105 VGPRs, two blocks per CU: 12.2 us vs 10.3 us at c3)
+#endif
+#ifndef LSS_BWD_MIN_WAVES
+#define LSS_BWD_MIN_WAVES 5  // occupancy floor of k_splat_bwd_tile, bf16 rows (waves per SIMD; 70 VGPRs give 7 anyway)
+#endif
 #ifndef LSS_BWD_TILE
 #define LSS_BWD_TILE 1  // 1: k_splat_bwd_tile (pixel tiles, coalesced loads and stores) where the shape allows
 #endif
@@ -1866,8 +1938,8 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd_reg(const GT* __restrict__
 constexpr int kBwdWaves = 8;
 constexpr int kBwdBlock = kBwdWaves * kWave;
 
-template <typename GT, typename DT, typename CT, bool NHWC>
-__global__ __launch_bounds__(kBwdBlock) void k_splat_bwd_tile(const GT* __restrict__ g,
+template <typename GT, typename DT, typename CT, bool NHWC, int MAXD>  // MAXD: D <= MAXD (48 or 64)
+__global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? LSS_BWD_MIN_WAVES : 4) void k_splat_bwd_tile(const GT* __restrict__ g,
                                                               const int32_t* __restrict__ cell_of,
                                                               const float* __restrict__ depth,
                                                               const CT* __restrict__ ctx_t, int D, int HW, int npix,
@@ -1875,24 +1947,55 @@ __global__ __launch_bounds__(kBwdBlock) void k_splat_bwd_tile(const GT* __restri
     constexpr int EPL = 16 / sizeof(GT);  // row elements per 16-B lane load
     constexpr int LPR = kC / EPL;         // lanes per row
     constexpr int RPI = kWave / LPR;      // rows per wave-instruction
-    constexpr int NI = kWave / RPI;       // instructions for 64 rows
-    constexpr int PPW = sizeof(GT) == 2 ? 2 : 1;  // pixels per wave, all gathers in flight
+    constexpr int NI = MAXD / RPI;        // instructions for MAXD rows
+    constexpr int PPW = sizeof(GT) == 2 ? LSS_BWD_PPW : 1;  // pixels per wave, all gathers in flight
     constexpr int PX = kBwdWaves * PPW;           // pixels per block
-    __shared__ float s_dep[64][PX];
-    __shared__ int s_cell[64][PX];
-    __shared__ float s_ctx[PX][kC];
-    __shared__ float s_out[64 + kC][PX + 1];
+    __shared__ float s_dep[MAXD + 1][PX];  // + a spare row for the lanes past the end
+    __shared__ int s_cell[MAXD + 1][PX];
+    __shared__ float s_ctx[PX + 1][kC];  // + a spare tile for the lanes past the end
+    __shared__ float s_out[MAXD + kC][PX + 1];
     const int q0 = xcd_block() * PX;
     if (q0 >= npix) return;  // block-uniform
+    [[maybe_unused]] const int tslot = blockIdx.x * kBwdWaves + (threadIdx.x >> 6);  // LSS_TRACE builds only
+    LSS_STAMP(tslot, 0);
     const int bn = q0 / HW, hw0 = q0 - bn * HW;  // HW % PX == 0: the tile lies in one image
     const size_t pb = (size_t)bn * D * HW + hw0;
-    for (int i = threadIdx.x; i < D * PX; i += kBwdBlock) {
+    // Every load below is unconditional (clamped index; an out-of-range value is dropped at the LDS
+    // write or zeroed by a select), so the compiler issues them back to back: one round trip for the
+    // staging, one for the gathers.
+    constexpr int kCtx16 = PX * kC * (int)sizeof(CT) / 16;  // 16-B pieces of the tile's context rows
+    constexpr int kCE = 16 / (int)sizeof(CT);
+    static_assert(kCtx16 <= kBwdBlock, "one context piece per thread");
+    const uint4 craw = reinterpret_cast<const uint4*>(ctx_t + (size_t)q0 * kC)[min((int)threadIdx.x, kCtx16 - 1)];
+    constexpr int kStage = (MAXD * PX + kBwdBlock - 1) / kBwdBlock;
+    float dv[kStage];
+    int cv[kStage];
+#pragma unroll
+    for (int t = 0; t < kStage; ++t) {
+        const int i = min((int)threadIdx.x + t * kBwdBlock, D * PX - 1);
         const int d = i / PX, j = i - d * PX;
-        s_dep[d][j] = depth[pb + (size_t)d * HW + j];
-        s_cell[d][j] = cell_of[pb + (size_t)d * HW + j];
+        dv[t] = depth[pb + (size_t)d * HW + j];
+        cv[t] = cell_of[pb + (size_t)d * HW + j];
     }
-    for (int i = threadIdx.x; i < PX * kC; i += kBwdBlock) s_ctx[i / kC][i % kC] = to_f32(ctx_t[(size_t)q0 * kC + i]);
+#pragma unroll
+    for (int t = 0; t < kStage; ++t) cv[t] = grad_row<NHWC>(cv[t], sg);  // gradient row index, or -1
+    // LDS writes without branches either (a lane past the end writes the spare row 63 / tile PX)
+#pragma unroll
+    for (int t = 0; t < kStage; ++t) {
+        const int i = min((int)threadIdx.x + t * kBwdBlock, MAXD * PX - 1);
+        const int at = i < D * PX ? i : MAXD * PX + (i % PX);  // the spare row MAXD is never read
+        s_dep[at / PX][at % PX] = dv[t];
+        s_cell[at / PX][at % PX] = cv[t];
+    }
+    {
+        float f[kCE];
+        unpack16(craw, (const CT*)nullptr, f);
+        const int e0 = min((int)threadIdx.x, kCtx16) * kCE;  // kCtx16: the spare tile s_ctx[PX]
+#pragma unroll
+        for (int e = 0; e < kCE; ++e) s_ctx[(e0 + e) / kC][(e0 + e) % kC] = f[e];
+    }
     __syncthreads();
+    LSS_STAMP(tslot, 1);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = lane / LPR, col = (lane % LPR) * EPL;
     uint4 raw[PPW][NI];
@@ -1901,12 +2004,11 @@ __global__ __launch_bounds__(kBwdBlock) void k_splat_bwd_tile(const GT* __restri
         const int jj = wave * PPW + i;
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
-            const int r = k * RPI + sub;
-            raw[i][k] = make_uint4(0u, 0u, 0u, 0u);
-            if (k * RPI < D && r < D) {
-                const int cell = s_cell[r][jj];
-                if (cell >= 0) raw[i][k] = *reinterpret_cast<const uint4*>(g + row_offset<NHWC>(cell, sg) + col);
-            }
+            // rows past D repeat row D - 1 (same line, no extra traffic); their values are zeroed
+            const int r = min(k * RPI + sub, D - 1);
+            const int row = s_cell[r][jj];
+            const uint4 v = *reinterpret_cast<const uint4*>(g + (size_t)max(row, 0) * kC + col);
+            raw[i][k] = keep_if(k * RPI + sub < D && row >= 0, v);
         }
     }
 #pragma unroll
@@ -1954,12 +2056,27 @@ __global__ __launch_bounds__(kBwdBlock) void k_splat_bwd_tile(const GT* __restri
 #pragma unroll
             for (int e = 0; e < EPL; ++e) s_out[D + col + e][jj] = dc[e];
     }
+    LSS_STAMP(tslot, 2);
     __syncthreads();
+    // d_depthnet_out: 16-B runs of consecutive pixels of one channel (HW % PX == 0 keeps them aligned)
+    constexpr int kOE = 16 / (int)sizeof(DT);  // pixels per 16-B store
+    constexpr int kRuns = PX / kOE;
+    static_assert(PX % kOE == 0 && (MAXD + kC) * kRuns <= 2 * kBwdBlock, "two stores per thread at most");
     DT* dst = d_dn + (size_t)bn * (D + kC) * HW + hw0;
-    for (int i = threadIdx.x; i < (D + kC) * PX; i += kBwdBlock) {
-        const int ch = i / PX, j = i - ch * PX;
-        dst[(size_t)ch * HW + j] = from_f32<DT>(s_out[ch][j]);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int i = threadIdx.x + t * kBwdBlock;
+        if (i < (D + kC) * kRuns) {
+            const int ch = i / kRuns, j0 = (i - ch * kRuns) * kOE;
+            DT v[kOE];
+#pragma unroll
+            for (int e = 0; e < kOE; ++e) v[e] = from_f32<DT>(s_out[ch][j0 + e]);
+            uint4 u;
+            __builtin_memcpy(&u, v, 16);
+            *reinterpret_cast<uint4*>(dst + (size_t)ch * HW + j0) = u;
+        }
     }
+    LSS_STAMP(tslot, 3);
 }
 
 template <typename GT, bool NHWC>
@@ -2243,9 +2360,9 @@ int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, in
     const int HW = dims->H * dims->W;
     const long npix = (long)dims->B * dims->N * HW;
     if (npix >= INT_MAX) return LSS_EUNSUPPORTED;
-    if (LSS_DN_IMPL == 2 && K % 32 == 0 && HW % 8 == 0 && pos_of == nullptr) {
-        hipLaunchKernelGGL(k_depthnet_lift2, dim3(xcd_grid(grid_blocks(npix, kDn2Pix))), dim3(kDn2Block), 0,
-                           (hipStream_t)stream, (const bf16*)feat, (const bf16*)weight, (const bf16*)bias, K, dims->D,
+    if (LSS_DN_IMPL == 2 && K == 512 && HW % 8 == 0 && pos_of == nullptr) {  // up1's 512 channels
+        hipLaunchKernelGGL((k_depthnet_lift2<512, kDn2Pix>), dim3(xcd_grid(grid_blocks(npix, kDn2Pix))), dim3(kDn2Block), 0,
+                           (hipStream_t)stream, (const bf16*)feat, (const bf16*)weight, (const bf16*)bias, dims->D,
                            HW, (int)npix, depth, (bf16*)ctx_t);
         return launch_status();
     }
@@ -2392,13 +2509,19 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
     const bool nhwc = rows_layout == LSS_NHWC;
 #define LSS_BWD(GT, DT, CT)                                                                                       \
     do {                                                                                                          \
-        constexpr int px = kBwdWaves * (sizeof(GT) == 2 ? 2 : 1);                                                 \
+        constexpr int px = kBwdWaves * (sizeof(GT) == 2 ? LSS_BWD_PPW : 1);                                                 \
         const dim3 grt(xcd_grid(npix / px)), blt(kBwdBlock);                                                      \
-        if (LSS_BWD_TILE && HW % px == 0 && nhwc)                                                                 \
-            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, true>), grt, blt, 0, s, (const GT*)g, cell_of, depth, \
-                               (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
+        if (LSS_BWD_TILE && HW % px == 0 && nhwc && dims->D <= 48)                                                \
+            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, true, 48>), grt, blt, 0, s, (const GT*)g, cell_of,  \
+                               depth, (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);              \
+        else if (LSS_BWD_TILE && HW % px == 0 && nhwc)                                                            \
+            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, true, 64>), grt, blt, 0, s, (const GT*)g, cell_of,  \
+                               depth, (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);              \
+        else if (LSS_BWD_TILE && HW % px == 0 && dims->D <= 48)                                                   \
+            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, false, 48>), grt, blt, 0, s, (const GT*)g, cell_of, \
+                               depth, (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);              \
         else if (LSS_BWD_TILE && HW % px == 0)                                                                    \
-            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, false>), grt, blt, 0, s, (const GT*)g, cell_of,     \
+            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, false, 64>), grt, blt, 0, s, (const GT*)g, cell_of, \
                                depth, (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);              \
         else if (LSS_BWD_REG && nhwc)                                                                             \
             hipLaunchKernelGGL((k_splat_bwd_reg<GT, DT, CT, true>), gr, bl, 0, s, (const GT*)g, cell_of, depth,   \

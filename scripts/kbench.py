@@ -25,8 +25,9 @@ VARIANTS = {
     "merged": ["LSS_SPLAT_IMPL=1"],
     "merged_late": ["LSS_SPLAT_IMPL=1", "LSS_MERGED_ZERO_LATE=1"],
     "dn1": ["LSS_DN_IMPL=1"],               # round-1 depthnet lift
-    "agg2": ["LSS_GEOM_AGG=2"],             # geometry: one atomic per run of equal adjacent cells
     "bwd0": ["LSS_BWD_TILE=0"],             # round-1 splat bwd
+    "bwdppw1": ["LSS_BWD_PPW=1", "LSS_BWD_MIN_WAVES=5"],  # tiled bwd, one pixel per wave
+    "dnpx32": ["LSS_DN_PIX=32"],            # fused lift, 32-pixel blocks (264 blocks at B=8)
 }
 VARIANTS_R1 = {  # round-1 knobs of the two-role kernel (kept for reference; pass --r1-variants)
     "skip_chunks": ["LSS_SPLAT_IMPL=0", "LSS_FWD_SKIP=1"],  # zero units only (timing decomposition; wrong output)
