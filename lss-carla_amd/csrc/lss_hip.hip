@@ -1448,6 +1448,135 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     }
 }
 
+// ---- NCHW (the reference layout), version 2: one block = one tile of YT consecutive cells of a BEV
+// row (b, z, x, y0..y0 + YT), 4 waves = 4 * NG lane groups of LPR lanes (8 lanes x 16 B per context
+// row for bf16 rows, the NHWC chunk's gather shape: 8 rows per wave instruction). The tile's cells are
+// split over the groups at cell boundaries with the entries balanced; a group sums its cells one by one
+// in canonical order (acc = fma(w, x, acc) entry by entry, the association of k_splat_fwd, so both
+// kernels agree bit for bit), KU entries in flight per batch, and leaves each cell's row in an LDS
+// tile [channel][y] zeroed beforehand (empty cells stay zero). The block then writes the tile one
+// channel plane run at a time with 16-B stores.
+#ifndef LSS_NCHW_IMPL
+#define LSS_NCHW_IMPL 2  // NCHW splat: 1 k_splat_fwd (lane = channel), 2 k_splat_fwd_nchw2 (lane groups)
+#endif
+constexpr int kN2Waves = 4;
+constexpr int kN2Block = kN2Waves * kWave;
+
+template <bool FUSED, typename RT, typename OutT>
+__global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __restrict__ depth,
+                                                             const RT* __restrict__ rows_base,
+                                                             const int32_t* __restrict__ cell_start,
+                                                             const long long* __restrict__ sorted_key,
+                                                             const int32_t* __restrict__ sorted_row, SplatGeo sg,
+                                                             int ntiles, OutT* __restrict__ out) {
+    using RS = RowSlice<RT>;
+    constexpr int KU = 8;  // entries per batch of a group (<= LPR: lane j of the group fetches entry j's key)
+    static_assert(KU <= RS::LPR, "one lane per entry of a batch");
+    constexpr int NGB = kN2Waves * RS::NG;  // lane groups per block
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int s_start[kMaxYT + 1];
+    const int tile = xcd_block();  // consecutive tiles (one sample's rows) on one XCD, as the CSR build wrote them
+    if (tile >= ntiles) return;    // block-uniform (the grid is rounded up to a multiple of 8)
+    const int bzx = tile / sg.ntiles_y;
+    const int y0 = (tile - bzx * sg.ntiles_y) * sg.YT;
+    const int ny = min(sg.YT, sg.Y - y0);
+    const int x = bzx % sg.X, bz = bzx / sg.X;
+    const int cell0 = bzx * sg.Y + y0;
+    const int S = sg.YT + 4;  // LDS row stride (floats; 16-B aligned rows)
+    for (int i = threadIdx.x; i <= ny; i += kN2Block) s_start[i] = cell_start[cell0 + i];
+    __syncthreads();
+    const int s0 = s_start[0], s1 = s_start[ny];
+    const bool empty = s0 == s1;
+    if (!empty) {
+        for (int i = threadIdx.x * 4; i < kC * S; i += kN2Block * 4)
+            *reinterpret_cast<float4*>(lds + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int lane = threadIdx.x & 63;
+        const int grp = (threadIdx.x >> 6) * RS::NG + lane / RS::LPR;
+        const int j = lane % RS::LPR, col = j * RS::EPL;
+        // the group's cells [cb, ce): first cell whose start is >= the group's share of the entries
+        const int span = s1 - s0;
+        auto lower = [&](int t) {  // first y in [0, ny] with s_start[y] >= t
+            int lo = 0, hi = ny;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_start[mid] >= t) hi = mid;
+                else lo = mid + 1;
+            }
+            return lo;
+        };
+        const int cb = grp == 0 ? 0 : lower(s0 + (int)(((long)grp * span) / NGB));
+        const int ce = grp == NGB - 1 ? ny : lower(s0 + (int)(((long)(grp + 1) * span) / NGB));
+        __syncthreads();  // the tile is zeroed before any cell lands in it
+        const int eend = s_start[ce];
+        float acc[RS::EPL];
+#pragma unroll
+        for (int i = 0; i < RS::EPL; ++i) acc[i] = 0.f;
+        int cur = -1;
+        auto flush = [&]() {
+            float* dst = lds + (size_t)col * S + (cur - cell0);
+#pragma unroll
+            for (int i = 0; i < RS::EPL; ++i) dst[i * S] = acc[i];
+        };
+        const int gl0 = lane - j;  // the group's first lane
+        for (int e = s_start[cb]; e < eend; e += KU) {
+            // lane j < KU of the group: entry e + j's key, context row and depth weight (round trips 1, 2)
+            const int ej = min(e + min(j, KU - 1), eend - 1);
+            const long long k = sorted_key[ej];
+            const int pj = (int)(k & 0xFFFFFFFF), cj = (int)(k >> 32);
+            const int rj = FUSED ? sorted_row[ej] : pj;
+            const float wj = FUSED ? depth[pj] : 1.f;
+            uint4 v[KU];
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                const int r = __shfl(rj, gl0 + u, kWave);
+                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)r * kC + col);
+            }
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                const int c = __shfl(cj, gl0 + u, kWave);
+                const float w = __shfl(wj, gl0 + u, kWave);
+                if (e + u < eend) {
+                    if (c != cur) {
+                        if (cur >= 0) flush();
+#pragma unroll
+                        for (int i = 0; i < RS::EPL; ++i) acc[i] = 0.f;
+                        cur = c;
+                    }
+                    float xv[RS::EPL];
+                    unpack16(v[u], (const RT*)nullptr, xv);
+#pragma unroll
+                    for (int i = 0; i < RS::EPL; ++i) acc[i] = FUSED ? fmaf(w, xv[i], acc[i]) : __fadd_rn(acc[i], xv[i]);
+                }
+            }
+        }
+        if (cur >= 0) flush();
+        __syncthreads();
+    }
+    // the tile, channel plane by channel plane: (B, Z*C, X, Y), channel z*C + c
+    const size_t XY = (size_t)sg.X * sg.Y;
+    OutT* obase = out + (size_t)bz * kC * XY + (size_t)x * sg.Y + y0;
+    constexpr int VN = 16 / (int)sizeof(OutT);
+    if ((sg.Y % VN) == 0 && (ny % VN) == 0 && (y0 % VN) == 0) {
+        const int nq = ny / VN;
+        for (int i = threadIdx.x; i < kC * nq; i += kN2Block) {
+            const int c = i / nq, yv = (i - c * nq) * VN;
+            float vals[VN];
+#pragma unroll
+            for (int t = 0; t < VN; t += 4) {
+                const float4 f = empty ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                       : *reinterpret_cast<const float4*>(lds + (size_t)c * S + yv + t);
+                vals[t] = f.x; vals[t + 1] = f.y; vals[t + 2] = f.z; vals[t + 3] = f.w;
+            }
+            store_vec(obase + c * XY + yv, vals);
+        }
+    } else {
+        for (int i = threadIdx.x; i < kC * ny; i += kN2Block) {
+            const int c = i / ny, yy = i - c * ny;
+            obase[c * XY + yy] = from_f32<OutT>(empty ? 0.f : lds[(size_t)c * S + yy]);
+        }
+    }
+}
+
 template <bool FUSED, typename RT, typename OutT>
 __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const float* __restrict__ depth,
                                                            const float* __restrict__ sorted_depth,
@@ -2453,6 +2582,29 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
     if (sg.YT > kMaxYT) return LSS_EUNSUPPORTED;
     const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
     const size_t lds = (size_t)kC * (sg.YT + 4) * sizeof(float);
+    if (LSS_NCHW_IMPL == 2) {
+        const dim3 gr2(xcd_grid(nblocks)), bl2(kN2Block);
+#define LSS_SPLAT2(F, RT, T)                                                                                      \
+    do {                                                                                                          \
+        if (e0 || e1)                                                                                             \
+            hipExtLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T>), gr2, bl2, (uint32_t)lds, s, e0, e1, 0, depth,   \
+                                  (const RT*)rows, cell_start, sorted_key, sorted_row, sg, nblocks, (T*)out);     \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T>), gr2, bl2, lds, s, depth, (const RT*)rows,           \
+                               cell_start, sorted_key, sorted_row, sg, nblocks, (T*)out);                         \
+    } while (0)
+        if (out_dtype == LSS_F32) {
+            if (!fused) LSS_SPLAT2(false, float, float);
+            else if (ctx_bf16) LSS_SPLAT2(true, bf16, float);
+            else LSS_SPLAT2(true, float, float);
+        } else {
+            if (!fused) LSS_SPLAT2(false, float, bf16);
+            else if (ctx_bf16) LSS_SPLAT2(true, bf16, bf16);
+            else LSS_SPLAT2(true, float, bf16);
+        }
+#undef LSS_SPLAT2
+        return launch_status();
+    }
 #define LSS_SPLAT(F, RT, T)                                                                                       \
     do {                                                                                                          \
         if (e0 || e1)                                                                                             \

@@ -22,12 +22,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
-    "merged": ["LSS_SPLAT_IMPL=1"],
-    "merged_late": ["LSS_SPLAT_IMPL=1", "LSS_MERGED_ZERO_LATE=1"],
-    "dn1": ["LSS_DN_IMPL=1"],               # round-1 depthnet lift
+    "nchw1": ["LSS_NCHW_IMPL=1"],           # round-1 NCHW splat (lane = channel)
     "bwd0": ["LSS_BWD_TILE=0"],             # round-1 splat bwd
-    "bwdppw1": ["LSS_BWD_PPW=1", "LSS_BWD_MIN_WAVES=5"],  # tiled bwd, one pixel per wave
-    "dnpx32": ["LSS_DN_PIX=32"],            # fused lift, 32-pixel blocks (264 blocks at B=8)
 }
 VARIANTS_R1 = {  # round-1 knobs of the two-role kernel (kept for reference; pass --r1-variants)
     "skip_chunks": ["LSS_SPLAT_IMPL=0", "LSS_FWD_SKIP=1"],  # zero units only (timing decomposition; wrong output)
@@ -248,6 +244,7 @@ def main():
             res[f"{m} splat_fwd nhwc bf16 (sorted depth)"] = stamped(lib, bev_bf, _lib.NHWC, mode=m, sd=sdepth)
             res[f"{m} splat_fwd nhwc bf16 (f32 ctx)"] = stamped(lib, bev_bf, _lib.NHWC, ctx=ctx_f, mode=m)
         res["warm splat_fwd nchw f32"] = stamped(lib, bev_f, _lib.NCHW)
+        res["step splat_fwd nchw f32"] = stamped(lib, bev_f, _lib.NCHW, mode="step")
     # the timing modes above rewrote ctx_t (the "step" mode reruns the lift): fresh reference output
     fwd(lib, bev_bf, _lib.NHWC)()
     ref_out = bev_bf.clone()
@@ -276,6 +273,14 @@ def main():
             res[f"{m} splat_fwd nhwc bf16 [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m)
             res[f"{m} splat_fwd nhwc bf16 (sorted depth) [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m,
                                                                                sd=vsd)
+        # NCHW fp32 (the reference layout): output vs the product kernel, then timed
+        ref_f = bev_f.clone()
+        fwd(lib, ref_f, _lib.NCHW)()
+        fwd(vl, bev_f, _lib.NCHW, vcsr)()
+        if not torch.equal(bev_f, ref_f):
+            print(f"WARNING variant {name}: NCHW output differs from the product kernel", flush=True)
+        res[f"warm splat_fwd nchw f32 [{name}]"] = stamped(vl, bev_f, _lib.NCHW, vcsr)
+        res[f"step splat_fwd nchw f32 [{name}]"] = stamped(vl, bev_f, _lib.NCHW, vcsr, mode="step")
     rows = torch.empty(ncells * 64, device=dev)
     g_f = torch.randn(B, Z * 64, X, Y, device=dev)
     res["bev_rows nchw f32"] = named("bev_rows nchw f32", lambda: _lib.check(lib.lss_bev_rows(
