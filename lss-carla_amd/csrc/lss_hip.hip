@@ -894,7 +894,7 @@ struct SplatGeo {
 #ifndef LSS_FWD_SKIP
 #define LSS_FWD_SKIP 0  // timing experiments only: 1 skips the chunks, 2 the zero fill (wrong output)
 #endif
-constexpr int kMaxYT = 128;            // cells per NCHW tile (LDS sizing)
+constexpr int kMaxYT = LSS_YT_MAX > 128 ? LSS_YT_MAX : 128;  // cells per NCHW tile (LDS sizing)
 constexpr int kFwdWaves = 8;           // waves per NCHW tile
 constexpr int kFwdBlock = kFwdWaves * kWave;
 constexpr int kPrefetch = LSS_PREFETCH;  // context-row loads in flight per wave
@@ -1459,8 +1459,18 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 #ifndef LSS_NCHW_IMPL
 #define LSS_NCHW_IMPL 2  // NCHW splat: 1 k_splat_fwd (lane = channel), 2 k_splat_fwd_nchw2 (lane groups)
 #endif
-constexpr int kN2Waves = 4;
+#ifndef LSS_NCHW_WAVES
+#define LSS_NCHW_WAVES 4  // waves per NCHW tile block (more lane groups share a dense tile's entries)
+#endif
+constexpr int kN2Waves = LSS_NCHW_WAVES;
 constexpr int kN2Block = kN2Waves * kWave;
+#ifndef LSS_NCHW_SKIP
+#define LSS_NCHW_SKIP 0  // timing experiments only (wrong output): 1 writes every tile as zeros
+#endif
+#ifndef LSS_NCHW_KU
+#define LSS_NCHW_KU 8  // context rows in flight per lane group and batch (the next batch's keys follow them)
+#endif
+
 
 template <bool FUSED, typename RT, typename OutT>
 __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __restrict__ depth,
@@ -1470,9 +1480,9 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
                                                              const int32_t* __restrict__ sorted_row, SplatGeo sg,
                                                              int ntiles, OutT* __restrict__ out) {
     using RS = RowSlice<RT>;
-    constexpr int KU = 8;  // entries per batch of a group (<= LPR: lane j of the group fetches entry j's key)
-    static_assert(KU <= RS::LPR, "one lane per entry of a batch");
-    constexpr int NGB = kN2Waves * RS::NG;  // lane groups per block
+    constexpr int KU = LSS_NCHW_KU;               // entries per batch of a group
+    constexpr int KPL = (KU + RS::LPR - 1) / RS::LPR;  // keys fetched per lane per batch
+    constexpr int NGB = kN2Waves * RS::NG;        // lane groups per block
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_start[kMaxYT + 1];
     const int tile = xcd_block();  // consecutive tiles (one sample's rows) on one XCD, as the CSR build wrote them
@@ -1483,30 +1493,40 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
     const int x = bzx % sg.X, bz = bzx / sg.X;
     const int cell0 = bzx * sg.Y + y0;
     const int S = sg.YT + 4;  // LDS row stride (floats; 16-B aligned rows)
+    [[maybe_unused]] const int tslot = tile * kN2Waves + (threadIdx.x >> 6);  // LSS_TRACE builds only
+    LSS_STAMP(tslot, 0);
     for (int i = threadIdx.x; i <= ny; i += kN2Block) s_start[i] = cell_start[cell0 + i];
     __syncthreads();
+    LSS_STAMP(tslot, 1);
     const int s0 = s_start[0], s1 = s_start[ny];
-    const bool empty = s0 == s1;
+    const bool empty = LSS_NCHW_SKIP || s0 == s1;
     if (!empty) {
         for (int i = threadIdx.x * 4; i < kC * S; i += kN2Block * 4)
             *reinterpret_cast<float4*>(lds + i) = make_float4(0.f, 0.f, 0.f, 0.f);
         const int lane = threadIdx.x & 63;
-        const int grp = (threadIdx.x >> 6) * RS::NG + lane / RS::LPR;
+        const int wgrp = lane / RS::LPR;  // the lane's group inside the wave
         const int j = lane % RS::LPR, col = j * RS::EPL;
-        // the group's cells [cb, ce): first cell whose start is >= the group's share of the entries
+        // the group's cells [cb, ce): first cell whose start is >= the group's share of the entries.
+        // lower_bound(t) over the non-decreasing s_start[0..ny] = the count of starts below t: two
+        // ballots per target over the starts held one per lane (y <= 127; s_start[128] = s1 is never
+        // below a target), no dependent LDS reads
         const int span = s1 - s0;
-        auto lower = [&](int t) {  // first y in [0, ny] with s_start[y] >= t
-            int lo = 0, hi = ny;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (s_start[mid] >= t) hi = mid;
-                else lo = mid + 1;
-            }
-            return lo;
+        const int sa = s_start[min(lane, ny)], sb = s_start[min(lane + kWave, ny)];
+        const bool ina = lane <= ny, inb = lane + kWave <= ny;
+        auto lower = [&](int t) {
+            return __popcll(__ballot(ina && sa < t)) + __popcll(__ballot(inb && sb < t));
         };
-        const int cb = grp == 0 ? 0 : lower(s0 + (int)(((long)grp * span) / NGB));
-        const int ce = grp == NGB - 1 ? ny : lower(s0 + (int)(((long)(grp + 1) * span) / NGB));
-        __syncthreads();  // the tile is zeroed before any cell lands in it
+        int cb = 0, ce = ny;
+#pragma unroll
+        for (int q = 0; q < RS::NG; ++q) {  // every lane runs every group's search (ballots are wave-wide)
+            const int gq = (threadIdx.x >> 6) * RS::NG + q;
+            const int lo = gq == 0 ? 0 : lower(s0 + (int)(((long)gq * span) / NGB));
+            const int hi = gq == NGB - 1 ? ny : lower(s0 + (int)(((long)(gq + 1) * span) / NGB));
+            if (q == wgrp) {
+                cb = lo;
+                ce = hi;
+            }
+        }
         const int eend = s_start[ce];
         float acc[RS::EPL];
 #pragma unroll
@@ -1518,23 +1538,45 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
             for (int i = 0; i < RS::EPL; ++i) dst[i * S] = acc[i];
         };
         const int gl0 = lane - j;  // the group's first lane
-        for (int e = s_start[cb]; e < eend; e += KU) {
-            // lane j < KU of the group: entry e + j's key, context row and depth weight (round trips 1, 2)
-            const int ej = min(e + min(j, KU - 1), eend - 1);
-            const long long k = sorted_key[ej];
-            const int pj = (int)(k & 0xFFFFFFFF), cj = (int)(k >> 32);
-            const int rj = FUSED ? sorted_row[ej] : pj;
-            const float wj = FUSED ? depth[pj] : 1.f;
+        // keys of a batch: lane j of the group holds entries e + j + LPR * t, t < KPL (clamped; the
+        // clamped copies are never summed)
+        long long kk[KPL];
+        int rr[KPL];
+        auto fetch_keys = [&](int e) {
+#pragma unroll
+            for (int t = 0; t < KPL; ++t) {
+                const int ej = min(e + j + RS::LPR * t, eend - 1);
+                kk[t] = sorted_key[ej];
+                rr[t] = FUSED ? sorted_row[ej] : 0;
+            }
+        };
+        int e = s_start[cb];
+        if (e < eend) fetch_keys(e);  // in flight across the barrier
+        __syncthreads();  // the tile is zeroed before any cell lands in it
+        LSS_STAMP(tslot, 4);
+        for (; e < eend; e += KU) {
+            // this batch's depth weights and context-row slices (round trip 2), then the next batch's
+            // keys (round trip 1 of the next batch, in flight behind them: no extra wait)
+            float wt[KPL];
+            int cc[KPL];
+#pragma unroll
+            for (int t = 0; t < KPL; ++t) {
+                const int pt = (int)(kk[t] & 0xFFFFFFFF);
+                cc[t] = (int)(kk[t] >> 32);
+                wt[t] = FUSED ? depth[pt] : 1.f;
+                if (!FUSED) rr[t] = pt;
+            }
             uint4 v[KU];
 #pragma unroll
             for (int u = 0; u < KU; ++u) {
-                const int r = __shfl(rj, gl0 + u, kWave);
+                const int r = __shfl(rr[u / RS::LPR], gl0 + u % RS::LPR, kWave);
                 v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)r * kC + col);
             }
+            if (e + KU < eend) fetch_keys(e + KU);
 #pragma unroll
             for (int u = 0; u < KU; ++u) {
-                const int c = __shfl(cj, gl0 + u, kWave);
-                const float w = __shfl(wj, gl0 + u, kWave);
+                const int c = __shfl(cc[u / RS::LPR], gl0 + u % RS::LPR, kWave);
+                const float w = __shfl(wt[u / RS::LPR], gl0 + u % RS::LPR, kWave);
                 if (e + u < eend) {
                     if (c != cur) {
                         if (cur >= 0) flush();
@@ -1552,6 +1594,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
         if (cur >= 0) flush();
         __syncthreads();
     }
+    LSS_STAMP(tslot, 2);
     // the tile, channel plane by channel plane: (B, Z*C, X, Y), channel z*C + c
     const size_t XY = (size_t)sg.X * sg.Y;
     OutT* obase = out + (size_t)bz * kC * XY + (size_t)x * sg.Y + y0;
@@ -1575,6 +1618,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
             obase[c * XY + yy] = from_f32<OutT>(empty ? 0.f : lds[(size_t)c * S + yy]);
         }
     }
+    LSS_STAMP(tslot, 3);
 }
 
 template <bool FUSED, typename RT, typename OutT>
@@ -2582,7 +2626,7 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
     if (sg.YT > kMaxYT) return LSS_EUNSUPPORTED;
     const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
     const size_t lds = (size_t)kC * (sg.YT + 4) * sizeof(float);
-    if (LSS_NCHW_IMPL == 2) {
+    if (LSS_NCHW_IMPL == 2 && sg.YT <= 128) {
         const dim3 gr2(xcd_grid(nblocks)), bl2(kN2Block);
 #define LSS_SPLAT2(F, RT, T)                                                                                      \
     do {                                                                                                          \

@@ -245,6 +245,7 @@ def main():
             res[f"{m} splat_fwd nhwc bf16 (f32 ctx)"] = stamped(lib, bev_bf, _lib.NHWC, ctx=ctx_f, mode=m)
         res["warm splat_fwd nchw f32"] = stamped(lib, bev_f, _lib.NCHW)
         res["step splat_fwd nchw f32"] = stamped(lib, bev_f, _lib.NCHW, mode="step")
+        res["warm splat_fwd nchw f32 (f32 ctx)"] = stamped(lib, bev_f, _lib.NCHW, ctx=ctx_f)
     # the timing modes above rewrote ctx_t (the "step" mode reruns the lift): fresh reference output
     fwd(lib, bev_bf, _lib.NHWC)()
     ref_out = bev_bf.clone()
@@ -281,6 +282,7 @@ def main():
             print(f"WARNING variant {name}: NCHW output differs from the product kernel", flush=True)
         res[f"warm splat_fwd nchw f32 [{name}]"] = stamped(vl, bev_f, _lib.NCHW, vcsr)
         res[f"step splat_fwd nchw f32 [{name}]"] = stamped(vl, bev_f, _lib.NCHW, vcsr, mode="step")
+        res[f"warm splat_fwd nchw f32 (f32 ctx) [{name}]"] = stamped(vl, bev_f, _lib.NCHW, vcsr, ctx=ctx_f)
     rows = torch.empty(ncells * 64, device=dev)
     g_f = torch.randn(B, Z * 64, X, Y, device=dev)
     res["bev_rows nchw f32"] = named("bev_rows nchw f32", lambda: _lib.check(lib.lss_bev_rows(

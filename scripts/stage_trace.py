@@ -19,7 +19,8 @@ sys.path.insert(0, REPO)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("kernel", choices=["lift", "bwd", "geom"])
+    ap.add_argument("kernel", choices=["lift", "bwd", "geom", "nchw"])
+    ap.add_argument("--config", default="c3")
     ap.add_argument("--cold", type=int, default=1)
     ap.add_argument("--lib", default="trace", help="variants/<name>.so, a LSS_TRACE=1 build")
     a = ap.parse_args()
@@ -29,7 +30,7 @@ def main():
     l = _lib.open_library(os.path.join(REPO, "lss-carla_amd", "variants", a.lib + ".so"))
     l.lss_debug_trace.argtypes = [ct.c_void_p, ct.c_int]
     dev = torch.device("cuda:0")
-    cfg, gc, _ = syn.config_confs("c3")
+    cfg, gc, _ = syn.config_confs(a.config)
     B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
     rig = {k: v.to(dev) for k, v in syn.make_rig(B, N, fd).items()}
     frustum = ref.create_frustum(fd, gc["dbound"]).to(dev)
@@ -46,6 +47,9 @@ def main():
     bdn = torch.zeros(D + 64, device=dev, dtype=torch.bfloat16)
     gbev = torch.randn(B, Z * 64, X, Y, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     d_dn = torch.empty(B * N, D + 64, H, W, device=dev, dtype=torch.bfloat16)
+    dnf = syn.make_depthnet_out(B, N, D, H, W).to(dev)
+    ctxf = torch.empty(B * N * H * W, 64, device=dev)
+    bevf = torch.empty(B, Z * 64, X, Y, device=dev)
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
     pinv, kinv = ops.camera_inverses(rig["post_rots"], rig["intrins"], "device")
     ro, tr, pt = [t.float().contiguous() for t in (rig["rots"], rig["trans"], rig["post_trans"])]
@@ -64,6 +68,12 @@ def main():
             _lib.check(l.lss_geometry_cells(_lib.ptr(frustum), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv),
                                             _lib.ptr(pinv), _lib.ptr(pt), dims, g, None, _lib.ptr(cell_of),
                                             _lib.ptr(counts), _lib.ptr(slot), st), "geom")
+        elif a.kernel == "nchw":  # config 2's forward: fp32 context rows, fp32 NCHW BEV
+            _lib.check(l.lss_lift_prep(_lib.ptr(dnf), _lib.F32, dims, _lib.ptr(depth), _lib.ptr(ctxf), _lib.F32,
+                                       None, None, st), "lift")
+            _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctxf), _lib.F32, None, _lib.ptr(plan.cell_start),
+                                       _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), None, dims, g,
+                                       _lib.ptr(bevf), _lib.F32, _lib.NCHW, st, None, None), "fwd")
         elif a.kernel == "lift":
             _lib.check(l.lss_depthnet_lift(_lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims,
                                            _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, None, None, st), "lift")
@@ -76,7 +86,7 @@ def main():
     torch.cuda.synchronize()
     buf = np.zeros((16384, 5), dtype=np.uint64)
     _lib.check(l.lss_debug_trace(buf.ctypes.data, 16384), "trace")
-    t = buf[:, :4].astype(np.int64)
+    t = buf[:, :5].astype(np.int64)
     live = (t[:, 0] > 0) & (t[:, 3] > 0)
     t0 = t[live, 0].min()
     rel = (t - t0) / 100.0  # 100 MHz ticks -> us
@@ -89,6 +99,11 @@ def main():
     print("stage (t1-t0)        ", q(rel[live, 1] - rel[live, 0]))
     print("compute (t2-t1)      ", q(rel[live, 2] - rel[live, 1]))
     print("tail (t3-t2)         ", q(rel[live, 3] - rel[live, 2]))
+    if a.kernel == "nchw":  # stamp 4: after the tile zeroing + group search barrier (occupied tiles)
+        occ = live & (t[:, 4] > 0)
+        print("setup (t4-t1)        ", q(rel[occ, 4] - rel[occ, 1]))
+        print("sums (t2-t4)         ", q(rel[occ, 2] - rel[occ, 4]))
+        print(f"occupied tiles: {occ.sum()} of {live.sum()} waves")
     print("total (t3-t0)        ", q(rel[live, 3] - rel[live, 0]))
     print("end                  ", q(rel[live, 3]))
     for tt in np.arange(0, rel[live, 3].max() + 0.5, 0.5):
