@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 10
+#define LSS_ABI_VERSION 11
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -99,6 +99,18 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
                   const int32_t* cell_count, int32_t ncells, const lss_dims_t* dims,
                   int32_t* cell_start, long long* sorted_key, int32_t* sorted_row, int32_t* pos_of,
                   void* scratch, lss_stream_t stream);
+
+/* lss_csr_build with a persistent workspace: the same outputs, bit for bit, in three kernels
+ * instead of four and no count memset -- a single-pass scan (decoupled look-back between blocks,
+ * bounded spins) and a scatter that also re-zeroes the scan's state and cell_count for the next
+ * call. Contract: `workspace` (lss_csr_workspace_bytes(ncells)) is zero-filled before its first
+ * use; cell_count is zero-filled before the first lss_geometry_cells / lss_cells_from_geom that
+ * counts into it; every call leaves both zero-filled again. One call at a time per workspace. */
+size_t lss_csr_workspace_bytes(int32_t ncells);
+int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime,
+                     int32_t* cell_count, int32_t ncells, const lss_dims_t* dims,
+                     int32_t* cell_start, long long* sorted_key, int32_t* sorted_row, int32_t* pos_of,
+                     void* scratch, void* workspace, lss_stream_t stream);
 
 /* Lift, part 1 (CamEncode.get_depth_dist + layout, src/models.py:49-59, 192-202):
  * depth (B*N, D, H, W) fp32 = softmax over D of depthnet_out[:, :D];

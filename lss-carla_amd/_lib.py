@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(_HERE, "liblss_hip.so")
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 class Dims(ctypes.Structure):
@@ -55,6 +55,8 @@ SIGNATURES = {
     "lss_cells_from_geom": (ctypes.c_int, [_p, _i32, _i32, _GRID, _p, _p, _p, _p]),
     "lss_csr_scratch_bytes": (ctypes.c_size_t, [_i32, _i32]),
     "lss_csr_build": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p, _p]),
+    "lss_csr_workspace_bytes": (ctypes.c_size_t, [_i32]),
+    "lss_csr_build_ws": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p, _p, _p]),
     "lss_lift_prep": (ctypes.c_int, [_p, _i32, _DIMS, _p, _p, _i32, _p, _p, _p]),
     "lss_depthnet_lift": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p, _p, _p]),
     "lss_splat_fwd": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _p, _p, _p]),

@@ -367,6 +367,107 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ 
     if (cell >= 0) key_out[cell_start[cell] + slot_of[p]] = ((long long)cell << 32) | (unsigned)p;
 }
 
+// ---- single-pass scan (lss_csr_build_ws): one launch in place of k_scan_partials + k_scan_apply.
+// Blocks take logical indices from a ticket counter in dispatch order, so a block only ever waits
+// for blocks that are already running (no residency assumption). Block k publishes its aggregate,
+// then wave 0 looks back over its predecessors' 8-byte {status, value} granules, 64 at a time,
+// up to the nearest inclusive prefix, and publishes its own inclusive prefix. Granules are written
+// with agent-scope (sc1, write-through) atomic stores and polled with agent-scope atomic loads --
+// the cross-XCD hand-off form of the R2 recipe (cdna_hip_programming.md, Guideline 16). Spins are
+// bounded: after kScanSpinLimit polls a block stops waiting, counts the predecessor as empty and
+// bumps the sticky timeout word (wrong output, never a hang). The scatter re-zeroes the ticket and
+// the granules after the scan, so every call starts from zeros.
+constexpr unsigned kScanSpinLimit = 1u << 22;
+struct ScanWs {  // lss_csr_workspace_bytes: [ticket, timeouts, pad x2][granule x nb]
+    unsigned ticket, timeouts, pad0, pad1;
+};
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restrict__ cnt, int ncells,
+                                                        ScanWs* __restrict__ ws, int32_t* __restrict__ cell_start) {
+    __shared__ int s_wave[32];
+    __shared__ int s_total;
+    __shared__ int s_blk, s_prefix;
+    unsigned long long* gran = reinterpret_cast<unsigned long long*>(ws + 1);
+    if (threadIdx.x == 0) s_blk = (int)atomicAdd(&ws->ticket, 1u);
+    __syncthreads();
+    const int lb = s_blk;
+    const int nb = (ncells + kScanItems - 1) / kScanItems;
+    const int base = lb * kScanItems + threadIdx.x * 4;
+    int c[4];
+    int v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        c[i] = (base + i < ncells) ? cnt[base + i] : 0;
+        v += c[i];
+    }
+    const int excl = block_exclusive_scan_1024(v, s_wave, &s_total);
+    if (threadIdx.x < kWave) {
+        const int lane = threadIdx.x;
+        const int agg = s_total;
+        int prefix = 0;
+        if (lb == 0) {
+            if (lane == 0) st_agent(&gran[0], (2ull << 32) | (unsigned)agg);
+        } else {
+            if (lane == 0) st_agent(&gran[lb], (1ull << 32) | (unsigned)agg);
+            for (int j = lb - 1;; j -= kWave) {
+                const int jj = j - lane;  // lanes past block 0 read as an inclusive prefix of 0
+                unsigned long long x = 2ull << 32;
+                for (unsigned spins = 0;; ++spins) {
+                    x = jj >= 0 ? ld_agent(&gran[jj]) : (2ull << 32);
+                    if (__all(x != 0ull)) break;
+                    if (spins >= kScanSpinLimit) {
+                        if (lane == 0) atomicAdd(&ws->timeouts, 1u);
+                        if (x == 0ull) x = 2ull << 32;  // give up: an empty inclusive prefix
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                const unsigned long long pm = __ballot((x >> 32) == 2ull);
+                const int upto = pm ? __builtin_ctzll(pm) : kWave - 1;  // nearest inclusive prefix
+                int val = lane <= upto ? (int)(unsigned)x : 0;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) val += __shfl_xor(val, o, kWave);
+                prefix += val;
+                if (pm) break;
+            }
+            if (lane == 0) st_agent(&gran[lb], (2ull << 32) | (unsigned)(prefix + agg));
+        }
+        if (lane == 0) s_prefix = prefix;
+    }
+    __syncthreads();
+    int run = s_prefix + excl;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (base + i < ncells) cell_start[base + i] = run;
+        run += c[i];
+    }
+    if (lb == nb - 1 && threadIdx.x == 0) cell_start[ncells] = s_prefix + s_total;
+}
+
+// k_scatter plus the reset for the next call: the scan's ticket and granules and the cell counts
+// (nothing reads them after the scan). The grid covers max(nprime, ncells) threads.
+__global__ __launch_bounds__(kBlock) void k_scatter_ws(const int32_t* __restrict__ cell_of,
+                                                       const int32_t* __restrict__ slot_of, int nprime,
+                                                       const int32_t* __restrict__ cell_start,
+                                                       long long* __restrict__ key_out, int32_t* __restrict__ cnt,
+                                                       int ncells, ScanWs* __restrict__ ws) {
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (t < nprime) {
+        const int cell = cell_of[t];
+        if (cell >= 0) key_out[cell_start[cell] + slot_of[t]] = ((long long)cell << 32) | (unsigned)t;
+    }
+    if (t < ncells) cnt[t] = 0;
+    const int nb = (ncells + kScanItems - 1) / kScanItems;
+    if (t < nb) reinterpret_cast<unsigned long long*>(ws + 1)[t] = 0ull;
+    if (t == 0) ws->ticket = 0u;
+}
+
 // The sorted list is cut into 64-entry chunks; the wave of chunk w owns the cells that START
 // in [64w, 64w + 64). It reads entries [64w - 1, 64w + 128): the owned cells (<= 64 entries each;
 // a longer last cell is flagged `big`) and the entry before the chunk (a cell that started earlier).
@@ -2498,6 +2599,38 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
     hipLaunchKernelGGL(k_scan_apply, dim3(xcd_grid(nb)), dim3(1024), 0, s, cell_count, ncells, partial, cell_start);
     hipLaunchKernelGGL(k_scatter, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0, s, cell_of, slot_of, nprime,
                        cell_start, tmp_key);
+    const int nchunks = (nprime + kWave - 1) / kWave;
+    hipLaunchKernelGGL(k_csr_canon, dim3(xcd_grid(grid_blocks(nchunks, kBlock / kWave))), dim3(kBlock), 0, s, tmp_key,
+                       cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row, cell_of, pos_of);
+    return launch_status();
+}
+
+size_t lss_csr_workspace_bytes(int32_t ncells) {
+    const size_t nb = (size_t)((ncells + kScanItems - 1) / kScanItems);
+    return sizeof(ScanWs) + sizeof(unsigned long long) * nb;
+}
+
+int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, int32_t* cell_count,
+                     int32_t ncells, const lss_dims_t* dims, int32_t* cell_start, long long* sorted_key,
+                     int32_t* sorted_row, int32_t* pos_of, void* scratch, void* workspace, lss_stream_t stream) {
+    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !sorted_row || !scratch || !workspace ||
+        nprime <= 0 || ncells <= 0)
+        return LSS_EINVAL;
+    int DHW = nprime, HW = nprime;  // no dims: the row of point p is p (per-point rows)
+    if (dims != nullptr) {
+        if (!dims_ok(dims)) return LSS_EINVAL;
+        DHW = dims->D * dims->H * dims->W;
+        HW = dims->H * dims->W;
+        if ((long)dims->B * dims->N * DHW != nprime) return LSS_EINVAL;
+    }
+    const int nb = (ncells + kScanItems - 1) / kScanItems;
+    const size_t poff = ((sizeof(int32_t) * (size_t)(nb + 1)) + 255) & ~(size_t)255;  // as lss_csr_build
+    long long* tmp_key = reinterpret_cast<long long*>(static_cast<char*>(scratch) + poff);
+    ScanWs* ws = static_cast<ScanWs*>(workspace);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_scan_lookback, dim3(nb), dim3(1024), 0, s, cell_count, ncells, ws, cell_start);
+    hipLaunchKernelGGL(k_scatter_ws, dim3(grid_blocks(std::max(nprime, ncells), kBlock)), dim3(kBlock), 0, s, cell_of,
+                       slot_of, nprime, cell_start, tmp_key, cell_count, ncells, ws);
     const int nchunks = (nprime + kWave - 1) / kWave;
     hipLaunchKernelGGL(k_csr_canon, dim3(xcd_grid(grid_blocks(nchunks, kBlock / kWave))), dim3(kBlock), 0, s, tmp_key,
                        cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row, cell_of, pos_of);

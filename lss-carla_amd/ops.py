@@ -162,8 +162,47 @@ class SplatPlan:
         return B * N * D * H * W
 
 
-def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev):
-    """Counting sort into the canonical CSR (lss_csr_build): cell_start, sorted_key, sorted_row."""
+class _PlanWorkspace:
+    """Persistent per-shape state of the plan (lss_csr_build_ws): the cell counts and the single-pass
+    scan's workspace, zero-filled once here and left zero-filled by every lss_csr_build_ws, so a
+    plan needs no count memset and no scan reset. One plan at a time per shape and device (the
+    model builds one per forward, on one stream). Created outside graph capture (the eager warm-up
+    steps); a plan captured before its workspace exists takes the stateless path."""
+
+    def __init__(self):
+        self._ws = {}
+
+    def get(self, dev: torch.device, ncells: int, nprime: int, create: bool):
+        key = (dev.index, ncells, nprime)
+        w = self._ws.get(key)
+        if w is None and create:
+            lib = _lib.load()
+            w = (torch.zeros(ncells, device=dev, dtype=torch.int32),
+                 torch.zeros(int(lib.lss_csr_workspace_bytes(ncells)), device=dev, dtype=torch.uint8),
+                 torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8))
+            self._ws[key] = w
+        return w
+
+    def clear(self):
+        self._ws.clear()
+
+
+PLAN_WS = _PlanWorkspace()
+USE_PLAN_WS = True  # False: a count memset + lss_csr_build (two-kernel scan) per plan
+
+
+def _plan_counts(dev: torch.device, ncells: int, nprime: int):
+    """(counts, workspace) for one plan: the persistent zero-filled pair, or fresh zeros and None."""
+    if USE_PLAN_WS:
+        capturing = dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
+        w = PLAN_WS.get(dev, ncells, nprime, create=not capturing)
+        if w is not None:
+            return w[0], w
+    return torch.zeros(ncells, device=dev, dtype=torch.int32), None
+
+
+def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None):
+    """Counting sort into the canonical CSR (lss_csr_build[_ws]): cell_start, sorted_key, sorted_row."""
     lib = _lib.load()
     B, N, D, H, W = dims
     nprime = B * N * D * H * W
@@ -171,6 +210,13 @@ def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev):
     sorted_key = torch.empty(nprime, device=dev, dtype=torch.int64)
     sorted_row = torch.empty(nprime, device=dev, dtype=torch.int32)
     pos_of = torch.empty(nprime, device=dev, dtype=torch.int32) if SORTED_DEPTH else None
+    if ws is not None:
+        _, workspace, scratch = ws
+        _lib.check(lib.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
+                                        make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key),
+                                        _lib.ptr(sorted_row), _lib.ptr(pos_of), _lib.ptr(scratch),
+                                        _lib.ptr(workspace), _lib.stream_handle(dev)), "lss_csr_build_ws")
+        return cell_start, sorted_key, sorted_row, pos_of
     scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
     _lib.check(lib.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
                                  make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key), _lib.ptr(sorted_row),
@@ -196,9 +242,9 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
     fr, ro, tr, pt = _f32c(frustum), _f32c(rots), _f32c(trans), _f32c(post_trans)
     cell_of = torch.empty(nprime, device=dev, dtype=torch.int32)
     geom = torch.empty(B, N, D, H, W, 3, device=dev, dtype=torch.float32) if want_geom else None
-    counts = slot_of = None
+    counts = slot_of = ws = None
     if want_csr:
-        counts = torch.zeros(ncells, device=dev, dtype=torch.int32)
+        counts, ws = _plan_counts(dev, ncells, nprime)
         slot_of = torch.empty(nprime, device=dev, dtype=torch.int32)
     dims = make_dims(B, N, D, H, W)
     g = grid.c_struct()
@@ -208,7 +254,7 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
     cell_start = sorted_key = sorted_row = pos_of = None
     if want_csr:
         cell_start, sorted_key, sorted_row, pos_of = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells,
-                                                                dev)
+                                                                dev, ws)
     return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom, pos_of)
 
 
@@ -221,12 +267,13 @@ def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
     ncells = grid.ncells(B)
     gm = _f32c(geom)
     cell_of = torch.empty(nprime, device=dev, dtype=torch.int32)
-    counts = torch.zeros(ncells, device=dev, dtype=torch.int32)
+    counts, ws = _plan_counts(dev, ncells, nprime)
     slot_of = torch.empty(nprime, device=dev, dtype=torch.int32)
     _lib.check(lib.lss_cells_from_geom(_lib.ptr(gm), nprime, nprime // B, grid.c_struct(), _lib.ptr(cell_of),
                                        _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)),
                "lss_cells_from_geom")
-    cell_start, sorted_key, sorted_row, pos_of = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev)
+    cell_start, sorted_key, sorted_row, pos_of = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev,
+                                                            ws)
     return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, None, pos_of)
 
 

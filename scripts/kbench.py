@@ -149,6 +149,20 @@ def main():
             counts.zero_()
             geom()
             csr()
+        wsb = torch.zeros(int(l.lss_csr_workspace_bytes(ncells)), device=dev, dtype=torch.uint8)
+        counts_ws = torch.zeros(ncells, device=dev, dtype=torch.int32)
+
+        def plan_ws():  # persistent zero-filled counts + look-back scan workspace (what ops uses)
+            _lib.check(l.lss_geometry_cells(_lib.ptr(frustum), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv),
+                                            _lib.ptr(pinv), _lib.ptr(pt), dims, g, None, _lib.ptr(cell_of),
+                                            _lib.ptr(counts_ws), _lib.ptr(slot), st()), "geom")
+            _lib.check(l.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot), nprime, _lib.ptr(counts_ws), ncells, dims,
+                                          _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), _lib.ptr(po), _lib.ptr(scr),
+                                          _lib.ptr(wsb), st()), "csr_ws")
+        res[f"geometry+csr_build_ws (no memset){tag}"] = named("csr_build", plan_ws)
+        plan_ws()
+        if not (torch.equal(cs, plan.cell_start) and torch.equal(sk, plan.sorted_key)):
+            print(f"WARNING {tag}: workspace CSR differs from the product plan", flush=True)
         res[f"memset counts{tag}"] = named("memset counts", lambda: counts.zero_())
         res[f"memset+geometry_cells{tag}"] = named("geometry_cells", geom_only)
         res[f"memset+geometry+csr_build{tag}"] = named("csr_build", plan3)

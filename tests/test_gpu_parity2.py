@@ -270,3 +270,34 @@ def test_all_points_in_one_cell(layout):
     bev.backward(gd)
     want = ref.lift_splat_backward_fp64(dn.numpy(), geom.numpy(), gup.numpy(), dx, bx, nx, D, 64)
     np.testing.assert_allclose(dnd.grad.cpu().numpy(), want, rtol=1e-4, atol=ATOL)
+
+
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_single_pass_scan_matches_two_kernel_csr(name):
+    """lss_csr_build_ws (look-back scan, persistent workspace) == lss_csr_build bit for bit, over
+    several consecutive calls (the workspace and counts must come back zero-filled each time); c5
+    has 313 scan blocks, so the look-back crosses several 64-block windows."""
+    lib = _lib.load()
+    cfg, gc, _ = syn.config_confs(name)
+    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
+    frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
+    grid = ops.GridSpec.from_conf(gc)
+    ncells = grid.ncells(B)
+    for it in range(3):
+        rig = _dev(syn.make_rig(B, N, fd, seed=it))
+        old, ops.USE_PLAN_WS = ops.USE_PLAN_WS, False
+        try:
+            want = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")
+        finally:
+            ops.USE_PLAN_WS = old
+        got = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")
+        torch.cuda.synchronize()
+        assert torch.equal(got.cell_start, want.cell_start)
+        assert torch.equal(got.sorted_key, want.sorted_key)
+        kept = int(want.cell_start[-1])
+        assert torch.equal(got.sorted_row[:kept], want.sorted_row[:kept])
+        counts, ws, _ = ops.PLAN_WS.get(DEV, ncells, want.nprime, create=False)
+        assert int(counts.abs().sum()) == 0, "counts not re-zeroed"
+        words = ws.view(torch.int32).cpu().numpy()
+        assert words[1] == 0, f"look-back spin timeouts: {words[1]}"
+        assert not words[4:].any() and words[0] == 0, "scan state not re-zeroed"
