@@ -77,6 +77,15 @@ int lss_geometry_cells(const float* frustum, const float* rots, const float* tra
                        float* out_geom, int32_t* cell_of, int32_t* cell_count, int32_t* slot_of,
                        lss_stream_t stream);
 
+/* lss_geometry_cells with the frustum given by its axes: axes = [xs (W) | ys (H) | ds (D)] fp32,
+ * the 1-D tensors create_frustum broadcasts (src/models.py:157-168: frustum[d, h, w] =
+ * (xs[w], ys[h], ds[d])). Same outputs, bit for bit, as lss_geometry_cells on that frustum. */
+int lss_geometry_cells_axes(const float* axes, const float* rots, const float* trans,
+                            const float* kinv, const float* pinv, const float* post_trans,
+                            const lss_dims_t* dims, const lss_grid_t* grid, float* out_geom,
+                            int32_t* cell_of, int32_t* cell_count, int32_t* slot_of,
+                            lss_stream_t stream);
+
 /* Quantise a given (Nprime, 3) fp32 geometry (voxel_pooling(geom_feats, x) boundary,
  * src/models.py:204-223). Same outputs as lss_geometry_cells; points_per_batch =
  * Nprime / B (src/models.py:214). */

@@ -52,6 +52,7 @@ SIGNATURES = {
     "lss_event_record": (ctypes.c_int, [_p, _p]),
     "lss_camera_inverse": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p]),
     "lss_geometry_cells": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _p, _p, _p, _p]),
+    "lss_geometry_cells_axes": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _p, _p, _p, _p]),
     "lss_cells_from_geom": (ctypes.c_int, [_p, _i32, _i32, _GRID, _p, _p, _p, _p]),
     "lss_csr_scratch_bytes": (ctypes.c_size_t, [_i32, _i32]),
     "lss_csr_build": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p, _p]),

@@ -242,11 +242,16 @@ __device__ __forceinline__ void geometry_point(const float* __restrict__ frustum
     }
 }
 
+// AXES: the frustum given as its three axes -- xs[W], ys[H], ds[D] -- instead of the (D, H, W, 3)
+// tensor: create_frustum builds it as the broadcast of exactly these 1-D tensors (src/models.py:
+// 157-168), so point (d, h, w) = (xs[w], ys[h], ds[d]) bit for bit; 71 floats read through the
+// caches instead of 12 B per point from HBM.
+template <bool AXES>
 __global__ __launch_bounds__(kBlock) void k_geometry_cells(
     const float* __restrict__ frustum, const float* __restrict__ rots, const float* __restrict__ trans,
     const float* __restrict__ kinv, const float* __restrict__ pinv, const float* __restrict__ post_trans,
-    int N, int DHW, int nprime, lss_grid_t g, float* __restrict__ out_geom, int32_t* __restrict__ cell_of,
-    int32_t* __restrict__ cell_count, int32_t* __restrict__ slot_of) {
+    int N, int DHW, int HW, int W, int nprime, lss_grid_t g, float* __restrict__ out_geom,
+    int32_t* __restrict__ cell_of, int32_t* __restrict__ cell_count, int32_t* __restrict__ slot_of) {
     LSS_STAMP(blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6), 0);
     const int p0 = blockIdx.x * kBlock + threadIdx.x;
     const bool live = p0 < nprime;
@@ -255,7 +260,16 @@ __global__ __launch_bounds__(kBlock) void k_geometry_cells(
     const int f = p - cam * DHW;
     const int b = cam / N;
     float e[3];
-    geometry_point(frustum, rots, trans, kinv, pinv, post_trans, cam, f, e);
+    if (AXES) {
+        const int d = f / HW, r = f - d * HW, h = r / W, w = r - h * W;
+        const float* xs = frustum;
+        const float* ys = frustum + W;
+        const float* ds = ys + HW / W;
+        const float fr[3] = {xs[w], ys[h], ds[d]};
+        geometry_point(fr, rots, trans, kinv, pinv, post_trans, cam, 0, e);
+    } else {
+        geometry_point(frustum, rots, trans, kinv, pinv, post_trans, cam, f, e);
+    }
     if (out_geom != nullptr && live) {
         out_geom[3 * (size_t)p + 0] = e[0];
         out_geom[3 * (size_t)p + 1] = e[1];
@@ -2557,9 +2571,25 @@ int lss_geometry_cells(const float* frustum, const float* rots, const float* tra
     const long DHW = (long)dims->D * dims->H * dims->W;
     const long nprime = (long)dims->B * dims->N * DHW;
     if (nprime >= INT_MAX) return LSS_EUNSUPPORTED;
-    hipLaunchKernelGGL(k_geometry_cells, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0, (hipStream_t)stream,
-                       frustum, rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW, (int)nprime, *grid, out_geom,
-                       cell_of, cell_count, slot_of);
+    hipLaunchKernelGGL(k_geometry_cells<false>, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, frustum, rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW,
+                       dims->H * dims->W, dims->W, (int)nprime, *grid, out_geom, cell_of, cell_count, slot_of);
+    return launch_status();
+}
+
+int lss_geometry_cells_axes(const float* axes, const float* rots, const float* trans, const float* kinv,
+                            const float* pinv, const float* post_trans, const lss_dims_t* dims,
+                            const lss_grid_t* grid, float* out_geom, int32_t* cell_of, int32_t* cell_count,
+                            int32_t* slot_of, lss_stream_t stream) {
+    if (!dims_ok(dims) || !grid_ok(grid) || !axes || !rots || !trans || !kinv || !pinv || !post_trans || !cell_of)
+        return LSS_EINVAL;
+    if (cell_count && !slot_of) return LSS_EINVAL;
+    const long DHW = (long)dims->D * dims->H * dims->W;
+    const long nprime = (long)dims->B * dims->N * DHW;
+    if (nprime >= INT_MAX) return LSS_EUNSUPPORTED;
+    hipLaunchKernelGGL(k_geometry_cells<true>, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, axes, rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW,
+                       dims->H * dims->W, dims->W, (int)nprime, *grid, out_geom, cell_of, cell_count, slot_of);
     return launch_status();
 }
 

@@ -224,6 +224,34 @@ def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None):
     return cell_start, sorted_key, sorted_row, pos_of
 
 
+_AXES_CACHE = {}
+
+
+def frustum_axes(frustum: torch.Tensor) -> Optional[torch.Tensor]:
+    """[xs (W) | ys (H) | ds (D)] if `frustum` (D, H, W, 3) is the broadcast of its three axes -- as
+    create_frustum builds it (src/models.py:157-168) -- else None (lss_geometry_cells_axes reads
+    71 floats instead of the 4 MB tensor). Checked once per tensor version, outside graph capture."""
+    key = (frustum.data_ptr(), frustum._version, tuple(frustum.shape), str(frustum.device))
+    if key in _AXES_CACHE:
+        return _AXES_CACHE[key]
+    if frustum.is_cuda and torch.cuda.is_current_stream_capturing():
+        return None
+    with torch.no_grad():
+        fr = frustum.float()
+        xs, ys, ds = fr[0, 0, :, 0], fr[0, :, 0, 1], fr[:, 0, 0, 2]
+        sep = (torch.equal(fr[..., 0], xs.expand_as(fr[..., 0])) and
+               torch.equal(fr[..., 1], ys[:, None].expand_as(fr[..., 1])) and
+               torch.equal(fr[..., 2], ds[:, None, None].expand_as(fr[..., 2])))
+        axes = torch.cat([xs, ys, ds]).contiguous() if sep else None
+    if len(_AXES_CACHE) > 16:
+        _AXES_CACHE.clear()
+    _AXES_CACHE[key] = axes
+    return axes
+
+
+USE_FRUSTUM_AXES = True
+
+
 def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, post_trans, grid: GridSpec,
                       inverse: str = "host", want_geom: bool = False, want_csr: bool = True,
                       inverses: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> SplatPlan:
@@ -248,9 +276,11 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
         slot_of = torch.empty(nprime, device=dev, dtype=torch.int32)
     dims = make_dims(B, N, D, H, W)
     g = grid.c_struct()
-    _lib.check(lib.lss_geometry_cells(_lib.ptr(fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv),
-                                      _lib.ptr(pt), dims, g, _lib.ptr(geom), _lib.ptr(cell_of), _lib.ptr(counts),
-                                      _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
+    axes = frustum_axes(frustum) if USE_FRUSTUM_AXES else None
+    geom_fn = lib.lss_geometry_cells_axes if axes is not None else lib.lss_geometry_cells
+    _lib.check(geom_fn(_lib.ptr(axes if axes is not None else fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv),
+                       _lib.ptr(pinv), _lib.ptr(pt), dims, g, _lib.ptr(geom), _lib.ptr(cell_of), _lib.ptr(counts),
+                       _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
     cell_start = sorted_key = sorted_row = pos_of = None
     if want_csr:
         cell_start, sorted_key, sorted_row, pos_of = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells,

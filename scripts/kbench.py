@@ -159,7 +159,17 @@ def main():
             _lib.check(l.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot), nprime, _lib.ptr(counts_ws), ncells, dims,
                                           _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), _lib.ptr(po), _lib.ptr(scr),
                                           _lib.ptr(wsb), st()), "csr_ws")
+        axes = ops.frustum_axes(frustum)
+
+        def plan_ws_axes():  # + the frustum as its three axes (what ops uses for create_frustum's frustum)
+            _lib.check(l.lss_geometry_cells_axes(_lib.ptr(axes), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv),
+                                                 _lib.ptr(pinv), _lib.ptr(pt), dims, g, None, _lib.ptr(cell_of),
+                                                 _lib.ptr(counts_ws), _lib.ptr(slot), st()), "geom")
+            _lib.check(l.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot), nprime, _lib.ptr(counts_ws), ncells, dims,
+                                          _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), _lib.ptr(po), _lib.ptr(scr),
+                                          _lib.ptr(wsb), st()), "csr_ws")
         res[f"geometry+csr_build_ws (no memset){tag}"] = named("csr_build", plan_ws)
+        res[f"geometry_axes+csr_build_ws (no memset){tag}"] = named("csr_build", plan_ws_axes)
         plan_ws()
         if not (torch.equal(cs, plan.cell_start) and torch.equal(sk, plan.sorted_key)):
             print(f"WARNING {tag}: workspace CSR differs from the product plan", flush=True)

@@ -301,3 +301,29 @@ def test_single_pass_scan_matches_two_kernel_csr(name):
         words = ws.view(torch.int32).cpu().numpy()
         assert words[1] == 0, f"look-back spin timeouts: {words[1]}"
         assert not words[4:].any() and words[0] == 0, "scan state not re-zeroed"
+
+
+@pytest.mark.parametrize("name", ["c1", "c3", "c5"])
+def test_frustum_axes_geometry_bit_exact(name):
+    """lss_geometry_cells_axes (the frustum's three axes) == lss_geometry_cells (the full tensor):
+    geometry, voxel ids and counts bit for bit."""
+    cfg, gc, _ = syn.config_confs(name)
+    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
+    frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
+    assert ops.frustum_axes(frustum) is not None
+    grid = ops.GridSpec.from_conf(gc)
+    rig = _dev(syn.make_rig(B, N, fd, seed=5))
+    plans = []
+    for use in (False, True):
+        old, ops.USE_FRUSTUM_AXES = ops.USE_FRUSTUM_AXES, use
+        try:
+            plans.append(ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host", want_geom=True))
+        finally:
+            ops.USE_FRUSTUM_AXES = old
+    a, b = plans
+    assert torch.equal(a.geom, b.geom) and torch.equal(a.cell_of, b.cell_of)
+    assert torch.equal(a.cell_start, b.cell_start) and torch.equal(a.sorted_key, b.sorted_key)
+    # a frustum that is not a broadcast of its axes keeps the full-tensor path
+    bent = frustum.clone()
+    bent[1, 2, 3, 0] += 0.25
+    assert ops.frustum_axes(bent) is None
