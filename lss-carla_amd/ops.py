@@ -249,7 +249,7 @@ def frustum_axes(frustum: torch.Tensor) -> Optional[torch.Tensor]:
     return axes
 
 
-USE_FRUSTUM_AXES = True
+USE_FRUSTUM_AXES = False  # measured: the two index divisions cost more than the 4 MB of frustum reads (11.2 vs 10.3 us)
 
 
 def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, post_trans, grid: GridSpec,
