@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--inverse", default="host", choices=["host", "device"],
                     help="host: torch.inverse on the CPU (the reference's; bit-exact ids), device: fp64 kernel")
     ap.add_argument("--fuse-depthnet", type=int, default=1, help="depthnet 1x1 conv inside the lift kernel (MFMA)")
+    ap.add_argument("--plan-side-stream", type=int, default=0,
+                    help="build the plan (geometry + CSR) on a side stream, concurrent with the trunk")
     ap.add_argument("--graph", type=int, default=1,
                     help="replay the step as HIP graphs (fwd+bwd, clip+Adam) with the gradient all-reduce "
                          "between them; 0 = eager (DDP for N>1)")
@@ -280,6 +282,7 @@ def build_model(args, dev, gc, dac):
     model.bev_layout = args.bev_layout
     model.inverse = args.inverse
     model.fuse_depthnet = bool(args.fuse_depthnet)
+    model.plan_side_stream = bool(args.plan_side_stream)
     if args.bev_layout == "nhwc":
         model.bevencode.to(memory_format=torch.channels_last)
     if args.trunk_channels_last:
@@ -456,7 +459,8 @@ def main():
                        "global_batch": world * B, "parallelism": f"dp{world}", "bev_layout": args.bev_layout,
                        "inverse": args.inverse, "fuse_depthnet": bool(args.fuse_depthnet),
                        "depthwise": args.dw_impl, "batchnorm": "hip" if args.hip_bn else "miopen",
-                       "step": "hipgraph" if args.graph else "eager", "flat_params": bool(args.flat_params)},
+                       "step": "hipgraph" if args.graph else "eager", "flat_params": bool(args.flat_params),
+                       "plan_side_stream": bool(args.plan_side_stream)},
             "roofline": {"kernel": "lss_splat_fwd", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,

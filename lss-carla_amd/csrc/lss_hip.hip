@@ -382,8 +382,8 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ 
 }
 
 // ---- single-pass scan (lss_csr_build_ws): one launch in place of k_scan_partials + k_scan_apply.
-// Block k waits only for blocks j < k, dispatched before it (ncells / 4096 blocks of 1024 threads:
-// 79 at c3, 313 at c5 -- all resident at once on 256 CUs x 2). Block k publishes its aggregate,
+// Blocks take logical indices from a ticket counter in start order, so block k only waits for
+// blocks j < k that are already running (no residency assumption). Block k publishes its aggregate,
 // then wave 0 looks back over its predecessors' 8-byte {status, value} granules, 64 at a time,
 // up to the nearest inclusive prefix, and publishes its own inclusive prefix. Granules are written
 // with agent-scope (sc1, write-through) atomic stores and polled with agent-scope atomic loads --
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ 
 // the granules after the scan, so every call starts from zeros.
 constexpr unsigned kScanSpinLimit = 1u << 22;
 #ifndef LSS_SCAN_TICKET
-#define LSS_SCAN_TICKET 0
+#define LSS_SCAN_TICKET 1  // 0: logical index = blockIdx (safe only when no other kernel holds CUs)
 #endif
 struct ScanWs {  // lss_csr_workspace_bytes: [ticket, timeouts, pad x2][granule x nb]
     unsigned ticket, timeouts, pad0, pad1;
@@ -411,9 +411,8 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
     __shared__ int s_total;
     __shared__ int s_prefix;
     unsigned long long* gran = reinterpret_cast<unsigned long long*>(ws + 1);
-    // Logical index = dispatch order. LSS_SCAN_TICKET=1 takes it from a ticket counter instead (a
-    // block then only waits for blocks already running, whatever the dispatcher does), at the price
-    // of one more device-wide round trip before the counts are read.
+    // Logical index from a ticket counter: a block then only ever waits for blocks that are already
+    // running, whatever else holds the CUs (the plan may run beside the trunk on another stream).
     int lb = blockIdx.x;
     if (LSS_SCAN_TICKET) {
         __shared__ int s_blk;

@@ -161,6 +161,10 @@ class SplatPlan:
         B, N, D, H, W = self.dims
         return B * N * D * H * W
 
+    def tensors(self):
+        return [t for t in (self.cell_of, self.cell_start, self.sorted_key, self.sorted_row, self.geom, self.pos_of)
+                if t is not None]
+
 
 class _PlanWorkspace:
     """Persistent per-shape state of the plan (lss_csr_build_ws): the cell counts and the single-pass
