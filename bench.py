@@ -48,6 +48,7 @@ os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(REPO, "tuning", "m
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+FORCE_PG = os.environ.get("LSS_BENCH_FORCE_PG", "0") == "1"  # rehearse the N>1 collectives on one GPU
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "LSS fwd+bwd frames/sec at B=8, 6×128×352, D=41 → 200×200 BEV; 1/2/4/8 GPU"
 
@@ -75,11 +76,17 @@ def parse():
     ap.add_argument("--inverse", default="host", choices=["host", "device"],
                     help="host: torch.inverse on the CPU (the reference's; bit-exact ids), device: fp64 kernel")
     ap.add_argument("--fuse-depthnet", type=int, default=1, help="depthnet 1x1 conv inside the lift kernel (MFMA)")
+    ap.add_argument("--sorted-depth", type=int, default=0,
+                    help="the CSR build writes each point's sorted position and the lift writes the depth weights "
+                         "in CSR order, so the channels-last splat reads them contiguously")
     ap.add_argument("--plan-side-stream", type=int, default=0,
                     help="build the plan (geometry + CSR) on a side stream, concurrent with the trunk")
     ap.add_argument("--graph", type=int, default=1,
                     help="replay the step as HIP graphs (fwd+bwd, clip+Adam) with the gradient all-reduce "
                          "between them; 0 = eager (DDP for N>1)")
+    ap.add_argument("--overlap-all-reduce", type=int, default=1,
+                    help="N>1: one flat master per backward group (BevEncode, trunk head, trunk), each all-reduced "
+                         "from its gradient hook on a side stream inside the captured backward")
     ap.add_argument("--flat-params", type=int, default=1,
                     help="trainable parameters as one fp32 master tensor with one bf16 working copy per step")
     ap.add_argument("--profile-steps", type=int, default=8,
@@ -128,6 +135,13 @@ def setup_dist(args):
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif FORCE_PG:
+        # one-GPU rehearsal of the N>1 step: a world-size-1 RCCL group, collectives issued anyway
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     else:
         torch.cuda.set_device(0)
     return world, rank, torch.device("cuda", local if world > 1 else 0)
@@ -283,6 +297,8 @@ def build_model(args, dev, gc, dac):
     model.inverse = args.inverse
     model.fuse_depthnet = bool(args.fuse_depthnet)
     model.plan_side_stream = bool(args.plan_side_stream)
+    from lss_carla_amd import ops
+    ops.SORTED_DEPTH = bool(args.sorted_depth)
     if args.bev_layout == "nhwc":
         model.bevencode.to(memory_format=torch.channels_last)
     if args.trunk_channels_last:
@@ -337,6 +353,10 @@ class FwdStep:
 def main():
     args = parse()
     maybe_launch_ranks(args)
+    # stdout carries exactly one line, the JSON result: anything else written to fd 1 from here on
+    # (RCCL's version banner, library chatter) goes to stderr
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     from lss_carla_amd import synthetic as syn
@@ -351,7 +371,7 @@ def main():
     world, rank, dev = setup_dist(args)
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     from lss_carla_amd import ops, parallel
-    from lss_carla_amd.flat_params import FlatParams
+    from lss_carla_amd.flat_params import FlatParams, FlatParamGroups, lss_backward_groups
     from lss_carla_amd.train_step import TrainStep
     import lss_carla_amd as L
 
@@ -379,16 +399,22 @@ def main():
             # one process per GPU without DDP: identical replicas, one flat gradient all-reduce
             parallel.broadcast_state(model)
             parallel.freeze_unused(model)
-            flat = FlatParams(model, cast_dtype=amp_dtype) if args.flat_params else None
+            overlap = bool(args.overlap_all_reduce) and (world > 1 or FORCE_PG)
+            if args.flat_params and overlap:
+                flat = FlatParamGroups(model, lss_backward_groups(), cast_dtype=amp_dtype)
+            elif args.flat_params:
+                flat = FlatParams(model, cast_dtype=amp_dtype)
+        overlap = bool(args.overlap_all_reduce) and (world > 1 or FORCE_PG) and flat is not None
         if flat is not None:
-            fwd, params = flat.bind(model), [flat.master]
+            fwd, params = flat.bind(model), (flat.masters if overlap else [flat.master])
         else:
             fwd = model if (args.graph or world == 1) else parallel.make_data_parallel(model, dev)
             params = [p for p in model.parameters() if p.requires_grad]
         loss_fn = L.SimpleLoss(2.13).to(dev)
         opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-7, fused=True, capturable=bool(args.graph))
         step = TrainStep(fwd, inputs, labels, loss_fn, opt, params, all_reduce=bool(args.graph or args.flat_params),
-                         amp_dtype=amp_dtype, max_grad_norm=5.0, pre_step=pre_step)
+                         amp_dtype=amp_dtype, max_grad_norm=5.0, pre_step=pre_step, overlap_all_reduce=overlap,
+                         force_collectives=FORCE_PG)
     else:
         step = FwdStep(model, inputs, pre_step)
     t_w = time.perf_counter()
@@ -400,7 +426,21 @@ def main():
 
     if args.graph:
         # eager warm-up on a side stream (MIOpen find, optimizer state), capture, 2 untimed replays
-        step.capture(warmup=max(args.warmup, 2), on_warmup=first)
+        try:
+            step.capture(warmup=max(args.warmup, 2), on_warmup=first)
+        except RuntimeError as e:
+            if not getattr(step, "overlap", False):
+                raise
+            # the collectives inside the capture failed: one flat all-reduce between the graphs instead
+            # (every rank runs the same code, so every rank takes this branch)
+            log(f"[rank {rank}] captured all-reduce failed ({e}); falling back to the serial all-reduce")
+            torch.cuda.synchronize()
+            flat = FlatParams(model, cast_dtype=amp_dtype)
+            params = [flat.master]
+            opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-7, fused=True, capturable=True)
+            step = TrainStep(flat.bind(model), inputs, labels, loss_fn, opt, params, all_reduce=True,
+                             amp_dtype=amp_dtype, max_grad_norm=5.0, pre_step=pre_step, force_collectives=FORCE_PG)
+            step.capture(warmup=2)
         for _ in range(2):
             step()
     else:
@@ -460,7 +500,10 @@ def main():
                        "inverse": args.inverse, "fuse_depthnet": bool(args.fuse_depthnet),
                        "depthwise": args.dw_impl, "batchnorm": "hip" if args.hip_bn else "miopen",
                        "step": "hipgraph" if args.graph else "eager", "flat_params": bool(args.flat_params),
-                       "plan_side_stream": bool(args.plan_side_stream)},
+                       "plan_side_stream": bool(args.plan_side_stream), "sorted_depth": bool(args.sorted_depth),
+                       "all_reduce": ("overlapped with backward (3 groups, captured)" if getattr(step, "overlap", False)
+                                      else "one flat all-reduce between the graphs" if (world > 1 or FORCE_PG)
+                                      else None)},
             "roofline": {"kernel": "lss_splat_fwd", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
@@ -476,8 +519,8 @@ def main():
             log(f"[rank 0] CPU baseline in {time.perf_counter() - t_c:.1f} s")
         else:
             res["cpu_baseline"] = None
-        print(json.dumps(res), flush=True)
-    if world > 1:
+        os.write(result_fd, (json.dumps(res) + "\n").encode())
+    if world > 1 or FORCE_PG:
         dist.destroy_process_group()
 
 

@@ -860,12 +860,15 @@ constexpr int kDn2Block = kDn2Waves * kWave;
 #define LSS_DN_IMPL 2  // 1: k_depthnet_lift (32x32x16, weights streamed from L2), 2: k_depthnet_lift2
 #endif
 
-template <int K, int PX>  // input channels (compile-time: straight-line code, every load up front), pixels per block
+template <int K, int PX, bool SD>  // input channels (compile-time: straight-line code, every load up front),
+                                   // pixels per block, SD: also write the weights in CSR order (pos_of)
 __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __restrict__ feat,
                                                               const bf16* __restrict__ weight,
                                                               const bf16* __restrict__ bias, int D, int HW,
                                                               int npix, float* __restrict__ depth,
-                                                              bf16* __restrict__ ctx_t) {
+                                                              bf16* __restrict__ ctx_t,
+                                                              const int32_t* __restrict__ pos_of,
+                                                              float* __restrict__ sorted_depth) {
     static_assert(K % 32 == 0 && K <= kDnMaxK, "K steps of 32 staged in LDS");
     static_assert(PX % 16 == 0, "16-pixel MFMA column tiles");
     constexpr int kRow = PX * 2 + 8;  // LDS bytes per channel row (+8: spread the banks, 8-B aligned)
@@ -882,6 +885,20 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
     const int O = D + kC;
     [[maybe_unused]] const int tslot = blockIdx.x * kDn2Waves + wave;  // LSS_TRACE builds only
     LSS_STAMP(tslot, 0);
+    // the CSR positions of this thread's softmax outputs (SD), in flight with everything else
+    constexpr int kParts = kDn2Block / PX;  // threads past kParts * PX sit the softmax out
+    constexpr int kPerPart = (64 + kParts - 1) / kParts;  // D <= 64 (D + C <= kDnMaxO)
+    const int p = threadIdx.x % PX, part = threadIdx.x / PX;
+    const bool sm = part < kParts;
+    int at[SD ? kPerPart : 1];
+    if (SD) {
+        const int qc = min(q0 + p, npix - 1), bnc = qc / HW, hwc = qc - bnc * HW;
+#pragma unroll
+        for (int i = 0; i < kPerPart; ++i) {
+            const int d = min(part + kParts * i, D - 1);
+            at[i] = pos_of[((size_t)bnc * D + d) * HW + hwc];
+        }
+    }
     // ---- loads: this wave's weight rows (A fragments) and the block's feature tile, all in flight
     const int arow = wave * 16 + (lane & 15);
     const int kq = 8 * (lane >> 4);  // k offset of the lane's 8 elements inside a 32-wide K step
@@ -949,9 +966,6 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
     __syncthreads();
     LSS_STAMP(tslot, 2);
     // ---- softmax over the D bins of each pixel: thread (part, p) covers bins part, part + 16, ...
-    constexpr int kParts = kDn2Block / PX;  // threads past kParts * PX sit the softmax out
-    const int p = threadIdx.x % PX, part = threadIdx.x / PX;
-    const bool sm = part < kParts;
     float m = -INFINITY;
     for (int d = part; sm && d < D; d += kParts) m = fmaxf(m, s_lg[d][p]);
     if (sm) s_red[0][part][p] = m;
@@ -970,7 +984,15 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
     if (sm && q < npix) {
         const int bn = q / HW, hw = q - bn * HW;
         float* dst = depth + (size_t)bn * D * HW + hw;
-        for (int d = part; d < D; d += kParts) dst[(size_t)d * HW] = expf(s_lg[d][p] - m) / sum;
+#pragma unroll
+        for (int i = 0; i < kPerPart; ++i) {
+            const int d = part + kParts * i;
+            if (d < D) {
+                const float v = expf(s_lg[d][p] - m) / sum;
+                dst[(size_t)d * HW] = v;
+                if (SD && at[SD ? i : 0] >= 0) sorted_depth[at[SD ? i : 0]] = v;  // the weight at its CSR position
+            }
+        }
     }
     for (int i = threadIdx.x; i < PX * kC; i += kDn2Block) {
         const int pp = i / kC, c = i - pp * kC;
@@ -2705,10 +2727,15 @@ int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, in
     const int HW = dims->H * dims->W;
     const long npix = (long)dims->B * dims->N * HW;
     if (npix >= INT_MAX) return LSS_EUNSUPPORTED;
-    if (LSS_DN_IMPL == 2 && K == 512 && HW % 8 == 0 && pos_of == nullptr) {  // up1's 512 channels
-        hipLaunchKernelGGL((k_depthnet_lift2<512, kDn2Pix>), dim3(xcd_grid(grid_blocks(npix, kDn2Pix))), dim3(kDn2Block), 0,
-                           (hipStream_t)stream, (const bf16*)feat, (const bf16*)weight, (const bf16*)bias, dims->D,
-                           HW, (int)npix, depth, (bf16*)ctx_t);
+    if (LSS_DN_IMPL == 2 && K == 512 && HW % 8 == 0) {  // up1's 512 channels
+        if (pos_of)
+            hipLaunchKernelGGL((k_depthnet_lift2<512, kDn2Pix, true>), dim3(xcd_grid(grid_blocks(npix, kDn2Pix))),
+                               dim3(kDn2Block), 0, (hipStream_t)stream, (const bf16*)feat, (const bf16*)weight,
+                               (const bf16*)bias, dims->D, HW, (int)npix, depth, (bf16*)ctx_t, pos_of, sorted_depth);
+        else
+            hipLaunchKernelGGL((k_depthnet_lift2<512, kDn2Pix, false>), dim3(xcd_grid(grid_blocks(npix, kDn2Pix))),
+                               dim3(kDn2Block), 0, (hipStream_t)stream, (const bf16*)feat, (const bf16*)weight,
+                               (const bf16*)bias, dims->D, HW, (int)npix, depth, (bf16*)ctx_t, nullptr, nullptr);
         return launch_status();
     }
     hipLaunchKernelGGL(k_depthnet_lift, dim3(xcd_grid(grid_blocks(npix, kDnPix))), dim3(kBlock), 0, (hipStream_t)stream,

@@ -87,8 +87,12 @@ def _gather(dst_views, grads, buf) -> None:
 
 
 class FlatParams:
-    def __init__(self, model: nn.Module, cast_dtype=torch.bfloat16):
+    def __init__(self, model: nn.Module, cast_dtype=torch.bfloat16, prefixes=None):
+        """prefixes: only the parameters whose dotted names start with one of these (a group of
+        FlatParamGroups); None: every trainable parameter."""
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        if prefixes is not None:
+            named = [(n, p) for n, p in named if any(n == pre or n.startswith(pre + ".") for pre in prefixes)]
         if not named:
             raise ValueError("FlatParams: no trainable parameters")
         for n, p in named:
@@ -126,3 +130,50 @@ class FlatParams:
     def views_of(self, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
         """Per-parameter views (the original shapes/strides) of a flat tensor laid out like master."""
         return dict(zip(self.names16 + self.names32, _views(flat, self.like16 + self.like32)))
+
+
+class FlatParamGroups:
+    """Several FlatParams over disjoint parameter groups, run as one module: one fp32 master (and one
+    gradient) per group. A group's gradient is complete as soon as the backward has passed all of its
+    parameters, so groups listed in the order the backward finishes them (the BEV encoder first, the
+    trunk's early blocks last) let TrainStep all-reduce each one while the backward continues."""
+
+    def __init__(self, model: nn.Module, groups, cast_dtype=torch.bfloat16):
+        trainable = [n for n, p in model.named_parameters() if p.requires_grad]
+        taken = set()
+        self.groups = []
+        for prefixes in groups:
+            names = [n for n in trainable if n not in taken and any(n == pre or n.startswith(pre + ".") for pre in prefixes)]
+            if names:
+                taken.update(names)
+                self.groups.append(FlatParams(model, cast_dtype=cast_dtype, prefixes=names))
+        rest = [n for n in trainable if n not in taken]
+        if rest:
+            self.groups.append(FlatParams(model, cast_dtype=cast_dtype, prefixes=rest))
+
+    @property
+    def masters(self) -> List[nn.Parameter]:
+        return [g.master for g in self.groups]
+
+    def views(self, grads: bool = False) -> Dict[str, torch.Tensor]:
+        """name -> view of the masters (or of their gradients)."""
+        out = {}
+        for g in self.groups:
+            out.update(g.views_of(g.master.grad if grads else g.master.detach()))
+        return out
+
+    def bind(self, model: nn.Module):
+        def run(*args, **kwargs):
+            tensors = {}
+            for g in self.groups:
+                tensors.update(g.tensors())
+            return torch.func.functional_call(model, tensors, args, kwargs, strict=False)
+        return run
+
+
+def lss_backward_groups(prefix: str = "") -> list:
+    """LiftSplatShoot's parameters in the order the backward completes them: BevEncode, then the
+    camera encoder's head (up1, depthnet) with the trunk's last blocks, then (the remainder group
+    FlatParamGroups adds) the rest of the trunk. `prefix`: the model's name inside a wrapper."""
+    late = [f"{prefix}camencode.trunk._blocks.{i}" for i in range(11, 16)]
+    return [[f"{prefix}bevencode"], [f"{prefix}camencode.up1", f"{prefix}camencode.depthnet"] + late]

@@ -15,7 +15,7 @@ import torch.multiprocessing as mp
 
 import lss_carla_amd as L
 from lss_carla_amd import parallel
-from lss_carla_amd.flat_params import FlatParams
+from lss_carla_amd.flat_params import FlatParams, FlatParamGroups, lss_backward_groups
 from lss_carla_amd.train_step import TrainStep
 from lss_carla_amd import synthetic as syn
 
@@ -178,33 +178,53 @@ def test_flat_params_match_autocast_gradients():
     assert torch.equal(net[0].bias.detach(), flat.views_of(flat.master.detach())["0.bias"])
 
 
-def _train_step(model, seed, world_reduce):
-    """One TrainStep (flat fp32 master, SimpleLoss, backward, all-reduce, clip 5.0, Adam) on `model`."""
+def _train_step(model, seed, world_reduce, overlap=False):
+    """One TrainStep (flat fp32 master, SimpleLoss, backward, all-reduce, clip 5.0, Adam) on `model`;
+    overlap: one master per backward group, each all-reduced from its gradient hook."""
     parallel.freeze_unused(model)
     wrapped = _CpuLSS(model)
-    flat = FlatParams(wrapped, cast_dtype=None)
+    if overlap:
+        flat = FlatParamGroups(wrapped, lss_backward_groups("model."), cast_dtype=None)
+        params = flat.masters
+    else:
+        flat = FlatParams(wrapped, cast_dtype=None)
+        params = [flat.master]
     imgs, rig, labels = _batch(seed)
-    opt = torch.optim.Adam([flat.master], lr=1e-3, weight_decay=1e-7)
+    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-7)
     inputs = (imgs, rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"])
-    step = TrainStep(flat.bind(wrapped), inputs, labels, L.SimpleLoss(2.13), opt, [flat.master],
-                     all_reduce=world_reduce, amp_dtype=None, max_grad_norm=5.0)
+    step = TrainStep(flat.bind(wrapped), inputs, labels, L.SimpleLoss(2.13), opt, params,
+                     all_reduce=world_reduce, amp_dtype=None, max_grad_norm=5.0, overlap_all_reduce=overlap)
     return step, flat
 
 
-def _worker_trainstep(rank, world, port, outdir):
+def _worker_trainstep(rank, world, port, outdir, overlap=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(2)
     parallel.init_from_env("gloo")
     m = _model()
     parallel.broadcast_state(m)
-    step, flat = _train_step(m, seed=20 + rank, world_reduce=True)
-    assert step.world == world
-    loss = step.eager()
+    step, flat = _train_step(m, seed=20 + rank, world_reduce=True, overlap=overlap)
+    assert step.world == world and step.overlap == overlap
+    if overlap:  # the summed gradients the hooks produced, then the update
+        loss = step.forward_backward()
+        grads = {n.removeprefix("model."): v.clone().contiguous() for n, v in flat.views(grads=True).items()}
+        step.update()
+    else:
+        loss = step.eager()
     assert torch.isfinite(loss)
     if rank == 0:
-        torch.save({"master": flat.master.detach().clone()}, os.path.join(outdir, "ts.pt"))
+        if overlap:
+            torch.save({"grads": grads, "params": {n.removeprefix("model."): v.clone().contiguous()
+                                                   for n, v in flat.views().items()}},
+                       os.path.join(outdir, "ts_overlap.pt"))
+        else:
+            torch.save({"master": flat.master.detach().clone()}, os.path.join(outdir, "ts.pt"))
     dist.destroy_process_group()
+
+
+def _worker_trainstep_overlap(rank, world, port, outdir):
+    _worker_trainstep(rank, world, port, outdir, overlap=True)
 
 
 @pytest.mark.timeout(600)
@@ -229,3 +249,31 @@ def test_train_step_world2_equals_single_process_average():
     want = flat.master.detach()
     assert got.shape == want.shape
     torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.timeout(600)
+def test_train_step_world2_overlapped_all_reduce():
+    """overlap_all_reduce: three parameter groups, each all-reduced from its gradient hook while the
+    backward continues -- the summed gradients are bit-identical to one all-reduce of the flat
+    gradient; the parameters after clip + Adam agree to the last bits (the clip norm is summed over
+    three tensors instead of one)."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_trainstep_overlap, args=(world, _free_port(), d), nprocs=world, join=True)
+        got = torch.load(os.path.join(d, "ts_overlap.pt"), weights_only=True)
+        mp.spawn(_worker_trainstep, args=(world, _free_port(), d), nprocs=world, join=True)
+        ref_master = torch.load(os.path.join(d, "ts.pt"), weights_only=True)["master"]
+    nthreads = torch.get_num_threads()
+    torch.set_num_threads(2)
+    gsum = None
+    for rank in range(world):  # the reference sum of the two ranks' flat gradients
+        step, flat = _train_step(_model(), seed=20 + rank, world_reduce=False)
+        step.forward_backward()
+        gsum = flat.master.grad.clone() if gsum is None else gsum + flat.master.grad
+    torch.set_num_threads(nthreads)
+    want_g = {n.removeprefix("model."): v for n, v in flat.views_of(gsum).items()}
+    want_p = {n.removeprefix("model."): v for n, v in flat.views_of(ref_master).items()}
+    assert set(got["grads"]) == set(want_g) == set(want_p)
+    for n in want_g:
+        assert torch.equal(got["grads"][n], want_g[n]), n
+        torch.testing.assert_close(got["params"][n], want_p[n], rtol=0, atol=1e-5, msg=n)

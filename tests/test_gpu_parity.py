@@ -462,3 +462,40 @@ def test_sorted_depth_positions_and_splat(cfg_name):
     _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, plan.c_dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
                                  _lib.ptr(plan.pos_of), _lib.ptr(sdepth), _lib.stream_handle(DEV)), "lift")
     assert torch.equal(sdepth[:kept], depth.reshape(-1)[pts])
+
+
+@pytest.mark.parametrize("cfg_name", ["c1", "c3"])
+def test_sorted_depth_fused_lift(cfg_name):
+    """The fused depthnet lift (k_depthnet_lift2) with pos_of writes the weights in CSR order too:
+    the copy equals depth[p] entry by entry and the splat over it gives the same bits."""
+    cfg, gc, _ = syn.config_confs(cfg_name)
+    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
+    rig = {k: v.to(DEV) for k, v in syn.make_rig(B, N, fd, seed=6).items()}
+    frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
+    D, H, W = frustum.shape[:3]
+    grid = ops.GridSpec.from_conf(gc)
+    ops.SORTED_DEPTH = True
+    try:
+        plan = ops.plan_from_cameras(frustum, **rig, grid=grid)
+    finally:
+        ops.SORTED_DEPTH = False
+    kept = int(plan.cell_start[-1])
+    pts = (plan.sorted_key[:kept] & 0xFFFFFFFF).long()
+    g = torch.Generator(device="cpu").manual_seed(7)
+    feat = torch.randn(B * N, 512, H, W, generator=g).to(DEV, torch.bfloat16)
+    wdn = (torch.randn(D + 64, 512, 1, 1, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    bdn = (torch.randn(D + 64, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    lib = _lib.load()
+    depth = torch.empty(B * N, D, H, W, device=DEV)
+    ctx_t = torch.empty(B * N * H * W, 64, device=DEV, dtype=torch.bfloat16)
+    sdepth = torch.zeros(plan.nprime, device=DEV)
+    _lib.check(lib.lss_depthnet_lift(_lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, plan.c_dims,
+                                     _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(plan.pos_of),
+                                     _lib.ptr(sdepth), _lib.stream_handle(DEV)), "depthnet_lift")
+    depth2 = torch.empty_like(depth)
+    ctx2 = torch.empty_like(ctx_t)
+    _lib.check(lib.lss_depthnet_lift(_lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, plan.c_dims,
+                                     _lib.ptr(depth2), _lib.ptr(ctx2), _lib.BF16, None, None,
+                                     _lib.stream_handle(DEV)), "depthnet_lift")
+    assert torch.equal(depth, depth2) and torch.equal(ctx_t, ctx2)  # the same kernel body either way
+    assert torch.equal(sdepth[:kept], depth.reshape(-1)[pts])
