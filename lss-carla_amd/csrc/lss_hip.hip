@@ -2045,6 +2045,7 @@ template <typename GT>
 __global__ __launch_bounds__(kBlock) void k_bev_rows(const GT* __restrict__ dbev, const int32_t* __restrict__ cell_start,
                                                      SplatGeo sg, GT* __restrict__ rows) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int s_start[kMaxYT + 1];
     const int tile = blockIdx.x;
     const int bzx = tile / sg.ntiles_y;
     const int y0 = (tile - bzx * sg.ntiles_y) * sg.YT;
@@ -2052,21 +2053,49 @@ __global__ __launch_bounds__(kBlock) void k_bev_rows(const GT* __restrict__ dbev
     const int x = bzx % sg.X;
     const int bz = bzx / sg.X;
     const int cell0 = bzx * sg.Y + y0;
-    if (uniform(cell_start[cell0]) == uniform(cell_start[cell0 + ny])) return;  // nothing pooled here
-    const int S = sg.YT + 1;
+    // the tile's cell starts in one round trip (occupancy of every cell read from LDS below)
+    for (int i = threadIdx.x; i <= ny; i += kBlock) s_start[i] = cell_start[cell0 + i];
+    __syncthreads();
+    if (s_start[0] == s_start[ny]) return;  // nothing pooled here (block-uniform)
+    const int S = sg.YT + 1;  // odd stride: the row-gather reads (lane = channel) are conflict-free
     const size_t XY = (size_t)sg.X * sg.Y;
     const GT* gbase = dbev + (size_t)bz * kC * XY + (size_t)x * sg.Y + y0;
-    for (int i = threadIdx.x; i < kC * ny; i += kBlock) {
-        const int c = i / ny, yy = i - c * ny;
-        lds[c * S + yy] = to_f32(gbase[c * XY + yy]);
+    constexpr int VN = 16 / (int)sizeof(GT);
+    if ((sg.Y % VN) == 0 && (ny % VN) == 0 && (y0 % VN) == 0) {
+        // 16-B loads, several in flight per thread before any LDS store
+        const int nq = ny / VN, total = kC * nq;
+        constexpr int kIt = 8;  // 64 x 100 cells: <= 7 loads per thread, all in flight
+        for (int i0 = threadIdx.x; i0 < total; i0 += kBlock * kIt) {
+            uint4 v[kIt];
+#pragma unroll
+            for (int t = 0; t < kIt; ++t) {
+                const int i = min(i0 + t * kBlock, total - 1);
+                const int c = i / nq, yv = (i - c * nq) * VN;
+                v[t] = *reinterpret_cast<const uint4*>(gbase + c * XY + yv);
+            }
+#pragma unroll
+            for (int t = 0; t < kIt; ++t) {
+                const int i = i0 + t * kBlock;
+                if (i < total) {
+                    const int c = i / nq, yv = (i - c * nq) * VN;
+                    float f[VN];
+                    unpack16(v[t], (const GT*)nullptr, f);
+#pragma unroll
+                    for (int e = 0; e < VN; ++e) lds[c * S + yv + e] = f[e];
+                }
+            }
+        }
+    } else {
+        for (int i = threadIdx.x; i < kC * ny; i += kBlock) {
+            const int c = i / ny, yy = i - c * ny;
+            lds[c * S + yy] = to_f32(gbase[c * XY + yy]);
+        }
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     for (int yy = wave; yy < ny; yy += kBlock / kWave) {
-        const int cell = cell0 + yy;
-        if (uniform(cell_start[cell + 1]) > uniform(cell_start[cell]))
-            rows[(size_t)cell * kC + lane] = from_f32<GT>(lds[lane * S + yy]);
+        if (s_start[yy + 1] > s_start[yy]) rows[(size_t)(cell0 + yy) * kC + lane] = from_f32<GT>(lds[lane * S + yy]);
     }
 }
 
