@@ -554,17 +554,25 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
     const int lane = threadIdx.x & 63;
     const int w = xcd_block() * (kBlock / kWave) + uniform(threadIdx.x >> 6);
     if (w >= nchunks) return;
-    const int total = *total_ptr;
     const int base = w * kWave;
     const int e0 = base + lane, e1 = base + kWave + lane;
+    // the entry count and the window's keys in ONE round trip: the keys are read unconditionally
+    // (clamped into the nprime-entry buffer) and masked with the count afterwards
+    const int total = *total_ptr;
+    const long long k0r = key_in[min(e0, nprime - 1)];
+    const long long k1r = key_in[min(e1, nprime - 1)];
+    int prev_at = max(base - 1, 0);
+    asm("" : "+v"(prev_at));  // a vector load issued with the others, not a scalar one sunk past the stores
+    const long long kpr = key_in[prev_at];
+    const int cofe = pos_out ? cell_of[min(e0, nprime - 1)] : 0;
     // sentinel tail: entries [total, nprime) hold key -1 (cell -1), so a reader needs no entry count
     if (e0 >= total && e0 < nprime) key_out[e0] = -1ll;
     // sorted position of every point (pos_out[p], -1 = dropped): dropped points here, kept ones below
-    if (pos_out && e0 < nprime && cell_of[e0] < 0) pos_out[e0] = -1;
+    if (pos_out && e0 < nprime && cofe < 0) pos_out[e0] = -1;
     if (base >= total) return;
-    const long long k0 = e0 < total ? key_in[e0] : -1ll;
-    const long long k1 = e1 < total ? key_in[e1] : -1ll;
-    const int prevcell = base > 0 ? (int)(key_in[base - 1] >> 32) : -2;
+    const long long k0 = e0 < total ? k0r : -1ll;
+    const long long k1 = e1 < total ? k1r : -1ll;
+    const int prevcell = base > 0 ? (int)(kpr >> 32) : -2;
     const int c0 = (int)(k0 >> 32), c1 = (int)(k1 >> 32);
     const int p0 = (int)(k0 & 0xFFFFFFFF), p1 = (int)(k1 & 0xFFFFFFFF);
     const ChunkCells cc = chunk_cells(base, total, c0, c1, prevcell, lane);
