@@ -327,3 +327,43 @@ def test_frustum_axes_geometry_bit_exact(name):
     bent = frustum.clone()
     bent[1, 2, 3, 0] += 0.25
     assert ops.frustum_axes(bent) is None
+
+
+@settings(max_examples=25, deadline=None)
+@given(seed=st.integers(0, 10_000), B=st.integers(1, 3), N=st.integers(1, 6), fH=st.integers(1, 9),
+       fW=st.integers(1, 24), D=st.integers(1, 60), half=st.sampled_from([10.0, 25.0, 50.0]),
+       dx=st.sampled_from([0.5, 1.0]), Z=st.sampled_from([1, 2]), bf16_nhwc=st.booleans())
+def test_random_shapes_fwd_bwd_vs_oracle(seed, B, N, fH, fW, D, half, dx, Z, bf16_nhwc):
+    """Hypothesis over shapes the configs never hit -- odd H*W (the lift / backward fallbacks), D up
+    to 60 (the D > 48 backward), one camera, coarse and fine grids, two z bins -- forward and backward
+    against the fp64 oracle (fp32 NCHW or bf16 channels-last)."""
+    fd = (16 * fH, 16 * fW)
+    gc = syn.grid_conf(xy=(-half, half, dx), z=(-10.0, 10.0, 20.0 / Z), dbound=(4.0, 4.0 + D, 1.0))
+    grid = ops.GridSpec.from_conf(gc)
+    rig = _random_rig(np.random.default_rng(seed), B, N, (fH, fW))
+    frustum = ref.create_frustum(fd, gc["dbound"])
+    assert frustum.shape[:3] == (D, fH, fW)
+    plan = ops.plan_from_cameras(frustum.to(DEV), **_dev(rig), grid=grid, inverse="host", want_geom=True)
+    geom = ref.get_geometry(frustum, **rig)
+    np.testing.assert_array_equal(plan.geom.cpu().numpy(), geom)
+    dx_, bx_, nx_ = ref.gen_dx_bx(gc["xbound"], gc["ybound"], gc["zbound"])
+    dtype, layout = (torch.bfloat16, _lib.NHWC) if bf16_nhwc else (torch.float32, _lib.NCHW)
+    dn = syn.make_depthnet_out(B, N, D, fH, fW, seed=seed)
+    dnd = dn.to(DEV, dtype).requires_grad_(True)
+    bev = ops.lift_splat(dnd, plan, dtype, layout)
+    dn_in = dn if dtype == torch.float32 else dn.to(torch.bfloat16).float()
+    _, new_x = ref.lift(dn_in, D, 64)
+    exact = ref.voxel_pooling_fp64(geom, ref.cam_feats_layout(new_x, B, N).numpy(), dx_, bx_, nx_)
+    got = bev.detach().float().cpu().numpy()
+    if dtype == torch.float32:
+        np.testing.assert_allclose(got, exact, rtol=0, atol=ATOL)
+    else:
+        assert (np.abs(got - exact) <= BF16_U * np.abs(exact) + 1e-4).all()
+    gup = torch.randn(bev.shape, generator=torch.Generator().manual_seed(seed + 1))
+    gd = gup.to(DEV, dtype)
+    if layout == _lib.NHWC:
+        gd = gd.contiguous(memory_format=torch.channels_last)
+    bev.backward(gd)
+    want_g = ref.lift_splat_backward_fp64(dn_in.numpy(), geom, gd.float().cpu().numpy(), dx_, bx_, nx_, D, 64)
+    tol = ATOL if dtype == torch.float32 else 2e-2
+    np.testing.assert_allclose(dnd.grad.float().cpu().numpy(), want_g, rtol=tol, atol=tol)
