@@ -861,6 +861,9 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
 constexpr int kDn2Pix = LSS_DN_PIX;             // pixels per block (16-pixel MFMA column tiles)
 constexpr int kDn2Waves = 8;                   // 8 x 16 = 128 output rows >= D + C
 constexpr int kDn2Block = kDn2Waves * kWave;
+#ifndef LSS_DN_ROT
+#define LSS_DN_ROT 0  // 1: rotate the K-step order per block (spreads the weight requests; changes fp32 sum order)
+#endif
 #ifndef LSS_DN_SKIP
 #define LSS_DN_SKIP 0  // timing experiments only (wrong output): 1 skips the weight loads, 2 the feature loads
 #endif
@@ -917,10 +920,13 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
     const int g = lane >> 4, c16 = lane & 15;
     const bf16* wrow = weight + (size_t)min(arow, O - 1) * K + kq;
     bf16x8 a[kSteps];
+    // LSS_DN_ROT: block b walks the K steps starting at b mod kSteps, so the blocks' weight requests
+    // are spread over the matrix instead of all hitting the same lines at once
+    const int rot = LSS_DN_ROT ? (int)(blockIdx.x % kSteps) : 0;
 #pragma unroll
     for (int s = 0; s < kSteps; ++s)
         a[s] = (LSS_DN_SKIP & 1) ? bf16x8{(short)lane, 1, 2, 3, 4, 5, 6, (short)s}
-                                 : *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
+                                 : *reinterpret_cast<const bf16x8*>(wrow + 32 * ((s + rot) & (kSteps - 1)));
     float bv[4];  // the bias of this lane's 4 output rows, in flight with the rest
 #pragma unroll
     for (int i = 0; i < 4; ++i) bv[i] = __bfloat162float(bias[min(wave * 16 + 4 * g + i, O - 1)]);
@@ -954,7 +960,8 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
         for (int t = 0; t < kTiles; ++t) {
             // lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3 of a 4 x 16 block; lane c of
             // the group receives column c (pixel 16t + c), rows 0..3 (4 consecutive channels)
-            const unsigned char* base = s_x + (32 * s + 8 * g + tq) * kRow + (16 * t + 4 * tp) * 2;
+            const int ss = (s + rot) & (kSteps - 1);
+            const unsigned char* base = s_x + (32 * ss + 8 * g + tq) * kRow + (16 * t + 4 * tp) * 2;
             const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                 (__attribute__((address_space(3))) v4s*)(base));
             const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(

@@ -216,10 +216,15 @@ def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None):
     pos_of = torch.empty(nprime, device=dev, dtype=torch.int32) if SORTED_DEPTH else None
     if ws is not None:
         _, workspace, scratch = ws
-        _lib.check(lib.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
-                                        make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key),
-                                        _lib.ptr(sorted_row), _lib.ptr(pos_of), _lib.ptr(scratch),
-                                        _lib.ptr(workspace), _lib.stream_handle(dev)), "lss_csr_build_ws")
+        try:
+            _lib.check(lib.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
+                                            make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key),
+                                            _lib.ptr(sorted_row), _lib.ptr(pos_of), _lib.ptr(scratch),
+                                            _lib.ptr(workspace), _lib.stream_handle(dev)), "lss_csr_build_ws")
+        except Exception:
+            counts.zero_()  # the call did not leave the persistent state zero-filled: restore it
+            workspace.zero_()
+            raise
         return cell_start, sorted_key, sorted_row, pos_of
     scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
     _lib.check(lib.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,

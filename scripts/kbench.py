@@ -22,8 +22,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
-    "nchw1": ["LSS_NCHW_IMPL=1"],           # round-1 NCHW splat (lane = channel)
-    "bwd0": ["LSS_BWD_TILE=0"],             # round-1 splat bwd
+    "mw8": ["LSS_MIN_WAVES=8"],            # <= 64 VGPRs: 8 waves per SIMD
+    "sw2": ["LSS_SPLAT_WAVES=2"],          # 2-wave blocks
+    "mw8_sw2": ["LSS_MIN_WAVES=8", "LSS_SPLAT_WAVES=2"],
+    "zs0": ["LSS_ZERO_STORE=0"],           # plain zero stores
 }
 VARIANTS_R1 = {  # round-1 knobs of the two-role kernel (kept for reference; pass --r1-variants)
     "skip_chunks": ["LSS_SPLAT_IMPL=0", "LSS_FWD_SKIP=1"],  # zero units only (timing decomposition; wrong output)
