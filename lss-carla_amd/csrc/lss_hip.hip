@@ -1273,7 +1273,26 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
 struct BevGeo {
     int X, Y, Z;
     int ncells;
+    int dhw, hw;            // points per camera, pixels per camera (context row of point p)
+    float inv_dhw, inv_hw;  // their reciprocals (row_of_point; exact for p < 2^24)
 };
+
+#ifndef LSS_ROW_FROM_P
+#define LSS_ROW_FROM_P 0  // 1: chunk waves compute each entry's context row from its point id (no sorted_row read; measured: no gain)
+#endif
+// Context row (pixel) of point p = ((bn*D + d)*H + h)*W + w: bn*HW + (h*W + w). Divisions by the
+// runtime D*H*W and H*W through the fp32 reciprocal plus one correction step each.
+__device__ __forceinline__ int row_of_point(int p, const BevGeo& g) {
+    int cam = (int)((float)p * g.inv_dhw);
+    int r = p - cam * g.dhw;
+    if (r < 0) { --cam; r += g.dhw; }
+    if (r >= g.dhw) { ++cam; r -= g.dhw; }
+    int q = (int)((float)r * g.inv_hw);
+    int hw = r - q * g.hw;
+    if (hw < 0) hw += g.hw;
+    if (hw >= g.hw) hw -= g.hw;
+    return cam * g.hw + hw;
+}
 
 template <typename OutT>
 __device__ __forceinline__ OutT* cell_row(OutT* out, int cell, const BevGeo& g) {
@@ -1456,7 +1475,8 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     const long long k0 = e0 < nprime ? sorted_key[e0] : -1ll;
     const long long k1 = e1 < nprime ? sorted_key[e1] : -1ll;
     int rs0 = 0, rs1 = 0;
-    if (FUSED) {
+    const bool row_from_p = LSS_ROW_FROM_P && g.dhw > 0;
+    if (FUSED && !row_from_p) {
         rs0 = e0 < nprime ? sorted_row[e0] : 0;
         rs1 = e1 < nprime ? sorted_row[e1] : 0;
     }
@@ -1473,6 +1493,9 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     if (!FUSED) {
         rs0 = p0;
         rs1 = p1;
+    } else if (row_from_p) {  // the sentinel (-1) and out-of-range entries get row 0 (never summed)
+        rs0 = p0 >= 0 ? row_of_point(p0, g) : 0;
+        rs1 = p1 >= 0 ? row_of_point(p1, g) : 0;
     }
     LSS_STAMP(w, 1);
     const Span sp = chunk_span(c0, c1, prevcell, lane);
@@ -2811,6 +2834,10 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         BevGeo g;
         g.X = sg.X; g.Y = sg.Y; g.Z = sg.Z;
         g.ncells = dims->B * sg.Z * sg.X * sg.Y;
+        g.hw = dims->H * dims->W;
+        g.dhw = nprime < (1 << 24) ? dims->D * g.hw : 0;  // 0: read sorted_row instead
+        g.inv_dhw = g.dhw ? 1.0f / (float)g.dhw : 0.f;
+        g.inv_hw = 1.0f / (float)g.hw;
         const int wpb = kSplatWaves;
         if (LSS_SPLAT_IMPL == 1) {
             const int nchunks = grid_blocks(nprime, kWave), nunits = grid_blocks(g.ncells, kWave);
