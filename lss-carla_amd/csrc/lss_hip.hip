@@ -382,9 +382,9 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ 
 }
 
 // ---- single-pass scan (lss_csr_build_ws): one launch in place of k_scan_partials + k_scan_apply.
-// Blocks take logical indices from a ticket counter in start order, so block k only waits for
-// blocks j < k that are already running (no residency assumption). Block k publishes its aggregate,
-// then wave 0 looks back over its predecessors' 8-byte {status, value} granules, 64 at a time,
+// Block k (blockIdx; workgroups are dispatched in index order, so it only waits for blocks already
+// dispatched -- no residency assumption) publishes its aggregate, then wave 0 looks back over its
+// predecessors' 8-byte {status, value} granules, 128 at a time,
 // up to the nearest inclusive prefix, and publishes its own inclusive prefix. Granules are written
 // with agent-scope (sc1, write-through) atomic stores and polled with agent-scope atomic loads --
 // the cross-XCD hand-off form of the R2 recipe (cdna_hip_programming.md, Guideline 16). Spins are
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ 
 // the granules after the scan, so every call starts from zeros.
 constexpr unsigned kScanSpinLimit = 1u << 22;
 #ifndef LSS_SCAN_TICKET
-#define LSS_SCAN_TICKET 1  // 0: logical index = blockIdx (safe only when no other kernel holds CUs)
+#define LSS_SCAN_TICKET 0  // 1: logical index from a ticket counter (one more atomic round trip)
 #endif
 struct ScanWs {  // lss_csr_workspace_bytes: [ticket, timeouts, pad x2][granule x nb]
     unsigned ticket, timeouts, pad0, pad1;
@@ -411,8 +411,10 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
     __shared__ int s_total;
     __shared__ int s_prefix;
     unsigned long long* gran = reinterpret_cast<unsigned long long*>(ws + 1);
-    // Logical index from a ticket counter: a block then only ever waits for blocks that are already
-    // running, whatever else holds the CUs (the plan may run beside the trunk on another stream).
+    // Logical index = blockIdx: workgroups of a launch are dispatched in index order, so block k only
+    // waits for blocks that were dispatched before it (at worst delayed while another kernel holds
+    // their XCD's CUs). LSS_SCAN_TICKET=1 takes the index from a ticket counter instead.
+    LSS_STAMP(blockIdx.x * 16 + (threadIdx.x >> 6), 0);
     int lb = blockIdx.x;
     if (LSS_SCAN_TICKET) {
         __shared__ int s_blk;
@@ -420,16 +422,22 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
         __syncthreads();
         lb = s_blk;
     }
+    LSS_STAMP(blockIdx.x * 16 + (threadIdx.x >> 6), 1);
     const int nb = (ncells + kScanItems - 1) / kScanItems;
     const int base = lb * kScanItems + threadIdx.x * 4;
-    int c[4];
-    int v = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        c[i] = (base + i < ncells) ? cnt[base + i] : 0;
-        v += c[i];
+    // 16-byte count loads / cell_start stores when both arrays allow it (uniform over the launch)
+    const bool vec = ((reinterpret_cast<uintptr_t>(cnt) | reinterpret_cast<uintptr_t>(cell_start)) & 15) == 0;
+    int4 c4 = make_int4(0, 0, 0, 0);
+    if (vec && base + 4 <= ncells) {
+        c4 = *reinterpret_cast<const int4*>(cnt + base);
+    } else if (base < ncells) {
+        c4.x = cnt[base];
+        if (base + 1 < ncells) c4.y = cnt[base + 1];
+        if (base + 2 < ncells) c4.z = cnt[base + 2];
+        if (base + 3 < ncells) c4.w = cnt[base + 3];
     }
-    const int excl = block_exclusive_scan_1024(v, s_wave, &s_total);
+    const int excl = block_exclusive_scan_1024(c4.x + c4.y + c4.z + c4.w, s_wave, &s_total);
+    LSS_STAMP(blockIdx.x * 16 + (threadIdx.x >> 6), 2);
     if (threadIdx.x < kWave) {
         const int lane = threadIdx.x;
         const int agg = s_total;
@@ -438,39 +446,50 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
             if (lane == 0) st_agent(&gran[0], (2ull << 32) | (unsigned)agg);
         } else {
             if (lane == 0) st_agent(&gran[lb], (1ull << 32) | (unsigned)agg);
-            for (int j = lb - 1;; j -= kWave) {
-                const int jj = j - lane;  // lanes past block 0 read as an inclusive prefix of 0
-                unsigned long long x = 2ull << 32;
+            // 128 predecessors per poll (two granules a lane: distances lane + 1 and lane + 65)
+            for (int j = lb - 1;; j -= 2 * kWave) {
+                const int j0 = j - lane, j1 = j0 - kWave;  // past block 0: an inclusive prefix of 0
+                unsigned long long x0 = 2ull << 32, x1 = 2ull << 32;
                 for (unsigned spins = 0;; ++spins) {
-                    x = jj >= 0 ? ld_agent(&gran[jj]) : (2ull << 32);
-                    if (__all(x != 0ull)) break;
+                    x0 = j0 >= 0 ? ld_agent(&gran[j0]) : (2ull << 32);
+                    x1 = j1 >= 0 ? ld_agent(&gran[j1]) : (2ull << 32);
+                    if (__all(x0 != 0ull && x1 != 0ull)) break;
                     if (spins >= kScanSpinLimit) {
                         if (lane == 0) atomicAdd(&ws->timeouts, 1u);
-                        if (x == 0ull) x = 2ull << 32;  // give up: an empty inclusive prefix
+                        if (x0 == 0ull) x0 = 2ull << 32;  // give up: an empty inclusive prefix
+                        if (x1 == 0ull) x1 = 2ull << 32;
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
-                const unsigned long long pm = __ballot((x >> 32) == 2ull);
-                const int upto = pm ? __builtin_ctzll(pm) : kWave - 1;  // nearest inclusive prefix
-                int val = lane <= upto ? (int)(unsigned)x : 0;
+                const unsigned long long pm0 = __ballot((x0 >> 32) == 2ull);
+                const unsigned long long pm1 = __ballot((x1 >> 32) == 2ull);
+                // nearest inclusive prefix: in the first 64, else in the second 64, else keep going
+                const int upto0 = pm0 ? __builtin_ctzll(pm0) : kWave - 1;
+                const int upto1 = pm0 ? -1 : (pm1 ? __builtin_ctzll(pm1) : kWave - 1);
+                int val = (lane <= upto0 ? (int)(unsigned)x0 : 0) + (lane <= upto1 ? (int)(unsigned)x1 : 0);
 #pragma unroll
                 for (int o = 32; o > 0; o >>= 1) val += __shfl_xor(val, o, kWave);
                 prefix += val;
-                if (pm) break;
+                if (pm0 | pm1) break;
             }
             if (lane == 0) st_agent(&gran[lb], (2ull << 32) | (unsigned)(prefix + agg));
         }
         if (lane == 0) s_prefix = prefix;
     }
     __syncthreads();
-    int run = s_prefix + excl;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (base + i < ncells) cell_start[base + i] = run;
-        run += c[i];
+    const int r0 = s_prefix + excl;
+    const int4 o4 = make_int4(r0, r0 + c4.x, r0 + c4.x + c4.y, r0 + c4.x + c4.y + c4.z);
+    if (vec && base + 4 <= ncells) {
+        *reinterpret_cast<int4*>(cell_start + base) = o4;
+    } else if (base < ncells) {
+        cell_start[base] = o4.x;
+        if (base + 1 < ncells) cell_start[base + 1] = o4.y;
+        if (base + 2 < ncells) cell_start[base + 2] = o4.z;
+        if (base + 3 < ncells) cell_start[base + 3] = o4.w;
     }
     if (lb == nb - 1 && threadIdx.x == 0) cell_start[ncells] = s_prefix + s_total;
+    LSS_STAMP(blockIdx.x * 16 + (threadIdx.x >> 6), 3);
 }
 
 // k_scatter plus the reset for the next call: the scan's ticket and granules and the cell counts

@@ -19,7 +19,7 @@ sys.path.insert(0, REPO)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("kernel", choices=["lift", "bwd", "geom", "nchw"])
+    ap.add_argument("kernel", choices=["lift", "bwd", "geom", "nchw", "scan"])
     ap.add_argument("--config", default="c3")
     ap.add_argument("--cold", type=int, default=1)
     ap.add_argument("--lib", default="trace", help="variants/<name>.so, a LSS_TRACE=1 build")
@@ -61,7 +61,27 @@ def main():
         l.lss_event_create(ct.byref(e0))
         l.lss_event_create(ct.byref(e1))
         l.lss_event_record(e0, st)
-        if a.kernel == "geom":
+        if a.kernel == "scan":  # k_scan_lookback: 1 after the ticket, 2 after the block scan, 3 end
+            if it == 0:
+                prod = _lib.load()
+                ncells = grid.ncells(B)
+                counts = torch.zeros(ncells, device=dev, dtype=torch.int32)
+                slot = torch.empty(plan.nprime, device=dev, dtype=torch.int32)
+                cell_of = torch.empty(plan.nprime, device=dev, dtype=torch.int32)
+                wsb = torch.zeros(int(l.lss_csr_workspace_bytes(ncells)), device=dev, dtype=torch.uint8)
+                scr = torch.empty(int(l.lss_csr_scratch_bytes(ncells, plan.nprime)), device=dev, dtype=torch.uint8)
+                cs = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
+                sk = torch.empty(plan.nprime, device=dev, dtype=torch.int64)
+                sr = torch.empty(plan.nprime, device=dev, dtype=torch.int32)
+            _lib.check(prod.lss_geometry_cells(_lib.ptr(frustum), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv),
+                                               _lib.ptr(pinv), _lib.ptr(pt), dims, g, None, _lib.ptr(cell_of),
+                                               _lib.ptr(counts), _lib.ptr(slot), st), "geom")
+            _lib.check(l.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot), plan.nprime, _lib.ptr(counts), ncells,
+                                          dims, _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), None, _lib.ptr(scr),
+                                          _lib.ptr(wsb), st), "csr")
+            if it == 3:
+                assert torch.equal(cs, plan.cell_start), "trace build CSR differs"
+        elif a.kernel == "geom":
             counts = torch.zeros(grid.ncells(B), device=dev, dtype=torch.int32)
             slot = torch.empty(plan.nprime, device=dev, dtype=torch.int32)
             cell_of = torch.empty(plan.nprime, device=dev, dtype=torch.int32)

@@ -303,6 +303,50 @@ def test_single_pass_scan_matches_two_kernel_csr(name):
         assert not words[4:].any() and words[0] == 0, "scan state not re-zeroed"
 
 
+@pytest.mark.parametrize("ncells,nprime,offset", [(7, 40, 0), (4097, 9000, 1), (600_001, 200_000, 0),
+                                                   (600_003, 150_000, 1)])
+def test_csr_build_ws_direct(ncells, nprime, offset):
+    """lss_csr_build_ws called directly (per-point rows, no dims) on random cells with ~10% dropped
+    points: ragged cell counts (not a multiple of 4 or of the 4096-cell scan block), 147 scan blocks
+    (the look-back crosses 128-block windows), and counts / cell_start 4 bytes off 16-byte alignment
+    (the scalar path). cell_start and the sorted keys exactly equal the host counting sort."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(ncells + nprime)
+    cell = torch.randint(0, ncells, (nprime,), generator=g, dtype=torch.int32)
+    cell[torch.rand(nprime, generator=g) < 0.1] = -1
+    kept = cell >= 0
+    counts_h = torch.bincount(cell[kept].long(), minlength=ncells).int()
+    order = torch.argsort(cell.long() * nprime + torch.arange(nprime), stable=True)
+    slot = torch.empty(nprime, dtype=torch.int32)  # rank of each point inside its cell
+    cs_h = torch.zeros(ncells + 1, dtype=torch.int64)
+    cs_h[1:] = torch.cumsum(counts_h.long(), 0)
+    pos = torch.empty(nprime, dtype=torch.int64)
+    pos[order] = torch.arange(nprime)
+    nneg = int((~kept).sum())
+    slot[kept] = (pos[kept] - nneg - cs_h[cell[kept].long()]).int()
+    slot[~kept] = 0
+    counts = torch.zeros(ncells + offset, device=DEV, dtype=torch.int32)[offset:]
+    counts.copy_(counts_h.to(DEV))
+    cell_start = torch.empty(ncells + 1 + offset, device=DEV, dtype=torch.int32)[offset:]
+    sorted_key = torch.empty(nprime, device=DEV, dtype=torch.int64)
+    sorted_row = torch.empty(nprime, device=DEV, dtype=torch.int32)
+    ws = torch.zeros(int(lib.lss_csr_workspace_bytes(ncells)), device=DEV, dtype=torch.uint8)
+    scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=DEV, dtype=torch.uint8)
+    cd, sd = cell.to(DEV), slot.to(DEV)
+    _lib.check(lib.lss_csr_build_ws(_lib.ptr(cd), _lib.ptr(sd), nprime, _lib.ptr(counts), ncells, None,
+                                    _lib.ptr(cell_start), _lib.ptr(sorted_key), _lib.ptr(sorted_row), None,
+                                    _lib.ptr(scratch), _lib.ptr(ws), _lib.stream_handle(DEV)), "lss_csr_build_ws")
+    torch.cuda.synchronize()
+    assert torch.equal(cell_start.cpu().long(), cs_h)
+    nk = int(cs_h[-1])
+    p = torch.arange(nprime)[kept]
+    want = torch.sort((cell[kept].long() << 32) | p)[0]
+    assert torch.equal(sorted_key[:nk].cpu(), want)
+    words = ws.view(torch.int32).cpu().numpy()
+    assert words[1] == 0, f"look-back spin timeouts: {words[1]}"
+    assert not words[4:].any() and words[0] == 0 and int(counts.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("name", ["c1", "c3", "c5"])
 def test_frustum_axes_geometry_bit_exact(name):
     """lss_geometry_cells_axes (the frustum's three axes) == lss_geometry_cells (the full tensor):
