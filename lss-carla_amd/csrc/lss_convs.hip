@@ -23,6 +23,10 @@
 
 #include "lss_convs.h"
 
+// The library is built with -ffp-contract=off for the geometry's reference op order (lss_hip.hip);
+// the conv-stack kernels here have no bit-exact contract, so they keep FMA contraction.
+#pragma clang fp contract(fast)
+
 namespace {
 
 using bf16 = __hip_bfloat16;

@@ -1060,7 +1060,7 @@ struct SplatGeo {
 #define LSS_YT_MAX 128
 #endif
 #ifndef LSS_MIN_WAVES
-#define LSS_MIN_WAVES 5  // occupancy floor of the channels-last splat (waves per SIMD; VGPR budget 512 / this)
+#define LSS_MIN_WAVES 7  // occupancy floor of the channels-last splat (waves per SIMD; VGPR budget 512 / this)
 #endif
 #ifndef LSS_INTERLEAVE
 #define LSS_INTERLEAVE 0  // dispatch order of the block groups: 0 chunks first, 1 interleaved, 2 zero fill first
@@ -1532,11 +1532,13 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                                           (~0ull << s) & (end >= kWave ? ~0ull : ((1ull << end) - 1));
         // The owned entries [s, end) (n <= 128) are split evenly over the NG groups of LPR lanes:
         // group q sums entries [s + n*q/NG, s + n*(q+1)/NG) cell by cell; lane j of a group owns row
-        // elements [EPL*j, EPL*j + EPL). A cell cut by group boundaries is summed in pieces: the
-        // group holding its first entry leaves its piece in part_last[q], every later group holding
-        // some of it leaves its piece in part_first[q]; after a wave barrier the group holding the
-        // cell's last entry adds the pieces in group order and stores the row. The association
-        // depends only on the CSR (deterministic), never on timing.
+        // elements [EPL*j, EPL*j + EPL). A cell cut by group boundaries is summed in pieces: every
+        // group after the one holding its first entry leaves its piece in part[q] (a group's only
+        // LDS piece: the cell it starts inside of); the group holding the first entry keeps its own
+        // piece in registers (its last cell) and, after a wave barrier, adds the later groups'
+        // pieces in group order and stores the row. One row slot per group (2 KB per wave) keeps
+        // the block at 16 KB of LDS, so 8 blocks (32 waves) fit a CU and the zero fill is resident
+        // beside the chunk waves. The association depends only on the CSR (deterministic).
         const int n = end - s;
         const int grp = lane / RS::LPR, col = (lane % RS::LPR) * RS::EPL;
         auto gbeg = [&](int q) { return s + (n * q) / RS::NG; };
@@ -1554,9 +1556,9 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                 *reinterpret_cast<float4*>(dst + col + i) = make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
         };
         auto finish = [&](bool last) {  // the cell `cur` ends at this point of the group
-            if (cur == first_cell && head_split) put(part + (RS::NG + grp) * kC);   // part_first[grp]
-            else if (last && tail_split) put(part + grp * kC);                       // part_last[grp]
-            else store_slice<RS::EPL>(cell_row(out, cur, g) + col, acc);
+            if (cur == first_cell && head_split) put(part + grp * kC);  // a later piece of a cut cell
+            else if (!(last && tail_split)) store_slice<RS::EPL>(cell_row(out, cur, g) + col, acc);
+            // else: the first piece of a cut cell stays in acc (combined after the barrier)
         };
         // round trip 2 (one per kUnroll entries of a group): row slices and depth weights in flight together
 #ifndef LSS_TRAP_EXP
@@ -1604,22 +1606,18 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
         }
         if (cur >= 0 && LSS_CHUNK_STOP != 2) finish(true);
         __builtin_amdgcn_wave_barrier();
-        // pieces of the cell cut at this group's start: summed here if the cell ends in this group
-        if (head_split && !(tail_split && meta[ge - 1].cell == first_cell) && LSS_CHUNK_STOP != 2) {
-            // the group holding the cell's first entry (owned cells start below 64: bit in `starts`)
-            const unsigned long long upto = starts & (gs >= kWave ? ~0ull : ((2ull << gs) - 1));
-            const int cstart = 63 - __builtin_clzll(upto);
-            int g0 = 0;
-            while (gbeg(g0 + 1) <= cstart) ++g0;
-            float sum[RS::EPL];
+        // the cell cut at this group's end, if it starts in this group: its first piece (acc) plus
+        // the later groups' pieces in group order (empty groups skipped; the cell ends where a
+        // group's first cell is another one)
+        if (tail_split && !(head_split && cur == first_cell) && LSS_CHUNK_STOP != 2) {
+            for (int q = grp + 1; q < RS::NG; ++q) {
+                const int qs = gbeg(q);
+                if (qs == gbeg(q + 1)) continue;  // empty group
+                if (meta[qs].cell != cur) break;
 #pragma unroll
-            for (int i = 0; i < RS::EPL; ++i) sum[i] = part[g0 * kC + col + i];
-            for (int q = g0 + 1; q <= grp; ++q) {
-                if (gbeg(q) == gbeg(q + 1)) continue;  // empty group
-#pragma unroll
-                for (int i = 0; i < RS::EPL; ++i) sum[i] = __fadd_rn(sum[i], part[(RS::NG + q) * kC + col + i]);
+                for (int i = 0; i < RS::EPL; ++i) acc[i] = __fadd_rn(acc[i], part[q * kC + col + i]);
             }
-            store_slice<RS::EPL>(cell_row(out, first_cell, g) + col, sum);
+            store_slice<RS::EPL>(cell_row(out, cur, g) + col, acc);
         }
         if (kChunkGap > 0) {
             // empty cells after each owned cell, up to kChunkGap of them (the next occupied cell is
@@ -1834,7 +1832,7 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(c
                                                            int nprime, int nchunk_blocks, int nzero_blocks,
                                                            OutT* __restrict__ out) {
     __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
-    __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][2 * RowSlice<RT>::NG * kC];
+    __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][RowSlice<RT>::NG * kC];
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     // Blocks come in groups of 8, one per XCD (blocks are dealt round-robin over the 8 XCDs). Chunk

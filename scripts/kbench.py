@@ -22,10 +22,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
-    "mw8": ["LSS_MIN_WAVES=8"],            # <= 64 VGPRs: 8 waves per SIMD
-    "sw2": ["LSS_SPLAT_WAVES=2"],          # 2-wave blocks
-    "mw8_sw2": ["LSS_MIN_WAVES=8", "LSS_SPLAT_WAVES=2"],
-    "zs0": ["LSS_ZERO_STORE=0"],           # plain zero stores
+    "mw8": ["LSS_MIN_WAVES=8"],            # <= 64 VGPRs: 8 waves per SIMD (a few spilled registers)
+    "mw6": ["LSS_MIN_WAVES=6"],            # the round-2 occupancy floor
+    "il1": ["LSS_INTERLEAVE=1"],           # chunk and zero-fill block groups interleaved
+    "zf": ["LSS_INTERLEAVE=2"],            # zero-fill groups dispatched first
+    "zu2": ["LSS_ZERO_UNITS=2"],           # 128 cells per zero-fill wave
 }
 VARIANTS_R1 = {  # round-1 knobs of the two-role kernel (kept for reference; pass --r1-variants)
     "skip_chunks": ["LSS_SPLAT_IMPL=0", "LSS_FWD_SKIP=1"],  # zero units only (timing decomposition; wrong output)

@@ -4,7 +4,7 @@ import subprocess
 import sys
 
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-Iinclude", "-c",
-       "-o", "/tmp/_lss_res.o", "lss-carla_amd/csrc/lss_hip.hip", "-Rpass-analysis=kernel-resource-usage"]
+       "-o", "/tmp/_lss_res.o", "lss-carla_amd/csrc/lss_hip.hip", "-Rpass-analysis=kernel-resource-usage"] + sys.argv[2:]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 cur, rows = None, []
 for line in out.splitlines():
