@@ -158,6 +158,30 @@ def splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes, ctx_bytes) -> int:
             + ncells * 64 * out_bytes)    # dense BEV, every element written once
 
 
+def write_ceiling(numel, dtype, dev, reps=10) -> dict:
+    """Measured HBM write ceiling for the splat's output: a memset of a BEV-sized buffer with L2 and
+    the Infinity Cache flushed (512 MiB written) before each launch -- the state the BEV buffer is in
+    when the splat runs inside a step (its lines were evicted by the trunk). hipEvents around the
+    launch; mean over `reps`."""
+    buf = torch.empty(numel, dtype=dtype, device=dev)
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    tot = 0.0
+    for i in range(reps + 2):
+        flush.zero_()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        buf.zero_()
+        e1.record()
+        torch.cuda.synchronize()
+        if i >= 2:
+            tot += e0.elapsed_time(e1)
+    us = tot / reps * 1e3
+    nbytes = numel * buf.element_size()
+    del buf, flush
+    return {"what": f"memset of the {nbytes / 1e6:.1f} MB BEV, L2 + Infinity Cache flushed before each launch",
+            "us": round(us, 2), "GB/s": round(nbytes / us / 1e3, 1)}
+
+
 # ----------------------------------------------------------------------------- HBM traffic (PMC)
 def measure_traffic(args, B) -> dict | None:
     """FETCH_SIZE and WRITE_SIZE of lss_splat_fwd per launch (rocprofv3, one pass per counter group),
@@ -487,6 +511,7 @@ def main():
         out_bytes = 2 if amp_dtype is not None else 4
         nbytes = splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes, ctx_bytes=out_bytes)
         achieved = nbytes / (splat_ms * 1e-3) / 1e9 if splat_ms else None
+        ceiling = write_ceiling(B * Z * 64 * X * Y, amp_dtype or torch.float32, dev)
         frames = world * B * args.steps
         what = "full train step (fwd+loss+bwd+clip+Adam)" if args.mode == "train" else "forward only"
         res = {
@@ -510,7 +535,9 @@ def main():
                          "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
                          "traffic_detail": traffic, "algorithmic_bytes": nbytes,
                          "avg_launch_us": round(splat_ms * 1e3, 2) if splat_ms else None,
-                         "timed_in": "eager steps after the timed replays, kernel-stamped hipEvents"},
+                         "timed_in": "eager steps after the timed replays, kernel-stamped hipEvents",
+                         "write_ceiling": dict(ceiling, splat_frac_of_ceiling=round(achieved / ceiling["GB/s"], 4)
+                                               if achieved else None)},
         }
         if args.cpu_baseline and world == 1 and args.config == "c3":
             log("[rank 0] timing the CPU baseline ...")

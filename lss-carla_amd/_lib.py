@@ -111,8 +111,8 @@ def open_library(path: str) -> ctypes.CDLL:
 def load() -> ctypes.CDLL:
     """Load (once) and type the product library; raise if it is absent or of another ABI."""
     global _lib
-    if _lib is None:
-        _lib = open_library(LIB_PATH)
+    if _lib is None:  # LSS_LIB: another build of the same ABI (A/B timing of tuning builds)
+        _lib = open_library(os.environ.get("LSS_LIB") or LIB_PATH)
     return _lib
 
 

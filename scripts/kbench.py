@@ -7,6 +7,7 @@ overhead) in three cache states:
   cold  512 MiB written before each launch (L2 and Infinity Cache flushed)
   step  caches flushed, then the CSR and the lift prep rebuilt right before the splat -- the order of
         a training step, where the plan is built after the trunk (models.LiftSplatShoot.get_voxels)
+  hot   as step, with ~0.3 ms of bf16 GEMMs before the plan (the trunk's clock / power state)
 
   python scripts/kbench.py --build-variants     # here (hipcc), before gpurun
   python scripts/kbench.py                      # on the GPU box
@@ -22,11 +23,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
-    "mw8": ["LSS_MIN_WAVES=8"],            # <= 64 VGPRs: 8 waves per SIMD (a few spilled registers)
-    "mw6": ["LSS_MIN_WAVES=6"],            # the round-2 occupancy floor
-    "il1": ["LSS_INTERLEAVE=1"],           # chunk and zero-fill block groups interleaved
-    "zf": ["LSS_INTERLEAVE=2"],            # zero-fill groups dispatched first
-    "zu2": ["LSS_ZERO_UNITS=2"],           # 128 cells per zero-fill wave
+    "to0": ["LSS_TILE_ORDER=0"],           # NCHW tiles in plain XCD-contiguous order (no center-out)
+    "yt40": ["LSS_YT_MAX=40"],             # NCHW tiles of 40 cells (5 per 200-cell row)
+    "yt20": ["LSS_YT_MAX=20"],             # NCHW tiles of 20 cells
+    "nw8": ["LSS_NCHW_WAVES=8"],           # 8 waves (32 lane groups) per NCHW tile
+    "ku16": ["LSS_NCHW_KU=16"],            # 16 context rows in flight per NCHW lane group
 }
 VARIANTS_R1 = {  # round-1 knobs of the two-role kernel (kept for reference; pass --r1-variants)
     "skip_chunks": ["LSS_SPLAT_IMPL=0", "LSS_FWD_SKIP=1"],  # zero units only (timing decomposition; wrong output)
@@ -231,15 +232,40 @@ def main():
                                   "fwd")
 
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    gemm_a = torch.randn(4096, 4096, device=dev).to(torch.bfloat16)
+    gemm_c = torch.empty_like(gemm_a)
+
+    def memset_after(mode):
+        """41 MB bf16 BEV memset in the given cache / clock state (kernel time only, hipEvents)."""
+        tot = 0.0
+        for i in range(23):
+            flush.zero_()
+            if mode == "hot":
+                for _ in range(4):
+                    torch.matmul(gemm_a, gemm_a, out=gemm_c)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            bev_bf.zero_()
+            e1.record()
+            torch.cuda.synchronize()
+            if i >= 3:
+                tot += e0.elapsed_time(e1)
+        return tot / 20 * 1e3
+    if not args.only:
+        res["memset_bev_bf16_41MB (flushed)"] = memset_after("cold")
+        res["memset_bev_bf16_41MB (flushed, after GEMMs)"] = memset_after("hot")
 
     def stamped(l, out, layout, csr=pcsr, ctx=None, mode="warm", iters=20, sd=None):
         cs, sk, its, po = csr
         ctx = ctx_t if ctx is None else ctx
         tot = 0.0
         for i in range(iters + 3):
-            if mode in ("cold", "step"):
+            if mode in ("cold", "step", "hot"):
                 flush.zero_()
-            if mode == "step":
+            if mode == "hot":
+                for _ in range(4):
+                    torch.matmul(gemm_a, gemm_a, out=gemm_c)
+            if mode in ("step", "hot"):
                 lib_plan(l, csr)
                 _lib.check(l.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx),
                                            _lib.dtype_code(ctx.dtype), _lib.ptr(po if sd is not None else None),
@@ -258,7 +284,7 @@ def main():
             l.lss_event_destroy(b)
         return tot / iters * 1e3
 
-    modes = ["warm"] + (["cold", "step"] if args.cold else [])
+    modes = ["warm"] + (["cold", "step", "hot"] if args.cold else [])
     fwd(lib, bev_bf, _lib.NHWC)()
     ref_out = bev_bf.clone()
     if not args.only or "splat_fwd" in args.only:
