@@ -18,6 +18,7 @@
 //   lss_splat_bwd           1 wave / pixel: 16-B gathers of D rows to LDS, d_ctx, d_depth, softmax bwd
 
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <hip/hip_bf16.h>
 #include <hip/hip_ext.h>
 #include <algorithm>
@@ -1063,7 +1064,7 @@ struct SplatGeo {
 #define LSS_MIN_WAVES 7  // occupancy floor of the channels-last splat (waves per SIMD; VGPR budget 512 / this)
 #endif
 #ifndef LSS_INTERLEAVE
-#define LSS_INTERLEAVE 0  // dispatch order of the block groups: 0 chunks first, 1 interleaved, 2 zero fill first
+#define LSS_INTERLEAVE -1  // dispatch order of the block groups: 0 chunks first, 1 interleaved, 2 zero fill first, -1 auto
 #endif
 #ifndef LSS_CHUNK_STOP
 #define LSS_CHUNK_STOP 0  // timing experiments only: chunk waves stop after round trip 1 (1) or 2 (2)
@@ -1830,7 +1831,7 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(c
                                                            const long long* __restrict__ sorted_key,
                                                            const int32_t* __restrict__ sorted_row, BevGeo g,
                                                            int nprime, int nchunk_blocks, int nzero_blocks,
-                                                           OutT* __restrict__ out) {
+                                                           int order, OutT* __restrict__ out) {
     __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
     __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][RowSlice<RT>::NG * kC];
     const int lane = threadIdx.x & 63;
@@ -1843,11 +1844,11 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(c
     const int gi = blockIdx.x >> 3, x = blockIdx.x & 7;
     int zgi = gi - ncg, cgi = gi;
     bool zero_role = gi >= ncg;
-    if (LSS_INTERLEAVE == 2) {
+    if (order == 2) {
         zero_role = gi < nzg;
         zgi = gi;
         cgi = gi - nzg;
-    } else if (LSS_INTERLEAVE == 1) {
+    } else if (order == 1) {
         const int G = ncg + nzg;
         zgi = (gi * nzg) / G;
         zero_role = ((gi + 1) * nzg) / G > zgi;
@@ -1859,8 +1860,8 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(c
         if (cb >= nchunk_blocks) return;
         const int w = cb * (kSplatWaves) + wave;
         LSS_STAMP(w, 0);
-        splat_chunk<FUSED, RT, OutT>(w, nprime, depth, sorted_depth, rows_base, sorted_key, sorted_row, cell_start, g, out, s_meta[wave],
-                                     s_part[wave], lane);
+        splat_chunk<FUSED, RT, OutT>(w, nprime, depth, sorted_depth, rows_base, sorted_key, sorted_row, cell_start, g, out,
+                                     s_meta[wave], s_part[wave], lane);
         LSS_STAMP(w, 3);
 #if LSS_TRACE
         if (lane == 0 && w < 16384) g_lss_trace[w][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
@@ -2576,6 +2577,19 @@ __global__ __launch_bounds__(kBlock) void k_seg_gather(const float* __restrict__
 // ----------------------------------------------------------------------------- host helpers
 inline int grid_blocks(long n, int per) { return (int)((n + per - 1) / per); }
 
+// Compute units of the current device, cached per device id (the library's only global state).
+inline int device_cus() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    int n = cache[dev].load(std::memory_order_relaxed);
+    if (n <= 0) {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cache[dev].store(n, std::memory_order_relaxed);
+    }
+    return n;
+}
+
 inline int choose_yt(int Y) {
     if (Y <= LSS_YT_MAX) return Y;
     for (int t = LSS_YT_MAX; t >= 16; t -= 4)
@@ -2885,6 +2899,13 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), wpb);
         const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), wpb);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);
+        // Dispatch order of the two roles: chunks first while every chunk wave finds a wave slot at
+        // once (c3: 5,386 chunk waves, 7,168 slots -- they all start at t = 0 and the zero waves take
+        // the slots left); interleaved once the chunk waves outnumber the slots (c5: 12,420), so the
+        // zero fill is not held back behind generations of chunk waves (c5 step-order 24.5 -> 23.4 us;
+        // interleaving at c3 costs 1.6 us).
+        const long slots = (long)device_cus() * 4 * LSS_MIN_WAVES;
+        const int order = LSS_INTERLEAVE >= 0 ? LSS_INTERLEAVE : ((long)nchunk_blocks * wpb > slots ? 1 : 0);
 // kernel-stamped events only when asked for: a plain launch is what a hipGraph capture records
 #define LSS_NHWC_FWD(F, RT, T)                                                                                     \
     do {                                                                                                           \
@@ -2892,11 +2913,11 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
             hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, sorted_depth,      \
                                   (const RT*)rows,                                                                 \
                                   cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks,      \
-                                  (T*)out);                                                                        \
+                                  order, (T*)out);                                                                 \
         else                                                                                                       \
             hipLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, depth, sorted_depth, (const RT*)rows,   \
                                cell_start,                                                                         \
-                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, (T*)out);           \
+                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, order, (T*)out);    \
     } while (0)
         if (out_dtype == LSS_F32) {
             if (!fused) LSS_NHWC_FWD(false, float, float);

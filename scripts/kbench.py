@@ -23,11 +23,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 VARIANTS = {
-    "to0": ["LSS_TILE_ORDER=0"],           # NCHW tiles in plain XCD-contiguous order (no center-out)
-    "yt40": ["LSS_YT_MAX=40"],             # NCHW tiles of 40 cells (5 per 200-cell row)
-    "yt20": ["LSS_YT_MAX=20"],             # NCHW tiles of 20 cells
-    "nw8": ["LSS_NCHW_WAVES=8"],           # 8 waves (32 lane groups) per NCHW tile
-    "ku16": ["LSS_NCHW_KU=16"],            # 16 context rows in flight per NCHW lane group
+    "cpw2": ["LSS_CHUNKS_PER_WAVE=2"],     # two chunks per chunk wave (half the chunk waves)
+    "cpw2_o0": ["LSS_CHUNKS_PER_WAVE=2", "LSS_INTERLEAVE=0"],
+    "cpw3": ["LSS_CHUNKS_PER_WAVE=3"],
+    "o0": ["LSS_INTERLEAVE=0"],            # chunks first always
 }
 VARIANTS_R1 = {  # round-1 knobs of the two-role kernel (kept for reference; pass --r1-variants)
     "skip_chunks": ["LSS_SPLAT_IMPL=0", "LSS_FWD_SKIP=1"],  # zero units only (timing decomposition; wrong output)
