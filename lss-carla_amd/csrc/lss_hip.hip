@@ -158,8 +158,57 @@ __device__ __forceinline__ int quantize_cell(float ex, float ey, float ez, const
 }
 
 #ifndef LSS_GEOM_AGG
-#define LSS_GEOM_AGG 1  // 1: one atomic per distinct cell of a wave (lanes of a cell share it), 0: one per point
+#define LSS_GEOM_AGG 3  // 3: one atomic per distinct cell of a block (LDS hash), 1: of a wave (ballots), 0: per point
 #endif
+#ifndef LSS_GEO_BLOCK
+#define LSS_GEO_BLOCK 256  // threads (points) per block of the geometry / cell kernels
+#endif
+constexpr int kGeoBlock = LSS_GEO_BLOCK;
+constexpr int kGeoHashBits = kGeoBlock <= 256 ? 9 : kGeoBlock <= 512 ? 10 : 11;
+constexpr int kGeoHash = 1 << kGeoHashBits;  // >= 2 entries per point of the block: short probe chains
+static_assert(kGeoHash >= 2 * kGeoBlock, "hash table at most half full");
+
+// The block's distinct cells: open-addressing table in LDS (key -1 = free; cnt = points, then base).
+struct GeoHash {
+    int key[kGeoHash];
+    int cnt[kGeoHash];
+};
+
+// LSS_GEOM_AGG 3: slots grouped per block. Every kept point inserts its cell into the block's LDS
+// table (multiplicative hash, linear probing) and takes a rank among the block's points of that cell
+// from an LDS atomic; then ONE returning device atomic per distinct cell of the block adds the
+// group's size to the count, and a point's slot is that old count plus its rank. At c3 a block of 256
+// points holds 67 k distinct (block, cell) pairs in all against 141 k (wave, cell) pairs; at c5 171 k
+// against 535 k -- and the device atomics, executed at the memory side, are what the kernel waits on.
+// Must be called by every thread of the block (cell = -1 for dropped / out-of-range points).
+__device__ __forceinline__ void emit_cell_block(int p, int cell, int32_t* cell_of, int32_t* cell_count,
+                                                int32_t* slot_of, bool live, GeoHash& h) {
+    if (live) cell_of[p] = cell;
+    if (cell_count == nullptr) return;  // block-uniform
+    for (int i = threadIdx.x; i < kGeoHash; i += kGeoBlock) {
+        h.key[i] = -1;
+        h.cnt[i] = 0;
+    }
+    __syncthreads();
+    const bool kept = live && cell >= 0;
+    int at = 0, rank = 0;
+    if (kept) {
+        at = (int)(((unsigned)cell * 2654435761u) >> (32 - kGeoHashBits));
+        for (;;) {
+            const int prev = atomicCAS(&h.key[at], -1, cell);
+            if (prev == -1 || prev == cell) break;
+            at = (at + 1) & (kGeoHash - 1);
+        }
+        rank = atomicAdd(&h.cnt[at], 1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kGeoHash; i += kGeoBlock) {
+        const int c = h.key[i];
+        if (c >= 0) h.cnt[i] = atomicAdd(cell_count + c, h.cnt[i]);
+    }
+    __syncthreads();
+    if (live) slot_of[p] = kept ? h.cnt[at] + rank : -1;
+}
 
 // Slot of point p inside its cell (arrival order; k_csr_canon fixes the order later). Atomics on
 // the counts execute at the memory side, so a wave first groups its lanes by cell (a ballot per
@@ -248,13 +297,13 @@ __device__ __forceinline__ void geometry_point(const float* __restrict__ frustum
 // 157-168), so point (d, h, w) = (xs[w], ys[h], ds[d]) bit for bit; 71 floats read through the
 // caches instead of 12 B per point from HBM.
 template <bool AXES>
-__global__ __launch_bounds__(kBlock) void k_geometry_cells(
+__global__ __launch_bounds__(kGeoBlock) void k_geometry_cells(
     const float* __restrict__ frustum, const float* __restrict__ rots, const float* __restrict__ trans,
     const float* __restrict__ kinv, const float* __restrict__ pinv, const float* __restrict__ post_trans,
     int N, int DHW, int HW, int W, int nprime, lss_grid_t g, float* __restrict__ out_geom,
     int32_t* __restrict__ cell_of, int32_t* __restrict__ cell_count, int32_t* __restrict__ slot_of) {
-    LSS_STAMP(blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6), 0);
-    const int p0 = blockIdx.x * kBlock + threadIdx.x;
+    LSS_STAMP(blockIdx.x * (kGeoBlock / kWave) + (threadIdx.x >> 6), 0);
+    const int p0 = blockIdx.x * kGeoBlock + threadIdx.x;
     const bool live = p0 < nprime;
     const int p = live ? p0 : nprime - 1;  // dead lanes recompute the last point, then write nothing
     const int cam = p / DHW;
@@ -276,23 +325,34 @@ __global__ __launch_bounds__(kBlock) void k_geometry_cells(
         out_geom[3 * (size_t)p + 1] = e[1];
         out_geom[3 * (size_t)p + 2] = e[2];
     }
-    [[maybe_unused]] const int tslot = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);  // LSS_TRACE builds
+    [[maybe_unused]] const int tslot = blockIdx.x * (kGeoBlock / kWave) + (threadIdx.x >> 6);  // LSS_TRACE builds
     LSS_STAMP(tslot, 1);
     const int cell = live ? quantize_cell(e[0], e[1], e[2], g, b) : -1;
     LSS_STAMP(tslot, 2);
-    emit_cell(p, cell, cell_of, cell_count, slot_of, live);
+    if (LSS_GEOM_AGG == 3) {
+        __shared__ GeoHash hash;
+        emit_cell_block(p, cell, cell_of, cell_count, slot_of, live, hash);
+    } else {
+        emit_cell(p, cell, cell_of, cell_count, slot_of, live);
+    }
     LSS_STAMP(tslot, 3);
 }
 
-__global__ __launch_bounds__(kBlock) void k_cells_from_geom(const float* __restrict__ geom, int nprime, int ppb,
-                                                            lss_grid_t g, int32_t* __restrict__ cell_of,
-                                                            int32_t* __restrict__ cell_count,
-                                                            int32_t* __restrict__ slot_of) {
-    const int p = blockIdx.x * kBlock + threadIdx.x;
-    const bool live = p < nprime;
+__global__ __launch_bounds__(kGeoBlock) void k_cells_from_geom(const float* __restrict__ geom, int nprime, int ppb,
+                                                               lss_grid_t g, int32_t* __restrict__ cell_of,
+                                                               int32_t* __restrict__ cell_count,
+                                                               int32_t* __restrict__ slot_of) {
+    const int p0 = blockIdx.x * kGeoBlock + threadIdx.x;
+    const bool live = p0 < nprime;
+    const int p = live ? p0 : nprime - 1;  // dead lanes stay for the block barriers, write nothing
     const int cell =
         live ? quantize_cell(geom[3 * (size_t)p], geom[3 * (size_t)p + 1], geom[3 * (size_t)p + 2], g, p / ppb) : -1;
-    emit_cell(p, cell, cell_of, cell_count, slot_of, live);
+    if (LSS_GEOM_AGG == 3) {
+        __shared__ GeoHash hash;
+        emit_cell_block(p, cell, cell_of, cell_count, slot_of, live, hash);
+    } else {
+        emit_cell(p, cell, cell_of, cell_count, slot_of, live);
+    }
 }
 
 // ----------------------------------------------------------------------------- CSR (counting sort)
@@ -1859,6 +1919,9 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(c
         const int cb = LSS_XCD_MAP ? x * ncg + cgi : cgi * 8 + x;
         if (cb >= nchunk_blocks) return;
         const int w = cb * (kSplatWaves) + wave;
+        // the last chunk block's spare waves own no entries (and must not read the entry before their
+        // base, past the end of sorted_key)
+        if (w * kWave >= nprime) return;
         LSS_STAMP(w, 0);
         splat_chunk<FUSED, RT, OutT>(w, nprime, depth, sorted_depth, rows_base, sorted_key, sorted_row, cell_start, g, out,
                                      s_meta[wave], s_part[wave], lane);
@@ -2700,7 +2763,7 @@ int lss_geometry_cells(const float* frustum, const float* rots, const float* tra
     const long DHW = (long)dims->D * dims->H * dims->W;
     const long nprime = (long)dims->B * dims->N * DHW;
     if (nprime >= INT_MAX) return LSS_EUNSUPPORTED;
-    hipLaunchKernelGGL(k_geometry_cells<false>, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_geometry_cells<false>, dim3(grid_blocks(nprime, kGeoBlock)), dim3(kGeoBlock), 0,
                        (hipStream_t)stream, frustum, rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW,
                        dims->H * dims->W, dims->W, (int)nprime, *grid, out_geom, cell_of, cell_count, slot_of);
     return launch_status();
@@ -2716,7 +2779,7 @@ int lss_geometry_cells_axes(const float* axes, const float* rots, const float* t
     const long DHW = (long)dims->D * dims->H * dims->W;
     const long nprime = (long)dims->B * dims->N * DHW;
     if (nprime >= INT_MAX) return LSS_EUNSUPPORTED;
-    hipLaunchKernelGGL(k_geometry_cells<true>, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_geometry_cells<true>, dim3(grid_blocks(nprime, kGeoBlock)), dim3(kGeoBlock), 0,
                        (hipStream_t)stream, axes, rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW,
                        dims->H * dims->W, dims->W, (int)nprime, *grid, out_geom, cell_of, cell_count, slot_of);
     return launch_status();
@@ -2726,7 +2789,7 @@ int lss_cells_from_geom(const float* geom, int32_t nprime, int32_t points_per_ba
                         int32_t* cell_of, int32_t* cell_count, int32_t* slot_of, lss_stream_t stream) {
     if (!geom || !cell_of || nprime <= 0 || points_per_batch <= 0 || !grid_ok(grid)) return LSS_EINVAL;
     if (cell_count && !slot_of) return LSS_EINVAL;
-    hipLaunchKernelGGL(k_cells_from_geom, dim3(grid_blocks(nprime, kBlock)), dim3(kBlock), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_cells_from_geom, dim3(grid_blocks(nprime, kGeoBlock)), dim3(kGeoBlock), 0, (hipStream_t)stream,
                        geom, nprime, points_per_batch, *grid, cell_of, cell_count, slot_of);
     return launch_status();
 }

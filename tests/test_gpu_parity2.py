@@ -373,7 +373,7 @@ def test_frustum_axes_geometry_bit_exact(name):
     assert ops.frustum_axes(bent) is None
 
 
-@settings(max_examples=25, deadline=None)
+@settings(max_examples=int(os.environ.get("LSS_HYP_EXAMPLES", "25")), deadline=None)
 @given(seed=st.integers(0, 10_000), B=st.integers(1, 3), N=st.integers(1, 6), fH=st.integers(1, 9),
        fW=st.integers(1, 24), D=st.integers(1, 60), half=st.sampled_from([10.0, 25.0, 50.0]),
        dx=st.sampled_from([0.5, 1.0]), Z=st.sampled_from([1, 2]), bf16_nhwc=st.booleans())
@@ -387,10 +387,21 @@ def test_random_shapes_fwd_bwd_vs_oracle(seed, B, N, fH, fW, D, half, dx, Z, bf1
     rig = _random_rig(np.random.default_rng(seed), B, N, (fH, fW))
     frustum = ref.create_frustum(fd, gc["dbound"])
     assert frustum.shape[:3] == (D, fH, fW)
+    print(f"example seed={seed} B={B} N={N} fH={fH} fW={fW} D={D} half={half} dx={dx} Z={Z} "
+          f"bf16_nhwc={bf16_nhwc}", flush=True)
     plan = ops.plan_from_cameras(frustum.to(DEV), **_dev(rig), grid=grid, inverse="host", want_geom=True)
     geom = ref.get_geometry(frustum, **rig)
     np.testing.assert_array_equal(plan.geom.cpu().numpy(), geom)
     dx_, bx_, nx_ = ref.gen_dx_bx(gc["xbound"], gc["ybound"], gc["zbound"])
+    # the plan's voxel ids and CSR against the oracle, before any kernel reads them
+    ids, kept = ref.quantize(geom, dx_, bx_, nx_)
+    cell = np.where(kept, ref.output_cell(ids, nx_), -1).reshape(-1)
+    np.testing.assert_array_equal(plan.cell_of.cpu().numpy().reshape(-1), cell)
+    cs = plan.cell_start.cpu().numpy().astype(np.int64)
+    np.testing.assert_array_equal(np.diff(cs), np.bincount(cell[cell >= 0], minlength=cs.size - 1))
+    pts = np.nonzero(cell >= 0)[0]
+    want_keys = np.sort((cell[pts].astype(np.int64) << 32) | pts)
+    np.testing.assert_array_equal(plan.sorted_key[:pts.size].cpu().numpy(), want_keys)
     dtype, layout = (torch.bfloat16, _lib.NHWC) if bf16_nhwc else (torch.float32, _lib.NCHW)
     dn = syn.make_depthnet_out(B, N, D, fH, fW, seed=seed)
     dnd = dn.to(DEV, dtype).requires_grad_(True)
