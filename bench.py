@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--overlap-all-reduce", type=int, default=1,
                     help="N>1: one flat master per backward group (BevEncode, trunk head, trunk), each all-reduced "
                          "from its gradient hook on a side stream inside the captured backward")
+    ap.add_argument("--param-groups", type=int, default=1,
+                    help="with --flat-params: one flat master per backward group (BevEncode, trunk head, trunk) "
+                         "at any world size, each group's gradient gathered as soon as the backward completes it")
     ap.add_argument("--flat-params", type=int, default=1,
                     help="trainable parameters as one fp32 master tensor with one bf16 working copy per step")
     ap.add_argument("--profile-steps", type=int, default=8,
@@ -424,13 +427,13 @@ def main():
             parallel.broadcast_state(model)
             parallel.freeze_unused(model)
             overlap = bool(args.overlap_all_reduce) and (world > 1 or FORCE_PG)
-            if args.flat_params and overlap:
+            if args.flat_params and (overlap or args.param_groups):
                 flat = FlatParamGroups(model, lss_backward_groups(), cast_dtype=amp_dtype)
             elif args.flat_params:
                 flat = FlatParams(model, cast_dtype=amp_dtype)
         overlap = bool(args.overlap_all_reduce) and (world > 1 or FORCE_PG) and flat is not None
         if flat is not None:
-            fwd, params = flat.bind(model), (flat.masters if overlap else [flat.master])
+            fwd, params = flat.bind(model), (flat.masters if isinstance(flat, FlatParamGroups) else [flat.master])
         else:
             fwd = model if (args.graph or world == 1) else parallel.make_data_parallel(model, dev)
             params = [p for p in model.parameters() if p.requires_grad]
@@ -525,6 +528,7 @@ def main():
                        "inverse": args.inverse, "fuse_depthnet": bool(args.fuse_depthnet),
                        "depthwise": args.dw_impl, "batchnorm": "hip" if args.hip_bn else "miopen",
                        "step": "hipgraph" if args.graph else "eager", "flat_params": bool(args.flat_params),
+                       "param_groups": bool(args.flat_params and args.param_groups),
                        "plan_side_stream": bool(args.plan_side_stream), "sorted_depth": bool(args.sorted_depth),
                        "all_reduce": ("overlapped with backward (3 groups, captured)" if getattr(step, "overlap", False)
                                       else "one flat all-reduce between the graphs" if (world > 1 or FORCE_PG)
