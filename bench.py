@@ -167,22 +167,29 @@ def write_ceiling(numel, dtype, dev, reps=10) -> dict:
     when the splat runs inside a step (its lines were evicted by the trunk). hipEvents around the
     launch; mean over `reps`."""
     buf = torch.empty(numel, dtype=dtype, device=dev)
+    src = torch.empty_like(buf)
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
-    tot = 0.0
-    for i in range(reps + 2):
-        flush.zero_()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        buf.zero_()
-        e1.record()
-        torch.cuda.synchronize()
-        if i >= 2:
-            tot += e0.elapsed_time(e1)
-    us = tot / reps * 1e3
+
+    def timed(fn) -> float:
+        tot = 0.0
+        for i in range(reps + 2):
+            flush.zero_()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            if i >= 2:
+                tot += e0.elapsed_time(e1)
+        return tot / reps * 1e3
+
+    us = timed(lambda: buf.zero_())
+    us_copy = timed(lambda: buf.copy_(src))  # the copy-kernel ceiling SURVEY 8(d) asks for: read + write
     nbytes = numel * buf.element_size()
-    del buf, flush
+    del buf, src, flush
     return {"what": f"memset of the {nbytes / 1e6:.1f} MB BEV, L2 + Infinity Cache flushed before each launch",
-            "us": round(us, 2), "GB/s": round(nbytes / us / 1e3, 1)}
+            "us": round(us, 2), "GB/s": round(nbytes / us / 1e3, 1),
+            "copy_us": round(us_copy, 2), "copy_GB/s": round(2 * nbytes / us_copy / 1e3, 1)}
 
 
 # ----------------------------------------------------------------------------- HBM traffic (PMC)
