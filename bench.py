@@ -92,7 +92,7 @@ def parse():
                          "at any world size, each group's gradient gathered as soon as the backward completes it")
     ap.add_argument("--flat-params", type=int, default=1,
                     help="trainable parameters as one fp32 master tensor with one bf16 working copy per step")
-    ap.add_argument("--profile-steps", type=int, default=8,
+    ap.add_argument("--profile-steps", type=int, default=20,
                     help="eager steps after the timed region on which the splat kernel is timed")
     ap.add_argument("--pmc-traffic", type=int, default=1, help="rocprofv3 FETCH_SIZE/WRITE_SIZE passes (rank 0, N=1)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
