@@ -1725,6 +1725,12 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 #define LSS_NCHW_WAVES 4  // waves per NCHW tile block (more lane groups share a dense tile's entries)
 #endif
 constexpr int kN2Waves = LSS_NCHW_WAVES;
+#ifndef LSS_NCHW_PAD
+#define LSS_NCHW_PAD 0  // 1: 4 more floats of LDS row padding (the round-2 stride: 27 KB tiles, 5 blocks per CU)
+#endif
+// LDS row stride of the NCHW tile: YT rounded up to 16 B. At YT = 100 the tile is 25.6 KB, so 6 blocks
+// fit a CU (1,536 of c2's 1,600 tiles resident at once instead of 1,280).
+__host__ __device__ constexpr int nchw2_stride(int yt) { return ((yt + 3) & ~3) + 4 * LSS_NCHW_PAD; }
 constexpr int kN2Block = kN2Waves * kWave;
 #ifndef LSS_NCHW_SKIP
 #define LSS_NCHW_SKIP 0  // timing experiments only (wrong output): 1 writes every tile as zeros
@@ -1754,7 +1760,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
     const int ny = min(sg.YT, sg.Y - y0);
     const int x = bzx % sg.X, bz = bzx / sg.X;
     const int cell0 = bzx * sg.Y + y0;
-    const int S = sg.YT + 4;  // LDS row stride (floats; 16-B aligned rows)
+    const int S = nchw2_stride(sg.YT);  // LDS row stride (floats; 16-B aligned rows)
     [[maybe_unused]] const int tslot = tile * kN2Waves + (threadIdx.x >> 6);  // LSS_TRACE builds only
     LSS_STAMP(tslot, 0);
     for (int i = threadIdx.x; i <= ny; i += kN2Block) s_start[i] = cell_start[cell0 + i];
@@ -2999,13 +3005,14 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
     const size_t lds = (size_t)kC * (sg.YT + 4) * sizeof(float);
     if (LSS_NCHW_IMPL == 2 && sg.YT <= 128) {
         const dim3 gr2(xcd_grid(nblocks)), bl2(kN2Block);
+        const size_t lds2 = (size_t)kC * nchw2_stride(sg.YT) * sizeof(float);
 #define LSS_SPLAT2(F, RT, T)                                                                                      \
     do {                                                                                                          \
         if (e0 || e1)                                                                                             \
-            hipExtLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T>), gr2, bl2, (uint32_t)lds, s, e0, e1, 0, depth,   \
+            hipExtLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T>), gr2, bl2, (uint32_t)lds2, s, e0, e1, 0, depth,  \
                                   (const RT*)rows, cell_start, sorted_key, sorted_row, sg, nblocks, (T*)out);     \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T>), gr2, bl2, lds, s, depth, (const RT*)rows,           \
+            hipLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T>), gr2, bl2, lds2, s, depth, (const RT*)rows,          \
                                cell_start, sorted_key, sorted_row, sg, nblocks, (T*)out);                         \
     } while (0)
         if (out_dtype == LSS_F32) {
