@@ -1477,7 +1477,7 @@ template <typename RT> struct RowSlice {
 };
 
 #ifndef LSS_ROW_NT
-#define LSS_ROW_NT 1  // 1: the chunk waves' row stores are non-temporal too (kbench hot state: c5 26.3 -> 23.5 us, c3 equal)
+#define LSS_ROW_NT 0  // 1: the chunk waves' row stores are non-temporal too (rocprof in the c3 graph replays: 12.7-13.0 vs 12.0-12.3 us plain)
 #endif
 template <int EPL>
 __device__ __forceinline__ void store_slice(float* dst, const float* a) {
