@@ -348,6 +348,39 @@ def test_csr_build_ws_direct(ncells, nprime, offset):
 
 
 @pytest.mark.parametrize("name", ["c1", "c3", "c5"])
+def test_geometry_slots_are_a_permutation_per_cell(name):
+    """lss_geometry_cells' slot_of (ranks from the block's LDS table + one device atomic per distinct
+    (block, cell)): the counts are each cell's points and the slots of a cell's points are exactly
+    0 .. count - 1 -- the contract the CSR scatter relies on."""
+    cfg, gc, _ = syn.config_confs(name)
+    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
+    frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
+    grid = ops.GridSpec.from_conf(gc)
+    rig = _dev(syn.make_rig(B, N, fd, seed=3))
+    plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")
+    ncells, nprime = grid.ncells(B), plan.nprime
+    pinv, kinv = ops.camera_inverses(rig["post_rots"], rig["intrins"], "host")
+    ro, tr, pt = [rig[k].float().contiguous() for k in ("rots", "trans", "post_trans")]
+    counts = torch.zeros(ncells, device=DEV, dtype=torch.int32)
+    slot = torch.full((nprime,), -7, device=DEV, dtype=torch.int32)
+    cell_of = torch.empty(nprime, device=DEV, dtype=torch.int32)
+    lib = _lib.load()
+    _lib.check(lib.lss_geometry_cells(_lib.ptr(frustum), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv),
+                                      _lib.ptr(pt), plan.c_dims, grid.c_struct(), None, _lib.ptr(cell_of),
+                                      _lib.ptr(counts), _lib.ptr(slot), _lib.stream_handle(DEV)), "geometry")
+    torch.cuda.synchronize()
+    assert torch.equal(cell_of, plan.cell_of)
+    cell, sl, cnt = cell_of.cpu().long(), slot.cpu().long(), counts.cpu().long()
+    kept = cell >= 0
+    assert (sl[~kept] == -1).all()
+    assert torch.equal(cnt, torch.bincount(cell[kept], minlength=ncells))
+    # (cell, slot) pairs of the kept points are unique and cover [0, count) per cell
+    key = cell[kept] * (int(cnt.max()) + 1) + sl[kept]
+    assert (sl[kept] >= 0).all() and (sl[kept] < cnt[cell[kept]]).all()
+    assert torch.unique(key).numel() == int(kept.sum())
+
+
+@pytest.mark.parametrize("name", ["c1", "c3", "c5"])
 def test_frustum_axes_geometry_bit_exact(name):
     """lss_geometry_cells_axes (the frustum's three axes) == lss_geometry_cells (the full tensor):
     geometry, voxel ids and counts bit for bit."""
