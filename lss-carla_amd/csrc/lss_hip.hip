@@ -1124,7 +1124,7 @@ struct SplatGeo {
 #define LSS_MIN_WAVES 7  // occupancy floor of the channels-last splat (waves per SIMD; VGPR budget 512 / this)
 #endif
 #ifndef LSS_INTERLEAVE
-#define LSS_INTERLEAVE -1  // dispatch order of the block groups: 0 chunks first, 1 interleaved, 2 zero fill first, -1 auto
+#define LSS_INTERLEAVE 0  // dispatch order of the block groups: 0 chunks first, 1 interleaved, 2 zero fill first, -1 by slots
 #endif
 #ifndef LSS_CHUNK_STOP
 #define LSS_CHUNK_STOP 0  // timing experiments only: chunk waves stop after round trip 1 (1) or 2 (2)
@@ -2968,11 +2968,11 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), wpb);
         const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), wpb);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);
-        // Dispatch order of the two roles: chunks first while every chunk wave finds a wave slot at
-        // once (c3: 5,386 chunk waves, 7,168 slots -- they all start at t = 0 and the zero waves take
-        // the slots left); interleaved once the chunk waves outnumber the slots (c5: 12,420), so the
-        // zero fill is not held back behind generations of chunk waves (c5 step-order 24.5 -> 23.4 us;
-        // interleaving at c3 costs 1.6 us).
+        // Dispatch order of the two roles: chunks first (c3: all 5,386 chunk waves start at t = 0 in
+        // the 7,168 wave slots and the zero waves take the slots left). LSS_INTERLEAVE=-1 interleaves
+        // once the chunk waves outnumber the slots (c5: 12,420): faster in kbench's step order (25.0
+        // -> 23.0 us) but not inside the c5 training step's graph replays (rocprof A/B on one box:
+        // 26.2 / 25.3 us interleaved vs 25.1 / 25.3 chunks first), so it is off.
         const long slots = (long)device_cus() * 4 * LSS_MIN_WAVES;
         const int order = LSS_INTERLEAVE >= 0 ? LSS_INTERLEAVE : ((long)nchunk_blocks * wpb > slots ? 1 : 0);
 // kernel-stamped events only when asked for: a plain launch is what a hipGraph capture records
