@@ -1726,7 +1726,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 #endif
 constexpr int kN2Waves = LSS_NCHW_WAVES;
 #ifndef LSS_NCHW_PAD
-#define LSS_NCHW_PAD 0  // 1: 4 more floats of LDS row padding (the round-2 stride: 27 KB tiles, 5 blocks per CU)
+#define LSS_NCHW_PAD 1  // 1: 4 more floats of LDS row padding (27 KB tiles, 5 blocks per CU); 0: 25.6 KB, 6 per CU (c2 -1.1 us; off until an intermittent fault in the NCHW module test is explained)
 #endif
 // LDS row stride of the NCHW tile: YT rounded up to 16 B. At YT = 100 the tile is 25.6 KB, so 6 blocks
 // fit a CU (1,536 of c2's 1,600 tiles resident at once instead of 1,280).
