@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 11
+#define LSS_ABI_VERSION 12
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -50,6 +50,15 @@ typedef void* lss_event_t;  /* a hipEvent_t */
 
 int lss_abi_version(void);
 const char* lss_error_string(int code);
+
+/* Debug builds (liblss_hip_debug.so, compiled with -DLSS_DEBUG=1) check every data-derived global
+ * index of the kernels -- cell ids, CSR positions and totals, point ids, feature and gradient rows --
+ * before use; a failed check is recorded (the index is replaced by 0 instead of faulting) and the
+ * kernels carry on. lss_debug_checks: 1 in a debug build, 0 otherwise. lss_debug_status copies
+ * {failures, first failure's check code, its value, its bound} to out4 (host, 4 ints; all zero in a
+ * release build) and zeroes the record if clear != 0. Synchronous (device-to-host copy). */
+int lss_debug_checks(void);
+int lss_debug_status(int32_t* out4, int32_t clear);
 
 /* Profiling helpers: hipEvents for the optional kernel-timestamp arguments of lss_splat_fwd. */
 int lss_event_create(lss_event_t* ev);
@@ -114,7 +123,12 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
  * bounded spins) and a scatter that also re-zeroes the scan's state and cell_count for the next
  * call. Contract: `workspace` (lss_csr_workspace_bytes(ncells)) is zero-filled before its first
  * use; cell_count is zero-filled before the first lss_geometry_cells / lss_cells_from_geom that
- * counts into it; every call leaves both zero-filled again. One call at a time per workspace. */
+ * counts into it; every call leaves both zero-filled again. One call at a time per workspace (the
+ * caller orders calls that share one: ops.py records the stream and event of its last use).
+ * Workspace header, 4 uint32: [0] scan ticket, [1] sticky count of look-back timeouts (a block that
+ * waited its spin limit for a predecessor sums that predecessor's counts itself: the output is exact
+ * either way), [2] spin-limit override (0: the built-in limit; s > 0: s - 1 polls -- tests of the
+ * timeout path), [3] unused. */
 size_t lss_csr_workspace_bytes(int32_t ncells);
 int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime,
                      int32_t* cell_count, int32_t ncells, const lss_dims_t* dims,

@@ -14,10 +14,11 @@ import torch  # noqa: F401  -- loads the HIP runtime (soname libamdhip64.so.7) b
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblss_hip.so")
+DEBUG_LIB_PATH = os.path.join(_HERE, "liblss_hip_debug.so")  # LSS_DEBUG=1: device-side index checks
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 class Dims(ctypes.Structure):
@@ -46,6 +47,8 @@ _GRID = ctypes.POINTER(Grid)
 SIGNATURES = {
     "lss_abi_version": (ctypes.c_int, []),
     "lss_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "lss_debug_checks": (ctypes.c_int, []),
+    "lss_debug_status": (ctypes.c_int, [_p, _i32]),
     "lss_event_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "lss_event_destroy": (ctypes.c_int, [_p]),
     "lss_event_elapsed_ms": (ctypes.c_int, [_p, _p, ctypes.POINTER(ctypes.c_float)]),
@@ -112,8 +115,17 @@ def load() -> ctypes.CDLL:
     """Load (once) and type the product library; raise if it is absent or of another ABI."""
     global _lib
     if _lib is None:  # LSS_LIB: another build of the same ABI (A/B timing of tuning builds)
-        _lib = open_library(os.environ.get("LSS_LIB") or LIB_PATH)
+        default = DEBUG_LIB_PATH if os.environ.get("LSS_DEBUG", "0") == "1" else LIB_PATH
+        _lib = open_library(os.environ.get("LSS_LIB") or default)
     return _lib
+
+
+def debug_status(clear: bool = True):
+    """(failures, first check code, value, bound) recorded by a LSS_DEBUG build's device checks; all
+    zero for the product library. Synchronous."""
+    out = (ctypes.c_int32 * 4)()
+    check(load().lss_debug_status(ctypes.cast(out, ctypes.c_void_p), int(clear)), "lss_debug_status")
+    return tuple(out)
 
 
 def check(code: int, what: str) -> None:

@@ -17,6 +17,9 @@ SOURCES = [os.path.join(HERE, "csrc", f) for f in ("lss_hip.hip", "lss_convs.hip
                                                             "lss_resample.hip", "lss_se.hip", "lss_simbev.hip")]
 HEADERS = [os.path.join(REPO, "include", h) for h in ("lss_hip.h", "lss_convs.h", "lss_simbev.h")]
 OUT = os.path.join(HERE, "liblss_hip.so")
+# LSS_DEBUG build: every data-derived index checked on the device (include/lss_hip.h, lss_debug_status);
+# loaded instead of the product library when LSS_DEBUG=1 (_lib.py)
+OUT_DEBUG = os.path.join(HERE, "liblss_hip_debug.so")
 ARCH = os.environ.get("LSS_OFFLOAD_ARCH", "gfx950")
 
 
@@ -46,25 +49,31 @@ def build_variant(name: str, defines) -> str:
     return out
 
 
-def up_to_date() -> bool:
-    if not os.path.exists(OUT):
+def up_to_date(out: str = OUT) -> bool:
+    if not os.path.exists(out):
         return False
-    t = os.path.getmtime(OUT)
+    t = os.path.getmtime(out)
     return all(os.path.getmtime(s) <= t for s in SOURCES + HEADERS + [__file__])
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and up_to_date():
-        return OUT
-    cmd = command()
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        sys.stderr.write(r.stdout + r.stderr)
-        raise RuntimeError(f"hipcc failed ({r.returncode}) building {OUT}")
-    if verbose and r.stderr.strip():
-        sys.stderr.write(r.stderr)
+def build(force: bool = False, verbose: bool = True, debug: bool = True) -> str:
+    """The product library and (debug=True) the LSS_DEBUG library, compiled concurrently."""
+    jobs = [(OUT, ())] + ([(OUT_DEBUG, ("LSS_DEBUG=1",))] if debug else [])
+    procs = []
+    for out, defines in jobs:
+        if not force and up_to_date(out):
+            continue
+        cmd = command(out, defines)
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append((out, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+    for out, p in procs:
+        so, se = p.communicate()
+        if p.returncode != 0:
+            sys.stderr.write(so + se)
+            raise RuntimeError(f"hipcc failed ({p.returncode}) building {out}")
+        if verbose and se.strip():
+            sys.stderr.write(se)
     return OUT
 
 

@@ -112,6 +112,48 @@ __device__ __forceinline__ int xcd_block() {
 }
 inline int xcd_grid(long nb) { return (int)(8 * ((nb + 7) / 8)); }
 
+// ---- LSS_DEBUG builds (liblss_hip_debug.so): every global index that comes from data (cell ids, CSR
+// positions, point ids, context rows) is checked before it is used. A failed check records
+// {count, code, value, bound} of the first failure in g_lss_dbg (read by lss_debug_status) and the
+// index is replaced by 0, so the kernel reports instead of faulting. Release builds compile the checks
+// away (dchk(i, n, code) is i).
+#ifndef LSS_DEBUG
+#define LSS_DEBUG 0
+#endif
+__device__ int g_lss_dbg[4];  // [failures, first code, first value, first bound]
+__device__ __attribute__((noinline)) void lss_dbg_fail(int code, long long v, long long hi) {
+    if (atomicAdd(&g_lss_dbg[0], 1) == 0) {
+        g_lss_dbg[1] = code;
+        g_lss_dbg[2] = (int)v;
+        g_lss_dbg[3] = (int)hi;
+    }
+}
+// i if 0 <= i < n; else record the failure and return 0
+__device__ __forceinline__ int dchk(int i, long long n, int code) {
+    if (LSS_DEBUG && (i < 0 || (long long)i >= n)) {
+        lss_dbg_fail(code, i, n);
+        return 0;
+    }
+    return i;
+}
+// a condition that must hold (records only)
+__device__ __forceinline__ void dassert(bool ok, int code, long long v, long long hi) {
+    if (LSS_DEBUG && !ok) lss_dbg_fail(code, v, hi);
+}
+// Check codes (lss_debug_status reports the first failure's code).
+enum : int {
+    kDbgScatterPos = 1,    // counting-sort scatter position outside [cell_start[cell], cell_start[cell + 1])
+    kDbgCsrTotal = 2,      // cell_start[ncells] > nprime
+    kDbgCsrMonotone = 3,   // cell_start decreasing
+    kDbgCanonPos = 4,      // k_csr_canon write position outside [0, total)
+    kDbgSplatPoint = 5,    // splat: point id outside [0, nprime)
+    kDbgSplatRow = 6,      // splat: context row outside [0, rows)
+    kDbgSplatCell = 7,     // splat: cell outside the tile / grid
+    kDbgBwdRow = 8,        // backward: gradient row outside [0, rows)
+    kDbgCell = 9,          // a cell id outside [-1, ncells)
+    kDbgSegRun = 10,       // QuickCumsum operator: run index outside [0, nseg)
+};
+
 // acc = 0; for k: acc = acc + m[k] * v[k]   -- fp32, each op rounded (CPU torch.matmul order).
 __device__ __forceinline__ float dot3_seq(float m0, float m1, float m2, float v0, float v1, float v2) {
     float acc = __fmul_rn(m0, v0);
@@ -430,6 +472,19 @@ __global__ __launch_bounds__(1024) void k_scan_apply(const int32_t* __restrict__
     if (lb == nb - 1 && threadIdx.x == 0) cell_start[ncells] = prefix + s_total;
 }
 
+// Position of a kept point's key in the counting sort: cell_start[cell] + slot (checked in LSS_DEBUG
+// builds: inside the cell's range, and that range inside the nprime-entry buffer).
+__device__ __forceinline__ int scatter_pos(int cell, int slot, const int32_t* __restrict__ cell_start, int nprime) {
+    const int a = cell_start[cell];
+    if (LSS_DEBUG) {
+        const int b = cell_start[cell + 1];
+        dassert(a <= b && b <= nprime, kDbgCsrTotal, b, nprime);
+        dassert(slot >= 0 && a + slot < b, kDbgScatterPos, slot, b - a);
+        return dchk(a + slot, nprime, kDbgScatterPos);
+    }
+    return a + slot;
+}
+
 // Counting-sort scatter: point p lands at cell_start[cell] + slot as the key (cell << 32) | p
 // (slot order inside a cell is the atomics' arrival order; k_csr_canon fixes it).
 __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ cell_of,
@@ -439,7 +494,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ 
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= nprime) return;
     const int cell = cell_of[p];
-    if (cell >= 0) key_out[cell_start[cell] + slot_of[p]] = ((long long)cell << 32) | (unsigned)p;
+    if (cell >= 0) key_out[scatter_pos(cell, slot_of[p], cell_start, nprime)] = ((long long)cell << 32) | (unsigned)p;
 }
 
 // ---- single-pass scan (lss_csr_build_ws): one launch in place of k_scan_partials + k_scan_apply.
@@ -449,16 +504,45 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ 
 // up to the nearest inclusive prefix, and publishes its own inclusive prefix. Granules are written
 // with agent-scope (sc1, write-through) atomic stores and polled with agent-scope atomic loads --
 // the cross-XCD hand-off form of the R2 recipe (cdna_hip_programming.md, Guideline 16). Spins are
-// bounded: after kScanSpinLimit polls a block stops waiting, counts the predecessor as empty and
-// bumps the sticky timeout word (wrong output, never a hang). The scatter re-zeroes the ticket and
+// bounded: after kScanSpinLimit polls a block stops waiting and computes the aggregate of every
+// predecessor that has not published yet straight from its cell counts (intact until the scatter
+// after the scan re-zeroes them), then keeps looking back -- the prefix is exact either way, a
+// timeout only costs time; the sticky timeout word counts them. The scatter re-zeroes the ticket and
 // the granules after the scan, so every call starts from zeros.
 constexpr unsigned kScanSpinLimit = 1u << 22;
 #ifndef LSS_SCAN_TICKET
 #define LSS_SCAN_TICKET 0  // 1: logical index from a ticket counter (one more atomic round trip)
 #endif
-struct ScanWs {  // lss_csr_workspace_bytes: [ticket, timeouts, pad x2][granule x nb]
-    unsigned ticket, timeouts, pad0, pad1;
+struct ScanWs {  // lss_csr_workspace_bytes: [ticket, timeouts, spin_limit_override, pad][granule x nb]
+    unsigned ticket, timeouts;
+    unsigned spin_override;  // 0: kScanSpinLimit polls; s > 0: s - 1 polls (tests of the timeout path)
+    unsigned pad;
 };
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+// Look-back granules still 0 (their block has not published): replaced by the block's aggregate
+// {status 1, sum of its kScanItems counts}, summed by the whole wave from `cnt`. jb = the block each
+// lane polled (>= 0 wherever x == 0).
+__device__ unsigned long long scan_fill_missing(unsigned long long x, int jb, const int32_t* __restrict__ cnt,
+                                                int ncells, int lane) {
+    unsigned long long miss = __ballot(x == 0ull);
+    while (miss) {
+        const int l = __builtin_ctzll(miss);
+        miss &= miss - 1;
+        const int blk = __builtin_amdgcn_readlane(jb, l);
+        const int lo = blk * kScanItems, hi = min(lo + kScanItems, ncells);
+        int s = 0;
+        for (int i = lo + lane; i < hi; i += kWave) s += cnt[i];
+        s = wave_sum_i(s);
+        if (lane == l) x = (1ull << 32) | (unsigned)s;
+    }
+    return x;
+}
 __device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -507,6 +591,9 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
             if (lane == 0) st_agent(&gran[0], (2ull << 32) | (unsigned)agg);
         } else {
             if (lane == 0) st_agent(&gran[lb], (1ull << 32) | (unsigned)agg);
+            const unsigned so = ws->spin_override;
+            const unsigned limit = so ? so - 1u : kScanSpinLimit;
+            bool gave_up = false;
             // 128 predecessors per poll (two granules a lane: distances lane + 1 and lane + 65)
             for (int j = lb - 1;; j -= 2 * kWave) {
                 const int j0 = j - lane, j1 = j0 - kWave;  // past block 0: an inclusive prefix of 0
@@ -515,10 +602,12 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
                     x0 = j0 >= 0 ? ld_agent(&gran[j0]) : (2ull << 32);
                     x1 = j1 >= 0 ? ld_agent(&gran[j1]) : (2ull << 32);
                     if (__all(x0 != 0ull && x1 != 0ull)) break;
-                    if (spins >= kScanSpinLimit) {
-                        if (lane == 0) atomicAdd(&ws->timeouts, 1u);
-                        if (x0 == 0ull) x0 = 2ull << 32;  // give up: an empty inclusive prefix
-                        if (x1 == 0ull) x1 = 2ull << 32;
+                    if (gave_up || spins >= limit) {
+                        // stop waiting: the unpublished predecessors' aggregates from their counts
+                        if (!gave_up && lane == 0) atomicAdd(&ws->timeouts, 1u);
+                        gave_up = true;
+                        x0 = scan_fill_missing(x0, j0, cnt, ncells, lane);
+                        x1 = scan_fill_missing(x1, j1, cnt, ncells, lane);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
@@ -563,7 +652,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter_ws(const int32_t* __restrict
     const int t = blockIdx.x * kBlock + threadIdx.x;
     if (t < nprime) {
         const int cell = cell_of[t];
-        if (cell >= 0) key_out[cell_start[cell] + slot_of[t]] = ((long long)cell << 32) | (unsigned)t;
+        if (cell >= 0) key_out[scatter_pos(cell, slot_of[t], cell_start, nprime)] = ((long long)cell << 32) | (unsigned)t;
     }
     if (t < ncells) cnt[t] = 0;
     const int nb = (ncells + kScanItems - 1) / kScanItems;
@@ -638,7 +727,9 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
     const int e0 = base + lane, e1 = base + kWave + lane;
     // the entry count and the window's keys in ONE round trip: the keys are read unconditionally
     // (clamped into the nprime-entry buffer) and masked with the count afterwards
-    const int total = *total_ptr;
+    const int total_in = *total_ptr;
+    if (LSS_DEBUG && w == 0 && lane == 0) dassert(total_in >= 0 && total_in <= nprime, kDbgCsrTotal, total_in, nprime);
+    const int total = min(total_in, nprime);  // (== total_in for any consistent count)
     const long long k0r = key_in[min(e0, nprime - 1)];
     const long long k1r = key_in[min(e1, nprime - 1)];
     int prev_at = max(base - 1, 0);
@@ -694,14 +785,16 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
         }
     }
     if (e0 >= cc.s && e0 < cc.end) {
-        key_out[cs0 + r0] = k0;
-        row_out[cs0 + r0] = point_row(p0, DHW, HW);
-        if (pos_out) pos_out[p0] = cs0 + r0;
+        const int at = dchk(cs0 + r0, total, kDbgCanonPos);
+        key_out[at] = k0;
+        row_out[at] = point_row(dchk(p0, nprime, kDbgSplatPoint), DHW, HW);
+        if (pos_out) pos_out[p0] = at;
     }
     if (e1 >= cc.s && e1 < cc.end) {
-        key_out[cs1 + r1] = k1;
-        row_out[cs1 + r1] = point_row(p1, DHW, HW);
-        if (pos_out) pos_out[p1] = cs1 + r1;
+        const int at = dchk(cs1 + r1, total, kDbgCanonPos);
+        key_out[at] = k1;
+        row_out[at] = point_row(dchk(p1, nprime, kDbgSplatPoint), DHW, HW);
+        if (pos_out) pos_out[p1] = at;
     }
     if (cc.big_start >= 0) {
         // one cell with more than 64 entries: ordered selection straight from memory (rare)
@@ -724,6 +817,17 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
             last = best;
         }
     }
+}
+
+// LSS_DEBUG builds: the finished CSR -- cell_start non-decreasing from 0 with cell_start[ncells] <=
+// nprime, every cell id in [-1, ncells) -- checked after every build.
+__global__ __launch_bounds__(kBlock) void k_debug_csr(const int32_t* __restrict__ cell_start, int ncells,
+                                                      const int32_t* __restrict__ cell_of, int nprime) {
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (t == 0) dassert(cell_start[0] == 0, kDbgCsrMonotone, cell_start[0], 0);
+    if (t < ncells) dassert(cell_start[t] <= cell_start[t + 1], kDbgCsrMonotone, t, ncells);
+    if (t == ncells) dassert(cell_start[t] <= nprime, kDbgCsrTotal, cell_start[t], nprime);
+    if (t < nprime) dassert(cell_of[t] >= -1 && cell_of[t] < ncells, kDbgCell, cell_of[t], ncells);
 }
 
 // ----------------------------------------------------------------------------- lift prep
@@ -1112,6 +1216,7 @@ __device__ __forceinline__ void unpack16(const uint4& u, const bf16*, float* o) 
 // ----------------------------------------------------------------------------- splat forward
 struct SplatGeo {
     int X, Y, Z, YT, ntiles_y;
+    int ncells, nprime, nrows;  // bounds of the data-derived indices (LSS_DEBUG checks): cells, points, feature rows
 };
 
 #ifndef LSS_PREFETCH
@@ -1196,7 +1301,7 @@ __device__ __forceinline__ void reduce_entries(int base, int s, int end, int c0,
 template <bool FUSED, typename RT>
 __device__ float reduce_big_cell(int start, int nprime, const long long* __restrict__ key,
                                  const int32_t* __restrict__ row, const float* __restrict__ depth,
-                                 const RT* __restrict__ rows_base, int lane, int* cell_out) {
+                                 const RT* __restrict__ rows_base, int lane, int* cell_out, int nrows) {
     const int cell = (int)(key[start] >> 32);
     *cell_out = cell;
     float acc = 0.f;
@@ -1206,8 +1311,8 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
         const bool mine = (int)(k >> 32) == cell;
         const unsigned long long m = __ballot(mine);
         const int n = __popcll(m);  // entries of the cell are contiguous from b
-        const int r = mine ? (FUSED ? row[e] : (int)(k & 0xFFFFFFFF)) : 0;
-        const float w = (FUSED && mine) ? depth[(int)(k & 0xFFFFFFFF)] : 1.f;
+        const int r = mine ? dchk(FUSED ? row[e] : (int)(k & 0xFFFFFFFF), nrows, kDbgSplatRow) : 0;
+        const float w = (FUSED && mine) ? depth[dchk((int)(k & 0xFFFFFFFF), nprime, kDbgSplatPoint)] : 1.f;
         for (int i = 0; i < n; ++i) {
             const float v = to_f32(rows_base[(size_t)__builtin_amdgcn_readlane(r, i) * kC + lane]);
             acc = FUSED ? fmaf(readlane_f(w, i), v, acc) : __fadd_rn(acc, v);
@@ -1286,7 +1391,7 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
                 if (stop == e) {  // one cell longer than 128 entries
                     int cell;
                     const float acc = reduce_big_cell<FUSED, RT>(e, nprime, sorted_key, sorted_row, depth, rows_base,
-                                                                 lane, &cell);
+                                                                 lane, &cell, sg.nrows);
                     flush(cell, acc);
                     e = s_start[min(cell - cell0 + 1, ny)];
                     continue;
@@ -1355,6 +1460,7 @@ struct BevGeo {
     int ncells;
     int dhw, hw;            // points per camera, pixels per camera (context row of point p)
     float inv_dhw, inv_hw;  // their reciprocals (row_of_point; exact for p < 2^24)
+    int nrows;              // feature rows (LSS_DEBUG bound of the gathered row index)
 };
 
 #ifndef LSS_ROW_FROM_P
@@ -1529,9 +1635,10 @@ struct alignas(16) EntryMeta {
 #endif
 template <int LPR, int KU>
 __device__ __forceinline__ float group_weight_load(const EntryMeta* __restrict__ meta,
-                                                   const float* __restrict__ depth, int e, int last, int lane) {
+                                                   const float* __restrict__ depth, int e, int last, int lane,
+                                                   int nprime) {
     static_assert(LPR >= KU, "one lane per entry of the batch");
-    return depth[meta[min(e + lane % LPR, last)].p];
+    return depth[dchk(meta[min(e + lane % LPR, last)].p, nprime, kDbgSplatPoint)];
 }
 // weight of entry e + u of the group (broadcast from the group's lane u; one VGPR held across the wait)
 template <int LPR>
@@ -1618,7 +1725,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
         };
         auto finish = [&](bool last) {  // the cell `cur` ends at this point of the group
             if (cur == first_cell && head_split) put(part + grp * kC);  // a later piece of a cut cell
-            else if (!(last && tail_split)) store_slice<RS::EPL>(cell_row(out, cur, g) + col, acc);
+            else if (!(last && tail_split)) store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + col, acc);
             // else: the first piece of a cut cell stays in acc (combined after the barrier)
         };
         // round trip 2 (one per kUnroll entries of a group): row slices and depth weights in flight together
@@ -1631,12 +1738,12 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
                 const int4 m = *reinterpret_cast<const int4*>(&meta[min(e + u, ge - 1)]);  // (row, p, cell, w)
-                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)m.x * kC + col);
-                if (!LSS_DEPTH_BCAST) wt[u] = (FUSED && !LSS_NO_DEPTH && !sorted_w) ? depth[m.y] : 1.f;
+                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)dchk(m.x, g.nrows, kDbgSplatRow) * kC + col);
+                if (!LSS_DEPTH_BCAST) wt[u] = (FUSED && !LSS_NO_DEPTH && !sorted_w) ? depth[dchk(m.y, nprime, kDbgSplatPoint)] : 1.f;
             }
             // depth weights: CSR-ordered copy (staged in meta), or one wave-wide gather + group broadcast
             const bool bcast = FUSED && !LSS_NO_DEPTH && !sorted_w && LSS_DEPTH_BCAST;
-            const float wd = bcast ? group_weight_load<RS::LPR, kUnroll>(meta, depth, e, ge - 1, lane) : 0.f;
+            const float wd = bcast ? group_weight_load<RS::LPR, kUnroll>(meta, depth, e, ge - 1, lane, nprime) : 0.f;
             if (LSS_CHUNK_STOP == 2) {
                 unsigned x = 0;
 #pragma unroll
@@ -1678,7 +1785,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 #pragma unroll
                 for (int i = 0; i < RS::EPL; ++i) acc[i] = __fadd_rn(acc[i], part[q * kC + col + i]);
             }
-            store_slice<RS::EPL>(cell_row(out, cur, g) + col, acc);
+            store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + col, acc);
         }
         if (kChunkGap > 0) {
             // empty cells after each owned cell, up to kChunkGap of them (the next occupied cell is
@@ -1698,8 +1805,8 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     if (big >= 0) {
         int cell;
         const float a2 = reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base,
-                                                    lane, &cell);
-        cell_row(out, cell, g)[lane] = from_f32<OutT>(a2);
+                                                    lane, &cell, g.nrows);
+        cell_row(out, dchk(cell, g.ncells, kDbgSplatCell), g)[lane] = from_f32<OutT>(a2);
         if (kChunkGap > 0) {
             const int nx = uniform(cell_start[cell + 1]);
             int nc = nx < nprime ? (int)(sorted_key[nx] >> 32) : -1;
@@ -1801,7 +1908,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
         for (int i = 0; i < RS::EPL; ++i) acc[i] = 0.f;
         int cur = -1;
         auto flush = [&]() {
-            float* dst = lds + (size_t)col * S + (cur - cell0);
+            float* dst = lds + (size_t)col * S + dchk(cur - cell0, ny, kDbgSplatCell);
 #pragma unroll
             for (int i = 0; i < RS::EPL; ++i) dst[i * S] = acc[i];
         };
@@ -1829,7 +1936,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
             int cc[KPL];
 #pragma unroll
             for (int t = 0; t < KPL; ++t) {
-                const int pt = (int)(kk[t] & 0xFFFFFFFF);
+                const int pt = dchk((int)(kk[t] & 0xFFFFFFFF), sg.nprime, kDbgSplatPoint);
                 cc[t] = (int)(kk[t] >> 32);
                 wt[t] = FUSED ? depth[pt] : 1.f;
                 if (!FUSED) rr[t] = pt;
@@ -1837,7 +1944,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
             uint4 v[KU];
 #pragma unroll
             for (int u = 0; u < KU; ++u) {
-                const int r = __shfl(rr[u / RS::LPR], gl0 + u % RS::LPR, kWave);
+                const int r = dchk(__shfl(rr[u / RS::LPR], gl0 + u % RS::LPR, kWave), sg.nrows, kDbgSplatRow);
                 v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)r * kC + col);
             }
             if (e + KU < eend) fetch_keys(e + KU);
@@ -2073,7 +2180,7 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES_M) void k_splat_fwd_nhwc
         }
         const bool bcast = FUSED && !sorted_w && LSS_DEPTH_BCAST;
         const float wd = bcast ? group_weight_load<LPR, kUnrollM>(meta, depth, gs < ge ? gs : s, gs < ge ? ge - 1 : s,
-                                                                  lane) : 0.f;
+                                                                  lane, nprime) : 0.f;
         // the zero unit's rows go out while the gathers are in flight (LSS_MERGED_ZERO_LATE: at the end)
         if (!LSS_MERGED_ZERO_LATE) zero_unit_rows<OutT>(zu * kWave, emask, g, out, lane);
         float acc[EPL];
@@ -2116,7 +2223,7 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES_M) void k_splat_fwd_nhwc
                 v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)m.x * kC + col);
                 if (!LSS_DEPTH_BCAST) wt[u] = (FUSED && !sorted_w) ? depth[m.y] : 1.f;
             }
-            const float wd2 = bcast ? group_weight_load<LPR, kUnrollM>(meta, depth, e, ge - 1, lane) : 0.f;
+            const float wd2 = bcast ? group_weight_load<LPR, kUnrollM>(meta, depth, e, ge - 1, lane, nprime) : 0.f;
 #pragma unroll
             for (int u = 0; u < kUnrollM; ++u)
                 if (e + u < ge)
@@ -2160,7 +2267,7 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES_M) void k_splat_fwd_nhwc
     if (big >= 0) {
         int cell;
         const float a2 = reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base, lane,
-                                                    &cell);
+                                                    &cell, g.nrows);
         cell_row(out, cell, g)[lane] = from_f32<OutT>(a2);
     }
 }
@@ -2480,7 +2587,7 @@ __global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? LSS_BWD_MIN_WAVES : 4)
             // rows past D repeat row D - 1 (same line, no extra traffic); their values are zeroed
             const int r = min(k * RPI + sub, D - 1);
             const int row = s_cell[r][jj];
-            const uint4 v = *reinterpret_cast<const uint4*>(g + (size_t)max(row, 0) * kC + col);
+            const uint4 v = *reinterpret_cast<const uint4*>(g + (size_t)dchk(max(row, 0), sg.nrows, kDbgBwdRow) * kC + col);
             raw[i][k] = keep_if(k * RPI + sub < D && row >= 0, v);
         }
     }
@@ -2628,18 +2735,18 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(const float* __restrict__ x,
 // QuickCumsum.backward (src/tools.py:212-219): dx[i] = g[run of row i] -- a pure gather.
 __global__ __launch_bounds__(kBlock) void k_seg_gather(const float* __restrict__ g, int C,
                                                        const int32_t* __restrict__ seg_of, long n_elems,
-                                                       float* __restrict__ dx) {
+                                                       float* __restrict__ dx, int nseg) {
     const long i = (long)blockIdx.x * kBlock + threadIdx.x;
     if ((C & 3) == 0) {
         const long e = i * 4;
         if (e >= n_elems) return;
         const long r = e / C;
         const int c = (int)(e - r * C);
-        *reinterpret_cast<float4*>(dx + e) = *reinterpret_cast<const float4*>(g + (size_t)seg_of[r] * C + c);
+        *reinterpret_cast<float4*>(dx + e) = *reinterpret_cast<const float4*>(g + (size_t)dchk(seg_of[r], nseg, kDbgSegRun) * C + c);
     } else {
         if (i >= n_elems) return;
         const long r = i / C;
-        dx[i] = g[(size_t)seg_of[r] * C + (int)(i - r * C)];
+        dx[i] = g[(size_t)dchk(seg_of[r], nseg, kDbgSegRun) * C + (int)(i - r * C)];
     }
 }
 
@@ -2666,19 +2773,31 @@ inline int choose_yt(int Y) {
     return LSS_YT_MAX;
 }
 
-inline SplatGeo splat_geo(const lss_grid_t* g) {
+// nrows: rows of the feature / gradient buffer the kernel gathers from (0: the dims' pixels)
+inline SplatGeo splat_geo(const lss_grid_t* g, const lss_dims_t* d, long nrows = 0) {
     SplatGeo s;
     s.X = g->nx[0];
     s.Y = g->nx[1];
     s.Z = g->nx[2];
     s.YT = choose_yt(s.Y);
     s.ntiles_y = (s.Y + s.YT - 1) / s.YT;
+    const long pix = (long)d->B * d->N * d->H * d->W;
+    s.ncells = (int)std::min<long>((long)d->B * s.Z * s.X * s.Y, INT_MAX);
+    s.nprime = (int)std::min<long>(pix * d->D, INT_MAX);
+    s.nrows = (int)std::min<long>(nrows > 0 ? nrows : pix, INT_MAX);
     return s;
 }
 
 inline int launch_status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
+}
+
+// LSS_DEBUG builds: the CSR invariants after every build (k_debug_csr); nothing in release builds.
+inline void debug_check_csr(const int32_t* cell_start, int ncells, const int32_t* cell_of, int nprime, hipStream_t s) {
+    if (!LSS_DEBUG) return;
+    hipLaunchKernelGGL(k_debug_csr, dim3(grid_blocks(std::max(ncells + 1, nprime), kBlock)), dim3(kBlock), 0, s,
+                       cell_start, ncells, cell_of, nprime);
 }
 
 inline bool dims_ok(const lss_dims_t* d) {
@@ -2830,6 +2949,7 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
     const int nchunks = (nprime + kWave - 1) / kWave;
     hipLaunchKernelGGL(k_csr_canon, dim3(xcd_grid(grid_blocks(nchunks, kBlock / kWave))), dim3(kBlock), 0, s, tmp_key,
                        cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row, cell_of, pos_of);
+    debug_check_csr(cell_start, ncells, cell_of, nprime, s);
     return launch_status();
 }
 
@@ -2862,7 +2982,21 @@ int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t npr
     const int nchunks = (nprime + kWave - 1) / kWave;
     hipLaunchKernelGGL(k_csr_canon, dim3(xcd_grid(grid_blocks(nchunks, kBlock / kWave))), dim3(kBlock), 0, s, tmp_key,
                        cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row, cell_of, pos_of);
+    debug_check_csr(cell_start, ncells, cell_of, nprime, s);
     return launch_status();
+}
+
+int lss_debug_checks(void) { return LSS_DEBUG ? 1 : 0; }
+
+int lss_debug_status(int32_t* out4, int32_t clear) {
+    if (!out4) return LSS_EINVAL;
+    hipError_t r = hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_lss_dbg), sizeof(int32_t) * 4, 0, hipMemcpyDeviceToHost);
+    if (r != hipSuccess) return (int)r;
+    if (clear) {
+        static const int32_t zeros[4] = {0, 0, 0, 0};
+        r = hipMemcpyToSymbol(HIP_SYMBOL(g_lss_dbg), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
+    }
+    return (int)r;
 }
 
 int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims, float* depth, void* ctx_t,
@@ -2922,10 +3056,10 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
     if (fused && (!depth || !ctx_t || !sorted_row)) return LSS_EINVAL;
     if (fused && ctx_dtype != LSS_F32 && ctx_dtype != LSS_BF16) return LSS_EINVAL;
     if (out_dtype != LSS_F32 && out_dtype != LSS_BF16) return LSS_EINVAL;
-    const SplatGeo sg = splat_geo(grid);
     const long nprime_l = (long)dims->B * dims->N * dims->D * dims->H * dims->W;
     if (nprime_l >= INT_MAX - 2 * kWave) return LSS_EUNSUPPORTED;
     const int nprime = (int)nprime_l;
+    const SplatGeo sg = splat_geo(grid, dims, fused ? 0 : nprime_l);  // lifted mode: one row per point
     const bool nhwc = out_layout == LSS_NHWC;
     const bool ctx_bf16 = fused && ctx_dtype == LSS_BF16;
     const void* rows = fused ? ctx_t : (const void*)x_rows;
@@ -2938,6 +3072,7 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         g.dhw = nprime < (1 << 24) ? dims->D * g.hw : 0;  // 0: read sorted_row instead
         g.inv_dhw = g.dhw ? 1.0f / (float)g.dhw : 0.f;
         g.inv_hw = 1.0f / (float)g.hw;
+        g.nrows = sg.nrows;
         const int wpb = kSplatWaves;
         if (LSS_SPLAT_IMPL == 1) {
             const int nchunks = grid_blocks(nprime, kWave), nunits = grid_blocks(g.ncells, kWave);
@@ -3053,7 +3188,8 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
 int lss_bev_rows(const void* dbev, int32_t g_dtype, const int32_t* cell_start, const lss_dims_t* dims,
                  const lss_grid_t* grid, void* rows, lss_stream_t stream) {
     if (!dims_ok(dims) || !grid_ok(grid) || !dbev || !cell_start || !rows) return LSS_EINVAL;
-    const SplatGeo sg = splat_geo(grid);
+    SplatGeo sg = splat_geo(grid, dims);
+    sg.nrows = sg.ncells;  // gradient rows: one per cell
     const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
     const size_t lds = (size_t)kC * (sg.YT + 1) * sizeof(float);
     hipStream_t s = (hipStream_t)stream;
@@ -3073,7 +3209,8 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
                   void* d_depthnet_out, int32_t d_dtype, lss_stream_t stream) {
     if (!dims_ok(dims) || !grid_ok(grid) || !g || !cell_of || !depth || !ctx_t || !d_depthnet_out) return LSS_EINVAL;
     if (dims->D > 64) return LSS_EUNSUPPORTED;
-    const SplatGeo sg = splat_geo(grid);
+    SplatGeo sg = splat_geo(grid, dims);
+    sg.nrows = sg.ncells;  // gradient rows: one per cell
     const int HW = dims->H * dims->W;
     const int npix = dims->B * dims->N * HW;
     const int wpb = kBlock / kWave;
@@ -3126,7 +3263,8 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
 int lss_splat_bwd_lifted(const void* g, int32_t g_dtype, int32_t rows_layout, const int32_t* cell_of, int32_t nprime,
                          const lss_dims_t* dims, const lss_grid_t* grid, float* dx, lss_stream_t stream) {
     if (!dims_ok(dims) || !grid_ok(grid) || !g || !cell_of || !dx || nprime <= 0) return LSS_EINVAL;
-    const SplatGeo sg = splat_geo(grid);
+    SplatGeo sg = splat_geo(grid, dims);
+    sg.nrows = sg.ncells;  // gradient rows: one per cell
     const dim3 gr(grid_blocks(16L * nprime, kBlock)), bl(kBlock);
     hipStream_t s = (hipStream_t)stream;
     const bool nhwc = rows_layout == LSS_NHWC;
@@ -3183,7 +3321,7 @@ int lss_segment_gather(const float* g, int32_t C, const int32_t* seg_of, int32_t
     const long elems = (long)n * C;
     const long threads = (C & 3) == 0 ? elems / 4 : elems;
     hipLaunchKernelGGL(k_seg_gather, dim3(grid_blocks(threads, kBlock)), dim3(kBlock), 0, (hipStream_t)stream, g, C,
-                       seg_of, elems, dx);
+                       seg_of, elems, dx, INT_MAX);  // (the run count is not part of this ABI: sign check only)
     return launch_status();
 }
 

@@ -15,6 +15,7 @@ Reference boundary replaced (shdragron/LSS-Carla):
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass
 from typing import Optional, Sequence, Tuple
 
@@ -166,24 +167,61 @@ class SplatPlan:
                 if t is not None]
 
 
+class PlanWs:
+    """Persistent state of the plans of one shape on one device (lss_csr_build_ws): the cell counts,
+    the single-pass scan's workspace (zero-filled once here and left zero-filled by every
+    lss_csr_build_ws, so a plan needs no count memset and no scan reset) and the counting sort's
+    scratch. The C ABI allows one plan at a time per workspace; the order between plans on different
+    streams is kept here: every eager plan records an event on its stream after its CSR build, and a
+    plan on another stream first waits for that event. A captured plan (hipGraph) records nothing:
+    torch.cuda.graph synchronises the device before capturing, and the graph's replays must be
+    ordered with other plans of the shape on that device (TrainStep replays and eager steps run on
+    one stream)."""
+
+    def __init__(self, dev: torch.device, ncells: int, nprime: int):
+        lib = _lib.load()
+        self.counts = torch.zeros(ncells, device=dev, dtype=torch.int32)
+        self.workspace = torch.zeros(int(lib.lss_csr_workspace_bytes(ncells)), device=dev, dtype=torch.uint8)
+        self.scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
+        self.last_stream = None
+        self.last_event = None
+
+    def __iter__(self):  # (counts, workspace, scratch)
+        return iter((self.counts, self.workspace, self.scratch))
+
+    def acquire(self, dev: torch.device, capturing: bool) -> None:
+        if capturing or self.last_event is None:
+            return
+        cur = torch.cuda.current_stream(dev)
+        if cur != self.last_stream:
+            cur.wait_event(self.last_event)
+
+    def release(self, dev: torch.device, capturing: bool) -> None:
+        if capturing:
+            return
+        cur = torch.cuda.current_stream(dev)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self.last_stream, self.last_event = cur, ev
+
+    def restore(self) -> None:
+        """After a failed plan: counts and scan state back to zeros (on the current stream)."""
+        self.counts.zero_()
+        self.workspace.zero_()
+
+
 class _PlanWorkspace:
-    """Persistent per-shape state of the plan (lss_csr_build_ws): the cell counts and the single-pass
-    scan's workspace, zero-filled once here and left zero-filled by every lss_csr_build_ws, so a
-    plan needs no count memset and no scan reset. One plan at a time per shape and device (the
-    model builds one per forward, on one stream). Created outside graph capture (the eager warm-up
+    """PlanWs per (device, ncells, nprime). Created outside graph capture (the eager warm-up
     steps); a plan captured before its workspace exists takes the stateless path."""
 
     def __init__(self):
         self._ws = {}
 
-    def get(self, dev: torch.device, ncells: int, nprime: int, create: bool):
+    def get(self, dev: torch.device, ncells: int, nprime: int, create: bool) -> Optional[PlanWs]:
         key = (dev.index, ncells, nprime)
         w = self._ws.get(key)
         if w is None and create:
-            lib = _lib.load()
-            w = (torch.zeros(ncells, device=dev, dtype=torch.int32),
-                 torch.zeros(int(lib.lss_csr_workspace_bytes(ncells)), device=dev, dtype=torch.uint8),
-                 torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8))
+            w = PlanWs(dev, ncells, nprime)
             self._ws[key] = w
         return w
 
@@ -196,13 +234,34 @@ USE_PLAN_WS = True  # False: a count memset + lss_csr_build (two-kernel scan) pe
 
 
 def _plan_counts(dev: torch.device, ncells: int, nprime: int):
-    """(counts, workspace) for one plan: the persistent zero-filled pair, or fresh zeros and None."""
+    """(counts, PlanWs) for one plan: the persistent zero-filled state (acquired: ordered after its
+    last user), or fresh zeros and None."""
     if USE_PLAN_WS:
         capturing = dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
         w = PLAN_WS.get(dev, ncells, nprime, create=not capturing)
         if w is not None:
-            return w[0], w
+            w.acquire(dev, capturing)
+            return w.counts, w
     return torch.zeros(ncells, device=dev, dtype=torch.int32), None
+
+
+def _counted_plan(dev: torch.device, ws: Optional[PlanWs], launch_cells, build_csr):
+    """launch_cells() counts into the plan's cell counts, build_csr() turns them into the CSR. With a
+    persistent workspace, a failure anywhere in between restores its zero-filled state (the counts
+    may already hold this plan's points), and success records its last use."""
+    if ws is None:
+        launch_cells()
+        return build_csr()
+    capturing = dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
+    try:
+        launch_cells()
+        out = build_csr()
+    except Exception:
+        if not capturing:
+            ws.restore()
+        raise
+    ws.release(dev, capturing)
+    return out
 
 
 def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None):
@@ -215,16 +274,10 @@ def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None):
     sorted_row = torch.empty(nprime, device=dev, dtype=torch.int32)
     pos_of = torch.empty(nprime, device=dev, dtype=torch.int32) if SORTED_DEPTH else None
     if ws is not None:
-        _, workspace, scratch = ws
-        try:
-            _lib.check(lib.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
-                                            make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key),
-                                            _lib.ptr(sorted_row), _lib.ptr(pos_of), _lib.ptr(scratch),
-                                            _lib.ptr(workspace), _lib.stream_handle(dev)), "lss_csr_build_ws")
-        except Exception:
-            counts.zero_()  # the call did not leave the persistent state zero-filled: restore it
-            workspace.zero_()
-            raise
+        _lib.check(lib.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
+                                        make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key),
+                                        _lib.ptr(sorted_row), _lib.ptr(pos_of), _lib.ptr(ws.scratch),
+                                        _lib.ptr(ws.workspace), _lib.stream_handle(dev)), "lss_csr_build_ws")
         return cell_start, sorted_key, sorted_row, pos_of
     scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
     _lib.check(lib.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
@@ -239,10 +292,13 @@ _AXES_CACHE = {}
 def frustum_axes(frustum: torch.Tensor) -> Optional[torch.Tensor]:
     """[xs (W) | ys (H) | ds (D)] if `frustum` (D, H, W, 3) is the broadcast of its three axes -- as
     create_frustum builds it (src/models.py:157-168) -- else None (lss_geometry_cells_axes reads
-    71 floats instead of the 4 MB tensor). Checked once per tensor version, outside graph capture."""
+    71 floats instead of the 4 MB tensor). Checked once per tensor version, outside graph capture; a
+    cache entry holds a weak reference to its tensor, so a new tensor at a freed tensor's address (and
+    version 0) never reuses its entry."""
     key = (frustum.data_ptr(), frustum._version, tuple(frustum.shape), str(frustum.device))
-    if key in _AXES_CACHE:
-        return _AXES_CACHE[key]
+    hit = _AXES_CACHE.get(key)
+    if hit is not None and hit[0]() is frustum:
+        return hit[1]
     if frustum.is_cuda and torch.cuda.is_current_stream_capturing():
         return None
     with torch.no_grad():
@@ -254,7 +310,7 @@ def frustum_axes(frustum: torch.Tensor) -> Optional[torch.Tensor]:
         axes = torch.cat([xs, ys, ds]).contiguous() if sep else None
     if len(_AXES_CACHE) > 16:
         _AXES_CACHE.clear()
-    _AXES_CACHE[key] = axes
+    _AXES_CACHE[key] = (weakref.ref(frustum), axes)
     return axes
 
 
@@ -287,13 +343,17 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
     g = grid.c_struct()
     axes = frustum_axes(frustum) if USE_FRUSTUM_AXES else None
     geom_fn = lib.lss_geometry_cells_axes if axes is not None else lib.lss_geometry_cells
-    _lib.check(geom_fn(_lib.ptr(axes if axes is not None else fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv),
-                       _lib.ptr(pinv), _lib.ptr(pt), dims, g, _lib.ptr(geom), _lib.ptr(cell_of), _lib.ptr(counts),
-                       _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
-    cell_start = sorted_key = sorted_row = pos_of = None
-    if want_csr:
-        cell_start, sorted_key, sorted_row, pos_of = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells,
-                                                                dev, ws)
+
+    def launch_cells():
+        _lib.check(geom_fn(_lib.ptr(axes if axes is not None else fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv),
+                           _lib.ptr(pinv), _lib.ptr(pt), dims, g, _lib.ptr(geom), _lib.ptr(cell_of),
+                           _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
+
+    if not want_csr:
+        launch_cells()
+        return SplatPlan((B, N, D, H, W), grid, cell_of, None, None, None, geom, None)
+    cell_start, sorted_key, sorted_row, pos_of = _counted_plan(
+        dev, ws, launch_cells, lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws))
     return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom, pos_of)
 
 
@@ -308,11 +368,14 @@ def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
     cell_of = torch.empty(nprime, device=dev, dtype=torch.int32)
     counts, ws = _plan_counts(dev, ncells, nprime)
     slot_of = torch.empty(nprime, device=dev, dtype=torch.int32)
-    _lib.check(lib.lss_cells_from_geom(_lib.ptr(gm), nprime, nprime // B, grid.c_struct(), _lib.ptr(cell_of),
-                                       _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)),
-               "lss_cells_from_geom")
-    cell_start, sorted_key, sorted_row, pos_of = _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev,
-                                                            ws)
+
+    def launch_cells():
+        _lib.check(lib.lss_cells_from_geom(_lib.ptr(gm), nprime, nprime // B, grid.c_struct(), _lib.ptr(cell_of),
+                                           _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)),
+                   "lss_cells_from_geom")
+
+    cell_start, sorted_key, sorted_row, pos_of = _counted_plan(
+        dev, ws, launch_cells, lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws))
     return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, None, pos_of)
 
 

@@ -303,6 +303,71 @@ def test_single_pass_scan_matches_two_kernel_csr(name):
         assert not words[4:].any() and words[0] == 0, "scan state not re-zeroed"
 
 
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_lookback_timeout_path_is_exact(name):
+    """The look-back scan's timeout path: with the spin limit overridden to 0 polls (workspace word 2),
+    a block that finds a predecessor unpublished at its first poll sums that predecessor's cell counts
+    itself instead of waiting. The CSR must still equal the two-kernel scan's bit for bit (the round-2
+    fallback counted such predecessors as empty: a silently wrong cell_start)."""
+    cfg, gc, _ = syn.config_confs(name)
+    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
+    frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
+    grid = ops.GridSpec.from_conf(gc)
+    ncells = grid.ncells(B)
+    rig = _dev(syn.make_rig(B, N, fd, seed=11))
+    old, ops.USE_PLAN_WS = ops.USE_PLAN_WS, False
+    try:
+        want = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")
+    finally:
+        ops.USE_PLAN_WS = old
+    ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")  # creates the workspace
+    ws = ops.PLAN_WS.get(DEV, ncells, want.nprime, create=False)
+    words = ws.workspace.view(torch.int32)
+    timeouts = 0
+    try:
+        words[2] = 1  # spin limit override: 0 polls
+        for _ in range(3):
+            got = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")
+            torch.cuda.synchronize()
+            assert torch.equal(got.cell_start, want.cell_start)
+            assert torch.equal(got.sorted_key, want.sorted_key)
+        timeouts = int(words[1])
+    finally:
+        words[1] = 0
+        words[2] = 0
+    print(f"{name}: {timeouts} blocks took the timeout path over 3 plans")
+    assert int(ws.counts.abs().sum()) == 0 and not words[4:].any() and int(words[0]) == 0
+
+
+def test_plan_workspace_is_ordered_across_streams():
+    """Plans of one shape built back to back on two streams share the persistent counts / scan state:
+    the second stream waits for the first plan's CSR build (PlanWs event), so both CSRs are exact."""
+    cfg, gc, _ = syn.config_confs("c3")
+    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
+    frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
+    grid = ops.GridSpec.from_conf(gc)
+    rigs = [_dev(syn.make_rig(B, N, fd, seed=s)) for s in (21, 22)]
+    old, ops.USE_PLAN_WS = ops.USE_PLAN_WS, False
+    try:
+        want = [ops.plan_from_cameras(frustum, **r, grid=grid, inverse="host") for r in rigs]
+    finally:
+        ops.USE_PLAN_WS = old
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)]
+    got = []
+    for _ in range(3):
+        for st, r in zip(streams, rigs):
+            with torch.cuda.stream(st):
+                p = ops.plan_from_cameras(frustum, **r, grid=grid, inverse="host")
+                for t in p.tensors():
+                    t.record_stream(st)
+                got.append(p)
+    torch.cuda.synchronize()
+    for i, p in enumerate(got):
+        w = want[i % 2]
+        assert torch.equal(p.cell_start, w.cell_start) and torch.equal(p.sorted_key, w.sorted_key)
+
+
 @pytest.mark.parametrize("ncells,nprime,offset", [(7, 40, 0), (4097, 9000, 1), (600_001, 200_000, 0),
                                                    (600_003, 150_000, 1)])
 def test_csr_build_ws_direct(ncells, nprime, offset):

@@ -34,6 +34,16 @@ def test_library_loads_and_exports_all_symbols():
     # host-side argument validation (no device work): NULL pointers are rejected
     assert lib.lss_camera_inverse(None, None, 0, None, None, None) == -1
     assert lib.lss_csr_scratch_bytes(4096, 100) == 256 + 8 * 100  # scan partials (aligned) + unsorted keys
+    assert lib.lss_debug_checks() == (1 if os.environ.get("LSS_DEBUG", "0") == "1" else 0)
+
+
+def test_debug_library_loads_and_exports_all_symbols():
+    """liblss_hip_debug.so (LSS_DEBUG=1: device-side index checks) exposes the same ABI."""
+    dbg = _lib.open_library(_lib.DEBUG_LIB_PATH)
+    for name in _declared():
+        assert hasattr(dbg, name), name
+    assert dbg.lss_debug_checks() == 1
+    assert dbg.lss_debug_status(None, 0) == -1  # NULL output rejected without touching a device
 
 
 def test_gridspec_matches_reference_quantiser_constants():
