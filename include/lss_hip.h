@@ -16,7 +16,8 @@
  *   cell   k = ((b*Z + z)*X + x)*Y + y,    -1 = dropped     (griddify order,
  *                                                              src/models.py:240-244)
  * H, W are the feature-map sizes (fH, fW = final_dim / 16). C must be 64
- * (camC is hard-coded, src/models.py:148); D <= 64.
+ * (camC is hard-coded, src/models.py:148); D <= 256 (the reference's dbound [4, 45, 1] gives
+ * D = 41; [4, 45, 0.5] gives 82).
  */
 #ifndef LSS_HIP_H
 #define LSS_HIP_H

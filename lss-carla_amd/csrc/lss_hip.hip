@@ -836,7 +836,7 @@ __global__ __launch_bounds__(kBlock) void k_debug_csr(const int32_t* __restrict_
 // back (one memory round trip). depth = softmax_D(logits) is written in the reference's
 // (B*N, D, H, W) layout (coalesced over pixels); the context is transposed through LDS to
 // pixel-major rows ctx_t[q*64 + c] (coalesced 256-B rows).
-template <typename InT, typename CT>
+template <typename InT, typename CT, int NI>  // NI = depth bins per wave part: D <= 4 * NI
 __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn, int D, int HW, int npix,
                                                       float* __restrict__ depth, CT* __restrict__ ctx_t,
                                                       const int32_t* __restrict__ pos_of,
@@ -853,19 +853,19 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
     const int qc = min(q, npix - 1);
     const int bn = qc / HW, hw = qc - bn * HW;
     const InT* src = dn + (size_t)bn * (D + kC) * HW + hw;
-    float cv[16], l[16];
-    int at[16];
+    float cv[16], l[NI];
+    int at[NI];
 #pragma unroll
     for (int i = 0; i < 16; ++i) cv[i] = to_f32(src[(size_t)(D + part * 16 + i) * HW]);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) l[i] = to_f32(src[(size_t)min(part + 4 * i, D - 1) * HW]);
+    for (int i = 0; i < NI; ++i) l[i] = to_f32(src[(size_t)min(part + 4 * i, D - 1) * HW]);
     if (pos_of) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) at[i] = pos_of[(bn * D + min(part + 4 * i, D - 1)) * HW + hw];
+        for (int i = 0; i < NI; ++i) at[i] = pos_of[(bn * D + min(part + 4 * i, D - 1)) * HW + hw];
     }
     float m = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < NI; ++i) {
         if (part + 4 * i >= D) l[i] = -INFINITY;
         m = fmaxf(m, l[i]);
     }
@@ -874,9 +874,9 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
     s_red[0][part][px] = m;
     __syncthreads();
     m = fmaxf(fmaxf(s_red[0][0][px], s_red[0][1][px]), fmaxf(s_red[0][2][px], s_red[0][3][px]));
-    float e[16], sum = 0.f;
+    float e[NI], sum = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < NI; ++i) {
         e[i] = (part + 4 * i < D) ? expf(l[i] - m) : 0.f;
         sum += e[i];
     }
@@ -886,7 +886,7 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
     if (live) {
         float* dst = depth + (size_t)bn * D * HW + hw;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < NI; ++i) {
             const int d = part + 4 * i;
             if (d < D) {
                 const float v = e[i] / sum;
@@ -2346,82 +2346,13 @@ __device__ __forceinline__ size_t row_offset(int cell, const SplatGeo& sg) {
     return (size_t)grad_row<NHWC>(cell, sg) * kC;
 }
 
-// One wave per pixel. The D gradient rows of the pixel's points are gathered into LDS with
-// 16-B lane loads (every load of the pixel in flight at once), then (lane = channel)
-// d_ctx[c] = sum_d g[d][c] depth[d] and (lane = depth bin) d_depth[d] = sum_c g[d][c] ctx[c],
-// softmax backward, write d_depthnet_out.
-template <typename GT, typename DT, typename CT, bool NHWC>
-__global__ __launch_bounds__(kBlock) void k_splat_bwd(const GT* __restrict__ g, const int32_t* __restrict__ cell_of,
-                                                      const float* __restrict__ depth,
-                                                      const CT* __restrict__ ctx_t, int D, int HW, int npix,
-                                                      SplatGeo sg, DT* __restrict__ d_dn) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    constexpr int EPL = 16 / sizeof(GT);    // row elements per 16-B lane load
-    constexpr int LPR = kC / EPL;           // lanes per row
-    constexpr int RPI = kWave / LPR;        // rows per wave-instruction
-    constexpr int NI = kWave / RPI;         // instructions for 64 rows
-    const int lane = threadIdx.x & 63;
-    const int wave = uniform(threadIdx.x >> 6);
-    const int RS = kC + 1;                  // LDS row stride: conflict-free column reads
-    float* R = lds + wave * (D * RS + kC);
-    float* cx = R + D * RS;
-    const int q = blockIdx.x * (kBlock / kWave) + wave;
-    const bool live = q < npix;
-    const int bn = live ? q / HW : 0, hw = live ? q - bn * HW : 0;
-    const size_t pbase = (size_t)bn * D * HW + hw;  // point (bn, d = 0, hw)
-    float my_depth = 0.f;
-    int my_cell = -1;
-    if (live && lane < D) {
-        my_depth = depth[pbase + (size_t)lane * HW];
-        my_cell = cell_of[pbase + (size_t)lane * HW];
-    }
-    if (live) cx[lane] = to_f32(ctx_t[(size_t)q * kC + lane]);
-    const int sub = lane / LPR, chunk = (lane % LPR) * EPL;
-    uint4 raw[NI];
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const int r = k * RPI + sub;
-        const int cell = __shfl(my_cell, r & 63, kWave);  // -1 beyond D
-        raw[k] = make_uint4(0u, 0u, 0u, 0u);
-        if (live && k * RPI < D && cell >= 0)
-            raw[k] = *reinterpret_cast<const uint4*>(g + row_offset<NHWC>(cell, sg) + chunk);
-    }
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const int r = k * RPI + sub;
-        if (k * RPI < D && r < D) {
-            float f[EPL];
-            unpack16(raw[k], (const GT*)nullptr, f);
-#pragma unroll
-            for (int e = 0; e < EPL; ++e) R[r * RS + chunk + e] = f[e];
-        }
-    }
-    __syncthreads();
-    if (!live) return;
-    // d_ctx (lane = c): over depth bins in order d = 0..D-1
-    float dctx = 0.f;
-    for (int d = 0; d < D; ++d) dctx = fmaf(R[d * RS + lane], readlane_f(my_depth, d), dctx);
-    // d_depth (lane = d): over channels
-    float dd = 0.f;
-    if (lane < D) {
-        const float* row = R + lane * RS;
-#pragma unroll 16
-        for (int c = 0; c < kC; ++c) dd = fmaf(row[c], cx[c], dd);
-    }
-    // softmax backward: dl = depth * (dd - sum_d depth*dd)
-    const float s = wave_sum(my_depth * dd);
-    const float dl = my_depth * (dd - s);
-    DT* dst = d_dn + (size_t)bn * (D + kC) * HW + hw;
-    if (lane < D) dst[(size_t)lane * HW] = from_f32<DT>(dl);
-    dst[(size_t)(D + lane) * HW] = from_f32<DT>(dctx);
-}
-
-// Register-only form of k_splat_bwd (no LDS, so occupancy is not capped by a 10.9 KB-per-wave
-// staging buffer): lane (sub, j) holds rows r = k*RPI + sub, channels [EPL*j, EPL*j + EPL) of the
-// pixel's D gradient rows. d_ctx: per-lane sums over its rows, then a butterfly over the RPI row
+// One wave per pixel, registers only: lane (sub, j) holds rows r = k*RPI + sub, channels
+// [EPL*j, EPL*j + EPL) of the pixel's D gradient rows, 64 rows (depth bins) per chunk, CH chunks
+// (D <= 64 CH). d_ctx: per-lane sums over its rows of every chunk, then a butterfly over the RPI row
 // groups; d_depth: per-row dot over the lane's channels, then a butterfly over the LPR lanes of the
-// row. Fixed association order (deterministic); the sums are fp32 like the LDS form.
-template <typename GT, typename DT, typename CT, bool NHWC>
+// row; lane l keeps bin 64k + l of chunk k. Fixed association order (deterministic). The general form
+// of the pixel-tile kernel below (any H*W, any D <= 64*CH).
+template <typename GT, typename DT, typename CT, bool NHWC, int CH>
 __global__ __launch_bounds__(kBlock) void k_splat_bwd_reg(const GT* __restrict__ g, const int32_t* __restrict__ cell_of,
                                                           const float* __restrict__ depth,
                                                           const CT* __restrict__ ctx_t, int D, int HW, int npix,
@@ -2435,68 +2366,78 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd_reg(const GT* __restrict__
     if (q >= npix) return;  // wave-uniform
     const int bn = q / HW, hw = q - bn * HW;
     const size_t pbase = (size_t)bn * D * HW + hw;  // point (bn, d = 0, hw)
-    const int dl_ = min(lane, D - 1);  // clamped, unconditional loads (see keep_if)
-    const float my_depth = keep_if(lane < D, depth[pbase + (size_t)dl_ * HW]);
-    int my_cell = cell_of[pbase + (size_t)dl_ * HW];
-    my_cell = lane < D ? grad_row<NHWC>(my_cell, sg) : -1;  // gradient row index (-1 stays -1)
     const int sub = lane / LPR, col = (lane % LPR) * EPL;
     float cx[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) cx[e] = to_f32(ctx_t[(size_t)q * kC + col + e]);
-    uint4 raw[NI];
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const int cell = __shfl(my_cell, (k * RPI + sub) & 63, kWave);  // -1 beyond D
-        // rows past D (cell -1) read row 0 (one line for the whole instruction) and are zeroed
-        raw[k] = keep_if(cell >= 0, *reinterpret_cast<const uint4*>(g + (size_t)max(cell, 0) * kC + col));
-    }
     float dc[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) dc[e] = 0.f;
-    float part[NI];
+    float my_depth[CH], dd[CH];
 #pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const float w = __shfl(my_depth, (k * RPI + sub) & 63, kWave);  // 0 beyond D
-        float f[EPL];
-        unpack16(raw[k], (const GT*)nullptr, f);
-        float t = 0.f;
+    for (int ch = 0; ch < CH; ++ch) {
+        const int d = ch * kWave + lane;
+        const int dl_ = min(d, D - 1);  // clamped, unconditional loads (see keep_if)
+        my_depth[ch] = keep_if(d < D, depth[pbase + (size_t)dl_ * HW]);
+        int my_cell = cell_of[pbase + (size_t)dl_ * HW];
+        my_cell = d < D ? grad_row<NHWC>(my_cell, sg) : -1;  // gradient row index (-1 stays -1)
+        uint4 raw[NI];
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) {
-            dc[e] = fmaf(f[e], w, dc[e]);
-            t = fmaf(f[e], cx[e], t);
+        for (int k = 0; k < NI; ++k) {
+            const int cell = __shfl(my_cell, (k * RPI + sub) & 63, kWave);  // -1 beyond D
+            // rows past D (cell -1) read row 0 (one line for the whole instruction) and are zeroed
+            raw[k] = keep_if(cell >= 0, *reinterpret_cast<const uint4*>(
+                                            g + (size_t)dchk(max(cell, 0), sg.nrows, kDbgBwdRow) * kC + col));
         }
-        part[k] = t;
+        float part[NI];
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const float w = __shfl(my_depth[ch], (k * RPI + sub) & 63, kWave);  // 0 beyond D
+            float f[EPL];
+            unpack16(raw[k], (const GT*)nullptr, f);
+            float t = 0.f;
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                dc[e] = fmaf(f[e], w, dc[e]);
+                t = fmaf(f[e], cx[e], t);
+            }
+            part[k] = t;
+        }
+        // d_depth of row k*RPI + sub: sum over the LPR lanes of the row
+#pragma unroll
+        for (int k = 0; k < NI; ++k)
+#pragma unroll
+            for (int o = 1; o < LPR; o <<= 1) part[k] += __shfl_xor(part[k], o, kWave);
+        // lane l takes row l of the chunk: instruction l / RPI, held by the lanes of row group l % RPI
+        float v_dd = 0.f;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const float v = __shfl(part[k], (lane % RPI) * LPR, kWave);
+            if (lane / RPI == k) v_dd = v;
+        }
+        dd[ch] = d < D ? v_dd : 0.f;
     }
     // d_ctx: sum over the RPI row groups (lanes j, j + LPR, j + 2 LPR, ...)
 #pragma unroll
     for (int o = LPR; o < kWave; o <<= 1)
 #pragma unroll
         for (int e = 0; e < EPL; ++e) dc[e] += __shfl_xor(dc[e], o, kWave);
-    // d_depth of row k*RPI + sub: sum over the LPR lanes of the row
+    // softmax backward: dl = depth * (dd - sum_d depth * dd)
+    float sd = 0.f;
 #pragma unroll
-    for (int k = 0; k < NI; ++k)
-#pragma unroll
-        for (int o = 1; o < LPR; o <<= 1) part[k] += __shfl_xor(part[k], o, kWave);
-    // lane d takes row d: instruction d / RPI, held by the lanes of row group d % RPI
-    float dd = 0.f;
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const float v = __shfl(part[k], (lane % RPI) * LPR, kWave);
-        if (lane / RPI == k) dd = v;
-    }
-    if (lane >= D) dd = 0.f;
-    const float s = wave_sum(my_depth * dd);
-    const float dl = my_depth * (dd - s);
+    for (int ch = 0; ch < CH; ++ch) sd += my_depth[ch] * dd[ch];
+    const float s = wave_sum(sd);
     DT* dst = d_dn + (size_t)bn * (D + kC) * HW + hw;
-    if (lane < D) dst[(size_t)lane * HW] = from_f32<DT>(dl);
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        const int d = ch * kWave + lane;
+        if (d < D) dst[(size_t)d * HW] = from_f32<DT>(my_depth[ch] * (dd[ch] - s));
+    }
     if (sub == 0)
 #pragma unroll
         for (int e = 0; e < EPL; ++e) dst[(size_t)(D + col + e) * HW] = from_f32<DT>(dc[e]);
 }
 
-#ifndef LSS_BWD_REG
-#define LSS_BWD_REG 1  // 1: k_splat_bwd_reg (registers + shuffles), 0: k_splat_bwd (LDS staging)
-#endif
 #ifndef LSS_BWD_PPW
 #define LSS_BWD_PPW 1  // pixels per wave of k_splat_bwd_tile for bf16 gradients (2: twice the gathers in flight per
                        // wave but 105 VGPRs, two blocks per CU: 12.2 us vs 10.3 us at c3)
@@ -2865,7 +2806,7 @@ int lss_event_record(lss_event_t ev, lss_stream_t stream) {
 const char* lss_error_string(int code) {
     if (code == 0) return "success";
     if (code == LSS_EINVAL) return "lss: invalid argument";
-    if (code == LSS_EUNSUPPORTED) return "lss: unsupported configuration (need C == 64, D <= 64)";
+    if (code == LSS_EUNSUPPORTED) return "lss: unsupported configuration (see include/lss_hip.h: C == 64, D <= 256; fused depthnet D + C <= 128)";
     if (code > 0) return hipGetErrorString((hipError_t)code);
     return "lss: unknown error";
 }
@@ -3002,20 +2943,28 @@ int lss_debug_status(int32_t* out4, int32_t clear) {
 int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims, float* depth, void* ctx_t,
                   int32_t ctx_dtype, const int32_t* pos_of, float* sorted_depth, lss_stream_t stream) {
     if (!dims_ok(dims) || !depthnet_out || !depth || !ctx_t || (pos_of && !sorted_depth)) return LSS_EINVAL;
-    if (dims->D > 64) return LSS_EUNSUPPORTED;
+    if (dims->D > 256) return LSS_EUNSUPPORTED;
     const int HW = dims->H * dims->W;
     const int npix = dims->B * dims->N * HW;
     const dim3 grid(xcd_grid(grid_blocks(npix, 64))), block(kBlock);
     hipStream_t s = (hipStream_t)stream;
-#define LSS_PREP(IT, CT) \
-    hipLaunchKernelGGL((k_lift_prep<IT, CT>), grid, block, 0, s, (const IT*)depthnet_out, dims->D, HW, npix, depth, \
-                       (CT*)ctx_t, pos_of, sorted_depth)
+    // depth bins per wave part: 16 (D <= 64, the reference's D = 41), 32, 64
+#define LSS_PREP_NI(IT, CT, NI)                                                                                    \
+    hipLaunchKernelGGL((k_lift_prep<IT, CT, NI>), grid, block, 0, s, (const IT*)depthnet_out, dims->D, HW, npix,  \
+                       depth, (CT*)ctx_t, pos_of, sorted_depth)
+#define LSS_PREP(IT, CT)                                                                                           \
+    do {                                                                                                           \
+        if (dims->D <= 64) LSS_PREP_NI(IT, CT, 16);                                                                \
+        else if (dims->D <= 128) LSS_PREP_NI(IT, CT, 32);                                                          \
+        else LSS_PREP_NI(IT, CT, 64);                                                                              \
+    } while (0)
     if (in_dtype == LSS_F32 && ctx_dtype == LSS_F32) LSS_PREP(float, float);
     else if (in_dtype == LSS_F32 && ctx_dtype == LSS_BF16) LSS_PREP(float, bf16);
     else if (in_dtype == LSS_BF16 && ctx_dtype == LSS_F32) LSS_PREP(bf16, float);
     else if (in_dtype == LSS_BF16 && ctx_dtype == LSS_BF16) LSS_PREP(bf16, bf16);
     else return LSS_EINVAL;
 #undef LSS_PREP
+#undef LSS_PREP_NI
     return launch_status();
 }
 
@@ -3208,44 +3157,50 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
                   const void* ctx_t, int32_t ctx_dtype, const lss_dims_t* dims, const lss_grid_t* grid,
                   void* d_depthnet_out, int32_t d_dtype, lss_stream_t stream) {
     if (!dims_ok(dims) || !grid_ok(grid) || !g || !cell_of || !depth || !ctx_t || !d_depthnet_out) return LSS_EINVAL;
-    if (dims->D > 64) return LSS_EUNSUPPORTED;
+    if (dims->D > 4 * kWave) return LSS_EUNSUPPORTED;  // D <= 256 (the register kernel's 4 chunks)
     SplatGeo sg = splat_geo(grid, dims);
     sg.nrows = sg.ncells;  // gradient rows: one per cell
     const int HW = dims->H * dims->W;
     const int npix = dims->B * dims->N * HW;
     const int wpb = kBlock / kWave;
-    const size_t lds = (size_t)wpb * (dims->D * (kC + 1) + kC) * sizeof(float);
     const dim3 gr(grid_blocks(npix, wpb)), bl(kBlock);
     hipStream_t s = (hipStream_t)stream;
     const bool nhwc = rows_layout == LSS_NHWC;
+    const int D = dims->D;
+    // pixel tiles (D <= 64, H*W a multiple of the tile) or the register kernel, 64 depth bins per chunk
+#define LSS_BWD_REGK(GT, DT, CT, NH)                                                                              \
+    do {                                                                                                          \
+        if (D <= kWave)                                                                                           \
+            hipLaunchKernelGGL((k_splat_bwd_reg<GT, DT, CT, NH, 1>), gr, bl, 0, s, (const GT*)g, cell_of, depth,  \
+                               (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                           \
+        else if (D <= 2 * kWave)                                                                                  \
+            hipLaunchKernelGGL((k_splat_bwd_reg<GT, DT, CT, NH, 2>), gr, bl, 0, s, (const GT*)g, cell_of, depth,  \
+                               (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                           \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_splat_bwd_reg<GT, DT, CT, NH, 4>), gr, bl, 0, s, (const GT*)g, cell_of, depth,  \
+                               (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                           \
+    } while (0)
 #define LSS_BWD(GT, DT, CT)                                                                                       \
     do {                                                                                                          \
-        constexpr int px = kBwdWaves * (sizeof(GT) == 2 ? LSS_BWD_PPW : 1);                                                 \
+        constexpr int px = kBwdWaves * (sizeof(GT) == 2 ? LSS_BWD_PPW : 1);                                       \
         const dim3 grt(xcd_grid(npix / px)), blt(kBwdBlock);                                                      \
-        if (LSS_BWD_TILE && HW % px == 0 && nhwc && dims->D <= 48)                                                \
+        const bool tile = LSS_BWD_TILE && HW % px == 0 && D <= 64;                                                \
+        if (tile && nhwc && D <= 48)                                                                              \
             hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, true, 48>), grt, blt, 0, s, (const GT*)g, cell_of,  \
-                               depth, (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);              \
-        else if (LSS_BWD_TILE && HW % px == 0 && nhwc)                                                            \
+                               depth, (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                    \
+        else if (tile && nhwc)                                                                                    \
             hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, true, 64>), grt, blt, 0, s, (const GT*)g, cell_of,  \
-                               depth, (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);              \
-        else if (LSS_BWD_TILE && HW % px == 0 && dims->D <= 48)                                                   \
+                               depth, (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                    \
+        else if (tile && D <= 48)                                                                                 \
             hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, false, 48>), grt, blt, 0, s, (const GT*)g, cell_of, \
-                               depth, (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);              \
-        else if (LSS_BWD_TILE && HW % px == 0)                                                                    \
+                               depth, (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                    \
+        else if (tile)                                                                                            \
             hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, false, 64>), grt, blt, 0, s, (const GT*)g, cell_of, \
-                               depth, (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);              \
-        else if (LSS_BWD_REG && nhwc)                                                                             \
-            hipLaunchKernelGGL((k_splat_bwd_reg<GT, DT, CT, true>), gr, bl, 0, s, (const GT*)g, cell_of, depth,   \
-                               (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
-        else if (LSS_BWD_REG)                                                                                     \
-            hipLaunchKernelGGL((k_splat_bwd_reg<GT, DT, CT, false>), gr, bl, 0, s, (const GT*)g, cell_of, depth,  \
-                               (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
+                               depth, (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                    \
         else if (nhwc)                                                                                            \
-            hipLaunchKernelGGL((k_splat_bwd<GT, DT, CT, true>), gr, bl, lds, s, (const GT*)g, cell_of, depth,     \
-                               (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
+            LSS_BWD_REGK(GT, DT, CT, true);                                                                       \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_splat_bwd<GT, DT, CT, false>), gr, bl, lds, s, (const GT*)g, cell_of, depth,    \
-                               (const CT*)ctx_t, dims->D, HW, npix, sg, (DT*)d_depthnet_out);                     \
+            LSS_BWD_REGK(GT, DT, CT, false);                                                                      \
     } while (0)
 #define LSS_BWD2(GT, DT) \
     do { if (ctx_dtype == LSS_BF16) LSS_BWD(GT, DT, bf16); else LSS_BWD(GT, DT, float); } while (0)
@@ -3257,6 +3212,7 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
     else return LSS_EINVAL;
 #undef LSS_BWD2
 #undef LSS_BWD
+#undef LSS_BWD_REGK
     return launch_status();
 }
 

@@ -153,6 +153,21 @@ def _resnet_layer(inplanes, planes, blocks, stride):
     return nn.Sequential(*layers)
 
 
+def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """A stride-1 1x1 nn.Conv2d applied as a GEMM over the channels (F.linear: hipBLASLt) on CUDA maps,
+    with the module's own weight and bias (same math). BevEncode's last conv (up2.4, 128 -> outC = 1
+    channels, src/models.py:115) on MIOpen is not safe to replay from a hipGraph: from the second
+    replay of the captured training step on, its weight and bias gradients came out as garbage
+    (1e35 / 1e-31; every other parameter's gradient replayed within MIOpen's run-to-run noise --
+    tests/test_gpu_captured_step.py)."""
+    if not (x.is_cuda and x.dim() == 4) or conv.kernel_size != (1, 1) or conv.stride != (1, 1) or conv.groups != 1 \
+            or conv.padding not in ((0, 0), "valid"):
+        return conv(x)
+    w = conv.weight.reshape(conv.out_channels, conv.in_channels)
+    y = F.linear(x.permute(0, 2, 3, 1), w, conv.bias)  # (N, H, W, O)
+    return y.permute(0, 3, 1, 2)  # (N, O, H, W), channels-last strides
+
+
 class BevEncode(nn.Module):
     """ResNet-18 stem + layer1-3 + two Up stages (src/models.py:92-130).
 
@@ -201,7 +216,7 @@ class BevEncode(nn.Module):
             x = resample.upsample_cat(x, None, int(u[0].scale_factor))
         else:
             x = u[0](x)
-        return u[4](bn_act(u[2], u[1](x), "relu"))
+        return conv1x1(u[4], bn_act(u[2], u[1](x), "relu"))
 
 
 _SIDE_STREAMS = {}
@@ -315,8 +330,9 @@ class LiftSplatShoot(nn.Module):
                 for t in plan.tensors():
                     t.record_stream(main)  # allocated on the side stream, read on this one
         out_dtype = self._bev_dtype(x.device)
-        if self.fuse_depthnet and out_dtype == torch.bfloat16:
-            # depthnet 1x1 conv + softmax + context layout in one MFMA kernel
+        if self.fuse_depthnet and out_dtype == torch.bfloat16 and self.D + self.camC <= 128:
+            # depthnet 1x1 conv + softmax + context layout in one MFMA kernel; its
+            # tile holds D + C <= 128 output channels (a larger dbound runs the conv as its own op)
             return ops.depthnet_lift_splat(feat, ce.depthnet.weight, ce.depthnet.bias, plan, out_dtype,
                                            self._layout())
         return ops.lift_splat(ce.depthnet(feat), plan, out_dtype, self._layout())

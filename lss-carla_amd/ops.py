@@ -81,14 +81,21 @@ def _f32c(t: torch.Tensor) -> torch.Tensor:
 def camera_inverses(post_rots: torch.Tensor, intrins: torch.Tensor, mode: str = "host"):
     """inv(post_rots), inv(intrins) as (B*N, 9) fp32 device tensors.
 
-    mode='host'   : torch.inverse on the CPU, exactly as src/models.py:180,186 (one D2H + H2D copy).
+    mode='host'   : torch.inverse on the CPU, exactly as src/models.py:180,186 (one D2H + H2D copy;
+                    no D2H copy when the device tensors carry their host copies, ``t._lss_host``,
+                    as simbev.finish_batch attaches them: then nothing synchronises the host).
     mode='device' : lss_camera_inverse (fp64 adjugate rounded to fp32), no host round trip.
     """
     dev = _require_cuda(post_rots, intrins)
     ncam = post_rots.shape[0] * post_rots.shape[1]
     if mode == "host":
-        pinv = torch.inverse(post_rots.detach().cpu().float()).reshape(ncam, 9)
-        kinv = torch.inverse(intrins.detach().cpu().float()).reshape(ncam, 9)
+        def host_copy(t):
+            h = getattr(t, "_lss_host", None)
+            if h is not None and tuple(h.shape) == tuple(t.shape) and not h.is_cuda:
+                return h
+            return t.detach().cpu()
+        pinv = torch.inverse(host_copy(post_rots).float()).reshape(ncam, 9).pin_memory()
+        kinv = torch.inverse(host_copy(intrins).float()).reshape(ncam, 9).pin_memory()
         return pinv.to(dev, non_blocking=True), kinv.to(dev, non_blocking=True)
     if mode != "device":
         raise ValueError(f"inverse mode must be 'host' or 'device', got {mode!r}")

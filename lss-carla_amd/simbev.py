@@ -106,6 +106,29 @@ def resample_table(in_size: int, out_size: int) -> Tuple[int, np.ndarray]:
     return k, tab
 
 
+_DEVICE_TABLES: Dict[Tuple[int, int, int], torch.Tensor] = {}
+
+
+def _device_table(inn: int, outn: int, dev: torch.device) -> Tuple[int, torch.Tensor]:
+    """(ksize, device int32 table) of one resize pass, uploaded once per (device, in, out) through
+    pinned memory without blocking the host (the pinned block is not reused before the copy ran)."""
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), inn, outn)
+    k, tab = resample_table(inn, outn)
+    t = _DEVICE_TABLES.get(key)
+    if t is None:
+        host = torch.from_numpy(tab if tab.size else np.zeros(1, dtype=np.int32)).pin_memory()
+        t = host.to(dev, non_blocking=True)
+        _DEVICE_TABLES[key] = t
+    return k, t
+
+
+def _to_device_pinned(buf: bytes, dev: torch.device) -> torch.Tensor:
+    """Host bytes -> a device uint8 tensor through a pinned staging block, non-blocking."""
+    host = torch.empty(len(buf), dtype=torch.uint8, pin_memory=True)
+    host.numpy()[:] = np.frombuffer(buf, dtype=np.uint8)
+    return host.to(dev, non_blocking=True)
+
+
 # ----------------------------------------------------------------------------- device kernels
 def augment_images(imgs_u8: torch.Tensor, augs: Sequence[dict], final_dim: Sequence[int]) -> torch.Tensor:
     """(n, H, W, 3) uint8 device images + one aug dict per image (resize_dims, crop, flip, rotate) ->
@@ -119,19 +142,23 @@ def augment_images(imgs_u8: torch.Tensor, augs: Sequence[dict], final_dim: Seque
         raise RuntimeError(f"{len(augs)} augmentation records for {n} images")
     fH, fW = int(final_dim[0]), int(final_dim[1])
     lib = _lib.load()
+    dev = imgs_u8.device
     params = (_lib.ImgAug * n)()
-    tables: List[np.ndarray] = []
-    offsets: Dict[Tuple[int, int], int] = {}
+    # the batch's resize tables: device-resident per (in, out) size, concatenated on the device (no
+    # host round trip per batch; the first use of a size uploads it without blocking)
+    tables: List[torch.Tensor] = []
+    offsets: Dict[Tuple[int, int], Tuple[int, int]] = {}
     off = 0
 
     def table(inn, outn):
         nonlocal off
         key = (inn, outn)
         if key not in offsets:
-            k, tab = resample_table(inn, outn)
+            k, tab = _device_table(inn, outn, dev)
             offsets[key] = (off, k)
-            tables.append(tab)
-            off += tab.size
+            if k:
+                tables.append(tab)
+                off += tab.numel()
         return offsets[key]
 
     for i, a in enumerate(augs):
@@ -150,10 +177,9 @@ def augment_images(imgs_u8: torch.Tensor, augs: Sequence[dict], final_dim: Seque
             p.affine[j] = co[j]
         p.h_off, p.h_ksize = table(W, rs_w)
         p.v_off, p.v_ksize = table(H, rs_h)
-    dev = imgs_u8.device
-    tab = torch.from_numpy(np.concatenate(tables) if tables and off else np.zeros(1, dtype=np.int32))
-    tab_d = tab.to(dev, non_blocking=False)
-    par_d = torch.frombuffer(bytearray(bytes(params)), dtype=torch.uint8).to(dev)
+    tab_d = (tables[0] if len(tables) == 1 else torch.cat(tables)) if tables else \
+        torch.zeros(1, device=dev, dtype=torch.int32)
+    par_d = _to_device_pinned(bytes(params), dev)
     src = imgs_u8.contiguous()
     out = torch.empty(n, 3, fH, fW, device=dev, dtype=torch.float32)
     _lib.check(lib.lss_simbev_images(_lib.ptr(src), n, H, W, _lib.ptr(par_d), _lib.ptr(tab_d), fH, fW,
@@ -315,6 +341,10 @@ def finish_batch(batch, final_dim, device):
         augs.extend([rec] * N)
     imgs = augment_images(src, augs, final_dim).view(B, N, 3, int(final_dim[0]), int(final_dim[1]))
     out = [imgs] + [t.to(device, non_blocking=True) for t in (rots, trans, intrins, post_rots, post_trans)]
+    # the host copies ride along: the model's host torch.inverse (src/models.py:180,186) reads them
+    # instead of copying the device tensors back (ops.camera_inverses), so no batch syncs the host
+    out[3]._lss_host = intrins
+    out[4]._lss_host = post_rots
     for t in rest[:-1]:
         out.append(t)  # lidar placeholder (VizData)
     out.append(vehicle_masks(rest[-1].to(device, non_blocking=True)))

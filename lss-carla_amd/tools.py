@@ -94,23 +94,12 @@ def get_batch_iou_device(preds: torch.Tensor, binimgs: torch.Tensor):
         return (pred & tgt).sum().float(), (pred | tgt).sum().float()
 
 
-def get_val_info(model, valloader, loss_fn, device, use_tqdm=True):
-    """Validation loss / IoU over a loader (src/tools.py:243-270).
-
-    Same results and the same return dict as the reference, but the per-batch ``.item()`` syncs
-    are gone: loss (x batch size) and the intersection / union counts accumulate on the device in
-    float64 and are read once at the end. As in the reference, the loss is divided by
-    ``len(valloader.dataset)`` and an empty union raises ZeroDivisionError.
-    """
-    model.eval()
+def val_totals(model, loader, loss_fn, device):
+    """The device accumulators of get_val_info: (sum of loss x batch size, intersection, union) as
+    float64 device tensors; nothing in the loop synchronises the host."""
     total_loss = torch.zeros((), device=device, dtype=torch.float64)
     total_intersect = torch.zeros((), device=device, dtype=torch.float64)
     total_union = torch.zeros((), device=device, dtype=torch.float64)
-    print("running eval...")
-    loader = valloader
-    if use_tqdm:
-        from tqdm import tqdm
-        loader = tqdm(valloader, desc="Validation")
     with torch.no_grad():
         for batch in loader:
             allimgs, rots, trans, intrins, post_rots, post_trans, binimgs = batch
@@ -121,6 +110,24 @@ def get_val_info(model, valloader, loss_fn, device, use_tqdm=True):
             i, u = get_batch_iou_device(preds, binimgs)
             total_intersect += i.double()
             total_union += u.double()
+    return total_loss, total_intersect, total_union
+
+
+def get_val_info(model, valloader, loss_fn, device, use_tqdm=True):
+    """Validation loss / IoU over a loader (src/tools.py:243-270).
+
+    Same results and the same return dict as the reference, but the per-batch ``.item()`` syncs
+    are gone: loss (x batch size) and the intersection / union counts accumulate on the device in
+    float64 (val_totals) and are read once at the end. As in the reference, the loss is divided by
+    ``len(valloader.dataset)`` and an empty union raises ZeroDivisionError.
+    """
+    model.eval()
+    print("running eval...")
+    loader = valloader
+    if use_tqdm:
+        from tqdm import tqdm
+        loader = tqdm(valloader, desc="Validation")
+    total_loss, total_intersect, total_union = val_totals(model, loader, loss_fn, device)
     model.train()
     return {
         "loss": total_loss.item() / len(valloader.dataset),

@@ -174,6 +174,64 @@ def test_config5_backward(layout):
         np.testing.assert_allclose(bev.detach().cpu().numpy(), exact, rtol=0, atol=ATOL)
 
 
+@pytest.mark.parametrize("layout,rows", [(_lib.NCHW, torch.float32), (_lib.NHWC, torch.float32),
+                                         (_lib.NHWC, torch.bfloat16)])
+def test_finer_dbound_d82_fwd_bwd(layout, rows):
+    """dbound [4, 45, 0.5] (D = 82: the reference accepts any dbound, src/models.py:161): lift + splat
+    forward and backward vs the fp64 oracle (lift_prep with 32 bins per wave part, the register
+    backward with two 64-bin chunks). bf16 rows: the oracle on the bf16-rounded depthnet output."""
+    gc = syn.grid_conf(dbound=(4.0, 45.0, 0.5))
+    B, N, fd = 2, 6, (128, 352)
+    rig = syn.make_rig(B, N, fd, seed=9, aug=True)
+    frustum = ref.create_frustum(fd, gc["dbound"])
+    D, H, W = frustum.shape[:3]
+    assert D == 82
+    dn = syn.make_depthnet_out(B, N, D, H, W, seed=9).to(rows).float()
+    plan = ops.plan_from_cameras(frustum.to(DEV), **_dev(rig), grid=ops.GridSpec.from_conf(gc))
+    dnd = dn.to(DEV).to(rows).requires_grad_(True)
+    out_dtype = torch.float32 if rows == torch.float32 else torch.bfloat16
+    bev = ops.lift_splat(dnd, plan, out_dtype, layout)
+    geom = ref.get_geometry(frustum, **rig)
+    dx, bx, nx = ref.gen_dx_bx(gc["xbound"], gc["ybound"], gc["zbound"])
+    _, new_x = ref.lift(dn, D, 64)
+    exact = ref.voxel_pooling_fp64(geom, ref.cam_feats_layout(new_x, B, N).numpy(), dx, bx, nx)
+    got = bev.detach().float().cpu().numpy()
+    if rows == torch.float32:
+        np.testing.assert_allclose(got, exact, rtol=1e-5, atol=ATOL)
+    else:
+        assert (np.abs(got - exact) <= BF16_U * np.abs(exact) + 1e-4).all()
+    dbev = torch.randn(bev.shape, generator=torch.Generator().manual_seed(10)).to(out_dtype)
+    gdev = dbev.to(DEV)
+    if layout == _lib.NHWC:
+        gdev = gdev.contiguous(memory_format=torch.channels_last)
+    bev.backward(gdev)
+    want = ref.lift_splat_backward_fp64(dn.numpy(), geom, dbev.float().numpy(), dx, bx, nx, D, 64)
+    g = dnd.grad.float().cpu().numpy()
+    if rows == torch.float32:
+        np.testing.assert_allclose(g, want, rtol=1e-4, atol=ATOL)
+    else:  # bf16 gradient output: one bf16 rounding of an fp32 sum
+        assert (np.abs(g - want) <= 2 * BF16_U * np.abs(want) + 1e-3).all(), np.abs(g - want).max()
+
+
+def test_module_d82_bf16_autocast_falls_back_to_unfused_depthnet():
+    """D + C = 146 > 128: the fused depthnet kernel cannot take it; under autocast the module runs the
+    depthnet conv as its own op and the lift kernels as usual (forward and backward finite, BEV of
+    the right shape)."""
+    gc = syn.grid_conf(dbound=(4.0, 45.0, 0.5))
+    fd = (128, 352)
+    import lss_carla_amd as L
+    m = L.compile_model(gc, syn.data_aug_conf(fd), 1).to(DEV)
+    m.bev_layout = "nhwc"
+    m.bevencode.to(memory_format=torch.channels_last)
+    rig = _dev(syn.make_rig(1, 6, fd, seed=2))
+    x = syn.make_images(1, 6, fd, seed=2).to(DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = m(x, **rig)
+    out.float().mean().backward()
+    assert out.shape == (1, 1, 200, 200) and torch.isfinite(out.float()).all()
+    assert torch.isfinite(m.camencode.depthnet.weight.grad).all()
+
+
 def test_config5_bf16_channels_last():
     cfg, gc, rig, frustum, dn = _setup("c5")
     plan = ops.plan_from_cameras(frustum.to(DEV), **_dev(rig), grid=ops.GridSpec.from_conf(gc))
