@@ -39,8 +39,17 @@ def _oracle_bev(feat, weight, bias, rig, frustum, gc, B, N):
     return ref.voxel_pooling_fp64(geom, ref.cam_feats_layout(new_x, B, N).numpy(), dx, bx, nx)
 
 
-def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs():
+@pytest.fixture
+def miopen_find():
+    """MIOpen's find (as bench.py runs it), restored afterwards: left on, every later test's new conv
+    shape would run the exhaustive search."""
+    old = torch.backends.cudnn.benchmark
     torch.backends.cudnn.benchmark = True
+    yield
+    torch.backends.cudnn.benchmark = old
+
+
+def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find):
     cfg, gc, dac = syn.config_confs("c3")
     B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
     torch.manual_seed(7)
