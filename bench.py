@@ -93,7 +93,12 @@ def parse():
     ap.add_argument("--flat-params", type=int, default=1,
                     help="trainable parameters as one fp32 master tensor with one bf16 working copy per step")
     ap.add_argument("--profile-steps", type=int, default=20,
-                    help="eager steps after the timed region on which the splat kernel is timed")
+                    help="steps after the timed region over which the splat kernel's time is averaged")
+    ap.add_argument("--in-graph-prof", type=int, default=1,
+                    help="rank 0, N=1, hipgraph: also time the splat inside the captured step's replays with a "
+                         "rocprofv3 --kernel-trace child run of this script (before this process touches the GPU)")
+    ap.add_argument("--watchdog", type=float, default=0.0,
+                    help="seconds after which a rank that has not finished exits non-zero (0: 300 + 2 s per step)")
     ap.add_argument("--pmc-traffic", type=int, default=1, help="rocprofv3 FETCH_SIZE/WRITE_SIZE passes (rank 0, N=1)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-runs", type=int, default=3, help="timed CPU runs per case (median; 1 warm-up before)")
@@ -231,6 +236,45 @@ def measure_traffic(args, B) -> dict | None:
     shutil.rmtree(tmp, ignore_errors=True)
     return {"fetch_bytes_raw": round(out["FETCH_SIZE"]), "write_bytes": round(out["WRITE_SIZE"]),
             "hbm_bytes_per_launch": round(2 * out["FETCH_SIZE"] + out["WRITE_SIZE"])}
+
+
+def measure_in_graph(args) -> dict | None:
+    """The splat's kernel time inside the captured step: a rocprofv3 --kernel-trace child run of this
+    script (same config, 10 timed replays, no eager profile steps), the k_splat_fwd launches of those
+    replays. Runs before this process initialises the GPU; None if rocprofv3 is missing or fails."""
+    prof = shutil.which("rocprofv3")
+    if prof is None or not args.graph:
+        return None
+    tmp = tempfile.mkdtemp(prefix="lss_trace_", dir="/tmp")
+    steps = 10
+    cmd = ["timeout", "-s", "KILL", "280", prof, "--kernel-trace", "--output-format", "csv", "-d", tmp, "-o", "run",
+           "--", sys.executable, os.path.abspath(__file__), "--config", args.config, "--batch", str(args.batch),
+           "--dtype", args.dtype, "--bev-layout", args.bev_layout, "--steps", str(steps), "--warmup", "3",
+           "--profile-steps", "0", "--pmc-traffic", "0", "--cpu-baseline", "0", "--in-graph-prof", "0",
+           "--mode", args.mode]
+    try:
+        r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), capture_output=True, text=True,
+                           timeout=300)
+    except subprocess.TimeoutExpired:
+        log("[bench] in-graph kernel trace timed out")
+        return None
+    files = glob.glob(os.path.join(tmp, "**", "*kernel_trace.csv"), recursive=True)
+    if r.returncode != 0 or not files:
+        log(f"[bench] in-graph kernel trace failed (rc={r.returncode}): {r.stderr[-400:]}")
+        return None
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            rows += [row for row in csv.DictReader(fh) if "k_splat_fwd" in row["Kernel_Name"]]
+    shutil.rmtree(tmp, ignore_errors=True)
+    rows.sort(key=lambda row: int(row["Start_Timestamp"]))
+    # the last launch is the eager step after the replays; the `steps` before it are the timed replays
+    sel = rows[-1 - steps:-1]
+    if len(sel) < steps:
+        return None
+    durs = [(int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3 for row in sel]
+    return {"us": round(sum(durs) / len(durs), 2), "min_us": round(min(durs), 2), "launches": len(durs),
+            "how": "rocprofv3 --kernel-trace of a child run of this script: the 10 timed graph replays"}
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -384,6 +428,21 @@ class FwdStep:
         return self.out
 
 
+def start_watchdog(seconds: float, rank: int):
+    """A rank that is still running after `seconds` (a hung collective or graph replay at N > 1) reports
+    itself and exits non-zero -- no re-exec; the launcher then ends the job."""
+    import threading
+
+    def fire():
+        log(f"[rank {rank}] watchdog: not finished after {seconds:.0f} s (hung replay or collective); exiting")
+        os._exit(3)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 def main():
     args = parse()
     maybe_launch_ranks(args)
@@ -401,8 +460,14 @@ def main():
         t_p = time.perf_counter()
         traffic = measure_traffic(args, B)  # child processes, before this process touches the GPU
         log(f"[rank 0] splat PMC traffic {traffic} ({time.perf_counter() - t_p:.1f} s)")
+    in_graph = None
+    if args.in_graph_prof and args.graph and world == 1 and rank == 0:
+        t_p = time.perf_counter()
+        in_graph = measure_in_graph(args)  # a child process, before this process touches the GPU
+        log(f"[rank 0] splat in the captured step: {in_graph} ({time.perf_counter() - t_p:.1f} s)")
 
     world, rank, dev = setup_dist(args)
+    watchdog = start_watchdog(args.watchdog or 300.0 + 2.0 * (args.steps + args.warmup + args.profile_steps), rank)
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     from lss_carla_amd import ops, parallel
     from lss_carla_amd.flat_params import FlatParams, FlatParamGroups, lss_backward_groups
@@ -496,7 +561,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # the splat kernel, timed with kernel-stamped events (hipExtLaunchKernel) on eager steps after the
+    # the splat kernel alone, kernel-stamped events (hipExtLaunchKernel) on eager steps after the
     # timed region, same inputs (a captured launch cannot carry kernel-stamped events)
     step.eager()  # the first eager step after the replays runs cold: not timed
     torch.cuda.synchronize()
@@ -507,10 +572,13 @@ def main():
     ops.SPLAT_PROFILE.enabled = False
     splat_ms = ops.SPLAT_PROFILE.avg_ms()
     ops.SPLAT_PROFILE.release()
+    per_rank_ms = [1e3 * elapsed / args.steps]
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        per_rank_ms = [1e3 * float(x.item()) / args.steps for x in allt]
+        elapsed = max(float(x.item()) for x in allt)
     log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f} s, out {float(out.float().mean()):.4f}")
 
     if rank == 0:
@@ -540,13 +608,16 @@ def main():
                        "all_reduce": ("overlapped with backward (3 groups, captured)" if getattr(step, "overlap", False)
                                       else "one flat all-reduce between the graphs" if (world > 1 or FORCE_PG)
                                       else None)},
+            "per_rank_ms_per_step": [round(x, 3) for x in per_rank_ms],
             "roofline": {"kernel": "lss_splat_fwd", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
                          "traffic_detail": traffic, "algorithmic_bytes": nbytes,
                          "avg_launch_us": round(splat_ms * 1e3, 2) if splat_ms else None,
-                         "timed_in": "eager steps after the timed replays, kernel-stamped hipEvents",
+                         "timed_in": "eager steps after the timed region, kernel-stamped hipEvents",
+                         "in_graph": dict(in_graph, frac=round(nbytes / (in_graph["us"] * 1e3) / HBM_PEAK_GBS, 4))
+                                     if in_graph else None,
                          "write_ceiling": dict(ceiling, splat_frac_of_ceiling=round(achieved / ceiling["GB/s"], 4)
                                                if achieved else None)},
         }
@@ -560,6 +631,7 @@ def main():
         os.write(result_fd, (json.dumps(res) + "\n").encode())
     if world > 1 or FORCE_PG:
         dist.destroy_process_group()
+    watchdog.cancel()
 
 
 if __name__ == "__main__":
