@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 12
+#define LSS_ABI_VERSION 13
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -45,6 +45,7 @@ typedef struct lss_grid {
 enum { LSS_F32 = 0, LSS_BF16 = 1 };          /* element types */
 enum { LSS_NCHW = 0, LSS_NHWC = 1 };         /* BEV memory layouts of a (B, Z*C, X, Y) tensor */
 enum { LSS_EINVAL = -1, LSS_EUNSUPPORTED = -2 };
+enum { LSS_SPLAT_EMPTY_FILLED = 1 };          /* lss_splat_fwd flags */
 
 typedef void* lss_stream_t; /* a hipStream_t */
 typedef void* lss_event_t;  /* a hipEvent_t */
@@ -143,10 +144,16 @@ int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t npr
  * depthnet_out is (B*N, D+C, H, W) contiguous, element type in_dtype. With pos_of (from
  * lss_csr_build; nullable) every kept point's weight is also written to sorted_depth[pos_of[p]]
  * (Nprime fp32): the splat then reads its weights contiguously, in CSR order, instead of
- * gathering depth[p] per entry. */
+ * gathering depth[p] per entry.
+ * Empty-row fill (bev nullable): bev is the channels-last (B, Z*C, X, Y) BEV of element type
+ * bev_dtype that lss_splat_fwd will write; blocks of this launch beside the lift's own write zeros
+ * into the rows of the cells that are empty by cell_start (of the plan, on bev_grid) -- work that
+ * needs no lift output, done on CUs the lift leaves idle. Pass LSS_SPLAT_EMPTY_FILLED to the
+ * splat then: it writes the occupied rows only. */
 int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims,
                   float* depth, void* ctx_t, int32_t ctx_dtype, const int32_t* pos_of,
-                  float* sorted_depth, lss_stream_t stream);
+                  float* sorted_depth, const int32_t* cell_start, const lss_grid_t* bev_grid, void* bev,
+                  int32_t bev_dtype, lss_stream_t stream);
 
 /* Depthnet + lift, part 1, fused (CamEncode.depthnet 1x1 conv + get_depth_dist + layout,
  * src/models.py:47, 55-59, 192-202): logits = weight . feat + bias on MFMA (bf16 in, fp32
@@ -155,11 +162,12 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
  * depthnet output (B*N, D+C, H, W) is never written. feat (B*N, K, H, W) contiguous, weight
  * (D+C, K) row-major, bias (D+C); dtype and ctx_dtype must be LSS_BF16; K % 16 == 0, K <= 512,
  * D + C <= 128 (else LSS_EUNSUPPORTED). The backward stays the conv's: d(logits) from
- * lss_splat_bwd feeds the 1x1 conv's weight / input gradients. pos_of / sorted_depth as in
- * lss_lift_prep. */
+ * lss_splat_bwd feeds the 1x1 conv's weight / input gradients. pos_of / sorted_depth and the
+ * empty-row fill (cell_start, bev_grid, bev, bev_dtype) as in lss_lift_prep. */
 int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
                       const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype,
-                      const int32_t* pos_of, float* sorted_depth, lss_stream_t stream);
+                      const int32_t* pos_of, float* sorted_depth, const int32_t* cell_start,
+                      const lss_grid_t* bev_grid, void* bev, int32_t bev_dtype, lss_stream_t stream);
 
 /* Splat forward: segmented per-cell sum written as the dense (B, Z*C, X, Y) BEV
  * (voxel_pooling + QuickCumsum.forward + griddify, src/models.py:233-246,
@@ -175,12 +183,14 @@ int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, in
  * unused in lifted mode, where the rows are the point ids). sorted_depth (nullable, fused mode):
  * the depth weights in CSR order as lss_lift_prep / lss_depthnet_lift wrote them; LSS_NHWC then
  * reads them with the keys instead of gathering depth[p] (the same values: identical results).
+ * flags: LSS_SPLAT_EMPTY_FILLED (LSS_NHWC only): the empty cells' rows are already zero (the
+ * lift's fill, lss_lift_prep / lss_depthnet_lift with bev), only the occupied rows are written.
  * ev_start / ev_stop (nullable) are stamped with the kernel's own start / end
  * (hipExtLaunchKernel), so their elapsed time is the kernel alone, never launch latency. */
 int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
                   const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
                   const float* sorted_depth, const lss_dims_t* dims, const lss_grid_t* grid,
-                  void* out, int32_t out_dtype, int32_t out_layout, lss_stream_t stream,
+                  void* out, int32_t out_dtype, int32_t out_layout, int32_t flags, lss_stream_t stream,
                   lss_event_t ev_start, lss_event_t ev_stop);
 
 /* Backward helpers. A "row" is the C gradient values of one cell.

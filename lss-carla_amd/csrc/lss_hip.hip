@@ -830,6 +830,66 @@ __global__ __launch_bounds__(kBlock) void k_debug_csr(const int32_t* __restrict_
     if (t < nprime) dassert(cell_of[t] >= -1 && cell_of[t] < ncells, kDbgCell, cell_of[t], ncells);
 }
 
+// ----------------------------------------------------------------------------- BEV rows (channels-last)
+struct BevGeo {
+    int X, Y, Z;
+    int ncells;
+    int dhw, hw;            // points per camera, pixels per camera (context row of point p)
+    float inv_dhw, inv_hw;  // their reciprocals (row_of_point; exact for p < 2^24)
+    int nrows;              // feature rows (LSS_DEBUG bound of the gathered row index)
+};
+
+// Element offset of cell k's row in the channels-last (B, X, Y, Z*C) BEV:
+// cell ((b*Z + z)*X + x)*Y + y -> ((b*X + x)*Y + y)*Z*C + z*C
+__device__ __forceinline__ size_t cell_row_offset(int cell, const BevGeo& g) {
+    if (g.Z == 1) return (size_t)cell * kC;  // rows of consecutive cells are contiguous
+    const int XY = g.X * g.Y;
+    const int bz = cell / XY, xy = cell - bz * XY;
+    const int b = bz / g.Z, z = bz - b * g.Z;
+    return (((size_t)b * XY + xy) * g.Z + z) * kC;
+}
+template <typename OutT>
+__device__ __forceinline__ OutT* cell_row(OutT* out, int cell, const BevGeo& g) {
+    return out + cell_row_offset(cell, g);
+}
+
+// Empty cells' BEV rows (channels-last, (B, X, Y, Z*C)) written as zeros, 64-cell units. The fill is
+// independent of the lift's data (it needs only cell_start), so the lift kernels run it in blocks of
+// their own on the CUs the lift leaves idle, and the splat then writes the occupied rows only
+// (lss_splat_fwd flag LSS_SPLAT_EMPTY_FILLED). Wave `w` of `nw` takes a contiguous run of units; all its
+// cell_start loads are issued before any store. Row bytes = 64 elements of `esize` bytes, 16-B
+// non-temporal stores.
+constexpr int kFillUnits = 8;  // units per wave per batch (their loads in flight together)
+__device__ void fill_empty_rows(int w, int nw, const int32_t* __restrict__ cell_start, const BevGeo& g,
+                                unsigned char* __restrict__ out, int esize, int lane) {
+    const int nunits = (g.ncells + kWave - 1) / kWave;
+    const int per = (nunits + nw - 1) / nw;
+    const int u_begin = w * per, u_end = min(nunits, u_begin + per);
+    const int lpr = kC * esize / 16, rps = kWave / lpr;  // lanes per row, rows per store instruction
+    for (int u0 = u_begin; u0 < u_end; u0 += kFillUnits) {
+        int a[kFillUnits], b[kFillUnits];
+#pragma unroll
+        for (int i = 0; i < kFillUnits; ++i) {  // clamped, unconditional: every load in flight at once
+            const int k = min((u0 + i) * kWave + lane, g.ncells - 1);
+            a[i] = cell_start[k];
+            b[i] = cell_start[k + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < kFillUnits; ++i) {
+            const int u = u0 + i;
+            if (u >= u_end) break;  // wave-uniform
+            const unsigned long long em = __ballot(u * kWave + lane < g.ncells && a[i] == b[i]);
+            for (int r0 = 0; r0 < kWave; r0 += rps) {
+                const int r = r0 + lane / lpr;
+                if ((em >> r) & 1ull) {
+                    const size_t off = cell_row_offset(u * kWave + r, g) * esize + (lane % lpr) * 16;
+                    __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, reinterpret_cast<u32x4*>(out + off));
+                }
+            }
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------- lift prep
 // One block = 64 consecutive pixels x 4 waves. Wave w owns depth bins d = w, w+4, ... and
 // context channels 16w..16w+15 of every pixel, so all of a thread's loads are issued back to
@@ -840,10 +900,19 @@ template <typename InT, typename CT, int NI>  // NI = depth bins per wave part: 
 __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn, int D, int HW, int npix,
                                                       float* __restrict__ depth, CT* __restrict__ ctx_t,
                                                       const int32_t* __restrict__ pos_of,
-                                                      float* __restrict__ sorted_depth) {
+                                                      float* __restrict__ sorted_depth, int nlift_groups,
+                                                      int nfill_groups, const int32_t* __restrict__ cell_start,
+                                                      BevGeo bg, unsigned char* __restrict__ bev, int esize) {
     __shared__ float s_ctx[kC][65];
     __shared__ float s_red[2][4][64];
-    const int q0 = xcd_block() * 64;
+    const int gi = blockIdx.x >> 3, xcd = blockIdx.x & 7;  // as k_depthnet_lift2: lift groups, then fill groups
+    if (gi >= nlift_groups) {
+        const int fb = xcd * nfill_groups + (gi - nlift_groups);
+        fill_empty_rows(fb * (kBlock / kWave) + (int)(threadIdx.x >> 6), nfill_groups * 8 * (kBlock / kWave),
+                        cell_start, bg, bev, esize, threadIdx.x & 63);
+        return;
+    }
+    const int q0 = (xcd * nlift_groups + gi) * 64;
     if (q0 >= npix) return;  // block-uniform
     const int px = threadIdx.x & 63, part = threadIdx.x >> 6;
     const int q = q0 + px;
@@ -899,6 +968,12 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
         const int r = i >> 6, c = i & 63;
         if (q0 + r < npix) ctx_t[(size_t)(q0 + r) * kC + c] = from_f32<CT>(s_ctx[c][r]);
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_empty(const int32_t* __restrict__ cell_start, BevGeo bg,
+                                                       unsigned char* __restrict__ bev, int esize) {
+    fill_empty_rows(blockIdx.x * (kBlock / kWave) + (int)(threadIdx.x >> 6), gridDim.x * (kBlock / kWave), cell_start,
+                    bg, bev, esize, threadIdx.x & 63);
 }
 
 // ----------------------------------------------------------------------------- depthnet + lift prep (fused)
@@ -1063,7 +1138,9 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
                                                               int npix, float* __restrict__ depth,
                                                               bf16* __restrict__ ctx_t,
                                                               const int32_t* __restrict__ pos_of,
-                                                              float* __restrict__ sorted_depth) {
+                                                              float* __restrict__ sorted_depth, int nlift_groups,
+                                                              int nfill_groups, const int32_t* __restrict__ cell_start,
+                                                              BevGeo bg, unsigned char* __restrict__ bev, int esize) {
     static_assert(K % 32 == 0 && K <= kDnMaxK, "K steps of 32 staged in LDS");
     static_assert(PX % 16 == 0, "16-pixel MFMA column tiles");
     constexpr int kRow = PX * 2 + 8;  // LDS bytes per channel row (+8: spread the banks, 8-B aligned)
@@ -1074,9 +1151,17 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
     __shared__ __attribute__((aligned(16))) unsigned char s_x[K * kRow];  // [k][pixel] bf16
     __shared__ float s_lg[kDnMaxO][PX + 1];                                  // bf16-rounded logits
     __shared__ float s_red[2][kDn2Block / PX][PX];
-    const int q0 = xcd_block() * PX;
-    if (q0 >= npix) return;  // block-uniform
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // blocks come in groups of 8 (one per XCD): nlift_groups of lift blocks (XCD x takes a contiguous
+    // run of pixel tiles), then nfill_groups of blocks that zero the BEV rows of the empty cells
+    const int gi = blockIdx.x >> 3, xcd = blockIdx.x & 7;
+    if (gi >= nlift_groups) {
+        const int fb = xcd * nfill_groups + (gi - nlift_groups);
+        fill_empty_rows(fb * kDn2Waves + wave, nfill_groups * 8 * kDn2Waves, cell_start, bg, bev, esize, lane);
+        return;
+    }
+    const int q0 = (xcd * nlift_groups + gi) * PX;
+    if (q0 >= npix) return;  // block-uniform
     const int O = D + kC;
     [[maybe_unused]] const int tslot = blockIdx.x * kDn2Waves + wave;  // LSS_TRACE builds only
     LSS_STAMP(tslot, 0);
@@ -1455,14 +1540,6 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
 //   zero waves: 64 consecutive cells each; the rows of the empty cells are written as zeros with
 //     16-B stores, so every BEV element is written exactly once.
 // The CSR's sentinel tail (key -1 past the last entry, lss_csr_build) spares a load of the count.
-struct BevGeo {
-    int X, Y, Z;
-    int ncells;
-    int dhw, hw;            // points per camera, pixels per camera (context row of point p)
-    float inv_dhw, inv_hw;  // their reciprocals (row_of_point; exact for p < 2^24)
-    int nrows;              // feature rows (LSS_DEBUG bound of the gathered row index)
-};
-
 #ifndef LSS_ROW_FROM_P
 #define LSS_ROW_FROM_P 0  // 1: chunk waves compute each entry's context row from its point id (no sorted_row read; measured: no gain)
 #endif
@@ -1478,16 +1555,6 @@ __device__ __forceinline__ int row_of_point(int p, const BevGeo& g) {
     if (hw < 0) hw += g.hw;
     if (hw >= g.hw) hw -= g.hw;
     return cam * g.hw + hw;
-}
-
-template <typename OutT>
-__device__ __forceinline__ OutT* cell_row(OutT* out, int cell, const BevGeo& g) {
-    // channels-last (B, X, Y, Z*C): cell ((b*Z + z)*X + x)*Y + y -> ((b*X + x)*Y + y)*Z*C + z*C
-    if (g.Z == 1) return out + (size_t)cell * kC;  // rows of consecutive cells are contiguous
-    const int XY = g.X * g.Y;
-    const int bz = cell / XY, xy = cell - bz * XY;
-    const int b = bz / g.Z, z = bz - b * g.Z;
-    return out + ((((size_t)b * XY + xy) * g.Z + z) * kC);
 }
 
 #ifndef LSS_ZERO_STORE
@@ -2749,6 +2816,33 @@ inline bool grid_ok(const lss_grid_t* g) {
     return g && g->nx[0] > 0 && g->nx[1] > 0 && g->nx[2] > 0 && g->dx[0] > 0.f && g->dx[1] > 0.f && g->dx[2] > 0.f;
 }
 
+// The empty-row fill that rides along a lift launch: channels-last BEV geometry and the number of
+// 8-block fill groups. bev == nullptr: no fill (0 groups).
+#ifndef LSS_FILL_WAVES
+#define LSS_FILL_WAVES 640  // fill waves beside the lift (c3: 80 idle CUs x 8 waves of k_depthnet_lift2)
+#endif
+struct FillPlan {
+    int groups = 0;
+    BevGeo bg{};
+    unsigned char* bev = nullptr;
+    int esize = 0;
+};
+inline int fill_plan(const lss_dims_t* dims, const lss_grid_t* grid, const int32_t* cell_start, void* bev,
+                     int32_t bev_dtype, int waves_per_block, FillPlan* fp) {
+    if (!bev) return 0;
+    if (!cell_start || !grid_ok(grid) || (bev_dtype != LSS_F32 && bev_dtype != LSS_BF16)) return LSS_EINVAL;
+    fp->bg = BevGeo{};
+    fp->bg.X = grid->nx[0];
+    fp->bg.Y = grid->nx[1];
+    fp->bg.Z = grid->nx[2];
+    fp->bg.ncells = dims->B * fp->bg.Z * fp->bg.X * fp->bg.Y;
+    fp->bev = static_cast<unsigned char*>(bev);
+    fp->esize = bev_dtype == LSS_F32 ? 4 : 2;
+    fp->groups = std::max(1, LSS_FILL_WAVES / (8 * waves_per_block));
+    return 0;
+}
+
+
 }  // namespace
 
 // ============================================================================= C ABI
@@ -2941,17 +3035,21 @@ int lss_debug_status(int32_t* out4, int32_t clear) {
 }
 
 int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims, float* depth, void* ctx_t,
-                  int32_t ctx_dtype, const int32_t* pos_of, float* sorted_depth, lss_stream_t stream) {
+                  int32_t ctx_dtype, const int32_t* pos_of, float* sorted_depth, const int32_t* cell_start,
+                  const lss_grid_t* bev_grid, void* bev, int32_t bev_dtype, lss_stream_t stream) {
     if (!dims_ok(dims) || !depthnet_out || !depth || !ctx_t || (pos_of && !sorted_depth)) return LSS_EINVAL;
     if (dims->D > 256) return LSS_EUNSUPPORTED;
+    FillPlan fp;
+    if (fill_plan(dims, bev_grid, cell_start, bev, bev_dtype, kBlock / kWave, &fp)) return LSS_EINVAL;
     const int HW = dims->H * dims->W;
     const int npix = dims->B * dims->N * HW;
-    const dim3 grid(xcd_grid(grid_blocks(npix, 64))), block(kBlock);
+    const int nlg = (grid_blocks(npix, 64) + 7) / 8;
+    const dim3 grid(8 * (nlg + fp.groups)), block(kBlock);
     hipStream_t s = (hipStream_t)stream;
     // depth bins per wave part: 16 (D <= 64, the reference's D = 41), 32, 64
 #define LSS_PREP_NI(IT, CT, NI)                                                                                    \
     hipLaunchKernelGGL((k_lift_prep<IT, CT, NI>), grid, block, 0, s, (const IT*)depthnet_out, dims->D, HW, npix,  \
-                       depth, (CT*)ctx_t, pos_of, sorted_depth)
+                       depth, (CT*)ctx_t, pos_of, sorted_depth, nlg, fp.groups, cell_start, fp.bg, fp.bev, fp.esize)
 #define LSS_PREP(IT, CT)                                                                                           \
     do {                                                                                                           \
         if (dims->D <= 64) LSS_PREP_NI(IT, CT, 16);                                                                \
@@ -2970,27 +3068,39 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
 
 int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
                       const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, const int32_t* pos_of,
-                      float* sorted_depth, lss_stream_t stream) {
+                      float* sorted_depth, const int32_t* cell_start, const lss_grid_t* bev_grid, void* bev,
+                      int32_t bev_dtype, lss_stream_t stream) {
     if (!dims_ok(dims) || !feat || !weight || !bias || !depth || !ctx_t || (pos_of && !sorted_depth)) return LSS_EINVAL;
     if (dtype != LSS_BF16 || ctx_dtype != LSS_BF16) return LSS_EUNSUPPORTED;
     if (K <= 0 || K % 16 != 0 || K > kDnMaxK || dims->D + kC > kDnMaxO) return LSS_EUNSUPPORTED;
     const int HW = dims->H * dims->W;
     const long npix = (long)dims->B * dims->N * HW;
     if (npix >= INT_MAX) return LSS_EUNSUPPORTED;
+    FillPlan fp;
+    hipStream_t s = (hipStream_t)stream;
     if (LSS_DN_IMPL == 2 && K == 512 && HW % 8 == 0) {  // up1's 512 channels
+        // one lift block per CU (its LDS); the fill blocks take the CUs left idle (c3: 176 lift blocks
+        // on 256 CUs), at least LSS_FILL_WAVES waves of them
+        if (fill_plan(dims, bev_grid, cell_start, bev, bev_dtype, kDn2Waves, &fp)) return LSS_EINVAL;
+        const int nlb = grid_blocks(npix, kDn2Pix), nlg = (nlb + 7) / 8;
+        if (fp.bev) fp.groups = std::max(fp.groups, (device_cus() - nlb + 7) / 8);
+        const dim3 gr(8 * (nlg + fp.groups)), bl(kDn2Block);
         if (pos_of)
-            hipLaunchKernelGGL((k_depthnet_lift2<512, kDn2Pix, true>), dim3(xcd_grid(grid_blocks(npix, kDn2Pix))),
-                               dim3(kDn2Block), 0, (hipStream_t)stream, (const bf16*)feat, (const bf16*)weight,
-                               (const bf16*)bias, dims->D, HW, (int)npix, depth, (bf16*)ctx_t, pos_of, sorted_depth);
+            hipLaunchKernelGGL((k_depthnet_lift2<512, kDn2Pix, true>), gr, bl, 0, s, (const bf16*)feat,
+                               (const bf16*)weight, (const bf16*)bias, dims->D, HW, (int)npix, depth, (bf16*)ctx_t,
+                               pos_of, sorted_depth, nlg, fp.groups, cell_start, fp.bg, fp.bev, fp.esize);
         else
-            hipLaunchKernelGGL((k_depthnet_lift2<512, kDn2Pix, false>), dim3(xcd_grid(grid_blocks(npix, kDn2Pix))),
-                               dim3(kDn2Block), 0, (hipStream_t)stream, (const bf16*)feat, (const bf16*)weight,
-                               (const bf16*)bias, dims->D, HW, (int)npix, depth, (bf16*)ctx_t, nullptr, nullptr);
+            hipLaunchKernelGGL((k_depthnet_lift2<512, kDn2Pix, false>), gr, bl, 0, s, (const bf16*)feat,
+                               (const bf16*)weight, (const bf16*)bias, dims->D, HW, (int)npix, depth, (bf16*)ctx_t,
+                               nullptr, nullptr, nlg, fp.groups, cell_start, fp.bg, fp.bev, fp.esize);
         return launch_status();
     }
-    hipLaunchKernelGGL(k_depthnet_lift, dim3(xcd_grid(grid_blocks(npix, kDnPix))), dim3(kBlock), 0, (hipStream_t)stream,
+    if (fill_plan(dims, bev_grid, cell_start, bev, bev_dtype, kBlock / kWave, &fp)) return LSS_EINVAL;
+    hipLaunchKernelGGL(k_depthnet_lift, dim3(xcd_grid(grid_blocks(npix, kDnPix))), dim3(kBlock), 0, s,
                        (const bf16*)feat, (const bf16*)weight, (const bf16*)bias, K, dims->D, HW, (int)npix, depth,
                        (bf16*)ctx_t, pos_of, sorted_depth);
+    if (fp.bev)  // this lift kernel has no fill role: the fill as a launch of its own
+        hipLaunchKernelGGL(k_fill_empty, dim3(8 * fp.groups), dim3(kBlock), 0, s, cell_start, fp.bg, fp.bev, fp.esize);
     return launch_status();
 }
 
@@ -2998,8 +3108,10 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
                   const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
                   const float* sorted_depth,
                   const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout,
-                  lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop) {
+                  int32_t flags, lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop) {
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
+    if (flags & ~LSS_SPLAT_EMPTY_FILLED) return LSS_EINVAL;
+    if ((flags & LSS_SPLAT_EMPTY_FILLED) && out_layout != LSS_NHWC) return LSS_EINVAL;
     if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_key || !out) return LSS_EINVAL;
     const bool fused = x_rows == nullptr;
     if (fused && (!depth || !ctx_t || !sorted_row)) return LSS_EINVAL;
@@ -3050,7 +3162,9 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
             return launch_status();
         }
         const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), wpb);
-        const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), wpb);
+        // the empty rows' zero fill: here, or already done beside the lift (LSS_SPLAT_EMPTY_FILLED)
+        const int nzero_blocks = (flags & LSS_SPLAT_EMPTY_FILLED)
+                                     ? 0 : grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), wpb);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);
         // Dispatch order of the two roles: chunks first (c3: all 5,386 chunk waves start at t = 0 in
         // the 7,168 wave slots and the zero waves take the slots left). LSS_INTERLEAVE=-1 interleaves

@@ -15,6 +15,7 @@ Reference boundary replaced (shdragron/LSS-Carla):
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 from dataclasses import dataclass
 from typing import Optional, Sequence, Tuple
@@ -397,12 +398,6 @@ class _SplatProfile:
     def __init__(self):
         self.enabled = False
         self.pairs = []
-        # Captured mode: while a hipGraph is being captured, bracket the launch with timing
-        # hipEvents on the capture stream (event-record nodes of the graph: a captured launch cannot
-        # carry kernel-stamped events). After each replay, graph_avg_ms() reads the pairs.
-        self.capture = False
-        self.graph_pairs = []
-        self.empty_pairs = []
 
     def reset(self, enabled: bool = True):
         self.release()
@@ -426,31 +421,6 @@ class _SplatProfile:
             _lib.check(lib.lss_event_elapsed_ms(a, b, ctypes.byref(ms)), "lss_event_elapsed_ms")
             tot += ms.value
         return tot / len(self.pairs)
-
-    def new_graph_pair(self, empty: bool = False):
-        lib = _lib.load()
-        a, b = ctypes.c_void_p(), ctypes.c_void_p()
-        _lib.check(lib.lss_event_create(ctypes.byref(a)), "lss_event_create")
-        _lib.check(lib.lss_event_create(ctypes.byref(b)), "lss_event_create")
-        (self.empty_pairs if empty else self.graph_pairs).append((a, b))
-        return a, b
-
-    @staticmethod
-    def _mean_ms(pairs) -> float:
-        lib = _lib.load()
-        tot = 0.0
-        for a, b in pairs:
-            ms = ctypes.c_float()
-            _lib.check(lib.lss_event_elapsed_ms(a, b, ctypes.byref(ms)), "lss_event_elapsed_ms")
-            tot += ms.value
-        return tot / len(pairs)
-
-    def graph_ms(self) -> Optional[Tuple[float, float]]:
-        """(bracketed ms, empty-pair ms) averaged over the captured pairs of the last replay: the
-        splat's duration is the first minus the second (one event-record node's own cost)."""
-        if not self.graph_pairs:
-            return None
-        return self._mean_ms(self.graph_pairs), self._mean_ms(self.empty_pairs)
 
     def release(self):
         if self.pairs:
@@ -485,29 +455,31 @@ def _sorted_depth_buffers(plan: SplatPlan, layout: int, dev):
     return None, None
 
 
-def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, layout: int, sorted_depth=None):
+def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, layout: int, sorted_depth=None,
+                      flags: int = 0):
     lib = _lib.load()
     dev = out.device
     e0, e1 = SPLAT_PROFILE.new_pair() if SPLAT_PROFILE.enabled else (None, None)
-    gpair = None
-    if SPLAT_PROFILE.capture and dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
-        # explicit event-record nodes in the captured graph (lss_event_record)
-        gpair = SPLAT_PROFILE.new_graph_pair()
-        _lib.check(lib.lss_event_record(gpair[0], _lib.stream_handle(dev)), "lss_event_record")
-        e0 = e1 = None
     ctx_code = _lib.dtype_code(ctx_t.dtype) if ctx_t is not None else _lib.F32
     _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), ctx_code, _lib.ptr(x_rows),
                                  _lib.ptr(plan.cell_start),
                                  _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), _lib.ptr(sorted_depth),
                                  plan.c_dims,
-                                 plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype), layout,
+                                 plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype), layout, flags,
                                  _lib.stream_handle(dev), e0, e1), "lss_splat_fwd")
-    if gpair is not None:
-        _lib.check(lib.lss_event_record(gpair[1], _lib.stream_handle(dev)), "lss_event_record")
-        # an empty pair right after: the cost of one event-record node, subtracted by graph_ms()
-        epair = SPLAT_PROFILE.new_graph_pair(empty=True)
-        _lib.check(lib.lss_event_record(epair[0], _lib.stream_handle(dev)), "lss_event_record")
-        _lib.check(lib.lss_event_record(epair[1], _lib.stream_handle(dev)), "lss_event_record")
+
+
+# The channels-last BEV's empty rows are zeroed by blocks of the lift launch (on the CUs the lift leaves
+# idle) instead of by the splat, which then writes the occupied rows only (LSS_SPLAT_EMPTY_FILLED).
+FILL_IN_LIFT = os.environ.get("LSS_FILL_IN_LIFT", "1") == "1"
+
+
+def _fill_args(plan: SplatPlan, out: torch.Tensor, layout: int):
+    """(cell_start, grid, bev, bev dtype) for the lift's empty-row fill and the splat's flags."""
+    if FILL_IN_LIFT and layout == _lib.NHWC:
+        return (_lib.ptr(plan.cell_start), plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype)), \
+            _lib.SPLAT_EMPTY_FILLED
+    return (None, None, None, 0), 0
 
 
 def _grad_rows(plan: SplatPlan, dbev: torch.Tensor) -> Tuple[torch.Tensor, int]:
@@ -552,13 +524,14 @@ class LiftSplat(torch.autograd.Function):
         # and halve the splat's gathered bytes
         ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=dn.dtype)
         pos_of, sorted_depth = _sorted_depth_buffers(plan, layout, dev)
-        _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.dtype_code(dn.dtype), plan.c_dims, _lib.ptr(depth),
-                                     _lib.ptr(ctx_t), _lib.dtype_code(ctx_t.dtype), _lib.ptr(pos_of),
-                                     _lib.ptr(sorted_depth), _lib.stream_handle(dev)),
-                   "lss_lift_prep")
         X, Y, Z = plan.grid.nx
         out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
-        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout, sorted_depth)
+        fill, flags = _fill_args(plan, out, layout)
+        _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.dtype_code(dn.dtype), plan.c_dims, _lib.ptr(depth),
+                                     _lib.ptr(ctx_t), _lib.dtype_code(ctx_t.dtype), _lib.ptr(pos_of),
+                                     _lib.ptr(sorted_depth), *fill, _lib.stream_handle(dev)),
+                   "lss_lift_prep")
+        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout, sorted_depth, flags)
         ctx.save_for_backward(depth, ctx_t)
         ctx.plan = plan
         ctx.dn_dtype = depthnet_out.dtype
@@ -615,13 +588,14 @@ class DepthnetLiftSplat(torch.autograd.Function):
         depth = torch.empty(B * N, D, H, W, device=dev, dtype=torch.float32)
         ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=torch.bfloat16)
         pos_of, sorted_depth = _sorted_depth_buffers(plan, layout, dev)
-        _lib.check(lib.lss_depthnet_lift(_lib.ptr(f), _lib.ptr(w), _lib.ptr(b), _lib.BF16, K, plan.c_dims,
-                                         _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(pos_of),
-                                         _lib.ptr(sorted_depth), _lib.stream_handle(dev)),
-                   "lss_depthnet_lift")
         X, Y, Z = plan.grid.nx
         out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
-        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout, sorted_depth)
+        fill, flags = _fill_args(plan, out, layout)
+        _lib.check(lib.lss_depthnet_lift(_lib.ptr(f), _lib.ptr(w), _lib.ptr(b), _lib.BF16, K, plan.c_dims,
+                                         _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(pos_of),
+                                         _lib.ptr(sorted_depth), *fill, _lib.stream_handle(dev)),
+                   "lss_depthnet_lift")
+        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout, sorted_depth, flags)
         ctx.save_for_backward(f, weight, depth, ctx_t)
         ctx.plan = plan
         return out

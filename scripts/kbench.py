@@ -184,7 +184,7 @@ def main():
             print(f"WARNING {tag}: CSR differs from the product plan", flush=True)
         res[f"depthnet_lift (fused, MFMA){tag}"] = named("depthnet_lift", lambda: _lib.check(l.lss_depthnet_lift(
             _lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims, _lib.ptr(depth), _lib.ptr(ctx_t),
-            _lib.BF16, None, None, st()), "depthnet_lift"))
+            _lib.BF16, None, None, None, None, None, 0, st()), "depthnet_lift"))
         res[f"splat_bwd nhwc bf16{tag}"] = named("splat_bwd nhwc bf16", lambda: _lib.check(l.lss_splat_bwd(
             _lib.ptr(g_bf), _lib.BF16, _lib.NHWC, _lib.ptr(plan.cell_of), _lib.ptr(depth), _lib.ptr(ctx_t),
             _lib.BF16, dims, g, _lib.ptr(d_dn), _lib.BF16, st()), "bwd"))
@@ -200,10 +200,10 @@ def main():
                                           lambda: ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device"))
     sdepth = torch.empty(nprime, device=dev)  # depth weights in CSR order (lift with pos_of)
     res["lift_prep"] = named("lift_prep", lambda: _lib.check(lib.lss_lift_prep(
-        _lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, None, None, st()), "lift"))
+        _lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, None, None, None, None, None, 0, st()), "lift"))
     res["lift_prep (+sorted depth)"] = named("lift_prep (+sorted depth)", lambda: _lib.check(lib.lss_lift_prep(
         _lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(plan.pos_of),
-        _lib.ptr(sdepth), st()), "lift"))
+        _lib.ptr(sdepth), None, None, None, 0, st()), "lift"))
     feat = torch.randn(B * N, 512, H, W, device=dev).to(torch.bfloat16)
     wdn = (torch.randn(D + 64, 512, 1, 1, device=dev) * 0.05).to(torch.bfloat16)
     bdn = torch.zeros(D + 64, device=dev, dtype=torch.bfloat16)
@@ -211,14 +211,14 @@ def main():
                                                 lambda: torch.nn.functional.conv2d(feat, wdn, bdn))
     res["depthnet_lift (fused, MFMA)"] = named("depthnet_lift (fused, MFMA)", lambda: _lib.check(lib.lss_depthnet_lift(
         _lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
-        None, None, st()), "depthnet_lift"))
+        None, None, None, None, None, 0, st()), "depthnet_lift"))
     res["depthnet_lift (+sorted depth)"] = named("depthnet_lift (+sorted depth)", lambda: _lib.check(
         lib.lss_depthnet_lift(_lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims, _lib.ptr(depth),
-                              _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(plan.pos_of), _lib.ptr(sdepth), st()),
+                              _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(plan.pos_of), _lib.ptr(sdepth), None, None, None, 0, st()),
         "depthnet_lift"))
     ctx_f = torch.empty(B * N * H * W, 64, device=dev)
     _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_f), _lib.F32,
-                                 _lib.ptr(plan.pos_of), _lib.ptr(sdepth), st()), "lift")
+                                 _lib.ptr(plan.pos_of), _lib.ptr(sdepth), None, None, None, 0, st()), "lift")
 
     pcsr = (plan.cell_start, plan.sorted_key, plan.sorted_row, plan.pos_of)
 
@@ -227,7 +227,7 @@ def main():
         ctx = ctx_t if ctx is None else ctx
         return lambda: _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx), _lib.dtype_code(ctx.dtype), None,
                                                   _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(its), _lib.ptr(sd), dims, g,
-                                                  _lib.ptr(out), _lib.dtype_code(out.dtype), layout, st(), None, None),
+                                                  _lib.ptr(out), _lib.dtype_code(out.dtype), layout, 0, st(), None, None),
                                   "fwd")
 
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
@@ -268,13 +268,13 @@ def main():
                 lib_plan(l, csr)
                 _lib.check(l.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx),
                                            _lib.dtype_code(ctx.dtype), _lib.ptr(po if sd is not None else None),
-                                           _lib.ptr(sd), st()), "lift")
+                                           _lib.ptr(sd), None, None, None, 0, st()), "lift")
             a, b = ct.c_void_p(), ct.c_void_p()
             l.lss_event_create(ct.byref(a))
             l.lss_event_create(ct.byref(b))
             _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx), _lib.dtype_code(ctx.dtype), None, _lib.ptr(cs),
                                        _lib.ptr(sk), _lib.ptr(its), _lib.ptr(sd), dims, g, _lib.ptr(out),
-                                       _lib.dtype_code(out.dtype), layout, st(), a, b), "fwd")
+                                       _lib.dtype_code(out.dtype), layout, 0, st(), a, b), "fwd")
             ms = ct.c_float()
             l.lss_event_elapsed_ms(a, b, ct.byref(ms))
             if i >= 3:
@@ -305,7 +305,7 @@ def main():
     d_dn = torch.empty_like(dn)
     def restore_lift():  # lib_rows rewrites depth / ctx_t through the fused lift
         _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, None,
-                                     None, st()), "lift")
+                                     None, None, None, None, 0, st()), "lift")
     lib_rows(lib, "")
     restore_lift()
     for path in sorted(glob.glob(os.path.join(REPO, "lss-carla_amd", "variants", "*.so"))) if args.variants else []:
@@ -321,7 +321,7 @@ def main():
             print(f"WARNING variant {name}: output differs from the product kernel", flush=True)
         vsd = torch.empty(nprime, device=dev)
         _lib.check(vl.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
-                                    _lib.ptr(vcsr[3]), _lib.ptr(vsd), st()), "lift")
+                                    _lib.ptr(vcsr[3]), _lib.ptr(vsd), None, None, None, 0, st()), "lift")
         for m in modes:
             res[f"{m} splat_fwd nhwc bf16 [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m)
             res[f"{m} splat_fwd nhwc bf16 (sorted depth) [{name}]"] = stamped(vl, bev_bf, _lib.NHWC, vcsr, mode=m,

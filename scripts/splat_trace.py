@@ -51,14 +51,14 @@ def main():
             flush.zero_()
             plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device")
         _lib.check(l.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16,
-                                   _lib.ptr(plan.pos_of), _lib.ptr(sdepth), st), "lift")
+                                   _lib.ptr(plan.pos_of), _lib.ptr(sdepth), None, None, None, 0, st), "lift")
         e0, e1 = ct.c_void_p(), ct.c_void_p()
         l.lss_event_create(ct.byref(e0))
         l.lss_event_create(ct.byref(e1))
         _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, None, _lib.ptr(plan.cell_start),
                                    _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), _lib.ptr(sdepth), dims, g,
                                    _lib.ptr(out),
-                                   _lib.BF16, _lib.NHWC, st, e0, e1), "fwd")
+                                   _lib.BF16, _lib.NHWC, 0, st, e0, e1), "fwd")
         ms = ct.c_float()
         l.lss_event_elapsed_ms(e0, e1, ct.byref(ms))
     torch.cuda.synchronize()

@@ -90,13 +90,13 @@ def main():
                                             _lib.ptr(counts), _lib.ptr(slot), st), "geom")
         elif a.kernel == "nchw":  # config 2's forward: fp32 context rows, fp32 NCHW BEV
             _lib.check(l.lss_lift_prep(_lib.ptr(dnf), _lib.F32, dims, _lib.ptr(depth), _lib.ptr(ctxf), _lib.F32,
-                                       None, None, st), "lift")
+                                       None, None, None, None, None, 0, st), "lift")
             _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctxf), _lib.F32, None, _lib.ptr(plan.cell_start),
                                        _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), None, dims, g,
-                                       _lib.ptr(bevf), _lib.F32, _lib.NCHW, st, None, None), "fwd")
+                                       _lib.ptr(bevf), _lib.F32, _lib.NCHW, 0, st, None, None), "fwd")
         elif a.kernel == "lift":
             _lib.check(l.lss_depthnet_lift(_lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims,
-                                           _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, None, None, st), "lift")
+                                           _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, None, None, None, None, None, 0, st), "lift")
         else:
             _lib.check(l.lss_splat_bwd(_lib.ptr(gbev), _lib.BF16, _lib.NHWC, _lib.ptr(plan.cell_of), _lib.ptr(depth),
                                        _lib.ptr(ctx), _lib.BF16, dims, g, _lib.ptr(d_dn), _lib.BF16, st), "bwd")

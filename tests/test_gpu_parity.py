@@ -372,7 +372,7 @@ def test_depthnet_lift_kernel_vs_conv_then_lift_prep(name):
     ctx_t = torch.empty(B * N * H * W, 64, device=DEV, dtype=torch.bfloat16)
     _lib.check(lib.lss_depthnet_lift(_lib.ptr(f), _lib.ptr(w.reshape(D + 64, -1).contiguous()), _lib.ptr(b),
                                      _lib.BF16, 512, plan.c_dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
-                                     None, None, _lib.stream_handle(DEV)), "depthnet_lift")
+                                     None, None, None, None, None, 0, _lib.stream_handle(DEV)), "depthnet_lift")
     # reference: the conv in fp64 from the same bf16 operands, rounded to bf16 like the autocast conv output
     logits = torch.einsum("nkhw,ok->nohw", feat.double(), weight.double().flatten(1)) + bias.double().view(1, -1, 1, 1)
     dn = logits.to(torch.bfloat16)
@@ -460,7 +460,7 @@ def test_sorted_depth_positions_and_splat(cfg_name):
     ctx_t = torch.empty(B * N * H * W, 64, device=DEV, dtype=torch.bfloat16)
     sdepth = torch.zeros(plan.nprime, device=DEV)
     _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, plan.c_dims, _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
-                                 _lib.ptr(plan.pos_of), _lib.ptr(sdepth), _lib.stream_handle(DEV)), "lift")
+                                 _lib.ptr(plan.pos_of), _lib.ptr(sdepth), None, None, None, 0, _lib.stream_handle(DEV)), "lift")
     assert torch.equal(sdepth[:kept], depth.reshape(-1)[pts])
 
 
@@ -491,11 +491,12 @@ def test_sorted_depth_fused_lift(cfg_name):
     sdepth = torch.zeros(plan.nprime, device=DEV)
     _lib.check(lib.lss_depthnet_lift(_lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, plan.c_dims,
                                      _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(plan.pos_of),
-                                     _lib.ptr(sdepth), _lib.stream_handle(DEV)), "depthnet_lift")
+                                     _lib.ptr(sdepth), None, None, None, 0, _lib.stream_handle(DEV)), "depthnet_lift")
     depth2 = torch.empty_like(depth)
     ctx2 = torch.empty_like(ctx_t)
     _lib.check(lib.lss_depthnet_lift(_lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, plan.c_dims,
                                      _lib.ptr(depth2), _lib.ptr(ctx2), _lib.BF16, None, None,
+                                     None, None, None, 0,
                                      _lib.stream_handle(DEV)), "depthnet_lift")
     assert torch.equal(depth, depth2) and torch.equal(ctx_t, ctx2)  # the same kernel body either way
     assert torch.equal(sdepth[:kept], depth.reshape(-1)[pts])
