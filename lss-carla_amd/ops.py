@@ -469,9 +469,12 @@ def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, 
                                  _lib.stream_handle(dev), e0, e1), "lss_splat_fwd")
 
 
-# The channels-last BEV's empty rows are zeroed by blocks of the lift launch (on the CUs the lift leaves
-# idle) instead of by the splat, which then writes the occupied rows only (LSS_SPLAT_EMPTY_FILLED).
-FILL_IN_LIFT = os.environ.get("LSS_FILL_IN_LIFT", "1") == "1"
+# Option (LSS_FILL_IN_LIFT=1): the channels-last BEV's empty rows are zeroed by blocks of the lift launch
+# (on the CUs the lift leaves idle) instead of by the splat, which then writes the occupied rows only
+# (LSS_SPLAT_EMPTY_FILLED). Measured in the c3 training step (rocprof, profiles/r03/fill_in_lift_ab.txt):
+# lift 11.3 -> 13.8 us, splat 11.8 -> 9.7 us -- the splat's chunk gathers alone take 9.7 us, so moving
+# the fill out saves nothing (hot path 58.3 vs 59.0 us). Off by default.
+FILL_IN_LIFT = os.environ.get("LSS_FILL_IN_LIFT", "0") == "1"
 
 
 def _fill_args(plan: SplatPlan, out: torch.Tensor, layout: int):

@@ -578,3 +578,35 @@ def test_random_shapes_fwd_bwd_vs_oracle(seed, B, N, fH, fW, D, half, dx, Z, bf1
     want_g = ref.lift_splat_backward_fp64(dn_in.numpy(), geom, gd.float().cpu().numpy(), dx_, bx_, nx_, D, 64)
     tol = ATOL if dtype == torch.float32 else 2e-2
     np.testing.assert_allclose(dnd.grad.float().cpu().numpy(), want_g, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_fill_in_lift_option_matches_fill_in_splat(fused):
+    """ops.FILL_IN_LIFT (the lift launch zeroes the empty rows, the splat writes occupied rows only):
+    the same channels-last BEV bit for bit as the splat's own fill, on a buffer pre-filled with NaN."""
+    cfg, gc, _ = syn.config_confs("c3")
+    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
+    rig = syn.make_rig(B, N, fd, seed=4)
+    frustum = ref.create_frustum(fd, gc["dbound"])
+    D, H, W = frustum.shape[:3]
+    plan = ops.plan_from_cameras(frustum.to(DEV), **_dev(rig), grid=ops.GridSpec.from_conf(gc))
+    g = torch.Generator().manual_seed(3)
+    feat = torch.randn(B * N, 512, H, W, generator=g).to(DEV, torch.bfloat16)
+    wdn = (torch.randn(D + 64, 512, 1, 1, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    bdn = (torch.randn(D + 64, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    dn = syn.make_depthnet_out(B, N, D, H, W, seed=4).to(DEV, torch.bfloat16)
+    outs = []
+    old = ops.FILL_IN_LIFT
+    try:
+        for fill in (False, True):
+            ops.FILL_IN_LIFT = fill
+            junk = torch.full((B, 64, 200, 200), float("nan"), device=DEV, dtype=torch.bfloat16)
+            del junk  # leaves NaN in the memory the next BEV is likely to get
+            with torch.no_grad():
+                bev = (ops.depthnet_lift_splat(feat, wdn, bdn, plan, torch.bfloat16, _lib.NHWC) if fused
+                       else ops.lift_splat(dn, plan, torch.bfloat16, _lib.NHWC))
+            outs.append(bev.clone())
+    finally:
+        ops.FILL_IN_LIFT = old
+    assert torch.isfinite(outs[1].float()).all()
+    assert torch.equal(outs[0], outs[1])
