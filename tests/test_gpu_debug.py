@@ -36,6 +36,7 @@ def test_debug_build_parity_subset():
     lib = os.path.join(REPO, "lss-carla_amd", "liblss_hip_debug.so")
     assert os.path.exists(lib), "liblss_hip_debug.so not built (__graft_entry__.build())"
     env = dict(os.environ, LSS_DEBUG="1", LSS_HYP_EXAMPLES="5")
+    env.pop("LSS_LIB", None)  # (an A/B run's release variant: the child takes the debug build)
     r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu",
                         "--timeout", "120", "--timeout-method", "thread"] + SUBSET,
                        cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
