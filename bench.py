@@ -253,14 +253,15 @@ def measure_in_graph(args) -> dict | None:
            "--profile-steps", "0", "--pmc-traffic", "0", "--cpu-baseline", "0", "--in-graph-prof", "0",
            "--mode", args.mode]
     try:
-        r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), capture_output=True, text=True,
-                           timeout=300)
+        # the child's progress lines pass through to this process's stderr (no long silence)
+        r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL,
+                           stderr=None, text=True, timeout=300)
     except subprocess.TimeoutExpired:
         log("[bench] in-graph kernel trace timed out")
         return None
     files = glob.glob(os.path.join(tmp, "**", "*kernel_trace.csv"), recursive=True)
     if r.returncode != 0 or not files:
-        log(f"[bench] in-graph kernel trace failed (rc={r.returncode}): {r.stderr[-400:]}")
+        log(f"[bench] in-graph kernel trace failed (rc={r.returncode})")
         return None
     rows = []
     for f in files:
@@ -519,9 +520,8 @@ def main():
     t_w = time.perf_counter()
 
     def first(i):
-        if i == 0:
-            torch.cuda.synchronize()
-            log(f"[rank {rank}] first step done in {time.perf_counter() - t_w:.1f} s")
+        torch.cuda.synchronize()  # (a progress line per warm-up step: a long MIOpen search is not a hang)
+        log(f"[rank {rank}] warm-up step {i + 1} done at {time.perf_counter() - t_w:.1f} s")
 
     if args.graph:
         # eager warm-up on a side stream (MIOpen find, optimizer state), capture, 2 untimed replays

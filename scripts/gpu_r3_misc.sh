@@ -2,7 +2,7 @@
 # in-tree find db), the default bench line, a kernel trace of the default bench for the per-step breakdown.
 set -o pipefail
 OUT=gpurun_out/r3; mkdir -p $OUT
-timeout -k 10 500 python bench.py --config c3 --dtype fp32 --bev-layout nchw --cpu-baseline 0 --miopen-find 0 > $OUT/bench_c3_fp32_nchw.json 2> $OUT/bench_c3_fp32_nchw.log; rc=$?
+timeout -k 10 500 python bench.py --config c3 --dtype fp32 --bev-layout nchw --cpu-baseline 0 --miopen-find 0 --in-graph-prof 0 > $OUT/bench_c3_fp32_nchw.json 2> $OUT/bench_c3_fp32_nchw.log; rc=$?
 echo "fp32=$rc"; tail -c 400 $OUT/bench_c3_fp32_nchw.json; [ $rc -ne 0 ] && { tail -5 $OUT/bench_c3_fp32_nchw.log; exit $rc; }
 timeout -k 10 700 python bench.py > $OUT/bench.json 2> $OUT/bench.log; rc=$?
 echo "bench=$rc"; tail -c 1500 $OUT/bench.json; [ $rc -ne 0 ] && tail -5 $OUT/bench.log
