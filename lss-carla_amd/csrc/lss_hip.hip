@@ -1900,7 +1900,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 #endif
 constexpr int kN2Waves = LSS_NCHW_WAVES;
 #ifndef LSS_NCHW_PAD
-#define LSS_NCHW_PAD 1  // 1: 4 more floats of LDS row padding (27 KB tiles, 5 blocks per CU); 0: 25.6 KB, 6 per CU (c2 -1.1 us; off until an intermittent fault in the NCHW module test is explained)
+#define LSS_NCHW_PAD 0  // 0: row stride YT rounded to 16 B (25.6 KB tiles, 6 blocks per CU; c2 in-step 16.4 -> 15.3 us, profiles/r03/pad0_eval.txt); 1: 4 more floats (27 KB, 5 per CU)
 #endif
 // LDS row stride of the NCHW tile: YT rounded up to 16 B. At YT = 100 the tile is 25.6 KB, so 6 blocks
 // fit a CU (1,536 of c2's 1,600 tiles resident at once instead of 1,280).
