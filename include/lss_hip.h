@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 13
+#define LSS_ABI_VERSION 14
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -168,6 +168,15 @@ int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, in
                       const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype,
                       const int32_t* pos_of, float* sorted_depth, const int32_t* cell_start,
                       const lss_grid_t* bev_grid, void* bev, int32_t bev_dtype, lss_stream_t stream);
+
+/* As lss_depthnet_lift, with feat channels-last: (B*N, H, W, K) = pixel-major rows of K bf16 (the
+ * memory of a torch.channels_last (B*N, K, H, W) tensor, as a channels-last Up stage produces it).
+ * K must be 512. One block per compute unit, each on one contiguous run of pixel rows; identical
+ * results to lss_depthnet_lift on the same values. */
+int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
+                           const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype,
+                           const int32_t* pos_of, float* sorted_depth, const int32_t* cell_start,
+                           const lss_grid_t* bev_grid, void* bev, int32_t bev_dtype, lss_stream_t stream);
 
 /* Splat forward: segmented per-cell sum written as the dense (B, Z*C, X, Y) BEV
  * (voxel_pooling + QuickCumsum.forward + griddify, src/models.py:233-246,

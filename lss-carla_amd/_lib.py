@@ -18,7 +18,7 @@ DEBUG_LIB_PATH = os.path.join(_HERE, "liblss_hip_debug.so")  # LSS_DEBUG=1: devi
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 13
+ABI_VERSION = 14
 SPLAT_EMPTY_FILLED = 1
 
 
@@ -65,6 +65,8 @@ SIGNATURES = {
     "lss_lift_prep": (ctypes.c_int, [_p, _i32, _DIMS, _p, _p, _i32, _p, _p, _p, _GRID, _p, _i32, _p]),
     "lss_depthnet_lift": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p, _p, _p, _GRID, _p, _i32,
                                          _p]),
+    "lss_depthnet_lift_nhwc": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p, _p, _p, _GRID, _p,
+                                              _i32, _p]),
     "lss_splat_fwd": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _i32, _p, _p,
                                      _p]),
     "lss_bev_rows": (ctypes.c_int, [_p, _i32, _p, _DIMS, _GRID, _p, _p]),

@@ -1285,6 +1285,175 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
     LSS_STAMP(tslot, 3);
 }
 
+// ---- depthnet + lift, version 3: pixel-major (channels-last) features, one block per CU.
+// The feature map (B*N, K, H, W) as the channels-last tensor of a channels-last Up stage: pixel q's K
+// channels are one contiguous K*2-byte row, so a block's pixel tile is ONE contiguous run of memory
+// (every line it touches is wholly its own) instead of K strided runs of 2*PX bytes (the NCHW tile of
+// k_depthnet_lift2 touched ~1.8 lines per 96 useful bytes and waited 6.5 us for them in the step).
+// The grid is one block per CU (the pixel count split as evenly as possible: c3's 8,448 pixels are
+// 256 tiles of 33), so every CU takes in its share of the features plus the weights, which every
+// block reads (from L2). The tile is staged in LDS as [pixel][k] (row stride K*2 + 16 B: the 16 rows
+// of a B fragment fall on different banks) and the B fragments (8 channels of one pixel per lane) are
+// plain 16-B LDS reads. Rows past the tile's pixel count are clamped copies of its last row and only
+// feed output columns that are never written. A fragments, epilogue (bias, bf16 rounding, softmax,
+// context rows) and the empty-row fill role as k_depthnet_lift2; identical results.
+constexpr int kDn3Waves = 8;             // 8 x 16 = 128 output rows >= D + C
+constexpr int kDn3Block = kDn3Waves * kWave;
+constexpr int kDn3MaxPix = 48;           // pixels per block at most: three 16-column MFMA tiles
+#ifndef LSS_DN3_PIX
+#define LSS_DN3_PIX 0  // pixels per block of k_depthnet_lift3: 0 one block per CU (at most 48 pixels each), else this many
+#endif
+
+template <int K, bool SD>
+__global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __restrict__ feat,
+                                                              const bf16* __restrict__ weight,
+                                                              const bf16* __restrict__ bias, int D, int HW,
+                                                              int npix, int nlift, float* __restrict__ depth,
+                                                              bf16* __restrict__ ctx_t,
+                                                              const int32_t* __restrict__ pos_of,
+                                                              float* __restrict__ sorted_depth, int nfill,
+                                                              const int32_t* __restrict__ cell_start, BevGeo bg,
+                                                              unsigned char* __restrict__ bev, int esize) {
+    static_assert(K % 32 == 0 && K <= kDnMaxK, "K steps of 32");
+    constexpr int PX = kDn3MaxPix;
+    constexpr int kTiles = PX / 16;
+    constexpr int kRow = K * 2 + 16;  // LDS bytes per pixel row
+    using bf16x8 = __attribute__((ext_vector_type(8))) short;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    __shared__ __attribute__((aligned(16))) unsigned char s_x[PX * kRow];  // [pixel][k] bf16
+    __shared__ float s_lg[kDnMaxO][PX + 1];                                // bf16-rounded logits
+    __shared__ float s_red[2][kDn3Block / PX][PX];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int blk = blockIdx.x;
+    if (blk >= nlift) {  // block-uniform: the empty-row fill role
+        fill_empty_rows((blk - nlift) * kDn3Waves + wave, nfill * kDn3Waves, cell_start, bg, bev, esize, lane);
+        return;
+    }
+    // pixel tile [q0, q1): the pixels split as evenly as possible over the nlift blocks
+    const int q0 = (int)(((long)npix * blk) / nlift), q1 = (int)(((long)npix * (blk + 1)) / nlift);
+    const int np = q1 - q0;  // 1 <= np <= PX (the host sizes nlift so)
+    const int O = D + kC;
+    [[maybe_unused]] const int tslot = blk * kDn3Waves + wave;  // LSS_TRACE builds only
+    LSS_STAMP(tslot, 0);
+    constexpr int kParts = kDn3Block / PX;                 // softmax: threads (part, p) of the block
+    constexpr int kPerPart = (64 + kParts - 1) / kParts;   // D <= 64 (D + C <= kDnMaxO)
+    const int p = threadIdx.x % PX, part = threadIdx.x / PX;
+    const bool sm = part < kParts;
+    int at[SD ? kPerPart : 1];
+    if (SD) {
+        const int qc = q0 + min(p, np - 1), bnc = qc / HW, hwc = qc - bnc * HW;
+#pragma unroll
+        for (int i = 0; i < kPerPart; ++i) {
+            const int d = min(part + kParts * i, D - 1);
+            at[i] = pos_of[((size_t)bnc * D + d) * HW + hwc];
+        }
+    }
+    // ---- loads, all in flight together: the tile (contiguous rows, 16 B per thread and load), then
+    // this wave's weight rows as A fragments, then its bias values (clamped addresses, no branches)
+    constexpr int kChunks = PX * K * 2 / 16;             // 16-B pieces of a full tile
+    constexpr int kFeatIt = (kChunks + kDn3Block - 1) / kDn3Block;
+    constexpr int kCPR = K * 2 / 16;                     // 16-B pieces per pixel row
+    const unsigned char* tile = reinterpret_cast<const unsigned char*>(feat + (size_t)q0 * K);
+    uint4 fv[kFeatIt];
+#pragma unroll
+    for (int t = 0; t < kFeatIt; ++t) {
+        const int i = threadIdx.x + t * kDn3Block;
+        const int r = min(i / kCPR, np - 1), c = i % kCPR;
+        fv[t] = (LSS_DN_SKIP & 2) ? make_uint4(r, c, t, 1u)
+                                  : *reinterpret_cast<const uint4*>(tile + (size_t)r * K * 2 + c * 16);
+    }
+    const int arow = wave * 16 + (lane & 15);
+    const int kq = 8 * (lane >> 4);
+    constexpr int kSteps = K / 32;
+    const int g = lane >> 4, c16 = lane & 15;
+    const bf16* wrow = weight + (size_t)min(arow, O - 1) * K + kq;
+    // (unconditional even for a wave past the output rows -- its clamped row is one cached line per
+    // K step -- so the compiler can count every load: a load under a branch makes it wait for the
+    // worst case, and the tile's LDS writes then waited for most of the weights)
+    bf16x8 a[kSteps];
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s)
+        a[s] = (LSS_DN_SKIP & 1) ? bf16x8{(short)lane, 1, 2, 3, 4, 5, 6, (short)s}
+                                 : *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
+    float bv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[i] = __bfloat162float(bias[min(wave * 16 + 4 * g + i, O - 1)]);
+#pragma unroll
+    for (int t = 0; t < kFeatIt; ++t) {
+        const int i = threadIdx.x + t * kDn3Block;
+        if (kChunks % kDn3Block == 0 || i < kChunks)
+            *reinterpret_cast<uint4*>(s_x + (i / kCPR) * kRow + (i % kCPR) * 16) = fv[t];
+    }
+    __syncthreads();
+    LSS_STAMP(tslot, 1);
+    // ---- MFMA: kTiles 16-pixel column tiles, K/32 steps. All tiles always (compile-time trip
+    // counts: the LDS reads and MFMAs pipeline); columns past the tile's pixels read clamped rows and
+    // only feed logits that are never read.
+    f32x4 acc[kTiles];
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t) acc[t] = f32x4{};
+    // (every wave, also one past the output rows: a branch here would let the compiler sink the
+    // weight loads into it, behind the barrier, one round trip per K step)
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t) {
+            // lane (g, c16) of the B fragment: pixel 16t + c16, channels 32s + 8g .. + 7
+            const bf16x8 b = *reinterpret_cast<const bf16x8*>(s_x + (16 * t + c16) * kRow + (32 * s + 8 * g) * 2);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], b, acc[t], 0, 0, 0);
+        }
+    }
+    // C/D: column (pixel) = lane & 15, row (output) = 4 (lane >> 4) + i
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int o = wave * 16 + 4 * g + i;
+            if (o < O) s_lg[o][16 * t + c16] = __bfloat162float(__float2bfloat16(acc[t][i] + bv[i]));
+        }
+    __syncthreads();
+    LSS_STAMP(tslot, 2);
+    // ---- softmax over the D bins of each pixel: thread (part, p) covers bins part, part + kParts, ...
+    const bool pl = sm && p < np;
+    float m = -INFINITY;
+    for (int d = part; pl && d < D; d += kParts) m = fmaxf(m, s_lg[d][p]);
+    if (sm) s_red[0][part][p] = m;
+    __syncthreads();
+    m = s_red[0][0][p];
+#pragma unroll
+    for (int j = 1; j < kParts; ++j) m = fmaxf(m, s_red[0][j][p]);
+    float sum = 0.f;
+    for (int d = part; pl && d < D; d += kParts) sum += expf(s_lg[d][p] - m);
+    if (sm) s_red[1][part][p] = sum;
+    __syncthreads();
+    sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < kParts; ++j) sum += s_red[1][j][p];
+    if (pl) {
+        const int q = q0 + p;
+        const int bn = q / HW, hw = q - bn * HW;
+        float* dst = depth + (size_t)bn * D * HW + hw;
+#pragma unroll
+        for (int i = 0; i < kPerPart; ++i) {
+            const int d = part + kParts * i;
+            if (d < D) {
+                const float v = expf(s_lg[d][p] - m) / sum;
+                dst[(size_t)d * HW] = v;
+                if (SD && at[SD ? i : 0] >= 0) sorted_depth[at[SD ? i : 0]] = v;
+            }
+        }
+    }
+    // context rows: the tile's np rows of 64 bf16 are one contiguous run; 8 channels per 16-B store
+    for (int i = threadIdx.x; i < np * (kC / 8); i += kDn3Block) {
+        const int pp = i / (kC / 8), c8 = (i - pp * (kC / 8)) * 8;
+        bf16 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = __float2bfloat16(s_lg[D + c8 + j][pp]);
+        *reinterpret_cast<uint4*>(ctx_t + (size_t)(q0 + pp) * kC + c8) = *reinterpret_cast<const uint4*>(v);
+    }
+    LSS_STAMP(tslot, 3);
+}
+
 // 16 bytes of fp32 or bf16 row elements -> fp32.
 __device__ __forceinline__ void unpack16(const uint4& u, const float*, float* o) {
     o[0] = __uint_as_float(u.x); o[1] = __uint_as_float(u.y); o[2] = __uint_as_float(u.z); o[3] = __uint_as_float(u.w);
@@ -3101,6 +3270,36 @@ int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, in
                        (bf16*)ctx_t, pos_of, sorted_depth);
     if (fp.bev)  // this lift kernel has no fill role: the fill as a launch of its own
         hipLaunchKernelGGL(k_fill_empty, dim3(8 * fp.groups), dim3(kBlock), 0, s, cell_start, fp.bg, fp.bev, fp.esize);
+    return launch_status();
+}
+
+int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
+                           const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, const int32_t* pos_of,
+                           float* sorted_depth, const int32_t* cell_start, const lss_grid_t* bev_grid, void* bev,
+                           int32_t bev_dtype, lss_stream_t stream) {
+    if (!dims_ok(dims) || !feat || !weight || !bias || !depth || !ctx_t || (pos_of && !sorted_depth)) return LSS_EINVAL;
+    if (dtype != LSS_BF16 || ctx_dtype != LSS_BF16) return LSS_EUNSUPPORTED;
+    if (K != 512 || dims->D + kC > kDnMaxO) return LSS_EUNSUPPORTED;
+    const int HW = dims->H * dims->W;
+    const long npix = (long)dims->B * dims->N * HW;
+    if (npix >= INT_MAX / 2) return LSS_EUNSUPPORTED;
+    FillPlan fp;
+    if (fill_plan(dims, bev_grid, cell_start, bev, bev_dtype, kDn3Waves, &fp)) return LSS_EINVAL;
+    // one block per CU, more only when a CU's share would pass kDn3MaxPix pixels; never more than
+    // the pixels (every block holds at least one)
+    const long nlift = LSS_DN3_PIX > 0 ? (npix + std::min(LSS_DN3_PIX, kDn3MaxPix) - 1) / std::min(LSS_DN3_PIX, kDn3MaxPix)
+                                       : std::min<long>(npix, std::max<long>(device_cus(), (npix + kDn3MaxPix - 1) / kDn3MaxPix));
+    const int nfill = fp.bev ? 8 * fp.groups : 0;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 gr((unsigned)(nlift + nfill)), bl(kDn3Block);
+    if (pos_of)
+        hipLaunchKernelGGL((k_depthnet_lift3<512, true>), gr, bl, 0, s, (const bf16*)feat, (const bf16*)weight,
+                           (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, depth, (bf16*)ctx_t, pos_of,
+                           sorted_depth, nfill, cell_start, fp.bg, fp.bev, fp.esize);
+    else
+        hipLaunchKernelGGL((k_depthnet_lift3<512, false>), gr, bl, 0, s, (const bf16*)feat, (const bf16*)weight,
+                           (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, depth, (bf16*)ctx_t, nullptr,
+                           nullptr, nfill, cell_start, fp.bg, fp.bev, fp.esize);
     return launch_status();
 }
 

@@ -37,6 +37,8 @@ from . import resample
 from .norm import bn_act
 from .tools import gen_dx_bx
 
+UP1_CHANNELS_LAST = True  # CamEncode.up1 on channels-last maps under bf16 autocast (see get_eff_depth)
+
 
 class Up(nn.Module):
     """Upsample x1, concatenate with x2, two conv-BN-ReLU (src/models.py:15-34)."""
@@ -97,7 +99,14 @@ class CamEncode(nn.Module):
                 endpoints.append(prev)
             prev = x
         endpoints.append(x)
-        return self.up1(endpoints[4], endpoints[3])
+        x5, x4 = endpoints[4], endpoints[3]
+        if UP1_CHANNELS_LAST and x5.is_cuda and x5.dtype == torch.bfloat16 and x4.dtype == torch.bfloat16:
+            # up1 channels-last (bf16 autocast): upsample + cat in one kernel, NHWC convs without
+            # layout transposes, and a pixel-major feature map -- each pixel's 512 channels one
+            # contiguous row -- for the fused depthnet lift (lss_depthnet_lift_nhwc)
+            x5 = x5.contiguous(memory_format=torch.channels_last)
+            x4 = x4.contiguous(memory_format=torch.channels_last)
+        return self.up1(x5, x4)
 
     def depthnet_out(self, x):
         """(B*N, 3, H, W) images -> (B*N, D+C, H/16, W/16) depth logits + context."""
@@ -139,7 +148,7 @@ class BasicBlock(nn.Module):
         if self.downsample is None:
             identity = x
         else:
-            identity = bn_act(self.downsample[1], self.downsample[0](x))
+            identity = bn_act(self.downsample[1], conv1x1(self.downsample[0], x))
         out = bn_act(self.bn1, self.conv1(x), "relu")
         return bn_act(self.bn2, self.conv2(out), "relu", residual=identity)
 
@@ -154,15 +163,20 @@ def _resnet_layer(inplanes, planes, blocks, stride):
 
 
 def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
-    """A stride-1 1x1 nn.Conv2d applied as a GEMM over the channels (F.linear: hipBLASLt) on CUDA maps,
-    with the module's own weight and bias (same math). BevEncode's last conv (up2.4, 128 -> outC = 1
-    channels, src/models.py:115) on MIOpen is not safe to replay from a hipGraph: from the second
-    replay of the captured training step on, its weight and bias gradients came out as garbage
-    (1e35 / 1e-31; every other parameter's gradient replayed within MIOpen's run-to-run noise --
+    """A 1x1 nn.Conv2d (stride s, no padding) applied as a GEMM over the channels of every s-th pixel
+    (F.linear: hipBLASLt) on CUDA maps, with the module's own weight and bias (same math). MIOpen's
+    channels-last 1x1 convolutions are not safe to replay from a hipGraph: from the second replay of
+    the captured training step on, the weight gradients of BevEncode's last conv (up2.4, 128 -> outC
+    = 1 channels, src/models.py:115) came out as garbage (1e35 / 1e-31) and those of the stride-2
+    downsample convs of layer2 / layer3 (torchvision BasicBlock) far from the eager step's
+    (relative 1.5-2.5 while every other parameter replayed within 1e-4 --
     tests/test_gpu_captured_step.py)."""
-    if not (x.is_cuda and x.dim() == 4) or conv.kernel_size != (1, 1) or conv.stride != (1, 1) or conv.groups != 1 \
-            or conv.padding not in ((0, 0), "valid"):
+    if not (x.is_cuda and x.dim() == 4) or conv.kernel_size != (1, 1) or conv.groups != 1 \
+            or conv.stride[0] != conv.stride[1] or conv.padding not in ((0, 0), "valid"):
         return conv(x)
+    s = conv.stride[0]
+    if s > 1:
+        x = x[:, :, ::s, ::s]
     w = conv.weight.reshape(conv.out_channels, conv.in_channels)
     y = F.linear(x.permute(0, 2, 3, 1), w, conv.bias)  # (N, H, W, O)
     return y.permute(0, 3, 1, 2)  # (N, O, H, W), channels-last strides

@@ -585,7 +585,10 @@ class DepthnetLiftSplat(torch.autograd.Function):
         if feat.shape != (B * N, K, H, W) or O != D + C_CAM or tuple(weight.shape[2:]) != (1, 1):
             raise RuntimeError(f"depthnet shapes feat {tuple(feat.shape)} weight {tuple(weight.shape)} do not match "
                                f"the plan (B*N={B * N}, D+C={D + C_CAM}, H={H}, W={W})")
-        f = feat.detach().contiguous()
+        # a channels-last feature map (pixel-major rows, as CamEncode's channels-last up1 gives it) goes
+        # to the pixel-row kernel; anything else is made NCHW-contiguous for the channel-plane kernel
+        nhwc = K == 512 and feat.dim() == 4 and feat.is_contiguous(memory_format=torch.channels_last)
+        f = feat.detach() if nhwc else feat.detach().contiguous()
         w = weight.detach().reshape(O, K).contiguous()
         b = bias.detach().contiguous()
         depth = torch.empty(B * N, D, H, W, device=dev, dtype=torch.float32)
@@ -594,10 +597,10 @@ class DepthnetLiftSplat(torch.autograd.Function):
         X, Y, Z = plan.grid.nx
         out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
         fill, flags = _fill_args(plan, out, layout)
-        _lib.check(lib.lss_depthnet_lift(_lib.ptr(f), _lib.ptr(w), _lib.ptr(b), _lib.BF16, K, plan.c_dims,
-                                         _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(pos_of),
-                                         _lib.ptr(sorted_depth), *fill, _lib.stream_handle(dev)),
-                   "lss_depthnet_lift")
+        lift = lib.lss_depthnet_lift_nhwc if nhwc else lib.lss_depthnet_lift
+        _lib.check(lift(_lib.ptr(f), _lib.ptr(w), _lib.ptr(b), _lib.BF16, K, plan.c_dims, _lib.ptr(depth),
+                        _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(pos_of), _lib.ptr(sorted_depth), *fill,
+                        _lib.stream_handle(dev)), "lss_depthnet_lift")
         _splat_fwd_launch(plan, depth, ctx_t, None, out, layout, sorted_depth, flags)
         ctx.save_for_backward(f, weight, depth, ctx_t)
         ctx.plan = plan
@@ -616,6 +619,23 @@ class DepthnetLiftSplat(torch.autograd.Function):
                                      _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, plan.c_dims, plan.grid.c_struct(),
                                      _lib.ptr(d_dn), _lib.BF16, _lib.stream_handle(depth.device)), "lss_splat_bwd")
         need = ctx.needs_input_grad
+        if feat.dim() == 4 and feat.is_contiguous(memory_format=torch.channels_last) and not feat.is_contiguous():
+            # channels-last features: the 1x1 conv's backward as plain GEMMs over pixel-major rows
+            # (hipBLASLt). MIOpen's channels-last 1x1 backward-weights solver is not replay-safe in a
+            # hipGraph (its weight gradient reads back as zeros from the first replay on).
+            O, K = weight.shape[0], weight.shape[1]
+            npix = B * N * H * W
+            dd = d_dn.permute(0, 2, 3, 1).reshape(npix, O)          # (pixels, O), one copy
+            fm = feat.permute(0, 2, 3, 1).reshape(npix, K)          # a view: the channels-last rows
+            w2 = weight.reshape(O, K).to(dd.dtype)
+            d_feat = d_w = d_b = None
+            if need[0]:
+                d_feat = torch.mm(dd, w2).view(B * N, H, W, K).permute(0, 3, 1, 2)  # channels-last
+            if need[1]:
+                d_w = torch.mm(dd.t(), fm).view(weight.shape).to(weight.dtype)
+            if need[2]:
+                d_b = dd.float().sum(0).to(weight.dtype)
+            return d_feat, d_w, d_b, None, None, None
         d_feat, d_w, d_b = torch.ops.aten.convolution_backward(
             d_dn, feat, weight, [weight.shape[0]], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
             [need[0], need[1], need[2]])

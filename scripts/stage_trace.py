@@ -19,7 +19,7 @@ sys.path.insert(0, REPO)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("kernel", choices=["lift", "bwd", "geom", "nchw", "scan"])
+    ap.add_argument("kernel", choices=["lift", "lift3", "bwd", "geom", "nchw", "scan"])
     ap.add_argument("--config", default="c3")
     ap.add_argument("--cold", type=int, default=1)
     ap.add_argument("--lib", default="trace", help="variants/<name>.so, a LSS_TRACE=1 build")
@@ -43,6 +43,7 @@ def main():
     depth = torch.empty(B * N, D, H, W, device=dev)
     ctx = torch.empty(B * N * H * W, 64, device=dev, dtype=torch.bfloat16)
     feat = torch.randn(B * N, 512, H, W, device=dev).to(torch.bfloat16)
+    feat_cl = feat.contiguous(memory_format=torch.channels_last)
     wdn = (torch.randn(D + 64, 512, 1, 1, device=dev) * 0.05).to(torch.bfloat16)
     bdn = torch.zeros(D + 64, device=dev, dtype=torch.bfloat16)
     gbev = torch.randn(B, Z * 64, X, Y, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -94,6 +95,10 @@ def main():
             _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctxf), _lib.F32, None, _lib.ptr(plan.cell_start),
                                        _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), None, dims, g,
                                        _lib.ptr(bevf), _lib.F32, _lib.NCHW, 0, st, None, None), "fwd")
+        elif a.kernel == "lift3":  # channels-last features (k_depthnet_lift3)
+            _lib.check(l.lss_depthnet_lift_nhwc(_lib.ptr(feat_cl), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims,
+                                                _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, None, None, None, None, None,
+                                                0, st), "lift3")
         elif a.kernel == "lift":
             _lib.check(l.lss_depthnet_lift(_lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims,
                                            _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, None, None, None, None, None, 0, st), "lift")

@@ -107,6 +107,7 @@ def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find):
         step()  # pre_step + graph replays
         torch.cuda.synchronize()
         rep = (g_bev.clone(), g_dw.clone(), step.static_loss.clone())
+        rep_all = {k: v.detach().clone() for k, v in flat.views(grads=True).items()}
         restore()
         w = model.camencode.depthnet.weight.detach().to(torch.bfloat16).cpu()  # this step's bf16 operands
         b = model.camencode.depthnet.bias.detach().to(torch.bfloat16).cpu()
@@ -124,6 +125,44 @@ def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find):
         torch.testing.assert_close(rep[2], eag[2], rtol=1e-5, atol=1e-6)
         rel = ((rep[1] - eag[1]).norm() / eag[1].norm()).item()
         assert rel < 1e-3, (i, rel, rep[1].norm().item(), eag[1].norm().item())
+        # every parameter's gradient, not only the hot path's: a conv solver that is not replay-safe
+        # shows up as a replayed gradient of zeros (or garbage) next to the eager one
+        if os.environ.get("LSS_CAPTURE_DIAG"):  # a third step with MIOpen off (PyTorch's own convs)
+            eag_all = {k: v.detach().clone() for k, v in flat.views(grads=True).items()}
+            restore()
+            torch.backends.cudnn.enabled = False
+            try:
+                step.eager()
+            finally:
+                torch.backends.cudnn.enabled = True
+            torch.cuda.synchronize()
+            nat_all = {k: v.detach().clone() for k, v in flat.views(grads=True).items()}
+            restore()
+            step.eager()  # a second eager step: run-to-run spread of the same computation
+            torch.cuda.synchronize()
+            eag2_all = {k: v.detach().clone() for k, v in flat.views(grads=True).items()}
+            dd = sorted(((((eag2_all[k] - e).norm() / max(e.norm().item(), 1e-12)).item(), k)
+                         for k, e in eag_all.items() if e.norm().item() > 1e-6), reverse=True)
+            print(f"rig {i}: eager vs eager: " + ", ".join(f"{k} {v:.2e}" for v, k in dd[:5]))
+            for name_, cmp in (("rep", rep_all), ("eag", eag_all)):
+                dd = sorted(((((cmp[k] - e).norm() / max(e.norm().item(), 1e-12)).item(), k)
+                             for k, e in nat_all.items() if e.norm().item() > 1e-6), reverse=True)
+                print(f"rig {i}: {name_} vs native-conv step: " + ", ".join(f"{k} {v:.2e}" for v, k in dd[:5]))
+            restore()
+            step.eager()
+            torch.cuda.synchronize()
+        diffs = []
+        for k, e in flat.views(grads=True).items():
+            en = e.norm().item()
+            if en < 1e-6:
+                continue
+            diffs.append((((rep_all[k] - e).norm() / en).item(), k, en, rep_all[k].norm().item(), e.numel()))
+        diffs.sort(reverse=True)
+        for d_ in diffs[:5]:
+            print(f"rig {i}: grad rel diff {d_[0]:.3e} {d_[1]} |eag| {d_[2]:.3e} |rep| {d_[3]:.3e} n {d_[4]}")
+        # a replay-safe step reproduces every gradient to MIOpen's run-to-run noise (~1e-4, also the
+        # ill-conditioned BN biases); a solver that is not replay-safe is off by O(1)
+        assert diffs[0][0] < 2e-2, diffs[0][:2]
         # replayed BEV vs the fp64 oracle on the eager step's bf16 operands
         exact = _oracle_bev(eag[3].to(torch.bfloat16).cpu(), w, b, r, frustum, gc, B, N)
         got = rep[0].float().cpu().numpy()

@@ -1,0 +1,135 @@
+"""Fused depthnet lift on channels-last features (lss_depthnet_lift_nhwc, k_depthnet_lift3).
+
+The kernel must give the same bits as the NCHW kernel (k_depthnet_lift2) on the same values -- same
+MFMA operands, same K order, same epilogue -- at every BASELINE config it serves, with and without the
+CSR-ordered depth copy and the empty-row fill; at pixel counts the NCHW kernel does not tile (odd
+feature maps, fewer pixels than CUs) it is checked against the fp64 conv + the oracle's lift
+(src/models.py:47, 52-59).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # collected on CPU CI, skipped there
+    pytest.skip("needs an MI355X", allow_module_level=True)
+
+from oracle import lss_ref as ref  # noqa: E402
+import lss_carla_amd as L  # noqa: E402
+from lss_carla_amd import _lib, ops  # noqa: E402
+from lss_carla_amd import synthetic as syn  # noqa: E402
+
+DEV = torch.device("cuda:0")
+
+
+def _inputs(B, N, H, W, D, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    feat = torch.randn(B * N, 512, H, W, generator=g).to(torch.bfloat16)
+    weight = (torch.randn(D + 64, 512, generator=g) * 0.05).to(torch.bfloat16)
+    bias = (torch.randn(D + 64, generator=g) * 0.1).to(torch.bfloat16)
+    return feat, weight, bias
+
+
+def _run(fn, feat, weight, bias, dims, pos_of=None, nprime=0, fill=(None, None, None, 0)):
+    B, N, D, H, W = dims.B, dims.N, dims.D, dims.H, dims.W
+    depth = torch.full((B * N, D, H, W), float("nan"), device=DEV)
+    ctx_t = torch.full((B * N * H * W, 64), float("nan"), device=DEV, dtype=torch.bfloat16)
+    sd = torch.zeros(nprime, device=DEV) if pos_of is not None else None
+    _lib.check(fn(_lib.ptr(feat), _lib.ptr(weight), _lib.ptr(bias), _lib.BF16, 512, dims, _lib.ptr(depth),
+                  _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(pos_of), _lib.ptr(sd), *fill, _lib.stream_handle(DEV)),
+               "depthnet_lift")
+    torch.cuda.synchronize()
+    return depth, ctx_t, sd
+
+
+@pytest.mark.parametrize("name", ["c1", "c3", "c5"])
+def test_nhwc_kernel_bit_identical_to_nchw_kernel(name):
+    cfg, gc, _ = syn.config_confs(name)
+    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
+    rig = {k: v.to(DEV) for k, v in syn.make_rig(B, N, fd, seed=2).items()}
+    frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
+    D, H, W = frustum.shape[:3]
+    ops.SORTED_DEPTH = True
+    try:
+        plan = ops.plan_from_cameras(frustum, **rig, grid=ops.GridSpec.from_conf(gc))
+    finally:
+        ops.SORTED_DEPTH = False
+    feat, weight, bias = (t.to(DEV) for t in _inputs(B, N, H, W, D, seed=5))
+    feat_cl = feat.contiguous(memory_format=torch.channels_last)
+    lib = _lib.load()
+    for pos in (None, plan.pos_of):
+        d0, c0, s0 = _run(lib.lss_depthnet_lift, feat, weight, bias, plan.c_dims, pos, plan.nprime)
+        d1, c1, s1 = _run(lib.lss_depthnet_lift_nhwc, feat_cl, weight, bias, plan.c_dims, pos, plan.nprime)
+        assert torch.equal(d0, d1) and torch.equal(c0, c1)
+        if pos is not None:
+            assert torch.equal(s0, s1)
+    # with the empty-row fill riding along: the splat over the filled BEV (occupied rows only) equals
+    # the full splat
+    X, Y, Z = plan.grid.nx
+    bev = torch.empty((B, Z * 64, X, Y), device=DEV, dtype=torch.bfloat16, memory_format=torch.channels_last).fill_(7.0)
+    d1, c1, _ = _run(lib.lss_depthnet_lift_nhwc, feat_cl, weight, bias, plan.c_dims,
+                     fill=(_lib.ptr(plan.cell_start), plan.grid.c_struct(), _lib.ptr(bev), _lib.BF16))
+    assert torch.equal(d0, d1) and torch.equal(c0, c1)
+    full = torch.empty_like(bev)
+    for out, flags in ((full, 0), (bev, _lib.SPLAT_EMPTY_FILLED)):
+        _lib.check(lib.lss_splat_fwd(_lib.ptr(d1), _lib.ptr(c1), _lib.BF16, None, _lib.ptr(plan.cell_start),
+                                     _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), None, plan.c_dims,
+                                     plan.grid.c_struct(), _lib.ptr(out), _lib.BF16, _lib.NHWC, flags,
+                                     _lib.stream_handle(DEV), None, None), "splat")
+    assert torch.equal(full, bev)
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 5, 7, 41), (2, 5, 9, 13, 41), (1, 1, 8, 22, 60), (8, 6, 8, 22, 41)])
+def test_nhwc_kernel_vs_fp64_conv(shape):
+    """Odd maps, fewer pixels than CUs, D = 60: logits rounded to bf16 as the autocast conv's output,
+    then the oracle's softmax / context layout."""
+    B, N, H, W, D = shape
+    feat, weight, bias = _inputs(B, N, H, W, D, seed=11)
+    dims = _lib.Dims(B, N, D, H, W, 64)
+    lib = _lib.load()
+    depth, ctx_t, _ = _run(lib.lss_depthnet_lift_nhwc, feat.to(DEV).contiguous(memory_format=torch.channels_last),
+                           weight.to(DEV), bias.to(DEV), dims)
+    logits = torch.einsum("nkhw,ok->nohw", feat.double(), weight.double()) + bias.double().view(1, -1, 1, 1)
+    dn = logits.to(torch.bfloat16)
+    want_depth, _ = ref.lift(dn.float(), D, 64)
+    want_ctx = dn[:, D:].permute(0, 2, 3, 1).reshape(-1, 64)
+    got_ctx = ctx_t.cpu()
+    assert (got_ctx != want_ctx).float().mean().item() < 1e-3  # a logit on a bf16 rounding boundary may flip
+    np.testing.assert_allclose(got_ctx.float().numpy(), want_ctx.float().numpy(), rtol=1e-2, atol=1e-2)
+    np.testing.assert_allclose(depth.cpu().numpy(), want_depth.numpy(), rtol=2e-2, atol=1e-4)
+
+
+def test_module_up1_channels_last_feeds_nhwc_lift():
+    """Under bf16 autocast CamEncode.up1 runs channels-last, so the fused lift takes the pixel-row
+    kernel; the BEV and the depthnet gradient match the NCHW up1 path."""
+    cfg, gc, dac = syn.config_confs("c2")
+    torch.manual_seed(0)
+    m = L.compile_model(gc, dac, 1).to(DEV).eval()
+    m.bev_layout = "nhwc"
+    rig = {k: v.to(DEV) for k, v in syn.make_rig(cfg["B"], cfg["N"], cfg["final_dim"], seed=1).items()}
+    imgs = syn.make_images(cfg["B"], cfg["N"], cfg["final_dim"]).to(DEV)
+    seen = []
+    orig = ops.DepthnetLiftSplat.forward
+
+    def spy(ctx, feat, *a):
+        seen.append(feat.is_contiguous(memory_format=torch.channels_last) and not feat.is_contiguous())
+        return orig(ctx, feat, *a)
+    outs = []
+    from lss_carla_amd import models
+    try:
+        ops.DepthnetLiftSplat.forward = staticmethod(spy)
+        for cl in (True, False):
+            models.UP1_CHANNELS_LAST = cl
+            m.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                bev = m.get_voxels(imgs, **rig)
+            bev.float().square().mean().backward()
+            outs.append((bev.detach().float(), m.camencode.depthnet.weight.grad.clone()))
+    finally:
+        models.UP1_CHANNELS_LAST = True
+        ops.DepthnetLiftSplat.forward = orig
+    assert seen == [True, False]
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=3e-2, atol=3e-2)
+    rel = (outs[0][1] - outs[1][1]).norm() / outs[1][1].norm()
+    assert rel < 3e-2, rel.item()
