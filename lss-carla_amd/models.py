@@ -165,12 +165,12 @@ def _resnet_layer(inplanes, planes, blocks, stride):
 def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """A 1x1 nn.Conv2d (stride s, no padding) applied as a GEMM over the channels of every s-th pixel
     (F.linear: hipBLASLt) on CUDA maps, with the module's own weight and bias (same math). MIOpen's
-    channels-last 1x1 convolutions are not safe to replay from a hipGraph: from the second replay of
-    the captured training step on, the weight gradients of BevEncode's last conv (up2.4, 128 -> outC
-    = 1 channels, src/models.py:115) came out as garbage (1e35 / 1e-31) and those of the stride-2
-    downsample convs of layer2 / layer3 (torchvision BasicBlock) far from the eager step's
-    (relative 1.5-2.5 while every other parameter replayed within 1e-4 --
-    tests/test_gpu_captured_step.py)."""
+    channels-last 1x1 backward is not safe to replay from a hipGraph: from the second replay of the
+    captured training step on, the weight gradient of BevEncode's last conv (up2.4, 128 -> outC = 1
+    channels, src/models.py:115) came out as garbage (1e35 / 1e-31), and that of the depthnet's 1x1
+    conv on channels-last features as zeros (tests/test_gpu_captured_step.py). BevEncode's stride-2
+    downsample convs (torchvision BasicBlock, layer2 / layer3) are channels-last 1x1 convs too and
+    take this path for the same reason."""
     if not (x.is_cuda and x.dim() == 4) or conv.kernel_size != (1, 1) or conv.groups != 1 \
             or conv.stride[0] != conv.stride[1] or conv.padding not in ((0, 0), "valid"):
         return conv(x)

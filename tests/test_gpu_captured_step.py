@@ -84,7 +84,12 @@ def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find):
                      pre_step=lambda: hinv.update(host["post_rots"], host["intrins"]))
     step.capture(warmup=2)
     g_bev = seen["bev"]  # written by every replay (graph pool)
-    g_dw = flat.views(grads=True)["camencode.depthnet.weight"]
+    def graph_grad_views():
+        out = {}
+        for grp, gg in zip(flat.groups, step.graph_grads):
+            out.update(grp.views_of(gg))
+        return out
+    g_dw = graph_grad_views()["camencode.depthnet.weight"]
     assert g_bev.dtype == torch.bfloat16 and g_bev.is_contiguous(memory_format=torch.channels_last)
     snap = [m.detach().clone() for m in masters]
 
@@ -107,7 +112,9 @@ def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find):
         step()  # pre_step + graph replays
         torch.cuda.synchronize()
         rep = (g_bev.clone(), g_dw.clone(), step.static_loss.clone())
-        rep_all = {k: v.detach().clone() for k, v in flat.views(grads=True).items()}
+        # the replay's gradients live in the graph's own buffers (step.graph_grads): after an eager
+        # step the masters' .grad point elsewhere
+        rep_all = {k: v.detach().clone() for k, v in graph_grad_views().items()}
         restore()
         w = model.camencode.depthnet.weight.detach().to(torch.bfloat16).cpu()  # this step's bf16 operands
         b = model.camencode.depthnet.bias.detach().to(torch.bfloat16).cpu()
@@ -127,30 +134,6 @@ def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find):
         assert rel < 1e-3, (i, rel, rep[1].norm().item(), eag[1].norm().item())
         # every parameter's gradient, not only the hot path's: a conv solver that is not replay-safe
         # shows up as a replayed gradient of zeros (or garbage) next to the eager one
-        if os.environ.get("LSS_CAPTURE_DIAG"):  # a third step with MIOpen off (PyTorch's own convs)
-            eag_all = {k: v.detach().clone() for k, v in flat.views(grads=True).items()}
-            restore()
-            torch.backends.cudnn.enabled = False
-            try:
-                step.eager()
-            finally:
-                torch.backends.cudnn.enabled = True
-            torch.cuda.synchronize()
-            nat_all = {k: v.detach().clone() for k, v in flat.views(grads=True).items()}
-            restore()
-            step.eager()  # a second eager step: run-to-run spread of the same computation
-            torch.cuda.synchronize()
-            eag2_all = {k: v.detach().clone() for k, v in flat.views(grads=True).items()}
-            dd = sorted(((((eag2_all[k] - e).norm() / max(e.norm().item(), 1e-12)).item(), k)
-                         for k, e in eag_all.items() if e.norm().item() > 1e-6), reverse=True)
-            print(f"rig {i}: eager vs eager: " + ", ".join(f"{k} {v:.2e}" for v, k in dd[:5]))
-            for name_, cmp in (("rep", rep_all), ("eag", eag_all)):
-                dd = sorted(((((cmp[k] - e).norm() / max(e.norm().item(), 1e-12)).item(), k)
-                             for k, e in nat_all.items() if e.norm().item() > 1e-6), reverse=True)
-                print(f"rig {i}: {name_} vs native-conv step: " + ", ".join(f"{k} {v:.2e}" for v, k in dd[:5]))
-            restore()
-            step.eager()
-            torch.cuda.synchronize()
         diffs = []
         for k, e in flat.views(grads=True).items():
             en = e.norm().item()
@@ -158,7 +141,7 @@ def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find):
                 continue
             diffs.append((((rep_all[k] - e).norm() / en).item(), k, en, rep_all[k].norm().item(), e.numel()))
         diffs.sort(reverse=True)
-        for d_ in diffs[:5]:
+        for d_ in diffs[:3]:
             print(f"rig {i}: grad rel diff {d_[0]:.3e} {d_[1]} |eag| {d_[2]:.3e} |rep| {d_[3]:.3e} n {d_[4]}")
         # a replay-safe step reproduces every gradient to MIOpen's run-to-run noise (~1e-4, also the
         # ill-conditioned BN biases); a solver that is not replay-safe is off by O(1)
