@@ -45,7 +45,7 @@ typedef struct lss_grid {
 enum { LSS_F32 = 0, LSS_BF16 = 1 };          /* element types */
 enum { LSS_NCHW = 0, LSS_NHWC = 1 };         /* BEV memory layouts of a (B, Z*C, X, Y) tensor */
 enum { LSS_EINVAL = -1, LSS_EUNSUPPORTED = -2 };
-enum { LSS_SPLAT_EMPTY_FILLED = 1 };          /* lss_splat_fwd flags */
+enum { LSS_SPLAT_EMPTY_FILLED = 1, LSS_SPLAT_UNORDERED = 2 };  /* lss_splat_fwd flags */
 
 typedef void* lss_stream_t; /* a hipStream_t */
 typedef void* lss_event_t;  /* a hipEvent_t */
@@ -130,7 +130,11 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
  * Workspace header, 4 uint32: [0] scan ticket, [1] sticky count of look-back timeouts (a block that
  * waited its spin limit for a predecessor sums that predecessor's counts itself: the output is exact
  * either way), [2] spin-limit override (0: the built-in limit; s > 0: s - 1 polls -- tests of the
- * timeout path), [3] unused. */
+ * timeout path), [3] unused.
+ * sorted_row == NULL (pos_of must then be NULL too): no canonical pass -- sorted_key is grouped by
+ * ascending cell with the sentinel tail as above, but the entries of a cell are in the order the
+ * counting sort's atomics gave them (one kernel fewer; lss_splat_fwd with LSS_SPLAT_UNORDERED puts
+ * every cell in canonical order itself, with identical results). */
 size_t lss_csr_workspace_bytes(int32_t ncells);
 int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime,
                      int32_t* cell_count, int32_t ncells, const lss_dims_t* dims,
@@ -194,6 +198,10 @@ int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bia
  * reads them with the keys instead of gathering depth[p] (the same values: identical results).
  * flags: LSS_SPLAT_EMPTY_FILLED (LSS_NHWC only): the empty cells' rows are already zero (the
  * lift's fill, lss_lift_prep / lss_depthnet_lift with bev), only the occupied rows are written.
+ * LSS_SPLAT_UNORDERED (LSS_NHWC only, sorted_depth NULL, sorted_row unused): sorted_key comes from
+ * lss_csr_build_ws without sorted_row -- arrival order inside each cell; each chunk wave ranks the
+ * entries of every cell by point id before summing, so the result is bit-identical to the
+ * canonical CSR's. Fused mode needs Nprime < 2^24 (rows from point ids), else LSS_EUNSUPPORTED.
  * ev_start / ev_stop (nullable) are stamped with the kernel's own start / end
  * (hipExtLaunchKernel), so their elapsed time is the kernel alone, never launch latency. */
 int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,

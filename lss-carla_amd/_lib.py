@@ -20,6 +20,7 @@ F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
 ABI_VERSION = 14
 SPLAT_EMPTY_FILLED = 1
+SPLAT_UNORDERED = 2
 
 
 class Dims(ctypes.Structure):

@@ -644,15 +644,18 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
 
 // k_scatter plus the reset for the next call: the scan's ticket and granules and the cell counts
 // (nothing reads them after the scan). The grid covers max(nprime, ncells) threads.
+// tail: key_out is the final CSR (no k_csr_canon after this: arrival order inside a cell), so the
+// scatter also writes its sentinel tail (key -1 at entries [cell_start[ncells], nprime)).
 __global__ __launch_bounds__(kBlock) void k_scatter_ws(const int32_t* __restrict__ cell_of,
                                                        const int32_t* __restrict__ slot_of, int nprime,
                                                        const int32_t* __restrict__ cell_start,
                                                        long long* __restrict__ key_out, int32_t* __restrict__ cnt,
-                                                       int ncells, ScanWs* __restrict__ ws) {
+                                                       int ncells, ScanWs* __restrict__ ws, int tail) {
     const int t = blockIdx.x * kBlock + threadIdx.x;
     if (t < nprime) {
         const int cell = cell_of[t];
         if (cell >= 0) key_out[scatter_pos(cell, slot_of[t], cell_start, nprime)] = ((long long)cell << 32) | (unsigned)t;
+        if (tail && t >= cell_start[ncells]) key_out[t] = -1ll;
     }
     if (t < ncells) cnt[t] = 0;
     const int nb = (ncells + kScanItems - 1) / kScanItems;
@@ -1882,6 +1885,53 @@ __device__ __forceinline__ float group_weight(float wd, int u, int lane) {
     return __shfl(wd, lane - lane % LPR + u, kWave);
 }
 
+// A cell with more than 64 entries of an unordered CSR (arrival order inside the cell): its point ids
+// staged in LDS (the wave's meta and piece slots: up to `cap` entries), sorted by rank, then summed in
+// canonical order exactly as reduce_big_cell (one channel per lane). A larger cell takes the canonical
+// order by repeated minimum selection straight from memory (slow; never seen at the BASELINE configs,
+// whose largest cell holds 64 points).
+template <bool FUSED, typename RT>
+__device__ float reduce_big_cell_unordered(int start, int nprime, const long long* __restrict__ key,
+                                           const int32_t* __restrict__ cell_start, const float* __restrict__ depth,
+                                           const RT* __restrict__ rows_base, const BevGeo& g, int* __restrict__ s_in,
+                                           int* __restrict__ s_sorted, int cap, int lane, int* cell_out) {
+    const int cell = (int)(key[start] >> 32);
+    *cell_out = cell;
+    const int n = uniform(min(cell_start[cell + 1], nprime) - start);
+    auto entry = [&](int p, float& acc) {
+        const int r = FUSED ? row_of_point(p, g) : p;
+        const float w = FUSED ? depth[dchk(p, nprime, kDbgSplatPoint)] : 1.f;
+        const float v = to_f32(rows_base[(size_t)dchk(r, g.nrows, kDbgSplatRow) * kC + lane]);
+        acc = FUSED ? fmaf(w, v, acc) : __fadd_rn(acc, v);
+    };
+    float acc = 0.f;
+    if (n <= cap) {
+        for (int i = lane; i < n; i += kWave) s_in[i] = (int)(key[start + i] & 0xFFFFFFFF);
+        __builtin_amdgcn_wave_barrier();
+        for (int i = lane; i < n; i += kWave) {
+            const int p = s_in[i];
+            int r = 0;
+            for (int j = 0; j < n; ++j) r += s_in[j] < p ? 1 : 0;  // point ids are distinct inside a cell
+            s_sorted[r] = p;
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int k = 0; k < n; ++k) entry(s_sorted[k], acc);
+        return acc;
+    }
+    int last = -1;
+    for (int k = 0; k < n; ++k) {
+        int best = INT_MAX;
+        for (int i = lane; i < n; i += kWave) {
+            const int v = (int)(key[start + i] & 0xFFFFFFFF);
+            if (v > last && v < best) best = v;
+        }
+        best = uniform(wave_min(best));
+        entry(best, acc);
+        last = best;
+    }
+    return acc;
+}
+
 template <bool FUSED, typename RT, typename OutT>
 __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __restrict__ depth,
                                             const float* __restrict__ sorted_depth,
@@ -1890,7 +1940,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                                             const int32_t* __restrict__ sorted_row,
                                             const int32_t* __restrict__ cell_start, const BevGeo& g,
                                             OutT* __restrict__ out, EntryMeta* __restrict__ meta,
-                                            float* __restrict__ part, int lane) {
+                                            float* __restrict__ part, int lane, bool unordered) {
     using RS = RowSlice<RT>;
     // round trip 1: keys (cell << 32 | point), context rows, the previous entry's cell
     const int base = w * kWave;
@@ -1898,7 +1948,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     const long long k0 = e0 < nprime ? sorted_key[e0] : -1ll;
     const long long k1 = e1 < nprime ? sorted_key[e1] : -1ll;
     int rs0 = 0, rs1 = 0;
-    const bool row_from_p = LSS_ROW_FROM_P && g.dhw > 0;
+    const bool row_from_p = (LSS_ROW_FROM_P || unordered) && g.dhw > 0;
     if (FUSED && !row_from_p) {
         rs0 = e0 < nprime ? sorted_row[e0] : 0;
         rs1 = e1 < nprime ? sorted_row[e1] : 0;
@@ -1928,8 +1978,73 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
         return;
     }
     if (end > 0) {
-        meta[lane] = EntryMeta{rs0, p0, c0, __float_as_int(sw0)};
-        meta[kWave + lane] = EntryMeta{rs1, p1, c1, __float_as_int(sw1)};
+        int d0 = lane, d1 = kWave + lane;  // the entries' positions in the window
+        if (unordered) {
+            // The CSR's entries are grouped by cell but in arrival order inside a cell (the plan ran
+            // without k_csr_canon): put every cell of the window into canonical order (ascending point
+            // id) here, so the sums below -- and their bits -- are those of the canonical CSR. Rank of
+            // an entry inside its run of equal cells: the run's point ids staged in LDS (this wave's
+            // piece slots, free until the sums), ties (the sentinel's -1) broken by position.
+            int* sp = reinterpret_cast<int*>(part);
+            sp[lane] = p0;
+            sp[kWave + lane] = p1;
+            __builtin_amdgcn_wave_barrier();
+            const int up0 = __shfl(c0, (lane + 63) & 63, kWave), up1 = __shfl(c1, (lane + 63) & 63, kWave);
+            const int c0_last = __builtin_amdgcn_readlane(c0, 63);
+            const unsigned long long st0 = __ballot(c0 != (lane == 0 ? prevcell : up0));
+            const unsigned long long st1 = __ballot(c1 != (lane == 0 ? c0_last : up1));
+            const unsigned long long le = ~0ull >> (63 - lane);
+            const unsigned long long after = lane == 63 ? 0ull : (~0ull << (lane + 1));
+            // run [cs, ce) of each held entry (a run cut by the window's start begins at 0)
+            const int cs0 = 63 - __builtin_clzll((st0 & le) | 1ull);
+            const int cs1 = (st1 & le) ? kWave + 63 - __builtin_clzll(st1 & le) : 63 - __builtin_clzll(st0 | 1ull);
+            const unsigned long long n0 = st0 & after, n1 = st1 & after;
+            const int ce0 = n0 ? (int)__builtin_ctzll(n0) : (st1 ? kWave + (int)__builtin_ctzll(st1) : 2 * kWave);
+            const int ce1 = n1 ? kWave + (int)__builtin_ctzll(n1) : 2 * kWave;
+            // one uniform loop over the longest run of the window, both entries at once, 4 steps
+            // unrolled: 8 independent LDS reads in flight (a per-lane loop waited for each read)
+            // only the owned cells [s, end) are ranked (the others keep their positions: a cell cut
+            // by the window's end is long and never summed from here)
+            const int ws0 = s, we0 = end;  // (window positions)
+            const int l0 = (lane >= ws0 && lane < we0) ? ce0 - cs0 : 0;
+            const int l1 = (kWave + lane >= ws0 && kWave + lane < we0) ? ce1 - cs1 : 0;
+            int lmax = 0;  // the longest owned run: gaps between the run starts, on the scalar unit
+            {
+                unsigned long long a = st0, b = st1;
+                int last = ws0;  // the first owned cell starts at s
+                a &= (ws0 >= kWave - 1) ? 0ull : (~0ull << (ws0 + 1));
+                while (a) {
+                    const int j = (int)__builtin_ctzll(a);
+                    a &= a - 1;
+                    if (j > we0) break;
+                    lmax = max(lmax, j - last);
+                    last = j;
+                }
+                while (b && last < we0) {
+                    const int j = kWave + (int)__builtin_ctzll(b);
+                    b &= b - 1;
+                    if (j > we0) break;
+                    lmax = max(lmax, j - last);
+                    last = j;
+                }
+                lmax = uniform(max(lmax, we0 - last));
+            }
+            int r0 = 0, r1 = 0;
+            for (int k = 0; k < lmax; k += 4) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int j0 = cs0 + k + u, j1 = cs1 + k + u;
+                    const int q0 = sp[min(j0, 2 * kWave - 1)], q1 = sp[min(j1, 2 * kWave - 1)];
+                    r0 += (k + u < l0 && (q0 < p0 || (q0 == p0 && j0 < lane))) ? 1 : 0;
+                    r1 += (k + u < l1 && (q1 < p1 || (q1 == p1 && j1 < kWave + lane))) ? 1 : 0;
+                }
+            }
+            if (l0 > 0) d0 = cs0 + r0;
+            if (l1 > 0) d1 = cs1 + r1;
+            __builtin_amdgcn_wave_barrier();
+        }
+        meta[d0] = EntryMeta{rs0, p0, c0, __float_as_int(sw0)};
+        meta[d1] = EntryMeta{rs1, p1, c1, __float_as_int(sw1)};
         __builtin_amdgcn_wave_barrier();
         const int up = __shfl(c0, (lane + 63) & 63, kWave);
         const unsigned long long starts = __ballot(c0 != (lane == 0 ? prevcell : up)) &
@@ -2040,8 +2155,12 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     }
     if (big >= 0) {
         int cell;
-        const float a2 = reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base,
-                                                    lane, &cell, g.nrows);
+        const float a2 = unordered
+            ? reduce_big_cell_unordered<FUSED, RT>(base + big, nprime, sorted_key, cell_start, depth, rows_base, g,
+                                                   reinterpret_cast<int*>(meta), reinterpret_cast<int*>(part),
+                                                   min(2 * kWave * 4, RS::NG * kC), lane, &cell)
+            : reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base, lane, &cell,
+                                         g.nrows);
         cell_row(out, dchk(cell, g.ncells, kDbgSplatCell), g)[lane] = from_f32<OutT>(a2);
         if (kChunkGap > 0) {
             const int nx = uniform(cell_start[cell + 1]);
@@ -2240,7 +2359,7 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(c
                                                            const long long* __restrict__ sorted_key,
                                                            const int32_t* __restrict__ sorted_row, BevGeo g,
                                                            int nprime, int nchunk_blocks, int nzero_blocks,
-                                                           int order, OutT* __restrict__ out) {
+                                                           int order, int unordered, OutT* __restrict__ out) {
     __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
     __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][RowSlice<RT>::NG * kC];
     const int lane = threadIdx.x & 63;
@@ -2273,7 +2392,7 @@ __global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(c
         if (w * kWave >= nprime) return;
         LSS_STAMP(w, 0);
         splat_chunk<FUSED, RT, OutT>(w, nprime, depth, sorted_depth, rows_base, sorted_key, sorted_row, cell_start, g, out,
-                                     s_meta[wave], s_part[wave], lane);
+                                     s_meta[wave], s_part[wave], lane, unordered != 0);
         LSS_STAMP(w, 3);
 #if LSS_TRACE
         if (lane == 0 && w < 16384) g_lss_trace[w][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
@@ -3165,8 +3284,11 @@ size_t lss_csr_workspace_bytes(int32_t ncells) {
 int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, int32_t* cell_count,
                      int32_t ncells, const lss_dims_t* dims, int32_t* cell_start, long long* sorted_key,
                      int32_t* sorted_row, int32_t* pos_of, void* scratch, void* workspace, lss_stream_t stream) {
-    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !sorted_row || !scratch || !workspace ||
-        nprime <= 0 || ncells <= 0)
+    // sorted_row == NULL (and pos_of == NULL): the CSR in arrival order inside each cell, no
+    // canonical pass (lss_splat_fwd LSS_SPLAT_UNORDERED puts each cell in order itself)
+    const bool canonical = sorted_row != nullptr;
+    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || (!canonical && pos_of) || !scratch ||
+        !workspace || nprime <= 0 || ncells <= 0)
         return LSS_EINVAL;
     int DHW = nprime, HW = nprime;  // no dims: the row of point p is p (per-point rows)
     if (dims != nullptr) {
@@ -3182,7 +3304,12 @@ int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t npr
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(k_scan_lookback, dim3(nb), dim3(1024), 0, s, cell_count, ncells, ws, cell_start);
     hipLaunchKernelGGL(k_scatter_ws, dim3(grid_blocks(std::max(nprime, ncells), kBlock)), dim3(kBlock), 0, s, cell_of,
-                       slot_of, nprime, cell_start, tmp_key, cell_count, ncells, ws);
+                       slot_of, nprime, cell_start, canonical ? tmp_key : sorted_key, cell_count, ncells, ws,
+                       canonical ? 0 : 1);
+    if (!canonical) {
+        debug_check_csr(cell_start, ncells, cell_of, nprime, s);
+        return launch_status();
+    }
     const int nchunks = (nprime + kWave - 1) / kWave;
     hipLaunchKernelGGL(k_csr_canon, dim3(xcd_grid(grid_blocks(nchunks, kBlock / kWave))), dim3(kBlock), 0, s, tmp_key,
                        cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row, cell_of, pos_of);
@@ -3309,11 +3436,13 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
                   const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout,
                   int32_t flags, lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop) {
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
-    if (flags & ~LSS_SPLAT_EMPTY_FILLED) return LSS_EINVAL;
+    if (flags & ~(LSS_SPLAT_EMPTY_FILLED | LSS_SPLAT_UNORDERED)) return LSS_EINVAL;
     if ((flags & LSS_SPLAT_EMPTY_FILLED) && out_layout != LSS_NHWC) return LSS_EINVAL;
+    const bool unordered = (flags & LSS_SPLAT_UNORDERED) != 0;
+    if (unordered && (out_layout != LSS_NHWC || sorted_depth || LSS_SPLAT_IMPL != 0)) return LSS_EINVAL;
     if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_key || !out) return LSS_EINVAL;
     const bool fused = x_rows == nullptr;
-    if (fused && (!depth || !ctx_t || !sorted_row)) return LSS_EINVAL;
+    if (fused && (!depth || !ctx_t || (!sorted_row && !unordered))) return LSS_EINVAL;
     if (fused && ctx_dtype != LSS_F32 && ctx_dtype != LSS_BF16) return LSS_EINVAL;
     if (out_dtype != LSS_F32 && out_dtype != LSS_BF16) return LSS_EINVAL;
     const long nprime_l = (long)dims->B * dims->N * dims->D * dims->H * dims->W;
@@ -3330,6 +3459,7 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         g.ncells = dims->B * sg.Z * sg.X * sg.Y;
         g.hw = dims->H * dims->W;
         g.dhw = nprime < (1 << 24) ? dims->D * g.hw : 0;  // 0: read sorted_row instead
+        if (unordered && fused && g.dhw == 0) return LSS_EUNSUPPORTED;  // rows from point ids: p < 2^24
         g.inv_dhw = g.dhw ? 1.0f / (float)g.dhw : 0.f;
         g.inv_hw = 1.0f / (float)g.hw;
         g.nrows = sg.nrows;
@@ -3379,11 +3509,11 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
             hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, sorted_depth,      \
                                   (const RT*)rows,                                                                 \
                                   cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks,      \
-                                  order, (T*)out);                                                                 \
+                                  order, (int)unordered, (T*)out);                                                 \
         else                                                                                                       \
             hipLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, depth, sorted_depth, (const RT*)rows,   \
-                               cell_start,                                                                         \
-                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, order, (T*)out);    \
+                               cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, order,  \
+                               (int)unordered, (T*)out);                                                           \
     } while (0)
         if (out_dtype == LSS_F32) {
             if (!fused) LSS_NHWC_FWD(false, float, float);

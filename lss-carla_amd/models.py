@@ -38,6 +38,7 @@ from .norm import bn_act
 from .tools import gen_dx_bx
 
 UP1_CHANNELS_LAST = True  # CamEncode.up1 on channels-last maps under bf16 autocast (see get_eff_depth)
+UNORDERED_PLAN = False  # channels-last BEV: plans without the canonical pass (the splat orders each cell); measured slower
 
 
 class Up(nn.Module):
@@ -328,16 +329,18 @@ class LiftSplatShoot(nn.Module):
             inv = ops.camera_inverses(post_rots, intrins, self.inverse)
         ce = self.camencode
         side = None
+        # the channels-last splat ranks each cell's entries itself: its plan skips the canonical pass
+        canonical = not (UNORDERED_PLAN and self._layout() == _lib.NHWC)
         if self.plan_side_stream and x.is_cuda:
             side, main = _side_stream(x.device), torch.cuda.current_stream(x.device)
             side.wait_stream(main)  # the rig and its inverses (staged by pre_step) are ready
             with torch.cuda.stream(side):
                 plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
-                                             inverses=inv)
+                                             inverses=inv, canonical=canonical)
         feat = ce.dropout(ce.get_eff_depth(x.view(B * N, C, imH, imW)))
         if side is None:
             plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
-                                         inverses=inv)
+                                         inverses=inv, canonical=canonical)
         else:
             main.wait_stream(side)
             if not torch.cuda.is_current_stream_capturing():  # (a captured graph's pool is never reused)

@@ -157,7 +157,8 @@ class SplatPlan:
     cell_start: torch.Tensor   # (ncells+1,) int32
     sorted_key: torch.Tensor   # (Nprime,) int64 (cell << 32 | point): ascending cell, then point id;
                                # only the first cell_start[-1] entries are meaningful
-    sorted_row: torch.Tensor   # (Nprime,) int32 context row (pixel) of each sorted entry
+    sorted_row: Optional[torch.Tensor]  # (Nprime,) int32 context row (pixel) of each sorted entry; None:
+                               # an unordered plan (arrival order inside each cell, no canonical pass)
     geom: Optional[torch.Tensor] = None
     pos_of: Optional[torch.Tensor] = None  # (Nprime,) int32 sorted position of each point, -1 = dropped
 
@@ -169,6 +170,11 @@ class SplatPlan:
     def nprime(self) -> int:
         B, N, D, H, W = self.dims
         return B * N * D * H * W
+
+    @property
+    def canonical(self) -> bool:
+        """Entries inside each cell in ascending point id (else arrival order: see plan_from_cameras)."""
+        return self.sorted_row is not None
 
     def tensors(self):
         return [t for t in (self.cell_of, self.cell_start, self.sorted_key, self.sorted_row, self.geom, self.pos_of)
@@ -272,14 +278,16 @@ def _counted_plan(dev: torch.device, ws: Optional[PlanWs], launch_cells, build_c
     return out
 
 
-def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None):
-    """Counting sort into the canonical CSR (lss_csr_build[_ws]): cell_start, sorted_key, sorted_row."""
+def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None, canonical: bool = True):
+    """Counting sort into the canonical CSR (lss_csr_build[_ws]): cell_start, sorted_key, sorted_row.
+    canonical=False (with a persistent workspace): no canonical pass, sorted_row None."""
     lib = _lib.load()
     B, N, D, H, W = dims
     nprime = B * N * D * H * W
+    canonical = canonical or ws is None or SORTED_DEPTH
     cell_start = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
     sorted_key = torch.empty(nprime, device=dev, dtype=torch.int64)
-    sorted_row = torch.empty(nprime, device=dev, dtype=torch.int32)
+    sorted_row = torch.empty(nprime, device=dev, dtype=torch.int32) if canonical else None
     pos_of = torch.empty(nprime, device=dev, dtype=torch.int32) if SORTED_DEPTH else None
     if ws is not None:
         _lib.check(lib.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
@@ -327,11 +335,16 @@ USE_FRUSTUM_AXES = False  # measured: the two index divisions cost more than the
 
 def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, post_trans, grid: GridSpec,
                       inverse: str = "host", want_geom: bool = False, want_csr: bool = True,
-                      inverses: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> SplatPlan:
+                      inverses: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                      canonical: bool = True) -> SplatPlan:
     """get_geometry + quantise + filter + counting sort, all on the device (src/models.py:170-231).
 
     `inverses` = a (pinv, kinv) pair from camera_inverses, if already computed (models.py computes
     them before the trunk, so the host round trip of inverse='host' never waits for device work).
+    canonical=False: the CSR without its canonical pass (k_csr_canon) -- grouped by ascending cell,
+    arrival order inside a cell, sorted_row None -- for the channels-last splat, which ranks each
+    cell's entries itself (LSS_SPLAT_UNORDERED; identical BEV bits). Taken only with the persistent
+    workspace (eager warm-up before capture) and without SORTED_DEPTH; else the plan is canonical.
     """
     dev = _require_cuda(frustum, rots, trans, intrins, post_rots, post_trans)
     lib = _lib.load()
@@ -361,12 +374,14 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
         launch_cells()
         return SplatPlan((B, N, D, H, W), grid, cell_of, None, None, None, geom, None)
     cell_start, sorted_key, sorted_row, pos_of = _counted_plan(
-        dev, ws, launch_cells, lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws))
+        dev, ws, launch_cells,
+        lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws, canonical))
     return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom, pos_of)
 
 
-def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
-    """Quantise a given (B, N, D, H, W, 3) geometry (voxel_pooling(geom_feats, x) boundary)."""
+def plan_from_geom(geom: torch.Tensor, grid: GridSpec, canonical: bool = True) -> SplatPlan:
+    """Quantise a given (B, N, D, H, W, 3) geometry (voxel_pooling(geom_feats, x) boundary).
+    canonical: as plan_from_cameras."""
     dev = _require_cuda(geom)
     lib = _lib.load()
     B, N, D, H, W, _ = geom.shape
@@ -383,7 +398,8 @@ def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
                    "lss_cells_from_geom")
 
     cell_start, sorted_key, sorted_row, pos_of = _counted_plan(
-        dev, ws, launch_cells, lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws))
+        dev, ws, launch_cells,
+        lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws, canonical))
     return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, None, pos_of)
 
 
@@ -459,6 +475,10 @@ def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, 
                       flags: int = 0):
     lib = _lib.load()
     dev = out.device
+    if not plan.canonical:
+        if layout != _lib.NHWC or sorted_depth is not None:
+            raise RuntimeError("lss_carla_amd: an unordered plan (canonical=False) feeds the channels-last splat only")
+        flags |= _lib.SPLAT_UNORDERED
     e0, e1 = SPLAT_PROFILE.new_pair() if SPLAT_PROFILE.enabled else (None, None)
     ctx_code = _lib.dtype_code(ctx_t.dtype) if ctx_t is not None else _lib.F32
     _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), ctx_code, _lib.ptr(x_rows),
