@@ -41,6 +41,17 @@ int lss_dwconv_bwd_weight(const void* x, const void* dy, int32_t dtype, int32_t 
                           int32_t K, int32_t stride, int32_t pad_top, int32_t pad_left, int32_t Ho, int32_t Wo,
                           int32_t ngroups, float* partial, void* stream);
 
+/* 1x1 convolution to one output channel (BevEncode's last conv, up2.4: 128 -> outC = 1,
+ * src/models.py:115) over channels-last bf16 rows x (P, C), C % 8 == 0 and 64 % (C / 8) == 0:
+ * y[r] = bf16(sum_c x[r, c] * w[c] + bias[0]) (fp32 accumulation; w holds the bf16-rounded weights
+ * as fp32, as autocast's conv operands; bias is a device scalar, nullable). Backward: dx[r, c] = bf16(dy[r] * w[c]) and partial
+ * (lss_head1_blocks(P), C + 1) fp32 = per block of rows, sum_r dy[r] * x[r, c] (columns 0..C-1) and
+ * sum_r dy[r] (column C); the caller sums the blocks (fixed order). */
+int lss_head1_blocks(int32_t P);
+int lss_head1_fwd(const void* x, const float* w, const float* bias, int32_t P, int32_t C, void* y, void* stream);
+int lss_head1_bwd(const void* x, const void* dy, const float* w, int32_t P, int32_t C, void* dx, float* partial,
+                  void* stream);
+
 /* Training-mode batch norm fused with an activation (and, for ReLU, a residual add), for
  * nn.BatchNorm2d followed by swish (EfficientNet-B0, src/models.py:68 and the MBConv blocks) or
  * ReLU (CamEncode.up1, BevEncode, src/models.py:15-34, 92-130):

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 14
+#define LSS_ABI_VERSION 15
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -140,6 +140,18 @@ int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t npr
                      int32_t* cell_count, int32_t ncells, const lss_dims_t* dims,
                      int32_t* cell_start, long long* sorted_key, int32_t* sorted_row, int32_t* pos_of,
                      void* scratch, void* workspace, lss_stream_t stream);
+
+/* The whole plan in one call, on the persistent workspace of lss_csr_build_ws: lss_geometry_cells
+ * (counting into cell_count; slot_of is scratch, Nprime ints) that also sums the counts of every
+ * group of 4096 cells into the workspace, a scan that reads each group's prefix from those sums
+ * (no look-back between blocks), the scatter and the canonical pass. Outputs -- cell_of,
+ * cell_start, sorted_key, sorted_row, pos_of (nullable) -- bit-identical to lss_geometry_cells +
+ * lss_csr_build_ws; same workspace contract (zero-filled, left zero-filled). */
+int lss_plan_ws(const float* frustum, const float* rots, const float* trans, const float* kinv,
+                const float* pinv, const float* post_trans, const lss_dims_t* dims, const lss_grid_t* grid,
+                int32_t* cell_of, int32_t* slot_of, int32_t* cell_count, int32_t* cell_start,
+                long long* sorted_key, int32_t* sorted_row, int32_t* pos_of, void* scratch, void* workspace,
+                lss_stream_t stream);
 
 /* Lift, part 1 (CamEncode.get_depth_dist + layout, src/models.py:49-59, 192-202):
  * depth (B*N, D, H, W) fp32 = softmax over D of depthnet_out[:, :D];

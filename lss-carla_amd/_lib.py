@@ -18,7 +18,7 @@ DEBUG_LIB_PATH = os.path.join(_HERE, "liblss_hip_debug.so")  # LSS_DEBUG=1: devi
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 14
+ABI_VERSION = 15
 SPLAT_EMPTY_FILLED = 1
 SPLAT_UNORDERED = 2
 
@@ -63,6 +63,7 @@ SIGNATURES = {
     "lss_csr_build": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p, _p]),
     "lss_csr_workspace_bytes": (ctypes.c_size_t, [_i32]),
     "lss_csr_build_ws": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p, _p, _p]),
+    "lss_plan_ws": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID] + [_p] * 10),
     "lss_lift_prep": (ctypes.c_int, [_p, _i32, _DIMS, _p, _p, _i32, _p, _p, _p, _GRID, _p, _i32, _p]),
     "lss_depthnet_lift": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p, _p, _p, _GRID, _p, _i32,
                                          _p]),
@@ -86,6 +87,9 @@ SIGNATURES = {
     "lss_dwconv_fwd": (ctypes.c_int, [_p, _i32, _p] + [_i32] * 10 + [_p, _p]),
     "lss_dwconv_bwd_data": (ctypes.c_int, [_p, _i32, _p] + [_i32] * 10 + [_p, _p]),
     "lss_dwconv_bwd_weight": (ctypes.c_int, [_p, _p, _i32] + [_i32] * 11 + [_p, _p]),
+    "lss_head1_blocks": (ctypes.c_int, [_i32]),
+    "lss_head1_fwd": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _p]),
+    "lss_head1_bwd": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _p, _p]),
     "lss_bn_groups": (ctypes.c_int, [_i32, _i32, _i32, _i32]),
     "lss_bn_fwd": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, ctypes.c_float, ctypes.c_float,
                                   _p, _p, _p, _i32, _i32, _p, _p, _p, _p, _p, _p, _p]),

@@ -308,9 +308,142 @@ struct BwdWeight {
     }
 };
 
+// ---- 1x1 convolution to ONE output channel over channels-last rows (BevEncode's last conv, up2.4:
+// 128 -> outC = 1, src/models.py:115). As a GEMM it is a GEMV: its weight gradient is a K = B*X*Y
+// reduction that hipBLASLt ran on 8 workgroups (MT16x16x512, ~210 us of a c3 step). Here a wave
+// reads 4 rows per instruction (16 lanes x 16 B = one 128-channel row), fp32 accumulation.
+constexpr int kHeadRows = 256;  // rows per block (64 per wave)
+
+template <int LPR>  // lanes per row: C / 8
+__global__ __launch_bounds__(kBlock) void k_head1_fwd(const uint4* __restrict__ x, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, int P, bf16* __restrict__ y) {
+    constexpr int RPI = kWave / LPR;  // rows per wave instruction
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int col = lane % LPR, sub = lane / LPR;
+    float wv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wv[i] = w[col * 8 + i];
+    const float b = bias ? *bias : 0.f;  // (a device value: a captured graph replays with the current bias)
+    const int r0 = blockIdx.x * kHeadRows + wave * (kHeadRows / 4);
+#pragma unroll 4
+    for (int it = 0; it < kHeadRows / 4 / RPI; ++it) {
+        const int r = r0 + it * RPI + sub;
+        float acc = 0.f;
+        if (r < P) {
+            const uint4 v = x[(size_t)r * LPR + col];
+            const unsigned u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                acc = fmaf(__uint_as_float(u[i] << 16), wv[2 * i], acc);
+                acc = fmaf(__uint_as_float(u[i] & 0xFFFF0000u), wv[2 * i + 1], acc);
+            }
+        }
+#pragma unroll
+        for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, kWave);
+        if (col == 0 && r < P) y[r] = __float2bfloat16(acc + b);
+    }
+}
+
+// dx[r, c] = dy[r] * w[c] (bf16); partial[block][c] = sum over the block's rows of dy[r] * x[r, c],
+// partial[block][C] = sum of dy[r] (fixed reduction order: deterministic).
+template <int LPR>
+__global__ __launch_bounds__(kBlock) void k_head1_bwd(const uint4* __restrict__ x, const bf16* __restrict__ dy,
+                                                      const float* __restrict__ w, int P, uint4* __restrict__ dx,
+                                                      float* __restrict__ partial) {
+    constexpr int RPI = kWave / LPR;
+    constexpr int C = LPR * 8;
+    __shared__ float s_part[4][C + 1];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int col = lane % LPR, sub = lane / LPR;
+    float wv[8], acc[8] = {};
+    float dsum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wv[i] = w[col * 8 + i];
+    const int r0 = blockIdx.x * kHeadRows + wave * (kHeadRows / 4);
+#pragma unroll 4
+    for (int it = 0; it < kHeadRows / 4 / RPI; ++it) {
+        const int r = r0 + it * RPI + sub;
+        if (r < P) {
+            const float g = __bfloat162float(dy[r]);
+            const uint4 v = x[(size_t)r * LPR + col];
+            const unsigned u[4] = {v.x, v.y, v.z, v.w};
+            unsigned o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float lo = __uint_as_float(u[i] << 16), hi = __uint_as_float(u[i] & 0xFFFF0000u);
+                acc[2 * i] = fmaf(g, lo, acc[2 * i]);
+                acc[2 * i + 1] = fmaf(g, hi, acc[2 * i + 1]);
+                const bf16 a = __float2bfloat16(g * wv[2 * i]), c = __float2bfloat16(g * wv[2 * i + 1]);
+                o[i] = (unsigned)*reinterpret_cast<const unsigned short*>(&a) |
+                       ((unsigned)*reinterpret_cast<const unsigned short*>(&c) << 16);
+            }
+            dx[(size_t)r * LPR + col] = make_uint4(o[0], o[1], o[2], o[3]);
+            if (col == 0) dsum += g;
+        }
+    }
+    // lanes of one column slice: reduce over the wave's row groups, then over the waves via LDS
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int off = LPR; off < kWave; off <<= 1) acc[i] += __shfl_xor(acc[i], off, kWave);
+#pragma unroll
+    for (int off = LPR; off < kWave; off <<= 1) dsum += __shfl_xor(dsum, off, kWave);
+    if (sub == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s_part[wave][col * 8 + i] = acc[i];
+        if (col == 0) s_part[wave][C] = dsum;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c <= C; c += kBlock)
+        partial[(size_t)blockIdx.x * (C + 1) + c] = ((s_part[0][c] + s_part[1][c]) + s_part[2][c]) + s_part[3][c];
+}
+
 }  // namespace
 
 extern "C" {
+
+int lss_head1_blocks(int32_t P) { return P > 0 ? (P + kHeadRows - 1) / kHeadRows : 0; }
+
+int lss_head1_fwd(const void* x, const float* w, const float* bias, int32_t P, int32_t C, void* y, void* stream) {
+    if (!x || !w || !y || P <= 0 || C <= 0 || C % 8 != 0 || 64 % (C / 8) != 0) return LSS_CONV_EINVAL;
+    const dim3 gr(lss_head1_blocks(P)), bl(kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    switch (C / 8) {
+        case 16: hipLaunchKernelGGL((k_head1_fwd<16>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
+        case 8: hipLaunchKernelGGL((k_head1_fwd<8>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
+        case 32: hipLaunchKernelGGL((k_head1_fwd<32>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
+        case 64: hipLaunchKernelGGL((k_head1_fwd<64>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
+        case 4: hipLaunchKernelGGL((k_head1_fwd<4>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
+        case 2: hipLaunchKernelGGL((k_head1_fwd<2>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
+        case 1: hipLaunchKernelGGL((k_head1_fwd<1>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
+        default: return LSS_CONV_EINVAL;
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+int lss_head1_bwd(const void* x, const void* dy, const float* w, int32_t P, int32_t C, void* dx, float* partial,
+                  void* stream) {
+    if (!x || !dy || !w || !dx || !partial || P <= 0 || C <= 0 || C % 8 != 0 || 64 % (C / 8) != 0)
+        return LSS_CONV_EINVAL;
+    const dim3 gr(lss_head1_blocks(P)), bl(kBlock);
+    hipStream_t s = (hipStream_t)stream;
+#define LSS_HEAD1_BWD(L)                                                                                          \
+    hipLaunchKernelGGL((k_head1_bwd<L>), gr, bl, 0, s, (const uint4*)x, (const bf16*)dy, w, P, (uint4*)dx, partial)
+    switch (C / 8) {
+        case 16: LSS_HEAD1_BWD(16); break;
+        case 8: LSS_HEAD1_BWD(8); break;
+        case 32: LSS_HEAD1_BWD(32); break;
+        case 64: LSS_HEAD1_BWD(64); break;
+        case 4: LSS_HEAD1_BWD(4); break;
+        case 2: LSS_HEAD1_BWD(2); break;
+        case 1: LSS_HEAD1_BWD(1); break;
+        default: return LSS_CONV_EINVAL;
+    }
+#undef LSS_HEAD1_BWD
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
 
 int lss_dwconv_fwd(const void* x, int32_t dtype, const float* w, int32_t N, int32_t C, int32_t Hi, int32_t Wi,
                    int32_t K, int32_t stride, int32_t pad_top, int32_t pad_left, int32_t Ho, int32_t Wo, void* y,

@@ -223,13 +223,30 @@ struct GeoHash {
 // points holds 67 k distinct (block, cell) pairs in all against 141 k (wave, cell) pairs; at c5 171 k
 // against 535 k -- and the device atomics, executed at the memory side, are what the kernel waits on.
 // Must be called by every thread of the block (cell = -1 for dropped / out-of-range points).
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+// agg (nullable): the counts are also summed per group of kScanItems cells into agg[cell / kScanItems]
+// (the block's groups -- one or two -- first in a small LDS table, then one atomic each), so the scan
+// reads every block's prefix directly (k_scan_agg) instead of looking back.
+constexpr int kGeoGroups = 16;
+constexpr int kAggRep = 16;  // replicas of every group sum (agg[g * kAggRep + block % kAggRep]): device
+                             // atomics on one address serialise at the memory side
 __device__ __forceinline__ void emit_cell_block(int p, int cell, int32_t* cell_of, int32_t* cell_count,
-                                                int32_t* slot_of, bool live, GeoHash& h) {
+                                                int32_t* slot_of, bool live, GeoHash& h, int32_t* agg = nullptr) {
     if (live) cell_of[p] = cell;
     if (cell_count == nullptr) return;  // block-uniform
+    __shared__ int s_gkey[kGeoGroups], s_gval[kGeoGroups];
     for (int i = threadIdx.x; i < kGeoHash; i += kGeoBlock) {
         h.key[i] = -1;
         h.cnt[i] = 0;
+    }
+    if (agg != nullptr && threadIdx.x < kGeoGroups) {
+        s_gkey[threadIdx.x] = -1;
+        s_gval[threadIdx.x] = 0;
     }
     __syncthreads();
     const bool kept = live && cell >= 0;
@@ -244,11 +261,37 @@ __device__ __forceinline__ void emit_cell_block(int p, int cell, int32_t* cell_o
         rank = atomicAdd(&h.cnt[at], 1);
     }
     __syncthreads();
+    // (every thread runs the same number of iterations: the group sums below use wave-wide ballots)
     for (int i = threadIdx.x; i < kGeoHash; i += kGeoBlock) {
         const int c = h.key[i];
-        if (c >= 0) h.cnt[i] = atomicAdd(cell_count + c, h.cnt[i]);
+        const int n = c >= 0 ? h.cnt[i] : 0;
+        if (c >= 0) h.cnt[i] = atomicAdd(cell_count + c, n);
+        if (agg != nullptr) {
+            // per wave: one sum per distinct group (usually one), then one LDS atomic by its leader
+            const int gk = c >= 0 ? c / kScanItems : -1;
+            unsigned long long rem = __ballot(c >= 0);
+            while (rem) {
+                const int l0 = __builtin_ctzll(rem);
+                const int g0 = __builtin_amdgcn_readlane(gk, l0);
+                const unsigned long long peers = __ballot(gk == g0) & rem;
+                rem &= ~peers;
+                const int sum = wave_sum_i(((peers >> (threadIdx.x & 63)) & 1ull) ? n : 0);
+                if ((int)(threadIdx.x & 63) == l0) {
+                    int at2 = g0 & (kGeoGroups - 1), probes = 0;
+                    for (; probes < kGeoGroups; ++probes) {
+                        const int prev = atomicCAS(&s_gkey[at2], -1, g0);
+                        if (prev == -1 || prev == g0) break;
+                        at2 = (at2 + 1) & (kGeoGroups - 1);
+                    }
+                    if (probes < kGeoGroups) atomicAdd(&s_gval[at2], sum);
+                    else atomicAdd(agg + g0 * kAggRep + (blockIdx.x % kAggRep), sum);  // (table full)
+                }
+            }
+        }
     }
     __syncthreads();
+    if (agg != nullptr && threadIdx.x < kGeoGroups && s_gkey[threadIdx.x] >= 0)
+        atomicAdd(agg + s_gkey[threadIdx.x] * kAggRep + (blockIdx.x % kAggRep), s_gval[threadIdx.x]);
     if (live) slot_of[p] = kept ? h.cnt[at] + rank : -1;
 }
 
@@ -343,7 +386,8 @@ __global__ __launch_bounds__(kGeoBlock) void k_geometry_cells(
     const float* __restrict__ frustum, const float* __restrict__ rots, const float* __restrict__ trans,
     const float* __restrict__ kinv, const float* __restrict__ pinv, const float* __restrict__ post_trans,
     int N, int DHW, int HW, int W, int nprime, lss_grid_t g, float* __restrict__ out_geom,
-    int32_t* __restrict__ cell_of, int32_t* __restrict__ cell_count, int32_t* __restrict__ slot_of) {
+    int32_t* __restrict__ cell_of, int32_t* __restrict__ cell_count, int32_t* __restrict__ slot_of,
+    int32_t* __restrict__ agg = nullptr) {
     LSS_STAMP(blockIdx.x * (kGeoBlock / kWave) + (threadIdx.x >> 6), 0);
     const int p0 = blockIdx.x * kGeoBlock + threadIdx.x;
     const bool live = p0 < nprime;
@@ -373,7 +417,7 @@ __global__ __launch_bounds__(kGeoBlock) void k_geometry_cells(
     LSS_STAMP(tslot, 2);
     if (LSS_GEOM_AGG == 3) {
         __shared__ GeoHash hash;
-        emit_cell_block(p, cell, cell_of, cell_count, slot_of, live, hash);
+        emit_cell_block(p, cell, cell_of, cell_count, slot_of, live, hash, agg);
     } else {
         emit_cell(p, cell, cell_of, cell_count, slot_of, live);
     }
@@ -519,11 +563,6 @@ struct ScanWs {  // lss_csr_workspace_bytes: [ticket, timeouts, spin_limit_overr
     unsigned pad;
 };
 
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
-}
 
 // Look-back granules still 0 (their block has not published): replaced by the block's aggregate
 // {status 1, sum of its kScanItems counts}, summed by the whole wave from `cnt`. jb = the block each
@@ -642,6 +681,48 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
     LSS_STAMP(blockIdx.x * 16 + (threadIdx.x >> 6), 3);
 }
 
+// ---- scan from per-group aggregates (lss_plan_ws): the geometry summed the counts of every group of
+// kScanItems cells into agg[], so block lb's prefix is agg[0] + ... + agg[lb - 1] -- read in the same
+// round trip as its counts, no look-back, no waiting on other blocks.
+__global__ __launch_bounds__(1024) void k_scan_agg(const int32_t* __restrict__ cnt, int ncells,
+                                                   const int32_t* __restrict__ agg, int32_t* __restrict__ cell_start) {
+    __shared__ int s_wave[32];
+    __shared__ int s_total;
+    __shared__ int s_red[16];
+    const int lb = blockIdx.x;
+    const int nb = (ncells + kScanItems - 1) / kScanItems;
+    const int base = lb * kScanItems + threadIdx.x * 4;
+    const bool vec = ((reinterpret_cast<uintptr_t>(cnt) | reinterpret_cast<uintptr_t>(cell_start)) & 15) == 0;
+    int4 c4 = make_int4(0, 0, 0, 0);
+    if (vec && base + 4 <= ncells) {
+        c4 = *reinterpret_cast<const int4*>(cnt + base);
+    } else if (base < ncells) {
+        c4.x = cnt[base];
+        if (base + 1 < ncells) c4.y = cnt[base + 1];
+        if (base + 2 < ncells) c4.z = cnt[base + 2];
+        if (base + 3 < ncells) c4.w = cnt[base + 3];
+    }
+    int pre = 0;
+    for (int i = threadIdx.x; i < lb * kAggRep; i += 1024) pre += agg[i];
+    pre = wave_sum_i(pre);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = pre;
+    const int excl = block_exclusive_scan_1024(c4.x + c4.y + c4.z + c4.w, s_wave, &s_total);  // (barriers)
+    int prefix = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) prefix += s_red[w];
+    const int r0 = prefix + excl;
+    const int4 o4 = make_int4(r0, r0 + c4.x, r0 + c4.x + c4.y, r0 + c4.x + c4.y + c4.z);
+    if (vec && base + 4 <= ncells) {
+        *reinterpret_cast<int4*>(cell_start + base) = o4;
+    } else if (base < ncells) {
+        cell_start[base] = o4.x;
+        if (base + 1 < ncells) cell_start[base + 1] = o4.y;
+        if (base + 2 < ncells) cell_start[base + 2] = o4.z;
+        if (base + 3 < ncells) cell_start[base + 3] = o4.w;
+    }
+    if (lb == nb - 1 && threadIdx.x == 0) cell_start[ncells] = prefix + s_total;
+}
+
 // k_scatter plus the reset for the next call: the scan's ticket and granules and the cell counts
 // (nothing reads them after the scan). The grid covers max(nprime, ncells) threads.
 // tail: key_out is the final CSR (no k_csr_canon after this: arrival order inside a cell), so the
@@ -650,7 +731,8 @@ __global__ __launch_bounds__(kBlock) void k_scatter_ws(const int32_t* __restrict
                                                        const int32_t* __restrict__ slot_of, int nprime,
                                                        const int32_t* __restrict__ cell_start,
                                                        long long* __restrict__ key_out, int32_t* __restrict__ cnt,
-                                                       int ncells, ScanWs* __restrict__ ws, int tail) {
+                                                       int ncells, ScanWs* __restrict__ ws, int tail,
+                                                       int32_t* __restrict__ agg = nullptr) {
     const int t = blockIdx.x * kBlock + threadIdx.x;
     if (t < nprime) {
         const int cell = cell_of[t];
@@ -660,6 +742,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter_ws(const int32_t* __restrict
     if (t < ncells) cnt[t] = 0;
     const int nb = (ncells + kScanItems - 1) / kScanItems;
     if (t < nb) reinterpret_cast<unsigned long long*>(ws + 1)[t] = 0ull;
+    if (agg != nullptr && t < nb * kAggRep) agg[t] = 0;
     if (t == 0) ws->ticket = 0u;
 }
 
@@ -3278,7 +3361,41 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
 
 size_t lss_csr_workspace_bytes(int32_t ncells) {
     const size_t nb = (size_t)((ncells + kScanItems - 1) / kScanItems);
-    return sizeof(ScanWs) + sizeof(unsigned long long) * nb;
+    // header, look-back granules, per-group aggregates (lss_plan_ws)
+    return sizeof(ScanWs) + sizeof(unsigned long long) * nb + sizeof(int32_t) * kAggRep * nb;
+}
+
+int lss_plan_ws(const float* frustum, const float* rots, const float* trans, const float* kinv, const float* pinv,
+                const float* post_trans, const lss_dims_t* dims, const lss_grid_t* grid, int32_t* cell_of,
+                int32_t* slot_of, int32_t* cell_count, int32_t* cell_start, long long* sorted_key, int32_t* sorted_row,
+                int32_t* pos_of, void* scratch, void* workspace, lss_stream_t stream) {
+    if (!dims_ok(dims) || !grid_ok(grid) || !frustum || !rots || !trans || !kinv || !pinv || !post_trans || !cell_of ||
+        !slot_of || !cell_count || !cell_start || !sorted_key || !sorted_row || !scratch || !workspace)
+        return LSS_EINVAL;
+    const long DHW = (long)dims->D * dims->H * dims->W;
+    const long nprime_l = (long)dims->B * dims->N * DHW;
+    const long ncells_l = (long)dims->B * grid->nx[0] * grid->nx[1] * grid->nx[2];
+    if (nprime_l >= INT_MAX || ncells_l >= INT_MAX) return LSS_EUNSUPPORTED;
+    const int nprime = (int)nprime_l, ncells = (int)ncells_l;
+    const int nb = (ncells + kScanItems - 1) / kScanItems;
+    ScanWs* ws = static_cast<ScanWs*>(workspace);
+    int32_t* agg = reinterpret_cast<int32_t*>(reinterpret_cast<unsigned long long*>(ws + 1) + nb);
+    const size_t poff = ((sizeof(int32_t) * (size_t)(nb + 1)) + 255) & ~(size_t)255;  // as lss_csr_build
+    long long* tmp_key = reinterpret_cast<long long*>(static_cast<char*>(scratch) + poff);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_geometry_cells<false>, dim3(grid_blocks(nprime, kGeoBlock)), dim3(kGeoBlock), 0, s, frustum,
+                       rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW, dims->H * dims->W, dims->W, nprime,
+                       *grid, nullptr, cell_of, cell_count, slot_of, agg);
+    hipLaunchKernelGGL(k_scan_agg, dim3(nb), dim3(1024), 0, s, cell_count, ncells, agg, cell_start);
+    hipLaunchKernelGGL(k_scatter_ws, dim3(grid_blocks(std::max(std::max(nprime, ncells), nb * kAggRep), kBlock)),
+                       dim3(kBlock), 0, s, cell_of, slot_of, nprime, cell_start, tmp_key, cell_count, ncells, ws, 0,
+                       agg);
+    const int nchunks = (nprime + kWave - 1) / kWave;
+    hipLaunchKernelGGL(k_csr_canon, dim3(xcd_grid(grid_blocks(nchunks, kBlock / kWave))), dim3(kBlock), 0, s, tmp_key,
+                       cell_start + ncells, nchunks, nprime, (int)DHW, dims->H * dims->W, sorted_key, sorted_row,
+                       cell_of, pos_of);
+    debug_check_csr(cell_start, ncells, cell_of, nprime, s);
+    return launch_status();
 }
 
 int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, int32_t* cell_count,

@@ -163,6 +163,56 @@ def _resnet_layer(inplanes, planes, blocks, stride):
     return nn.Sequential(*layers)
 
 
+class _Head1x1(torch.autograd.Function):
+    """A 1x1 conv to ONE output channel over channels-last bf16 maps on lss_head1_* (include/lss_convs.h):
+    as a GEMM it is a GEMV whose weight gradient -- a reduction over every pixel of the BEV -- ran on a
+    handful of hipBLASLt workgroups (~210 us per c3 step); here one pass over the input each way."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
+    def forward(ctx, x, weight, bias):
+        lib = _lib.load()
+        N, C, H, W = x.shape
+        x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        w = weight.detach().to(torch.bfloat16).reshape(C).float()  # the bf16 operand, as fp32
+        b = bias.detach().to(torch.bfloat16).float().reshape(1) if bias is not None else None
+        y = torch.empty(N, 1, H, W, device=x.device, dtype=torch.bfloat16)
+        _lib.check(lib.lss_head1_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), N * H * W, C, _lib.ptr(y),
+                                     _lib.stream_handle(x.device)), "lss_head1_fwd")
+        ctx.save_for_backward(x, w)
+        ctx.meta = (weight.shape, weight.dtype, None if bias is None else bias.dtype)
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        lib = _lib.load()
+        x, w = ctx.saved_tensors
+        wshape, wdtype, bdtype = ctx.meta
+        N, C, H, W = x.shape
+        P = N * H * W
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = torch.empty_like(x)  # channels-last, as x
+        part = torch.empty(int(lib.lss_head1_blocks(P)), C + 1, device=x.device, dtype=torch.float32)
+        _lib.check(lib.lss_head1_bwd(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(w), P, C, _lib.ptr(dx), _lib.ptr(part),
+                                     _lib.stream_handle(x.device)), "lss_head1_bwd")
+        tot = part.sum(0)
+        dw = tot[:C].reshape(wshape).to(wdtype)
+        db = tot[C:].to(bdtype) if bdtype is not None else None
+        return dx, dw, db
+
+
+def _head1_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    C = x.shape[1] if x.dim() == 4 else 0
+    bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
+                                          and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+    return (USE_HIP_HEAD1 and conv.out_channels == 1 and x.is_cuda and x.dim() == 4 and bf16 and C % 8 == 0
+            and C // 8 > 0 and 64 % (C // 8) == 0 and x.is_contiguous(memory_format=torch.channels_last))
+
+
+USE_HIP_HEAD1 = True  # BevEncode's last conv (one output channel) on lss_head1_* instead of a hipBLASLt GEMV
+
+
 def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """A 1x1 nn.Conv2d (stride s, no padding) applied as a GEMM over the channels of every s-th pixel
     (F.linear: hipBLASLt) on CUDA maps, with the module's own weight and bias (same math). MIOpen's
@@ -176,6 +226,8 @@ def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
             or conv.stride[0] != conv.stride[1] or conv.padding not in ((0, 0), "valid"):
         return conv(x)
     s = conv.stride[0]
+    if s == 1 and _head1_eligible(conv, x):
+        return _Head1x1.apply(x, conv.weight, conv.bias)
     if s > 1:
         x = x[:, :, ::s, ::s]
     w = conv.weight.reshape(conv.out_channels, conv.in_channels)

@@ -330,6 +330,7 @@ def frustum_axes(frustum: torch.Tensor) -> Optional[torch.Tensor]:
     return axes
 
 
+USE_PLAN_WS_CALL = False  # plans through lss_plan_ws (aggregate scan): measured slower (geometry +4 us for scan -0.7 us)
 USE_FRUSTUM_AXES = False  # measured: the two index divisions cost more than the 4 MB of frustum reads (11.2 vs 10.3 us)
 
 
@@ -373,6 +374,21 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
     if not want_csr:
         launch_cells()
         return SplatPlan((B, N, D, H, W), grid, cell_of, None, None, None, geom, None)
+    if USE_PLAN_WS_CALL and ws is not None and canonical and geom is None and axes is None:
+        # the whole plan in one call: the scan reads each block's prefix from group sums the
+        # geometry kernel leaves (no look-back); outputs identical to the calls below
+        def whole_plan():
+            cs = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
+            sk = torch.empty(nprime, device=dev, dtype=torch.int64)
+            sr = torch.empty(nprime, device=dev, dtype=torch.int32)
+            po = torch.empty(nprime, device=dev, dtype=torch.int32) if SORTED_DEPTH else None
+            _lib.check(lib.lss_plan_ws(_lib.ptr(fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv),
+                                       _lib.ptr(pt), dims, g, _lib.ptr(cell_of), _lib.ptr(slot_of), _lib.ptr(counts),
+                                       _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), _lib.ptr(po), _lib.ptr(ws.scratch),
+                                       _lib.ptr(ws.workspace), _lib.stream_handle(dev)), "lss_plan_ws")
+            return cs, sk, sr, po
+        cell_start, sorted_key, sorted_row, pos_of = _counted_plan(dev, ws, lambda: None, whole_plan)
+        return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom, pos_of)
     cell_start, sorted_key, sorted_row, pos_of = _counted_plan(
         dev, ws, launch_cells,
         lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws, canonical))

@@ -267,3 +267,34 @@ def test_mbconv_hip_se_vs_torch_autocast():
             E.USE_HIP_SE = True
     for a, b in zip(*outs):
         assert _rel(a, b) < 5e-2, _rel(a, b)
+
+
+@pytest.mark.parametrize("shape", [(8, 128, 200, 200), (2, 64, 7, 9), (1, 256, 3, 5)])
+def test_head1x1_matches_fp32_conv(shape):
+    """BevEncode's last conv (one output channel, src/models.py:115) on lss_head1_*: forward and the
+    three gradients vs the fp32 conv of the same bf16 operands."""
+    from lss_carla_amd import models
+    N, C, H, W = shape
+    g = torch.Generator().manual_seed(C + H)
+    conv = torch.nn.Conv2d(C, 1, 1).to(DEV)
+    x = torch.randn(N, C, H, W, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xr = x.detach().clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        assert models._head1_eligible(conv, xr)
+        y = models.conv1x1(conv, xr)
+    assert y.shape == (N, 1, H, W) and y.dtype == torch.bfloat16
+    gy = torch.randn(N, 1, H, W, generator=g).to(DEV, torch.bfloat16)
+    y.backward(gy)
+    w = conv.weight.detach().to(torch.bfloat16).double()
+    b = conv.bias.detach().to(torch.bfloat16).double()
+    xd = x.double().requires_grad_(True)
+    wd = w.clone().requires_grad_(True)
+    bd = b.clone().requires_grad_(True)
+    want = torch.nn.functional.conv2d(xd, wd, bd)
+    want.backward(gy.double())
+    torch.testing.assert_close(y.double(), want, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(xr.grad.double(), xd.grad, rtol=2e-2, atol=1e-3)
+    for got, ref_ in ((conv.weight.grad, wd.grad), (conv.bias.grad, bd.grad)):
+        # the gradient of autocast's bf16 operand is bf16 (as the conv's own): rounding 2^-9
+        rel = ((got.double() - ref_).norm() / ref_.norm()).item()
+        assert rel < 4e-3, rel
