@@ -3,7 +3,8 @@
 // MBConv blocks), CamEncode.up1 / BevEncode's BN + ReLU (src/models.py:15-34, 92-130).
 //
 // Activations fp32 or bf16, NCHW or channels-last (NHWC); statistics, affine parameters and all
-// arithmetic fp32. Two launches per direction:
+// arithmetic fp32. Two launches per direction (one for NCHW maps small enough for one block per
+// channel: k_bn_fused_nchw / k_bn_bwd_fused_nchw):
 //   forward  1. per-group shifted sums of x - K_c and (x - K_c)^2 (K_c = the channel's first
 //               element, so the one-pass variance does not cancel);
 //            2. every block folds the group sums of its channel(s) in a fixed order (all blocks
@@ -325,6 +326,98 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_apply_nchw(const T* __restric
     });
 }
 
+// ---- one group per channel (G == 1: every map of 8 x 22 pixels or less at B*N = 48): statistics and
+// apply in ONE launch, a block per channel -- the second pass re-reads the channel (<= 17 KB at c3)
+// from the cache the first pass filled. Same sums, same fold, same bits as the two launches above.
+template <int V, typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_fused_nchw(const T* __restrict__ x, const T* __restrict__ res, BnGeo g,
+                                                          BnParams P, int act, T* __restrict__ y) {
+    __shared__ float s_red[2][kBlock / kWave];
+    __shared__ float s_coef[2];
+    const int c = blockIdx.x;
+    const float k = first_nchw(x, c, g);
+    float s1 = 0.f, s2 = 0.f;
+    for_chunk_nchw<V, T>(g, 1, c, 0, [&](size_t i) {
+        float v[V];
+        ldv<V>(x + i, v);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const float d = v[j] - k;
+            s1 += d;
+            s2 = fmaf(d, d, s2);
+        }
+    });
+    block_pair_sum(s1, s2, s_red);
+    if (threadIdx.x == 0) {
+        float sc, sh;
+        finalize_channel(s1, s2, k, (float)g.N * (float)g.HW, c, g.C, P, true, sc, sh);
+        s_coef[0] = sc;
+        s_coef[1] = sh;
+    }
+    __syncthreads();
+    const float sc = s_coef[0], sh = s_coef[1];
+    for_chunk_nchw<V, T>(g, 1, c, 0, [&](size_t i) {
+        float v[V], r[V];
+        ldv<V>(x + i, v);
+        if (res) ldv<V>(res + i, r);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            float z = fmaf(v[j], sc, sh);
+            if (res) z += r[j];
+            v[j] = act_fwd(z, act);
+        }
+        stv<V>(y + i, v);
+    });
+}
+
+template <int V, typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_bwd_fused_nchw(const T* __restrict__ dy, const T* __restrict__ x,
+                                                              const T* __restrict__ y, BnGeo g,
+                                                              const float* __restrict__ stats, int act,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                              T* __restrict__ dx, T* __restrict__ dres) {
+    __shared__ float s_red[2][kBlock / kWave];
+    __shared__ float s_coef[2];
+    const int c = blockIdx.x;
+    const float mean = stats[c], rstd = stats[g.C + c], sc = stats[2 * g.C + c], sh = stats[3 * g.C + c];
+    float sg = 0.f, sgx = 0.f;
+    for_chunk_nchw<V, T>(g, 1, c, 0, [&](size_t i) {
+        float d[V], xv[V], yv[V];
+        ldv<V>(dy + i, d);
+        ldv<V>(x + i, xv);
+        if (act == LSS_ACT_RELU) ldv<V>(y + i, yv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const float gr = grad_pre(d[j], act == LSS_ACT_RELU ? yv[j] : 0.f, fmaf(xv[j], sc, sh), act);
+            sg += gr;
+            sgx = fmaf(gr, (xv[j] - mean) * rstd, sgx);
+        }
+    });
+    block_pair_sum(sg, sgx, s_red);
+    if (threadIdx.x == 0) {
+        if (dgamma) dgamma[c] = sgx;
+        if (dbeta) dbeta[c] = sg;
+        const float n = (float)g.N * (float)g.HW;
+        s_coef[0] = sg / n;
+        s_coef[1] = sgx / n;
+    }
+    __syncthreads();
+    const float mg = s_coef[0], mgx = s_coef[1];
+    for_chunk_nchw<V, T>(g, 1, c, 0, [&](size_t i) {
+        float d[V], xv[V], yv[V], o[V], gr[V];
+        ldv<V>(dy + i, d);
+        ldv<V>(x + i, xv);
+        if (act == LSS_ACT_RELU) ldv<V>(y + i, yv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            gr[j] = grad_pre(d[j], act == LSS_ACT_RELU ? yv[j] : 0.f, fmaf(xv[j], sc, sh), act);
+            o[j] = sc * (gr[j] - mg - (xv[j] - mean) * rstd * mgx);
+        }
+        stv<V>(dx + i, o);
+        if (dres) stv<V>(dres + i, gr);
+    });
+}
+
 // ============================================================================= NHWC (channels-last)
 // block q: pixels [M q / G, M (q+1) / G) x all C channels; thread = 8 consecutive channels of a pixel.
 // Partials (C, G, 2) as in NCHW; a separate fold kernel (one wave per channel) turns them into the
@@ -346,34 +439,54 @@ __device__ __forceinline__ void for_chunk_nhwc(const BnGeo& g, int G, int q, F&&
     for (; r < r1; r += step) f(r * g.C + c0, -1, -1, -1);
 }
 
-// per-thread 8-channel sums -> per-channel block sums in LDS [C][2] -> partial[q][c][2]
-__device__ __forceinline__ void nhwc_block_sums(const BnGeo& g, int G, int q, const float* a, const float* b, int c0,
+// per-thread 8-channel sums -> per-channel block sums -> partial[c][q][2]. The threads sharing a channel
+// octet are lane, lane + cg, ... (cg = C / 8 divides kBlock, a power of two): a butterfly over those
+// lanes inside each wave, then the waves' rows in LDS ([wave][C][2], zero where a wave holds none of
+// a channel) added in wave order -- fixed association, two barriers (a serial round per thread of an
+// octet took kBlock / cg barriers: 32 at C = 64).
+__device__ __forceinline__ void nhwc_block_sums(const BnGeo& g, int G, int q, float* a, float* b, int c0,
                                                 bool active, float* s_acc, float* __restrict__ partial) {
-    for (int i = threadIdx.x; i < 2 * g.C; i += kBlock) s_acc[i] = 0.f;
-    __syncthreads();
-    // fixed order: threads holding the same channels add in thread order, one thread group at a time
     const int cg = g.C / 8;
-    const int rounds = kBlock / cg;  // threads sharing a channel group (the grid stride keeps each on one group)
-    for (int rd = 0; rd < rounds; ++rd) {
-        if (active && (int)threadIdx.x / cg == rd) {
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    constexpr int NW = kBlock / kWave;
+    if (!active) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                s_acc[2 * (c0 + j)] += a[j];
-                s_acc[2 * (c0 + j) + 1] += b[j];
-            }
-        }
-        __syncthreads();
+        for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
     }
+    for (int o = cg; o < kWave; o <<= 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            a[j] += __shfl_xor(a[j], o, kWave);
+            b[j] += __shfl_xor(b[j], o, kWave);
+        }
+    }
+    for (int i = threadIdx.x; i < NW * 2 * g.C; i += kBlock) s_acc[i] = 0.f;
+    __syncthreads();
+    if (active && lane < cg) {
+        float* row = s_acc + (size_t)wave * 2 * g.C;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            row[2 * (c0 + j)] = a[j];
+            row[2 * (c0 + j) + 1] = b[j];
+        }
+    }
+    __syncthreads();
     for (int c = threadIdx.x; c < g.C; c += kBlock) {
-        partial[((size_t)c * G + q) * 2] = s_acc[2 * c];
-        partial[((size_t)c * G + q) * 2 + 1] = s_acc[2 * c + 1];
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            sa += s_acc[(size_t)w * 2 * g.C + 2 * c];
+            sb += s_acc[(size_t)w * 2 * g.C + 2 * c + 1];
+        }
+        partial[((size_t)c * G + q) * 2] = sa;
+        partial[((size_t)c * G + q) * 2 + 1] = sb;
     }
 }
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_bn_stats_nhwc(const T* __restrict__ x, BnGeo g, int G,
                                                           float* __restrict__ partial) {
-    extern __shared__ float s_dyn[];  // [C][2]
+    extern __shared__ float s_dyn[];  // [waves][C][2]
     const int cg = g.C / 8;
     const int c0 = ((int)threadIdx.x % cg) * 8;  // a thread's channel group is fixed (kBlock % cg == 0)
     float k[8];
@@ -475,7 +588,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_stats_nhwc(const T* __restric
                                                               const T* __restrict__ y, BnGeo g, int G,
                                                               const float* __restrict__ stats, int act,
                                                               float* __restrict__ partial) {
-    extern __shared__ float s_dyn[];  // [C][2]
+    extern __shared__ float s_dyn[];  // [waves][C][2]
     const int cg = g.C / 8;
     const int c0 = ((int)threadIdx.x % cg) * 8;
     float mean[8], rstd[8], sc[8], sh[8];
@@ -558,6 +671,10 @@ inline bool bn_ok(const BnGeo& g, int layout) {
     return layout == LSS_CONV_NCHW;
 }
 
+#ifndef LSS_BN_FUSED
+#define LSS_BN_FUSED 1  // NCHW, one group per channel: statistics + apply in one launch (k_bn_fused_nchw)
+#endif
+
 inline int vec_nchw(int HW) { return HW % 8 == 0 ? 8 : (HW % 4 == 0 ? 4 : 1); }
 
 inline int apply_blocks(const BnGeo& g) {  // grid-stride elementwise passes: up to 8 blocks per CU
@@ -601,14 +718,20 @@ int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layou
         T* yy = (T*)y;                                                                                             \
         if (layout == LSS_CONV_NHWC) {                                                                             \
             const size_t lds = 2 * C * sizeof(float);                                                              \
-            hipLaunchKernelGGL(k_bn_stats_nhwc<T>, dim3(G), dim3(kBlock), lds, s, xx, g, G, partial);              \
+            hipLaunchKernelGGL(k_bn_stats_nhwc<T>, dim3(G), dim3(kBlock), (kBlock / kWave) * lds, s, xx, g, G,     \
+                               partial);                                                                           \
             hipLaunchKernelGGL(k_bn_fold_nhwc<T>, dim3((C + 3) / 4), dim3(kBlock), 0, s, partial, G, xx, g, P);   \
             hipLaunchKernelGGL(k_bn_apply_nhwc<T>, dim3(apply_blocks(g)), dim3(kBlock), lds, s, xx, rr, g,        \
                                save_mean, (int)act, yy);                                                           \
         } else {                                                                                                   \
             const int V = vec_nchw(HW);                                                                            \
             const dim3 gr(C * G), bl(kBlock);                                                                      \
-            if (V == 8) {                                                                                          \
+            if (G == 1 && LSS_BN_FUSED) {                                                                          \
+                if (V == 8) hipLaunchKernelGGL((k_bn_fused_nchw<8, T>), gr, bl, 0, s, xx, rr, g, P, (int)act, yy); \
+                else if (V == 4) hipLaunchKernelGGL((k_bn_fused_nchw<4, T>), gr, bl, 0, s, xx, rr, g, P, (int)act, \
+                                                    yy);                                                           \
+                else hipLaunchKernelGGL((k_bn_fused_nchw<1, T>), gr, bl, 0, s, xx, rr, g, P, (int)act, yy);        \
+            } else if (V == 8) {                                                                                   \
                 hipLaunchKernelGGL((k_bn_stats_nchw<8, T>), gr, bl, 0, s, xx, g, G, partial);                     \
                 hipLaunchKernelGGL((k_bn_apply_nchw<8, T>), gr, bl, 0, s, xx, rr, g, G, partial, P, (int)act, yy); \
             } else if (V == 4) {                                                                                   \
@@ -650,7 +773,7 @@ int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int3
         T* o = (T*)dx;                                                                                             \
         T* orr = (T*)dresidual;                                                                                    \
         if (layout == LSS_CONV_NHWC) {                                                                             \
-            hipLaunchKernelGGL(k_bn_bwd_stats_nhwc<T>, dim3(G), dim3(kBlock), 2 * C * sizeof(float), s, d, xx, yy, \
+            hipLaunchKernelGGL(k_bn_bwd_stats_nhwc<T>, dim3(G), dim3(kBlock), 8 * C * sizeof(float), s, d, xx, yy, \
                                g, G, stats, (int)act, partial);                                                    \
             hipLaunchKernelGGL(k_bn_bwd_fold_nhwc, dim3((C + 3) / 4), dim3(kBlock), 0, s, partial, G, g, dgamma,  \
                                dbeta, coef);                                                                       \
@@ -659,7 +782,17 @@ int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int3
         } else {                                                                                                   \
             const int V = vec_nchw(HW);                                                                            \
             const dim3 gr(C * G), bl(kBlock);                                                                      \
-            if (V == 8) {                                                                                          \
+            if (G == 1 && LSS_BN_FUSED) {                                                                          \
+                if (V == 8)                                                                                        \
+                    hipLaunchKernelGGL((k_bn_bwd_fused_nchw<8, T>), gr, bl, 0, s, d, xx, yy, g, stats, (int)act,  \
+                                       dgamma, dbeta, o, orr);                                                     \
+                else if (V == 4)                                                                                   \
+                    hipLaunchKernelGGL((k_bn_bwd_fused_nchw<4, T>), gr, bl, 0, s, d, xx, yy, g, stats, (int)act,  \
+                                       dgamma, dbeta, o, orr);                                                     \
+                else                                                                                               \
+                    hipLaunchKernelGGL((k_bn_bwd_fused_nchw<1, T>), gr, bl, 0, s, d, xx, yy, g, stats, (int)act,  \
+                                       dgamma, dbeta, o, orr);                                                     \
+            } else if (V == 8) {                                                                                   \
                 hipLaunchKernelGGL((k_bn_bwd_stats_nchw<8, T>), gr, bl, 0, s, d, xx, yy, g, G, stats, (int)act,    \
                                    partial);                                                                       \
                 hipLaunchKernelGGL((k_bn_bwd_apply_nchw<8, T>), gr, bl, 0, s, d, xx, yy, g, G, stats, partial,    \

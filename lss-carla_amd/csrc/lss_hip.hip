@@ -235,6 +235,7 @@ __device__ __forceinline__ int wave_sum_i(int v) {
 constexpr int kGeoGroups = 16;
 constexpr int kAggRep = 16;  // replicas of every group sum (agg[g * kAggRep + block % kAggRep]): device
                              // atomics on one address serialise at the memory side
+template <bool AGG = false>
 __device__ __forceinline__ void emit_cell_block(int p, int cell, int32_t* cell_of, int32_t* cell_count,
                                                 int32_t* slot_of, bool live, GeoHash& h, int32_t* agg = nullptr) {
     if (live) cell_of[p] = cell;
@@ -244,7 +245,7 @@ __device__ __forceinline__ void emit_cell_block(int p, int cell, int32_t* cell_o
         h.key[i] = -1;
         h.cnt[i] = 0;
     }
-    if (agg != nullptr && threadIdx.x < kGeoGroups) {
+    if (AGG && threadIdx.x < kGeoGroups) {
         s_gkey[threadIdx.x] = -1;
         s_gval[threadIdx.x] = 0;
     }
@@ -266,7 +267,7 @@ __device__ __forceinline__ void emit_cell_block(int p, int cell, int32_t* cell_o
         const int c = h.key[i];
         const int n = c >= 0 ? h.cnt[i] : 0;
         if (c >= 0) h.cnt[i] = atomicAdd(cell_count + c, n);
-        if (agg != nullptr) {
+        if (AGG) {
             // per wave: one sum per distinct group (usually one), then one LDS atomic by its leader
             const int gk = c >= 0 ? c / kScanItems : -1;
             unsigned long long rem = __ballot(c >= 0);
@@ -290,7 +291,7 @@ __device__ __forceinline__ void emit_cell_block(int p, int cell, int32_t* cell_o
         }
     }
     __syncthreads();
-    if (agg != nullptr && threadIdx.x < kGeoGroups && s_gkey[threadIdx.x] >= 0)
+    if (AGG && threadIdx.x < kGeoGroups && s_gkey[threadIdx.x] >= 0)
         atomicAdd(agg + s_gkey[threadIdx.x] * kAggRep + (blockIdx.x % kAggRep), s_gval[threadIdx.x]);
     if (live) slot_of[p] = kept ? h.cnt[at] + rank : -1;
 }
@@ -381,7 +382,7 @@ __device__ __forceinline__ void geometry_point(const float* __restrict__ frustum
 // tensor: create_frustum builds it as the broadcast of exactly these 1-D tensors (src/models.py:
 // 157-168), so point (d, h, w) = (xs[w], ys[h], ds[d]) bit for bit; 71 floats read through the
 // caches instead of 12 B per point from HBM.
-template <bool AXES>
+template <bool AXES, bool AGG = false>  // AGG: also the per-group count sums (lss_plan_ws)
 __global__ __launch_bounds__(kGeoBlock) void k_geometry_cells(
     const float* __restrict__ frustum, const float* __restrict__ rots, const float* __restrict__ trans,
     const float* __restrict__ kinv, const float* __restrict__ pinv, const float* __restrict__ post_trans,
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(kGeoBlock) void k_geometry_cells(
     LSS_STAMP(tslot, 2);
     if (LSS_GEOM_AGG == 3) {
         __shared__ GeoHash hash;
-        emit_cell_block(p, cell, cell_of, cell_count, slot_of, live, hash, agg);
+        emit_cell_block<AGG>(p, cell, cell_of, cell_count, slot_of, live, hash, agg);
     } else {
         emit_cell(p, cell, cell_of, cell_count, slot_of, live);
     }
@@ -1394,7 +1395,8 @@ template <int K, bool SD>
 __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __restrict__ feat,
                                                               const bf16* __restrict__ weight,
                                                               const bf16* __restrict__ bias, int D, int HW,
-                                                              int npix, int nlift, float* __restrict__ depth,
+                                                              int npix, int nlift, int nlgrid,
+                                                              float* __restrict__ depth,
                                                               bf16* __restrict__ ctx_t,
                                                               const int32_t* __restrict__ pos_of,
                                                               float* __restrict__ sorted_depth, int nfill,
@@ -1410,11 +1412,15 @@ __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __rest
     __shared__ float s_lg[kDnMaxO][PX + 1];                                // bf16-rounded logits
     __shared__ float s_red[2][kDn3Block / PX][PX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int blk = blockIdx.x;
-    if (blk >= nlift) {  // block-uniform: the empty-row fill role
-        fill_empty_rows((blk - nlift) * kDn3Waves + wave, nfill * kDn3Waves, cell_start, bg, bev, esize, lane);
+    if ((int)blockIdx.x >= nlgrid) {  // block-uniform: the empty-row fill role
+        fill_empty_rows(((int)blockIdx.x - nlgrid) * kDn3Waves + wave, nfill * kDn3Waves, cell_start, bg, bev, esize,
+                        lane);
         return;
     }
+    // XCD x takes one contiguous run of pixel tiles (c3: sample x), as the splat's chunk blocks take
+    // the CSR: the context rows a splat gathers were written through its own XCD's L2
+    const int blk = LSS_XCD_MAP ? ((int)blockIdx.x & 7) * (nlgrid >> 3) + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
+    if (blk >= nlift) return;
     // pixel tile [q0, q1): the pixels split as evenly as possible over the nlift blocks
     const int q0 = (int)(((long)npix * blk) / nlift), q1 = (int)(((long)npix * (blk + 1)) / nlift);
     const int np = q1 - q0;  // 1 <= np <= PX (the host sizes nlift so)
@@ -2015,6 +2021,9 @@ __device__ float reduce_big_cell_unordered(int start, int nprime, const long lon
     return acc;
 }
 
+#ifndef LSS_SPLAT_UNORDERED_CODE
+#define LSS_SPLAT_UNORDERED_CODE 1  // 0: the chunk waves' in-cell ranking (LSS_SPLAT_UNORDERED) compiled out
+#endif
 template <bool FUSED, typename RT, typename OutT>
 __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __restrict__ depth,
                                             const float* __restrict__ sorted_depth,
@@ -2062,7 +2071,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     }
     if (end > 0) {
         int d0 = lane, d1 = kWave + lane;  // the entries' positions in the window
-        if (unordered) {
+        if (LSS_SPLAT_UNORDERED_CODE && unordered) {
             // The CSR's entries are grouped by cell but in arrival order inside a cell (the plan ran
             // without k_csr_canon): put every cell of the window into canonical order (ascending point
             // id) here, so the sums below -- and their bits -- are those of the canonical CSR. Rank of
@@ -2238,7 +2247,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     }
     if (big >= 0) {
         int cell;
-        const float a2 = unordered
+        const float a2 = (LSS_SPLAT_UNORDERED_CODE && unordered)
             ? reduce_big_cell_unordered<FUSED, RT>(base + big, nprime, sorted_key, cell_start, depth, rows_base, g,
                                                    reinterpret_cast<int*>(meta), reinterpret_cast<int*>(part),
                                                    min(2 * kWave * 4, RS::NG * kC), lane, &cell)
@@ -3383,7 +3392,7 @@ int lss_plan_ws(const float* frustum, const float* rots, const float* trans, con
     const size_t poff = ((sizeof(int32_t) * (size_t)(nb + 1)) + 255) & ~(size_t)255;  // as lss_csr_build
     long long* tmp_key = reinterpret_cast<long long*>(static_cast<char*>(scratch) + poff);
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_geometry_cells<false>, dim3(grid_blocks(nprime, kGeoBlock)), dim3(kGeoBlock), 0, s, frustum,
+    hipLaunchKernelGGL((k_geometry_cells<false, true>), dim3(grid_blocks(nprime, kGeoBlock)), dim3(kGeoBlock), 0, s, frustum,
                        rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW, dims->H * dims->W, dims->W, nprime,
                        *grid, nullptr, cell_of, cell_count, slot_of, agg);
     hipLaunchKernelGGL(k_scan_agg, dim3(nb), dim3(1024), 0, s, cell_count, ncells, agg, cell_start);
@@ -3534,16 +3543,17 @@ int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bia
     const long nlift = LSS_DN3_PIX > 0 ? (npix + std::min(LSS_DN3_PIX, kDn3MaxPix) - 1) / std::min(LSS_DN3_PIX, kDn3MaxPix)
                                        : std::min<long>(npix, std::max<long>(device_cus(), (npix + kDn3MaxPix - 1) / kDn3MaxPix));
     const int nfill = fp.bev ? 8 * fp.groups : 0;
+    const int nlgrid = xcd_grid(nlift);
     hipStream_t s = (hipStream_t)stream;
-    const dim3 gr((unsigned)(nlift + nfill)), bl(kDn3Block);
+    const dim3 gr((unsigned)(nlgrid + nfill)), bl(kDn3Block);
     if (pos_of)
         hipLaunchKernelGGL((k_depthnet_lift3<512, true>), gr, bl, 0, s, (const bf16*)feat, (const bf16*)weight,
-                           (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, depth, (bf16*)ctx_t, pos_of,
+                           (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, nlgrid, depth, (bf16*)ctx_t, pos_of,
                            sorted_depth, nfill, cell_start, fp.bg, fp.bev, fp.esize);
     else
         hipLaunchKernelGGL((k_depthnet_lift3<512, false>), gr, bl, 0, s, (const bf16*)feat, (const bf16*)weight,
-                           (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, depth, (bf16*)ctx_t, nullptr,
-                           nullptr, nfill, cell_start, fp.bg, fp.bev, fp.esize);
+                           (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, nlgrid, depth, (bf16*)ctx_t,
+                           nullptr, nullptr, nfill, cell_start, fp.bg, fp.bev, fp.esize);
     return launch_status();
 }
 
@@ -3557,6 +3567,7 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
     if ((flags & LSS_SPLAT_EMPTY_FILLED) && out_layout != LSS_NHWC) return LSS_EINVAL;
     const bool unordered = (flags & LSS_SPLAT_UNORDERED) != 0;
     if (unordered && (out_layout != LSS_NHWC || sorted_depth || LSS_SPLAT_IMPL != 0)) return LSS_EINVAL;
+    if (unordered && !LSS_SPLAT_UNORDERED_CODE) return LSS_EUNSUPPORTED;
     if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_key || !out) return LSS_EINVAL;
     const bool fused = x_rows == nullptr;
     if (fused && (!depth || !ctx_t || (!sorted_row && !unordered))) return LSS_EINVAL;

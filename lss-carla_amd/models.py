@@ -27,6 +27,8 @@ Extra knobs (not in the reference, defaults reproduce it):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -37,7 +39,8 @@ from . import resample
 from .norm import bn_act
 from .tools import gen_dx_bx
 
-UP1_CHANNELS_LAST = True  # CamEncode.up1 on channels-last maps under bf16 autocast (see get_eff_depth)
+# CamEncode.up1 on channels-last maps under bf16 autocast (see get_eff_depth); LSS_UP1_CL=0: NCHW (A/B)
+UP1_CHANNELS_LAST = os.environ.get("LSS_UP1_CL", "1") != "0"
 UNORDERED_PLAN = False  # channels-last BEV: plans without the canonical pass (the splat orders each cell); measured slower
 
 

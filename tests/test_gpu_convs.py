@@ -82,6 +82,8 @@ BN_CASES = [  # (N, C, H, W, layout)
     (3, 32, 64, 176, "nchw"),
     (4, 96, 8, 22, "nchw"),
     (5, 40, 4, 11, "nchw"),
+    (2, 16, 5, 7, "nchw"),     # one group per channel (the fused single-launch kernels), V = 1
+    (48, 8, 8, 22, "nchw"),    # the trunk's 8 x 22 maps at B*N = 48: one group, V = 8
     (2, 64, 100, 100, "nhwc"),
     (2, 256, 25, 25, "nhwc"),
     (3, 24, 7, 9, "nhwc"),
