@@ -25,6 +25,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "lss_convs.h"
 
 // The library is built with -ffp-contract=off for the geometry's reference op order (lss_hip.hip);
@@ -418,6 +420,158 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_fused_nchw(const T* __restric
     });
 }
 
+// bf16, one group per channel, at most IT vectors of V elements per thread: the same two launches'
+// work with every load of the channel issued up front and the channel held in registers (packed
+// bf16) between the statistics and the apply -- one read of x (and dy) instead of two, and no
+// round trip per loop iteration. Same sums in the same order as k_bn_fused_nchw (bit-identical).
+template <int V> struct PackedBf16;
+template <> struct PackedBf16<8> {
+    uint4 u;
+    __device__ __forceinline__ void load(const bf16* p) { u = *reinterpret_cast<const uint4*>(p); }
+    __device__ __forceinline__ void get(float* o) const {
+        const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            o[2 * i] = __uint_as_float(w[i] << 16);
+            o[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+        }
+    }
+};
+template <> struct PackedBf16<4> {
+    uint2 u;
+    __device__ __forceinline__ void load(const bf16* p) { u = *reinterpret_cast<const uint2*>(p); }
+    __device__ __forceinline__ void get(float* o) const {
+        o[0] = __uint_as_float(u.x << 16); o[1] = __uint_as_float(u.x & 0xFFFF0000u);
+        o[2] = __uint_as_float(u.y << 16); o[3] = __uint_as_float(u.y & 0xFFFF0000u);
+    }
+};
+
+// the element offset of vector e of channel c (one group: images 0..N-1), e clamped into range
+__device__ __forceinline__ size_t chan_vec(const BnGeo& g, int c, int per, int count, int e, int V) {
+    const int ec = min(e, count - 1);
+    const int nl = ec / per, p = (ec - nl * per) * V;
+    return ((size_t)nl * g.C + c) * g.HW + p;
+}
+
+template <int V, int IT>
+__global__ __launch_bounds__(kBlock) void k_bn_fused_reg_nchw(const bf16* __restrict__ x, const bf16* __restrict__ res,
+                                                              BnGeo g, BnParams P, int act, bf16* __restrict__ y) {
+    __shared__ float s_red[2][kBlock / kWave];
+    __shared__ float s_coef[2];
+    const int c = blockIdx.x;
+    const int per = g.HW / V, count = per * g.N;
+    PackedBf16<V> raw[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) raw[it].load(x + chan_vec(g, c, per, count, (int)threadIdx.x + it * kBlock, V));
+    const float k = first_nchw(x, c, g);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        if ((int)threadIdx.x + it * kBlock < count) {
+            float v[V];
+            raw[it].get(v);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const float d = v[j] - k;
+                s1 += d;
+                s2 = fmaf(d, d, s2);
+            }
+        }
+    }
+    block_pair_sum(s1, s2, s_red);
+    if (threadIdx.x == 0) {
+        float sc, sh;
+        finalize_channel(s1, s2, k, (float)g.N * (float)g.HW, c, g.C, P, true, sc, sh);
+        s_coef[0] = sc;
+        s_coef[1] = sh;
+    }
+    __syncthreads();
+    const float sc = s_coef[0], sh = s_coef[1];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = (int)threadIdx.x + it * kBlock;
+        if (e < count) {
+            const size_t i = chan_vec(g, c, per, count, e, V);
+            float v[V], r[V];
+            raw[it].get(v);
+            if (res) ldv<V>(res + i, r);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                float z = fmaf(v[j], sc, sh);
+                if (res) z += r[j];
+                v[j] = act_fwd(z, act);
+            }
+            stv<V>(y + i, v);
+        }
+    }
+}
+
+template <int V, int IT>
+__global__ __launch_bounds__(kBlock) void k_bn_bwd_fused_reg_nchw(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                                  const bf16* __restrict__ y, BnGeo g,
+                                                                  const float* __restrict__ stats, int act,
+                                                                  float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                                  bf16* __restrict__ dx, bf16* __restrict__ dres) {
+    __shared__ float s_red[2][kBlock / kWave];
+    __shared__ float s_coef[2];
+    const int c = blockIdx.x;
+    const int per = g.HW / V, count = per * g.N;
+    const bool relu = act == LSS_ACT_RELU;
+    PackedBf16<V> rd[IT], rx[IT], ry[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const size_t i = chan_vec(g, c, per, count, (int)threadIdx.x + it * kBlock, V);
+        rd[it].load(dy + i);
+        rx[it].load(x + i);
+        ry[it].load((relu ? y : x) + i);  // (unconditional: a load under a branch waits for the worst case)
+    }
+    const float mean = stats[c], rstd = stats[g.C + c], sc = stats[2 * g.C + c], sh = stats[3 * g.C + c];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        if ((int)threadIdx.x + it * kBlock < count) {
+            float d[V], xv[V], yv[V];
+            rd[it].get(d);
+            rx[it].get(xv);
+            ry[it].get(yv);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const float gr = grad_pre(d[j], relu ? yv[j] : 0.f, fmaf(xv[j], sc, sh), act);
+                sg += gr;
+                sgx = fmaf(gr, (xv[j] - mean) * rstd, sgx);
+            }
+        }
+    }
+    block_pair_sum(sg, sgx, s_red);
+    if (threadIdx.x == 0) {
+        if (dgamma) dgamma[c] = sgx;
+        if (dbeta) dbeta[c] = sg;
+        const float n = (float)g.N * (float)g.HW;
+        s_coef[0] = sg / n;
+        s_coef[1] = sgx / n;
+    }
+    __syncthreads();
+    const float mg = s_coef[0], mgx = s_coef[1];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = (int)threadIdx.x + it * kBlock;
+        if (e < count) {
+            const size_t i = chan_vec(g, c, per, count, e, V);
+            float d[V], xv[V], yv[V], o[V], gr[V];
+            rd[it].get(d);
+            rx[it].get(xv);
+            ry[it].get(yv);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                gr[j] = grad_pre(d[j], relu ? yv[j] : 0.f, fmaf(xv[j], sc, sh), act);
+                o[j] = sc * (gr[j] - mg - (xv[j] - mean) * rstd * mgx);
+            }
+            stv<V>(dx + i, o);
+            if (dres) stv<V>(dres + i, gr);
+        }
+    }
+}
+
 // ============================================================================= NHWC (channels-last)
 // block q: pixels [M q / G, M (q+1) / G) x all C channels; thread = 8 consecutive channels of a pixel.
 // Partials (C, G, 2) as in NCHW; a separate fold kernel (one wave per channel) turns them into the
@@ -675,6 +829,11 @@ inline bool bn_ok(const BnGeo& g, int layout) {
 #define LSS_BN_FUSED 1  // NCHW, one group per channel: statistics + apply in one launch (k_bn_fused_nchw)
 #endif
 
+// register-resident one-group kernels: bf16, V in {8, 4}, at most 8 vectors per thread
+template <typename T> inline bool fused_reg(int V, long cnt) {
+    return std::is_same<T, bf16>::value && (V == 8 || V == 4) && cnt <= 8 * kBlock;
+}
+
 inline int vec_nchw(int HW) { return HW % 8 == 0 ? 8 : (HW % 4 == 0 ? 4 : 1); }
 
 inline int apply_blocks(const BnGeo& g) {  // grid-stride elementwise passes: up to 8 blocks per CU
@@ -726,7 +885,21 @@ int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layou
         } else {                                                                                                   \
             const int V = vec_nchw(HW);                                                                            \
             const dim3 gr(C * G), bl(kBlock);                                                                      \
-            if (G == 1 && LSS_BN_FUSED) {                                                                          \
+            const long cnt = (long)N * (HW / V);                                                                   \
+            if (G == 1 && LSS_BN_FUSED && fused_reg<T>(V, cnt)) {                                                  \
+                if (V == 8 && cnt <= 4 * kBlock)                                                                   \
+                    hipLaunchKernelGGL((k_bn_fused_reg_nchw<8, 4>), gr, bl, 0, s, (const bf16*)xx,                \
+                                       (const bf16*)rr, g, P, (int)act, (bf16*)yy);                                \
+                else if (V == 8)                                                                                   \
+                    hipLaunchKernelGGL((k_bn_fused_reg_nchw<8, 8>), gr, bl, 0, s, (const bf16*)xx,                \
+                                       (const bf16*)rr, g, P, (int)act, (bf16*)yy);                                \
+                else if (cnt <= 4 * kBlock)                                                                        \
+                    hipLaunchKernelGGL((k_bn_fused_reg_nchw<4, 4>), gr, bl, 0, s, (const bf16*)xx,                \
+                                       (const bf16*)rr, g, P, (int)act, (bf16*)yy);                                \
+                else                                                                                               \
+                    hipLaunchKernelGGL((k_bn_fused_reg_nchw<4, 8>), gr, bl, 0, s, (const bf16*)xx,                \
+                                       (const bf16*)rr, g, P, (int)act, (bf16*)yy);                                \
+            } else if (G == 1 && LSS_BN_FUSED) {                                                                   \
                 if (V == 8) hipLaunchKernelGGL((k_bn_fused_nchw<8, T>), gr, bl, 0, s, xx, rr, g, P, (int)act, yy); \
                 else if (V == 4) hipLaunchKernelGGL((k_bn_fused_nchw<4, T>), gr, bl, 0, s, xx, rr, g, P, (int)act, \
                                                     yy);                                                           \
@@ -782,7 +955,22 @@ int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int3
         } else {                                                                                                   \
             const int V = vec_nchw(HW);                                                                            \
             const dim3 gr(C * G), bl(kBlock);                                                                      \
-            if (G == 1 && LSS_BN_FUSED) {                                                                          \
+            const long cnt = (long)N * (HW / V);                                                                   \
+            if (G == 1 && LSS_BN_FUSED && fused_reg<T>(V, cnt)) {                                                  \
+                const bf16 *db = (const bf16*)d, *xb = (const bf16*)xx, *yb = (const bf16*)yy;                     \
+                if (V == 8 && cnt <= 4 * kBlock)                                                                   \
+                    hipLaunchKernelGGL((k_bn_bwd_fused_reg_nchw<8, 4>), gr, bl, 0, s, db, xb, yb, g, stats,       \
+                                       (int)act, dgamma, dbeta, (bf16*)o, (bf16*)orr);                             \
+                else if (V == 8)                                                                                   \
+                    hipLaunchKernelGGL((k_bn_bwd_fused_reg_nchw<8, 8>), gr, bl, 0, s, db, xb, yb, g, stats,       \
+                                       (int)act, dgamma, dbeta, (bf16*)o, (bf16*)orr);                             \
+                else if (cnt <= 4 * kBlock)                                                                        \
+                    hipLaunchKernelGGL((k_bn_bwd_fused_reg_nchw<4, 4>), gr, bl, 0, s, db, xb, yb, g, stats,       \
+                                       (int)act, dgamma, dbeta, (bf16*)o, (bf16*)orr);                             \
+                else                                                                                               \
+                    hipLaunchKernelGGL((k_bn_bwd_fused_reg_nchw<4, 8>), gr, bl, 0, s, db, xb, yb, g, stats,       \
+                                       (int)act, dgamma, dbeta, (bf16*)o, (bf16*)orr);                             \
+            } else if (G == 1 && LSS_BN_FUSED) {                                                                   \
                 if (V == 8)                                                                                        \
                     hipLaunchKernelGGL((k_bn_bwd_fused_nchw<8, T>), gr, bl, 0, s, d, xx, yy, g, stats, (int)act,  \
                                        dgamma, dbeta, o, orr);                                                     \

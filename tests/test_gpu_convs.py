@@ -83,7 +83,8 @@ BN_CASES = [  # (N, C, H, W, layout)
     (4, 96, 8, 22, "nchw"),
     (5, 40, 4, 11, "nchw"),
     (2, 16, 5, 7, "nchw"),     # one group per channel (the fused single-launch kernels), V = 1
-    (48, 8, 8, 22, "nchw"),    # the trunk's 8 x 22 maps at B*N = 48: one group, V = 8
+    (48, 8, 8, 22, "nchw"),    # the trunk's 8 x 22 maps at B*N = 48: one group, V = 8, 8 vectors a thread
+    (96, 8, 4, 11, "nchw"),    # 4 x 11 maps: one group, V = 4, 8 vectors a thread (register-resident)
     (2, 64, 100, 100, "nhwc"),
     (2, 256, 25, 25, "nhwc"),
     (3, 24, 7, 9, "nhwc"),

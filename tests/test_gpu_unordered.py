@@ -114,7 +114,7 @@ def test_module_unordered_plan_same_bev_and_grads():
     m.bev_layout = "nhwc"
     rig = {k: v.to(DEV) for k, v in syn.make_rig(cfg["B"], cfg["N"], cfg["final_dim"], seed=1, aug=True).items()}
     imgs = syn.make_images(cfg["B"], cfg["N"], cfg["final_dim"]).to(DEV)
-    outs = []
+    outs, prev = [], models.UNORDERED_PLAN
     try:
         for flag in (True, False):
             models.UNORDERED_PLAN = flag
@@ -124,7 +124,7 @@ def test_module_unordered_plan_same_bev_and_grads():
             bev.float().square().mean().backward()
             outs.append((bev.detach(), m.camencode.depthnet.weight.grad.clone()))
     finally:
-        models.UNORDERED_PLAN = True
+        models.UNORDERED_PLAN = prev
     assert torch.equal(outs[0][0], outs[1][0])  # the BEV bit for bit
     # the gradient within run-to-run noise (BevEncode's MIOpen backward is not bitwise reproducible)
     rel = ((outs[0][1] - outs[1][1]).norm() / outs[1][1].norm()).item()
