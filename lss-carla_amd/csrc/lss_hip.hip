@@ -1391,6 +1391,10 @@ constexpr int kDn3MaxPix = 48;           // pixels per block at most: three 16-c
 #define LSS_DN3_PIX 0  // pixels per block of k_depthnet_lift3: 0 one block per CU (at most 48 pixels each), else this many
 #endif
 
+#ifndef LSS_DN3_SLICES
+#define LSS_DN3_SLICES 2  // K slices of k_depthnet_lift3's loads: slice 0 multiplied while the rest arrive
+#endif
+
 template <int K, bool SD>
 __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __restrict__ feat,
                                                               const bf16* __restrict__ weight,
@@ -1440,59 +1444,74 @@ __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __rest
             at[i] = pos_of[((size_t)bnc * D + d) * HW + hwc];
         }
     }
-    // ---- loads, all in flight together: the tile (contiguous rows, 16 B per thread and load), then
-    // this wave's weight rows as A fragments, then its bias values (clamped addresses, no branches)
-    constexpr int kChunks = PX * K * 2 / 16;             // 16-B pieces of a full tile
-    constexpr int kFeatIt = (kChunks + kDn3Block - 1) / kDn3Block;
+    // ---- loads, all in flight together, in kParts K slices: slice h of the tile (channels
+    // [h K/kParts, (h+1) K/kParts) of every pixel row, 16 B per thread and load), then this wave's
+    // weight A fragments for the slice's K steps; then the bias values (clamped addresses, no
+    // branches). Loads complete in order, so slice 0 is staged and multiplied while the later slices
+    // are still arriving (the per-CU intake, ~161 KB at c3, is the stage's bound).
+    constexpr int kSlices = LSS_DN3_SLICES;
     constexpr int kCPR = K * 2 / 16;                     // 16-B pieces per pixel row
+    constexpr int kSCPR = kCPR / kSlices;                // ... per pixel row and slice
+    constexpr int kSChunks = PX * kSCPR;                 // 16-B pieces of a slice
+    constexpr int kSIt = (kSChunks + kDn3Block - 1) / kDn3Block;
+    constexpr int kSteps = K / 32;
+    constexpr int kSSteps = kSteps / kSlices;
+    static_assert(kCPR % kSlices == 0 && kSteps % kSlices == 0, "K slices");
     const unsigned char* tile = reinterpret_cast<const unsigned char*>(feat + (size_t)q0 * K);
-    uint4 fv[kFeatIt];
-#pragma unroll
-    for (int t = 0; t < kFeatIt; ++t) {
-        const int i = threadIdx.x + t * kDn3Block;
-        const int r = min(i / kCPR, np - 1), c = i % kCPR;
-        fv[t] = (LSS_DN_SKIP & 2) ? make_uint4(r, c, t, 1u)
-                                  : *reinterpret_cast<const uint4*>(tile + (size_t)r * K * 2 + c * 16);
-    }
     const int arow = wave * 16 + (lane & 15);
     const int kq = 8 * (lane >> 4);
-    constexpr int kSteps = K / 32;
     const int g = lane >> 4, c16 = lane & 15;
     const bf16* wrow = weight + (size_t)min(arow, O - 1) * K + kq;
     // (unconditional even for a wave past the output rows -- its clamped row is one cached line per
     // K step -- so the compiler can count every load: a load under a branch makes it wait for the
     // worst case, and the tile's LDS writes then waited for most of the weights)
+    uint4 fv[kSlices][kSIt];
     bf16x8 a[kSteps];
 #pragma unroll
-    for (int s = 0; s < kSteps; ++s)
-        a[s] = (LSS_DN_SKIP & 1) ? bf16x8{(short)lane, 1, 2, 3, 4, 5, 6, (short)s}
-                                 : *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
+    for (int h = 0; h < kSlices; ++h) {
+#pragma unroll
+        for (int t = 0; t < kSIt; ++t) {
+            const int i = threadIdx.x + t * kDn3Block;
+            const int r = min(i / kSCPR, np - 1), c = h * kSCPR + i % kSCPR;
+            fv[h][t] = (LSS_DN_SKIP & 2) ? make_uint4(r, c, t, 1u)
+                                         : *reinterpret_cast<const uint4*>(tile + (size_t)r * K * 2 + c * 16);
+        }
+#pragma unroll
+        for (int s = h * kSSteps; s < (h + 1) * kSSteps; ++s)
+            a[s] = (LSS_DN_SKIP & 1) ? bf16x8{(short)lane, 1, 2, 3, 4, 5, 6, (short)s}
+                                     : *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
+    }
     float bv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) bv[i] = __bfloat162float(bias[min(wave * 16 + 4 * g + i, O - 1)]);
-#pragma unroll
-    for (int t = 0; t < kFeatIt; ++t) {
-        const int i = threadIdx.x + t * kDn3Block;
-        if (kChunks % kDn3Block == 0 || i < kChunks)
-            *reinterpret_cast<uint4*>(s_x + (i / kCPR) * kRow + (i % kCPR) * 16) = fv[t];
-    }
-    __syncthreads();
-    LSS_STAMP(tslot, 1);
-    // ---- MFMA: kTiles 16-pixel column tiles, K/32 steps. All tiles always (compile-time trip
-    // counts: the LDS reads and MFMAs pipeline); columns past the tile's pixels read clamped rows and
-    // only feed logits that are never read.
+    // ---- per slice: stage it in LDS, then its MFMA steps over kTiles 16-pixel column tiles. All
+    // tiles always (compile-time trip counts: the LDS reads and MFMAs pipeline); columns past the
+    // tile's pixels read clamped rows and only feed logits that are never read. Same K order as one
+    // slice: identical results.
     f32x4 acc[kTiles];
 #pragma unroll
     for (int t = 0; t < kTiles; ++t) acc[t] = f32x4{};
-    // (every wave, also one past the output rows: a branch here would let the compiler sink the
-    // weight loads into it, behind the barrier, one round trip per K step)
 #pragma unroll
-    for (int s = 0; s < kSteps; ++s) {
+    for (int h = 0; h < kSlices; ++h) {
 #pragma unroll
-        for (int t = 0; t < kTiles; ++t) {
-            // lane (g, c16) of the B fragment: pixel 16t + c16, channels 32s + 8g .. + 7
-            const bf16x8 b = *reinterpret_cast<const bf16x8*>(s_x + (16 * t + c16) * kRow + (32 * s + 8 * g) * 2);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], b, acc[t], 0, 0, 0);
+        for (int t = 0; t < kSIt; ++t) {
+            const int i = threadIdx.x + t * kDn3Block;
+            if (kSChunks % kDn3Block == 0 || i < kSChunks)
+                *reinterpret_cast<uint4*>(s_x + (i / kSCPR) * kRow + (h * kSCPR + i % kSCPR) * 16) = fv[h][t];
+        }
+        __syncthreads();
+        if (h == 0) LSS_STAMP(tslot, 1);
+        // (every wave, also one past the output rows: a branch here would let the compiler sink the
+        // weight loads into it, behind the barrier, one round trip per K step)
+#pragma unroll
+        for (int s = h * kSSteps; s < (h + 1) * kSSteps; ++s) {
+#pragma unroll
+            for (int t = 0; t < kTiles; ++t) {
+                // lane (g, c16) of the B fragment: pixel 16t + c16, channels 32s + 8g .. + 7
+                const bf16x8 b =
+                    *reinterpret_cast<const bf16x8*>(s_x + (16 * t + c16) * kRow + (32 * s + 8 * g) * 2);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], b, acc[t], 0, 0, 0);
+            }
         }
     }
     // C/D: column (pixel) = lane & 15, row (output) = 4 (lane >> 4) + i
