@@ -3,7 +3,7 @@
 # --kernel-trace --stats run of the same bench (per-kernel summary + per-step breakdown), the c5 and
 # c2 lines and the reference-layout fp32 NCHW training line.  usage: bash scripts/gpu_r3_lines.sh [steps...]
 set -o pipefail
-OUT=gpurun_out/r3s2; mkdir -p $OUT
+OUT=${OUT:-gpurun_out/r3s2}; mkdir -p $OUT
 for s in ${*:-c3 prof c5 c2 fp32}; do
   case $s in
     c3) timeout -k 10 600 python3 -u bench.py > $OUT/bench_c3.json 2> $OUT/bench_c3.log; rc=$? ;;
