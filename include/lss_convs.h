@@ -52,6 +52,17 @@ int lss_head1_fwd(const void* x, const float* w, const float* bias, int32_t P, i
 int lss_head1_bwd(const void* x, const void* dy, const float* w, int32_t P, int32_t C, void* dx, float* partial,
                   void* stream);
 
+/* Per-sample scale (+ residual) over N samples of `per` contiguous bf16 elements each (any memory
+ * format that is sample-major: NCHW or channels-last), per % 8 == 0, 16-B aligned pointers:
+ * y = bf16(x * scale[n] + res) (res nullable: y = bf16(x * scale[n])), scale[n] = mask[n] / keep with
+ * mask[n] = floor(bf16(keep + u[n])), u the N bf16 uniform draws (torch.rand in the activations'
+ * dtype), 0 < keep <= 1. The MBConv residual with stochastic depth (efficientnet_pytorch
+ * drop_connect: inputs / keep_prob * floor(keep_prob + rand), then the skip add; the reference's
+ * trunk, src/models.py:43) in one pass, the mask computed in the kernel; its backward is the
+ * res == NULL form on the output gradient with the same draws. */
+int lss_scale_add(const void* x, const void* u, float keep, const void* res, int64_t N, int64_t per, void* y,
+                  void* stream);
+
 /* Training-mode batch norm fused with an activation (and, for ReLU, a residual add), for
  * nn.BatchNorm2d followed by swish (EfficientNet-B0, src/models.py:68 and the MBConv blocks) or
  * ReLU (CamEncode.up1, BevEncode, src/models.py:15-34, 92-130):

@@ -398,6 +398,50 @@ __global__ __launch_bounds__(kBlock) void k_head1_bwd(const uint4* __restrict__ 
         partial[(size_t)blockIdx.x * (C + 1) + c] = ((s_part[0][c] + s_part[1][c]) + s_part[2][c]) + s_part[3][c];
 }
 
+// ----------------------------------------------------------------------------- per-sample scale (+ add)
+// y = bf16(x * scale[n] (+ r)) over sample-major bf16 tensors, scale[n] from the sample's draw, 8 elements (16 B) per thread: the
+// MBConv residual with stochastic depth (efficientnet_pytorch drop_connect, x / keep * mask +
+// inputs) in one pass instead of three; with r == nullptr, its backward dx = bf16(dy * scale[n]).
+__device__ __forceinline__ void unpack8(const uint4& u, float* o) {
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        o[2 * i] = __uint_as_float(w[i] << 16);
+        o[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+}
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+    const bf16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+    return (unsigned)*reinterpret_cast<const unsigned short*>(&x) |
+           ((unsigned)*reinterpret_cast<const unsigned short*>(&y) << 16);
+}
+
+// the sample's scale from its uniform draw u (bf16): mask = floor(bf16(keep + u)) as torch computes
+// floor(keep + rand(..., dtype=bf16)), scale = mask / keep
+__device__ __forceinline__ float drop_scale(const bf16* u, long long n, float keep) {
+    const float t = __bfloat162float(__float2bfloat16(keep + __bfloat162float(u[n])));
+    return floorf(t) / keep;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scale_add(const uint4* __restrict__ x, const bf16* __restrict__ u,
+                                                      float keep, const uint4* __restrict__ r, long long per8,
+                                                      long long n8, uint4* __restrict__ y) {
+    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n8) return;
+    const float sc = drop_scale(u, i / per8, keep);
+    float v[8], w[8];
+    unpack8(x[i], v);
+    if (r) {
+        unpack8(r[i], w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], sc, w[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] *= sc;
+    }
+    y[i] = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+}
+
 }  // namespace
 
 extern "C" {
@@ -468,6 +512,20 @@ int lss_dwconv_bwd_weight(const void* x, const void* dy, int32_t dtype, int32_t 
         return LSS_CONV_EINVAL;
     const DwGeo g{C, Hi, Wi, Ho, Wo, pad_top, pad_left, N * C};
     return dispatch_kst<BwdWeight>(K, stride, dtype, x, dy, g, (int)N, (int)ngroups, partial, (hipStream_t)stream);
+}
+
+int lss_scale_add(const void* x, const void* u, float keep, const void* res, int64_t N, int64_t per, void* y,
+                  void* stream) {
+    if (!x || !u || !y || !(keep > 0.f && keep <= 1.f) || N <= 0 || per <= 0 || per % 8 != 0 ||
+        ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(res) | reinterpret_cast<uintptr_t>(y)) & 15))
+        return LSS_CONV_EINVAL;
+    const long long n8 = (long long)N * per / 8;
+    const long long nb = (n8 + kBlock - 1) / kBlock;
+    if (nb > INT_MAX) return LSS_CONV_EINVAL;
+    hipLaunchKernelGGL(k_scale_add, dim3((unsigned)nb), dim3(kBlock), 0, (hipStream_t)stream, (const uint4*)x, (const bf16*)u,
+                       keep, (const uint4*)res, (long long)(per / 8), n8, (uint4*)y);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
 }
 
 }  // extern "C"

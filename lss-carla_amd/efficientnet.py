@@ -175,6 +175,63 @@ def drop_connect(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
     return x / keep * mask
 
 
+USE_HIP_DROP_ADD = True
+
+
+class _HipScaleAdd(torch.autograd.Function):
+    """y = bf16(x * scale[n] + res), scale[n] = floor(keep + u[n]) / keep computed in the kernel from
+    the sample's draw u (``lss_scale_add``: one launch instead of the mask's add / floor and the
+    divide, multiply and add); backward dx = bf16(dy * scale[n]), dres = dy."""
+
+    @staticmethod
+    def forward(ctx, x, res, u, keep):
+        from . import _lib
+        lib = _lib.load()
+        y = torch.empty_like(x)
+        N = x.shape[0]
+        _lib.check(lib.lss_scale_add(_lib.ptr(x), _lib.ptr(u), keep, _lib.ptr(res), N, x.numel() // N, _lib.ptr(y),
+                                     _lib.stream_handle(x.device)), "lss_scale_add")
+        ctx.save_for_backward(u)
+        ctx.keep = keep
+        ctx.fmt = torch.channels_last if not x.is_contiguous() else torch.contiguous_format
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+        lib = _lib.load()
+        (u,) = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=ctx.fmt)
+        dx = torch.empty_like(dy)
+        N = dy.shape[0]
+        _lib.check(lib.lss_scale_add(_lib.ptr(dy), _lib.ptr(u), ctx.keep, None, N, dy.numel() // N, _lib.ptr(dx),
+                                     _lib.stream_handle(dy.device)), "lss_scale_add")
+        return dx, dy, None, None
+
+
+def _scale_add_eligible(x: torch.Tensor, res: torch.Tensor) -> bool:
+    if not (USE_HIP_DROP_ADD and x.is_cuda and x.dtype == torch.bfloat16 and res.dtype == torch.bfloat16
+            and x.dim() == 4 and x.shape == res.shape and (x.numel() // x.shape[0]) % 8 == 0):
+        return False
+    for fmt in (torch.contiguous_format, torch.channels_last):
+        if x.is_contiguous(memory_format=fmt) and res.is_contiguous(memory_format=fmt):
+            return all(t.data_ptr() % 16 == 0 for t in (x, res))
+    return False
+
+
+def drop_connect_add(x: torch.Tensor, inputs: torch.Tensor, p: float, training: bool) -> torch.Tensor:
+    """``drop_connect(x, p, training) + inputs`` (the MBConv skip, src/models.py:43 via
+    efficientnet_pytorch): the same per-sample draw (``rand`` in x's dtype; the mask
+    ``floor(keep + rand)`` is formed in the kernel exactly as torch forms it), applied as one fused
+    scale-and-add on bf16 activations (fp32 arithmetic, one rounding instead of three)."""
+    if not training or not p:
+        return x + inputs
+    if not _scale_add_eligible(x, inputs):
+        return drop_connect(x, p, training) + inputs
+    u = torch.rand((x.shape[0],), dtype=x.dtype, device=x.device)  # the same draw as drop_connect's
+    return _HipScaleAdd.apply(x, inputs, u, 1.0 - p)
+
+
 class MBConvBlock(nn.Module):
     def __init__(self, k: int, stride: int, expand: int, in_f: int, out_f: int, image_size, se_ratio=0.25):
         super().__init__()
@@ -216,9 +273,7 @@ class MBConvBlock(nn.Module):
         x = squeeze_excite(x, self._se_reduce, self._se_expand)
         x = bn_act(self._bn2, self._project_conv(x))
         if self.stride == 1 and self.in_f == self.out_f:
-            if drop_connect_rate:
-                x = drop_connect(x, drop_connect_rate, self.training)
-            x = x + inputs
+            x = drop_connect_add(x, inputs, drop_connect_rate, self.training)
         return x
 
 

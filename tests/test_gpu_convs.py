@@ -301,3 +301,43 @@ def test_head1x1_matches_fp32_conv(shape):
         # the gradient of autocast's bf16 operand is bf16 (as the conv's own): rounding 2^-9
         rel = ((got.double() - ref_).norm() / ref_.norm()).item()
         assert rel < 4e-3, rel
+
+
+# ----------------------------------------------------------------------------- drop_connect + skip
+from lss_carla_amd import efficientnet as E  # noqa: E402
+
+
+@pytest.mark.parametrize("shape,cl", [((48, 40, 16, 44), False), ((48, 80, 8, 22), True), ((6, 24, 5, 7), False)])
+def test_drop_connect_add_vs_fp64(shape, cl):
+    """The fused MBConv skip with stochastic depth (lss_scale_add) against the reference's
+    ``inputs / keep * floor(keep + rand) + skip`` in fp64 on the same Bernoulli draw; (6, 24, 5, 7)
+    (per-sample size not a multiple of 8) takes the torch composition."""
+    g = torch.Generator().manual_seed(shape[1])
+    mf = torch.channels_last if cl else torch.contiguous_format
+    x = torch.randn(shape, generator=g).bfloat16().to(DEV).contiguous(memory_format=mf).requires_grad_(True)
+    r = torch.randn(shape, generator=g).bfloat16().to(DEV).contiguous(memory_format=mf).requires_grad_(True)
+    p, keep = 0.2, 0.8
+    torch.cuda.manual_seed(7)
+    y = E.drop_connect_add(x, r, p, True)
+    torch.cuda.manual_seed(7)
+    mask = torch.floor(keep + torch.rand((shape[0], 1, 1, 1), dtype=torch.bfloat16, device=DEV))
+    if shape[0] >= 48:
+        assert 0 < int(mask.sum()) < shape[0]  # some samples dropped, some kept
+    dy = torch.randn(shape, generator=g).bfloat16().to(DEV).contiguous(memory_format=mf)
+    y.backward(dy)
+    md = mask.double().cpu()
+    ref = x.detach().double().cpu() / keep * md + r.detach().double().cpu()
+    torch.testing.assert_close(y.detach().double().cpu(), ref, rtol=8e-3, atol=8e-3)
+    torch.testing.assert_close(x.grad.double().cpu(), dy.double().cpu() / keep * md, rtol=8e-3, atol=8e-3)
+    assert torch.equal(r.grad, dy)
+    assert y.is_contiguous(memory_format=mf)
+    # the in-kernel mask is torch's floor(keep + rand) bit for bit: dropped samples are the skip exactly
+    drop = mask.reshape(-1) == 0
+    assert torch.equal(y.detach()[drop], r.detach()[drop]) and torch.equal(x.grad[drop], torch.zeros_like(x.grad[drop]))
+
+
+def test_drop_connect_add_eval_is_plain_add():
+    x = torch.randn(4, 16, 4, 4, device=DEV).bfloat16()
+    r = torch.randn(4, 16, 4, 4, device=DEV).bfloat16()
+    assert torch.equal(E.drop_connect_add(x, r, 0.2, False), x + r)
+    assert torch.equal(E.drop_connect_add(x, r, None, True), x + r)
