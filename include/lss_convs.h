@@ -122,6 +122,12 @@ int lss_se_bwd(const void* dy, const void* x, int32_t N, int32_t C, int32_t HW, 
                int32_t sq, const float* r, const float* sig, float* t, float* dh_part, float* de, float* dr, float* dm,
                void* dx, void* stream);
 
+/* The SE convs' parameter gradients from the backward's per-image values, in one launch (fp32, the N
+ * images summed in order): dw1 (sq, C) = dr^T m, db1 (sq) = sum_n dr, dw2 (C, sq) = de^T h,
+ * db2 (C) = sum_n de. */
+int lss_se_wgrad(const float* de, const float* h, const float* dr, const float* m, int32_t N, int32_t C, int32_t sq,
+                 float* dw1, float* db1, float* dw2, float* db2, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -100,6 +100,7 @@ SIGNATURES = {
     "lss_upsample_bwd": (ctypes.c_int, [_p] + [_i32] * 7 + [_p, _p]),
     "lss_se_fwd": (ctypes.c_int, [_p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p, _p]),
     "lss_se_bwd": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "lss_se_wgrad": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -10,7 +10,7 @@
 //             k_se_scale (y = x * sig)
 //   backward  k_se_dot (t = sum_hw g*x per plane) -> k_se_mlpb1 / k_se_mlpb2 (sigmoid, expand,
 //             swish, reduce backward -> de, dr, dm) -> k_se_dx (dx = g*sig + dm/HW);
-//             the four small weight / bias gradients are GEMMs the caller runs.
+//             k_se_wgrad: the four weight / bias gradients in one launch.
 // All sums fp32 in a fixed order (deterministic).
 
 #include <hip/hip_runtime.h>
@@ -264,6 +264,36 @@ __global__ __launch_bounds__(kBlock) void k_se_dx(const unsigned short* __restri
     st4(dx + i, v);
 }
 
+// The four parameter gradients of the two 1x1 convs in one launch, one thread per output, the N
+// images summed in order (deterministic): dw2[c][j] = sum_n de[n][c] h[n][j] (C, sq),
+// dw1[j][c] = sum_n dr[n][j] m[n][c] (sq, C), db1[j] = sum_n dr[n][j], db2[c] = sum_n de[n][c].
+__global__ __launch_bounds__(kBlock) void k_se_wgrad(const float* __restrict__ de, const float* __restrict__ h,
+                                                     const float* __restrict__ dr, const float* __restrict__ m,
+                                                     int N, int C, int sq, float* __restrict__ dw1,
+                                                     float* __restrict__ db1, float* __restrict__ dw2,
+                                                     float* __restrict__ db2) {
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    const int cs = C * sq;
+    float a = 0.f;
+    if (t < cs) {  // dw2, lanes over j: de broadcast, h coalesced
+        const int c = t / sq, j = t - c * sq;
+        for (int n = 0; n < N; ++n) a = fmaf(de[(size_t)n * C + c], h[(size_t)n * sq + j], a);
+        dw2[t] = a;
+    } else if (t < 2 * cs) {  // dw1, lanes over c: m coalesced
+        const int u = t - cs, j = u / C, c = u - j * C;
+        for (int n = 0; n < N; ++n) a = fmaf(dr[(size_t)n * sq + j], m[(size_t)n * C + c], a);
+        dw1[u] = a;
+    } else if (t < 2 * cs + sq) {
+        const int j = t - 2 * cs;
+        for (int n = 0; n < N; ++n) a += dr[(size_t)n * sq + j];
+        db1[j] = a;
+    } else if (t < 2 * cs + sq + C) {
+        const int c = t - 2 * cs - sq;
+        for (int n = 0; n < N; ++n) a += de[(size_t)n * C + c];
+        db2[c] = a;
+    }
+}
+
 inline int launch_status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
@@ -309,6 +339,17 @@ int lss_se_bwd(const void* dy, const void* x, int32_t N, int32_t C, int32_t HW, 
     hipLaunchKernelGGL(k_se_mlpb2, dim3(N * nchunk), dim3(kBlock), 0, s, dh_part, r, w1, C, sq, dr, dm);
     hipLaunchKernelGGL(k_se_dx, dim3(blocks(n4, kBlock)), dim3(kBlock), 0, s, (const unsigned short*)dy, sig, dm, HW,
                        n4, (unsigned short*)dx);
+    return launch_status();
+}
+
+int lss_se_wgrad(const float* de, const float* h, const float* dr, const float* m, int32_t N, int32_t C, int32_t sq,
+                 float* dw1, float* db1, float* dw2, float* db2, void* stream) {
+    if (!de || !h || !dr || !m || !dw1 || !db1 || !dw2 || !db2 || N <= 0 || C <= 0 || C > kMaxC || sq <= 0 ||
+        sq > kWave)
+        return LSS_CONV_EINVAL;
+    const int total = 2 * C * sq + sq + C;
+    hipLaunchKernelGGL(k_se_wgrad, dim3(blocks(total, kBlock)), dim3(kBlock), 0, (hipStream_t)stream, de, h, dr, m, N,
+                       C, sq, dw1, db1, dw2, db2);
     return launch_status();
 }
 

@@ -283,8 +283,8 @@ USE_HIP_SE = True
 class _HipSqueezeExcite(torch.autograd.Function):
     """x * sigmoid(W2 swish(W1 avg_pool(x) + b1) + b2) on the lss_se_* kernels (NCHW bf16 x, fp32
     weights rounded to bf16 in-kernel as autocast's conv would). Backward: two streaming kernels
-    (sum_hw dy*x, then dx = dy*sig + dm/HW) around a per-image MLP backward; the weight / bias
-    gradients are four small fp32 GEMMs / sums."""
+    (sum_hw dy*x, then dx = dy*sig + dm/HW) around a per-image MLP backward; the four weight /
+    bias gradients in one more launch (lss_se_wgrad)."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2):
@@ -323,9 +323,12 @@ class _HipSqueezeExcite(torch.autograd.Function):
         _lib.check(lib.lss_se_bwd(_lib.ptr(dy), _lib.ptr(x), N, C, H * W, _lib.ptr(W1), _lib.ptr(W2), sq, _lib.ptr(r),
                                   _lib.ptr(sig), _lib.ptr(t), _lib.ptr(dh_part), _lib.ptr(de), _lib.ptr(dr),
                                   _lib.ptr(dm), _lib.ptr(dx), _lib.stream_handle(x.device)), "lss_se_bwd")
-        dw2 = (de.t() @ h).reshape(w2s).to(w2t)
-        dw1 = (dr.t() @ m).reshape(w1s).to(w1t)
-        return dx, dw1, dr.sum(0).to(b1t), dw2, de.sum(0).to(b2t)
+        dw1, db1 = torch.empty(sq, C, **f32), torch.empty(sq, **f32)
+        dw2, db2 = torch.empty(C, sq, **f32), torch.empty(C, **f32)
+        _lib.check(lib.lss_se_wgrad(_lib.ptr(de), _lib.ptr(h), _lib.ptr(dr), _lib.ptr(m), N, C, sq, _lib.ptr(dw1),
+                                    _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2), _lib.stream_handle(x.device)),
+                   "lss_se_wgrad")
+        return dx, dw1.reshape(w1s).to(w1t), db1.to(b1t), dw2.reshape(w2s).to(w2t), db2.to(b2t)
 
 
 def squeeze_excite(x: torch.Tensor, se_reduce: nn.Conv2d, se_expand: nn.Conv2d) -> torch.Tensor:
