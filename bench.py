@@ -471,6 +471,8 @@ def main():
     watchdog = start_watchdog(args.watchdog or 300.0 + 2.0 * (args.steps + args.warmup + args.profile_steps), rank)
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     from lss_carla_amd import ops, parallel
+    if world > 1:
+        parallel.control_group()  # the gloo group for collective decisions, created on every rank here
     from lss_carla_amd.flat_params import FlatParams, FlatParamGroups, lss_backward_groups
     from lss_carla_amd.train_step import TrainStep
     import lss_carla_amd as L
@@ -523,25 +525,44 @@ def main():
         torch.cuda.synchronize()  # (a progress line per warm-up step: a long MIOpen search is not a hang)
         log(f"[rank {rank}] warm-up step {i + 1} done at {time.perf_counter() - t_w:.1f} s")
 
+    sync = None
+    fell_back = None
     if args.graph:
-        # eager warm-up on a side stream (MIOpen find, optimizer state), capture, 2 untimed replays
-        try:
-            step.capture(warmup=max(args.warmup, 2), on_warmup=first)
-        except RuntimeError as e:
-            if not getattr(step, "overlap", False):
-                raise
-            # the collectives inside the capture failed: one flat all-reduce between the graphs instead
-            # (every rank runs the same code, so every rank takes this branch)
-            log(f"[rank {rank}] captured all-reduce failed ({e}); falling back to the serial all-reduce")
+        # eager warm-up on a side stream (MIOpen find, optimizer state), capture, 2 untimed replays.
+        # The capture's outcome is agreed by all ranks before any replay (parallel.capture_collectively):
+        # if the collectives inside one rank's capture failed, EVERY rank takes the serial all-reduce.
+        def serial_step():
             torch.cuda.synchronize()
-            flat = FlatParams(model, cast_dtype=amp_dtype)
-            params = [flat.master]
-            opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-7, fused=True, capturable=True)
-            step = TrainStep(flat.bind(model), inputs, labels, loss_fn, opt, params, all_reduce=True,
+            flat_s = FlatParams(model, cast_dtype=amp_dtype)
+            opt_s = torch.optim.Adam([flat_s.master], lr=1e-3, weight_decay=1e-7, fused=True, capturable=True)
+            return TrainStep(flat_s.bind(model), inputs, labels, loss_fn, opt_s, [flat_s.master], all_reduce=True,
                              amp_dtype=amp_dtype, max_grad_norm=5.0, pre_step=pre_step, force_collectives=FORCE_PG)
-            step.capture(warmup=2)
+        overlapped = args.mode == "train" and getattr(step, "overlap", False)
+        fail = os.environ.get("LSS_BENCH_FAIL_CAPTURE_RANK", "") == str(rank)  # rehearsal of the fallback
+        step, fell_back = parallel.capture_collectively(step, max(args.warmup, 2),
+                                                        serial_step if overlapped else None, first, fail)
+        if fell_back:
+            log(f"[rank {rank}] every rank falls back to the serial all-reduce ({fell_back})")
         for _ in range(2):
             step()
+        if args.mode == "train" and world > 1:
+            # the replicas must be bit-identical after the updates (train_simbev.py:245-248): checksums
+            # of every master gathered over the control group
+            ok = parallel.replicas_in_sync(step.params)
+            if not ok and getattr(step, "overlap", False):
+                log(f"[rank {rank}] replicas differ after the overlapped captured all-reduce: re-broadcasting "
+                    "rank 0's parameters, serial all-reduce")
+                parallel.broadcast_state(model)
+                step = serial_step()
+                step.capture(warmup=2)
+                for _ in range(2):
+                    step()
+                fell_back = "replicas differed after the overlapped captured all-reduce"
+                ok = parallel.replicas_in_sync(step.params)
+            if not ok:
+                log(f"[rank {rank}] replicas differ after the untimed replays; not reporting a number")
+                sys.exit(4)
+            sync = {"checked": "checksums of every fp32 master, all ranks", "after_warmup": ok}
     else:
         for i in range(args.warmup):
             step()
@@ -580,6 +601,8 @@ def main():
         per_rank_ms = [1e3 * float(x.item()) / args.steps for x in allt]
         elapsed = max(float(x.item()) for x in allt)
     log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f} s, out {float(out.float().mean()):.4f}")
+    if sync is not None:
+        sync["after_timed"] = parallel.replicas_in_sync(step.params)
 
     if rank == 0:
         D, H, W = model.frustum.shape[:3]
@@ -609,6 +632,7 @@ def main():
                                       else "one flat all-reduce between the graphs" if (world > 1 or FORCE_PG)
                                       else None)},
             "per_rank_ms_per_step": [round(x, 3) for x in per_rank_ms],
+            "replicas_in_sync": sync, "capture_fallback": fell_back,
             "roofline": {"kernel": "lss_splat_fwd", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,

@@ -70,6 +70,16 @@ int lss_event_elapsed_ms(lss_event_t start, lss_event_t stop, float* ms); /* syn
  * event-record node to the graph (so every replay stamps the event), not a capture dependency. */
 int lss_event_record(lss_event_t ev, lss_stream_t stream);
 
+/* Measurement kernels (bench.py's roofline ceiling; not on the model's path).
+ * lss_ceiling_store: `bytes` (multiple of 16, dst 16-B aligned) written with 16-B vector stores,
+ *   per_thread vectors per lane (grid-strided), flavor 0 plain / 1 non-temporal; optional
+ *   kernel-stamped events as lss_splat_fwd.
+ * lss_ceiling_read: a 16-B-load sweep over `bytes` (sets the cache state before a timed launch);
+ *   sink (4 B, device) is never written in practice. */
+int lss_ceiling_store(void* dst, size_t bytes, int32_t per_thread, int32_t flavor, lss_stream_t stream,
+                      lss_event_t ev_start, lss_event_t ev_stop);
+int lss_ceiling_read(const void* src, size_t bytes, void* sink, lss_stream_t stream);
+
 /* Device 3x3 inverses of post_rots and intrins (fp64 adjugate, rounded to fp32).
  * Replaces torch.inverse(post_rots.cpu()) / torch.inverse(intrins.cpu())
  * of src/models.py:180,186 without a device->host round trip. */

@@ -55,6 +55,8 @@ SIGNATURES = {
     "lss_event_destroy": (ctypes.c_int, [_p]),
     "lss_event_elapsed_ms": (ctypes.c_int, [_p, _p, ctypes.POINTER(ctypes.c_float)]),
     "lss_event_record": (ctypes.c_int, [_p, _p]),
+    "lss_ceiling_store": (ctypes.c_int, [_p, ctypes.c_size_t, _i32, _i32, _p, _p, _p]),
+    "lss_ceiling_read": (ctypes.c_int, [_p, ctypes.c_size_t, _p, _p]),
     "lss_camera_inverse": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p]),
     "lss_geometry_cells": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _p, _p, _p, _p]),
     "lss_geometry_cells_axes": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _p, _p, _p, _p]),

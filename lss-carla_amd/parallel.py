@@ -71,6 +71,84 @@ def broadcast_state(model: torch.nn.Module, src: int = 0) -> None:
             dist.broadcast(t.data, src)
 
 
+# ----------------------------------------------------------------------------- one-shot N > 1 safety
+# The driver's multi-GPU bench runs once, unattended: every decision that could send ranks down
+# different paths (a graph capture that raised on one rank only) is taken collectively, over a
+# host-side gloo group that does not depend on the state of the RCCL communicator, and the replicas
+# are checked bit for bit after the untimed replays (train_simbev.py:245-248 is the update they must
+# agree on).
+_CONTROL = None
+
+
+def control_group():
+    """A gloo group over all ranks for host-side decisions; created collectively on first use (every
+    rank must call it at the same point). The world group itself when that is already gloo."""
+    global _CONTROL
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    if _CONTROL is None:
+        _CONTROL = dist.group.WORLD if dist.get_backend() == "gloo" else dist.new_group(backend="gloo")
+    return _CONTROL
+
+
+def all_ranks_ok(ok: bool) -> bool:
+    """True iff `ok` holds on every rank (MIN over the control group); `ok` itself at world size 1."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=control_group())
+    return bool(t.item())
+
+
+def replica_checksums(tensors) -> torch.Tensor:
+    """(n, 2) int64 per tensor: the sum of its elements' bit patterns and a position-weighted sum of
+    them (weights 1..65521), wrapped mod 2^64 -- equal on two replicas iff (with overwhelming
+    probability) the tensors are bit-identical. Computed where the tensors live; returned on the CPU."""
+    rows = []
+    for t in tensors:
+        flat = t.detach().contiguous().reshape(-1)
+        int_dt = {4: torch.int32, 2: torch.int16, 8: torch.int64}.get(flat.element_size())
+        bits = (flat.view(int_dt) if int_dt is not None else flat.view(torch.uint8)).to(torch.int64)
+        w = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 65521 + 1
+        rows.append(torch.stack([bits.sum(), (bits * w).sum()]))
+    return torch.stack(rows).cpu() if rows else torch.zeros(0, 2, dtype=torch.int64)
+
+
+def replicas_in_sync(tensors) -> bool:
+    """True iff every rank holds bit-identical `tensors` (e.g. the masters after an update): the
+    checksums of all ranks gathered over the control group and compared with rank 0's."""
+    c = replica_checksums(tensors)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return True
+    allc = [torch.empty_like(c) for _ in range(dist.get_world_size())]
+    dist.all_gather(allc, c, group=control_group())
+    return all(torch.equal(x, allc[0]) for x in allc)
+
+
+def capture_collectively(step, warmup: int, fallback=None, on_warmup=None, fail: bool = False):
+    """Capture `step` (train_step.TrainStep or anything with .capture(warmup, on_warmup)) on every
+    rank, or on none: each rank's success is agreed over the control group before any replay, so a
+    capture that raised on one rank sends EVERY rank to `fallback()` (a factory of the step to use
+    instead, captured here with 2 warm-up steps). Returns (step, reason) -- reason None when `step`
+    itself was captured everywhere, else why the fallback was taken. fail: force this rank's
+    capture to raise (tests of the decision)."""
+    err = None
+    try:
+        if fail:
+            raise RuntimeError("capture failure forced on this rank")
+        step.capture(warmup=warmup, on_warmup=on_warmup)
+    except RuntimeError as e:
+        err = e
+    if all_ranks_ok(err is None):
+        return step, None
+    if fallback is None:
+        raise RuntimeError(f"graph capture failed on {'this' if err else 'another'} rank") from err
+    reason = f"this rank's capture raised: {err}" if err is not None else "another rank's capture raised"
+    new = fallback()
+    new.capture(warmup=2)
+    return new, reason
+
+
 def max_over_ranks(value: float, device: torch.device) -> float:
     if not (dist.is_available() and dist.is_initialized()):
         return value

@@ -213,6 +213,7 @@ def _worker_trainstep(rank, world, port, outdir, overlap=False):
     else:
         loss = step.eager()
     assert torch.isfinite(loss)
+    assert parallel.replicas_in_sync(step.params)  # bench.py's check after the untimed replays
     if rank == 0:
         if overlap:
             torch.save({"grads": grads, "params": {n.removeprefix("model."): v.clone().contiguous()
@@ -277,3 +278,62 @@ def test_train_step_world2_overlapped_all_reduce():
     for n in want_g:
         assert torch.equal(got["grads"][n], want_g[n]), n
         torch.testing.assert_close(got["params"][n], want_p[n], rtol=0, atol=1e-5, msg=n)
+
+
+class _FakeStep:
+    """Stands in for train_step.TrainStep in the capture decision: capture() records its call."""
+
+    def __init__(self, name):
+        self.name, self.captured_with = name, None
+
+    def capture(self, warmup=2, on_warmup=None):
+        self.captured_with = warmup
+
+
+def _worker_capture_decision(rank, world, port, outdir, fail_rank):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    parallel.init_from_env("gloo")
+    assert parallel.control_group() is not None
+    step, reason = parallel.capture_collectively(_FakeStep("overlapped"), 3, fallback=lambda: _FakeStep("serial"),
+                                                 fail=(rank == fail_rank))
+    # replicas: identical tensors agree; a one-ulp change on rank 1 is seen by every rank
+    t = [torch.linspace(-1, 1, 1000), torch.arange(7, dtype=torch.float32)]
+    same = parallel.replicas_in_sync(t)
+    if rank == 1:
+        t[0][500] = torch.nextafter(t[0][500], torch.tensor(2.0))
+    diff = parallel.replicas_in_sync(t)
+    torch.save({"step": step.name, "warmup": step.captured_with, "reason": reason, "same": same, "diff": diff},
+               os.path.join(outdir, f"cap{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("fail_rank", [-1, 0, 1])
+def test_capture_fallback_is_a_collective_decision(fail_rank):
+    """bench.py's N > 1 capture path (parallel.capture_collectively): when one rank's capture raises,
+    EVERY rank takes the serial all-reduce step (captured with 2 warm-up steps); when none does, every
+    rank keeps its captured step. parallel.replicas_in_sync: True on identical replicas, False on every
+    rank when one element of one rank differs by one ulp."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_capture_decision, args=(world, _free_port(), d, fail_rank), nprocs=world, join=True)
+        got = [torch.load(os.path.join(d, f"cap{r}.pt"), weights_only=True) for r in range(world)]
+    for r, g in enumerate(got):
+        if fail_rank < 0:
+            assert (g["step"], g["warmup"], g["reason"]) == ("overlapped", 3, None)
+        else:
+            assert (g["step"], g["warmup"]) == ("serial", 2)
+            assert ("this rank" if r == fail_rank else "another rank") in g["reason"]
+        assert g["same"] is True and g["diff"] is False
+
+
+def test_replica_checksums_single_process():
+    """World size 1: always in sync; the checksum tells bit patterns apart (-0.0 vs 0.0, bf16 views)."""
+    a = torch.zeros(10)
+    b = a.clone()
+    b[3] = -0.0
+    assert not torch.equal(parallel.replica_checksums([a]), parallel.replica_checksums([b]))
+    assert torch.equal(parallel.replica_checksums([a.bfloat16()]), parallel.replica_checksums([a.bfloat16()]))
+    assert parallel.replicas_in_sync([a]) is True
