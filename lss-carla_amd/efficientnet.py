@@ -370,6 +370,21 @@ def set_batchnorm_native(module: nn.Module) -> int:
     return n
 
 
+def load_state_dict_file(path: str) -> dict:
+    """A state dict from a file, by loaders that execute nothing from it: safetensors for
+    ``.safetensors``, else ``torch.load(weights_only=True)`` (a ``{"state_dict": ...}`` wrapper is
+    unwrapped). CPU tensors."""
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        return dict(load_file(path, device="cpu"))
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(sd, dict) and "state_dict" in sd and isinstance(sd["state_dict"], dict):
+        sd = sd["state_dict"]
+    if not isinstance(sd, dict) or not all(isinstance(v, torch.Tensor) for v in sd.values()):
+        raise RuntimeError(f"{path}: not a state dict of tensors")
+    return sd
+
+
 class EfficientNetB0(nn.Module):
     """The trunk of ``CamEncode`` (module names of efficientnet_pytorch.EfficientNet)."""
 
@@ -393,6 +408,38 @@ class EfficientNetB0(nn.Module):
         self._avg_pooling = nn.AdaptiveAvgPool2d(1)
         self._dropout = nn.Dropout(0.2)
         self._fc = nn.Linear(1280, num_classes)
+
+    @classmethod
+    def from_pretrained(cls, model_name: str = "efficientnet-b0", weights_path: str | None = None,
+                        load_fc: bool = True, num_classes: int = 1000) -> "EfficientNetB0":
+        """``EfficientNet.from_pretrained`` (src/models.py:43) from a LOCAL file: nothing is fetched.
+
+        weights_path: an efficientnet_pytorch-format state dict of B0 (the package's published
+        ``efficientnet-b0-355c32eb.pth``, or any ``torch.save(model.state_dict())`` of either
+        module; ``.safetensors`` also read). Default: $LSS_EFFICIENTNET_B0_WEIGHTS. Loaded with a
+        loader that executes nothing from the file (``torch.load(weights_only=True)`` /
+        safetensors). As the package's ``load_pretrained_weights``: every key of the model must be
+        in the file (``num_batches_tracked`` excepted: older checkpoints lack it), the ``_fc``
+        keys are skipped with ``load_fc=False`` (then ``num_classes`` may differ), and a key the
+        model does not have is an error."""
+        if model_name != "efficientnet-b0":
+            raise ValueError(f"only efficientnet-b0 is built here, not {model_name!r}")
+        import os
+        path = weights_path or os.environ.get("LSS_EFFICIENTNET_B0_WEIGHTS")
+        if not path:
+            raise RuntimeError("EfficientNetB0.from_pretrained needs a local weights file (weights_path= or "
+                               "$LSS_EFFICIENTNET_B0_WEIGHTS): there is no download")
+        sd = load_state_dict_file(path)
+        if not load_fc:
+            sd = {k: v for k, v in sd.items() if not k.startswith("_fc.")}
+        model = cls(num_classes)
+        ret = model.load_state_dict(sd, strict=False)
+        missing = [k for k in ret.missing_keys if not k.endswith("num_batches_tracked")
+                   and (load_fc or not k.startswith("_fc."))]
+        if missing or ret.unexpected_keys:
+            raise RuntimeError(f"{path}: not an efficientnet-b0 state dict (missing {missing[:5]}, "
+                               f"unexpected {ret.unexpected_keys[:5]})")
+        return model
 
     @staticmethod
     def _swish(x: torch.Tensor) -> torch.Tensor:

@@ -82,7 +82,11 @@ class CamEncode(nn.Module):
     def __init__(self, D, C, downsample):
         super().__init__()
         self.D, self.C = D, C
-        self.trunk = EfficientNetB0()
+        # src/models.py:43 loads ImageNet weights with EfficientNet.from_pretrained("efficientnet-b0"),
+        # a download; here they come from a local file when $LSS_EFFICIENTNET_B0_WEIGHTS names one
+        # (an unchanged train_simbev.py then trains from them), else the trunk is randomly initialised
+        wpath = os.environ.get("LSS_EFFICIENTNET_B0_WEIGHTS")
+        self.trunk = EfficientNetB0.from_pretrained("efficientnet-b0", wpath) if wpath else EfficientNetB0()
         self.up1 = Up(320 + 112, 512)
         self.dropout = nn.Dropout(0.2)
         self.depthnet = nn.Conv2d(512, self.D + self.C, kernel_size=1, padding=0)
