@@ -598,6 +598,8 @@ __device__ __forceinline__ void for_chunk_nhwc(const BnGeo& g, int G, int q, F&&
 // lanes inside each wave, then the waves' rows in LDS ([wave][C][2], zero where a wave holds none of
 // a channel) added in wave order -- fixed association, two barriers (a serial round per thread of an
 // octet took kBlock / cg barriers: 32 at C = 64).
+// dynamic LDS floats per channel of nhwc_block_sums' [wave][C][2] rows (stats kernels, both directions)
+constexpr int kNhwcStatsLds = (kBlock / kWave) * 2;
 __device__ __forceinline__ void nhwc_block_sums(const BnGeo& g, int G, int q, float* a, float* b, int c0,
                                                 bool active, float* s_acc, float* __restrict__ partial) {
     const int cg = g.C / 8;
@@ -877,8 +879,8 @@ int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layou
         T* yy = (T*)y;                                                                                             \
         if (layout == LSS_CONV_NHWC) {                                                                             \
             const size_t lds = 2 * C * sizeof(float);                                                              \
-            hipLaunchKernelGGL(k_bn_stats_nhwc<T>, dim3(G), dim3(kBlock), (kBlock / kWave) * lds, s, xx, g, G,     \
-                               partial);                                                                           \
+            hipLaunchKernelGGL(k_bn_stats_nhwc<T>, dim3(G), dim3(kBlock), kNhwcStatsLds * C * sizeof(float), s, xx, \
+                               g, G, partial);                                                                     \
             hipLaunchKernelGGL(k_bn_fold_nhwc<T>, dim3((C + 3) / 4), dim3(kBlock), 0, s, partial, G, xx, g, P);   \
             hipLaunchKernelGGL(k_bn_apply_nhwc<T>, dim3(apply_blocks(g)), dim3(kBlock), lds, s, xx, rr, g,        \
                                save_mean, (int)act, yy);                                                           \
@@ -946,7 +948,7 @@ int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int3
         T* o = (T*)dx;                                                                                             \
         T* orr = (T*)dresidual;                                                                                    \
         if (layout == LSS_CONV_NHWC) {                                                                             \
-            hipLaunchKernelGGL(k_bn_bwd_stats_nhwc<T>, dim3(G), dim3(kBlock), 8 * C * sizeof(float), s, d, xx, yy, \
+            hipLaunchKernelGGL(k_bn_bwd_stats_nhwc<T>, dim3(G), dim3(kBlock), kNhwcStatsLds * C * sizeof(float), s, d, xx, yy, \
                                g, G, stats, (int)act, partial);                                                    \
             hipLaunchKernelGGL(k_bn_bwd_fold_nhwc, dim3((C + 3) / 4), dim3(kBlock), 0, s, partial, G, g, dgamma,  \
                                dbeta, coef);                                                                       \

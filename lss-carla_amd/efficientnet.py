@@ -202,6 +202,8 @@ class _HipScaleAdd(torch.autograd.Function):
         lib = _lib.load()
         (u,) = ctx.saved_tensors
         dy = dy.to(torch.bfloat16).contiguous(memory_format=ctx.fmt)
+        if dy.data_ptr() % 16:  # a contiguous view at an unaligned offset: the kernel's 16-B loads need a copy
+            dy = dy.clone(memory_format=ctx.fmt)
         dx = torch.empty_like(dy)
         N = dy.shape[0]
         _lib.check(lib.lss_scale_add(_lib.ptr(dy), _lib.ptr(u), ctx.keep, None, N, dy.numel() // N, _lib.ptr(dx),

@@ -91,8 +91,11 @@ def camera_inverses(post_rots: torch.Tensor, intrins: torch.Tensor, mode: str = 
     ncam = post_rots.shape[0] * post_rots.shape[1]
     if mode == "host":
         def host_copy(t):
+            # the attached host copy only while the device tensor is unchanged since it was attached
+            # (an in-place copy_ into a reused batch buffer bumps _version: then read the device tensor)
             h = getattr(t, "_lss_host", None)
-            if h is not None and tuple(h.shape) == tuple(t.shape) and not h.is_cuda:
+            if (h is not None and tuple(h.shape) == tuple(t.shape) and not h.is_cuda
+                    and getattr(t, "_lss_host_version", None) == t._version):
                 return h
             return t.detach().cpu()
         pinv = torch.inverse(host_copy(post_rots).float()).reshape(ncam, 9).pin_memory()
@@ -623,8 +626,11 @@ class DepthnetLiftSplat(torch.autograd.Function):
                                f"the plan (B*N={B * N}, D+C={D + C_CAM}, H={H}, W={W})")
         # a channels-last feature map (pixel-major rows, as CamEncode's channels-last up1 gives it) goes
         # to the pixel-row kernel; anything else is made NCHW-contiguous for the channel-plane kernel
+        # (k_depthnet_lift3 reads 16-B vectors of the rows: a view at an unaligned offset is copied)
         nhwc = K == 512 and feat.dim() == 4 and feat.is_contiguous(memory_format=torch.channels_last)
         f = feat.detach() if nhwc else feat.detach().contiguous()
+        if f.data_ptr() % 16:
+            f = f.clone(memory_format=torch.channels_last if nhwc else torch.contiguous_format)
         w = weight.detach().reshape(O, K).contiguous()
         b = bias.detach().contiguous()
         depth = torch.empty(B * N, D, H, W, device=dev, dtype=torch.float32)

@@ -343,8 +343,8 @@ def finish_batch(batch, final_dim, device):
     out = [imgs] + [t.to(device, non_blocking=True) for t in (rots, trans, intrins, post_rots, post_trans)]
     # the host copies ride along: the model's host torch.inverse (src/models.py:180,186) reads them
     # instead of copying the device tensors back (ops.camera_inverses), so no batch syncs the host
-    out[3]._lss_host = intrins
-    out[4]._lss_host = post_rots
+    out[3]._lss_host, out[3]._lss_host_version = intrins, out[3]._version
+    out[4]._lss_host, out[4]._lss_host_version = post_rots, out[4]._version
     for t in rest[:-1]:
         out.append(t)  # lidar placeholder (VizData)
     out.append(vehicle_masks(rest[-1].to(device, non_blocking=True)))

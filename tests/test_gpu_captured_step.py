@@ -5,8 +5,11 @@ persistent workspace pointers baked into the graph), replayed over two different
 
 Each replay is compared with an eager step from the same parameters and inputs (the BEV bit for bit,
 the loss, camencode.depthnet.weight's clipped gradient), and the replayed BEV with the fp64 oracle on
-the same bf16 operands (reference: train_simbev.py:231-248 -> src/models.py:248-259). Dropout and
-drop-connect are off (their masks come from different RNG streams in a graph and eagerly)."""
+the same bf16 operands (reference: train_simbev.py:231-248 -> src/models.py:248-259). Run twice: with
+dropout and drop-connect off, and with both at their defaults (the benched step: torch.rand's draw
+feeding lss_scale_add's in-kernel mask) -- then the CUDA generator is seeded identically before the
+replay and before the eager step (graph-safe Philox: the same draws), and two replays without a
+reseed must draw different masks."""
 import os
 
 import numpy as np
@@ -49,16 +52,20 @@ def miopen_find():
     torch.backends.cudnn.benchmark = old
 
 
-def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find):
+@pytest.mark.parametrize("stochastic", [False, True], ids=["deterministic", "dropout_dropconnect"])
+def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find, stochastic):
     cfg, gc, dac = syn.config_confs("c3")
     B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
     torch.manual_seed(7)
     model = L.compile_model(gc, dac, outC=1).to(DEV)
     model.bev_layout, model.fuse_depthnet = "nhwc", True
     model.bevencode.to(memory_format=torch.channels_last)
-    model.camencode.dropout.p = 0.0
-    model.bevencode.dropout.p = 0.0
-    model.camencode.trunk._global_params.drop_connect_rate = 0.0
+    if not stochastic:
+        model.camencode.dropout.p = 0.0
+        model.bevencode.dropout.p = 0.0
+        model.camencode.trunk._global_params.drop_connect_rate = 0.0
+    else:
+        assert model.camencode.trunk._global_params.drop_connect_rate == 0.2
     model.train()
     parallel.freeze_unused(model)
     flat = FlatParamGroups(model, lss_backward_groups(), cast_dtype=torch.bfloat16)
@@ -109,6 +116,7 @@ def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find):
     for i, r in enumerate(rigs):
         set_rig(r)
         restore()
+        torch.cuda.manual_seed(1000 + i)  # the same Philox stream for the replay and the eager step
         step()  # pre_step + graph replays
         torch.cuda.synchronize()
         rep = (g_bev.clone(), g_dw.clone(), step.static_loss.clone())
@@ -118,6 +126,7 @@ def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find):
         restore()
         w = model.camencode.depthnet.weight.detach().to(torch.bfloat16).cpu()  # this step's bf16 operands
         b = model.camencode.depthnet.bias.detach().to(torch.bfloat16).cpu()
+        torch.cuda.manual_seed(1000 + i)
         loss_e = step.eager()
         torch.cuda.synchronize()
         e_dw = flat.views(grads=True)["camencode.depthnet.weight"].clone()
@@ -156,3 +165,11 @@ def test_captured_c3_step_matches_eager_and_oracle_over_two_rigs(miopen_find):
         results.append(rep[0])
     # the two rigs really produced different BEVs through the same graph
     assert not torch.equal(results[0], results[1])
+    if stochastic:  # two replays, same rig and parameters, no reseed: new dropout / drop-connect masks
+        bevs = []
+        for _ in range(2):
+            restore()
+            step()
+            torch.cuda.synchronize()
+            bevs.append(g_bev.clone())
+        assert not torch.equal(bevs[0], bevs[1]), "the replays drew the same masks"
