@@ -73,14 +73,7 @@ def parse():
                     help="depthwise convs of the trunk: HIP kernels, MIOpen, PyTorch native, MIOpen in fp32")
     ap.add_argument("--miopen-find", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
     ap.add_argument("--hip-bn", type=int, default=1, help="BatchNorm + activation on the lss_bn_* kernels")
-    ap.add_argument("--inverse", default="host", choices=["host", "device"],
-                    help="host: torch.inverse on the CPU (the reference's; bit-exact ids), device: fp64 kernel")
     ap.add_argument("--fuse-depthnet", type=int, default=1, help="depthnet 1x1 conv inside the lift kernel (MFMA)")
-    ap.add_argument("--sorted-depth", type=int, default=0,
-                    help="the CSR build writes each point's sorted position and the lift writes the depth weights "
-                         "in CSR order, so the channels-last splat reads them contiguously")
-    ap.add_argument("--plan-side-stream", type=int, default=0,
-                    help="build the plan (geometry + CSR) on a side stream, concurrent with the trunk")
     ap.add_argument("--graph", type=int, default=1,
                     help="replay the step as HIP graphs (fwd+bwd, clip+Adam) with the gradient all-reduce "
                          "between them; 0 = eager (DDP for N>1)")
@@ -167,18 +160,49 @@ def splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes, ctx_bytes) -> int:
 
 
 def write_ceiling(numel, dtype, dev, reps=10) -> dict:
-    """Measured HBM write ceiling for the splat's output: a memset of a BEV-sized buffer with L2 and
-    the Infinity Cache flushed (512 MiB written) before each launch -- the state the BEV buffer is in
-    when the splat runs inside a step (its lines were evicted by the trunk). hipEvents around the
-    launch; mean over `reps`."""
+    """Measured HBM write ceiling for the splat's output buffer: lss_ceiling_store, a hand-written
+    16-B streaming-store kernel (consecutive lanes on consecutive 16 B, `per_thread` stores per lane,
+    non-temporal or plain) over a BEV-sized buffer, kernel-stamped events (the kernel alone), mean
+    over `reps` launches, each after a 512 MiB read sweep (lss_ceiling_read: L2 and the Infinity
+    Cache hold clean lines, as after the trunk's reads; the ceiling) and after a 512 MiB write (dirty
+    lines the stores must evict first; reported beside it). The fastest store form is the ceiling.
+    Also the torch memset (fill kernel) and copy (read + write) of the same buffer, read-swept."""
+    import ctypes as ct
+    from lss_carla_amd import _lib
+    lib = _lib.load()
     buf = torch.empty(numel, dtype=dtype, device=dev)
     src = torch.empty_like(buf)
+    nbytes = numel * buf.element_size()
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    st = _lib.stream_handle(dev)
+
+    def prepare(state):
+        if state == "read":
+            _lib.check(lib.lss_ceiling_read(_lib.ptr(flush), flush.numel(), _lib.ptr(sink), st), "ceiling_read")
+        else:
+            flush.zero_()
+
+    def stamped(per_thread, flavor, state) -> float:
+        tot = 0.0
+        for i in range(reps + 2):
+            prepare(state)
+            a, b = ct.c_void_p(), ct.c_void_p()
+            lib.lss_event_create(ct.byref(a))
+            lib.lss_event_create(ct.byref(b))
+            _lib.check(lib.lss_ceiling_store(_lib.ptr(buf), nbytes, per_thread, flavor, st, a, b), "ceiling_store")
+            ms = ct.c_float()
+            lib.lss_event_elapsed_ms(a, b, ct.byref(ms))
+            lib.lss_event_destroy(a)
+            lib.lss_event_destroy(b)
+            if i >= 2:
+                tot += ms.value
+        return tot / reps * 1e3
 
     def timed(fn) -> float:
         tot = 0.0
         for i in range(reps + 2):
-            flush.zero_()
+            prepare("read")
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             fn()
@@ -188,13 +212,25 @@ def write_ceiling(numel, dtype, dev, reps=10) -> dict:
                 tot += e0.elapsed_time(e1)
         return tot / reps * 1e3
 
-    us = timed(lambda: buf.zero_())
+    forms = {}
+    for pt in CEILING_PER_THREAD:
+        for fl, fname in ((1, "nt"), (0, "plain")):
+            forms[f"pt{pt}_{fname}"] = {"read": round(stamped(pt, fl, "read"), 2),
+                                        "dirty": round(stamped(pt, fl, "dirty"), 2)}
+    best = min(forms, key=lambda k: forms[k]["read"])
+    us = forms[best]["read"]
+    us_memset = timed(lambda: buf.zero_())
     us_copy = timed(lambda: buf.copy_(src))  # the copy-kernel ceiling SURVEY 8(d) asks for: read + write
-    nbytes = numel * buf.element_size()
     del buf, src, flush
-    return {"what": f"memset of the {nbytes / 1e6:.1f} MB BEV, L2 + Infinity Cache flushed before each launch",
-            "us": round(us, 2), "GB/s": round(nbytes / us / 1e3, 1),
+    return {"what": f"lss_ceiling_store: 16-B streaming stores over the {nbytes / 1e6:.1f} MB BEV buffer after a "
+                    f"512 MiB read sweep, fastest form ({best}); kernel-stamped events",
+            "us": round(us, 2), "GB/s": round(nbytes / us / 1e3, 1), "form": best, "forms_us": forms,
+            "dirty_us": forms[best]["dirty"], "dirty_GB/s": round(nbytes / forms[best]["dirty"] / 1e3, 1),
+            "memset_us": round(us_memset, 2), "memset_GB/s": round(nbytes / us_memset / 1e3, 1),
             "copy_us": round(us_copy, 2), "copy_GB/s": round(2 * nbytes / us_copy / 1e3, 1)}
+
+
+CEILING_PER_THREAD = (1, 4)
 
 
 # ----------------------------------------------------------------------------- HBM traffic (PMC)
@@ -373,11 +409,7 @@ def build_model(args, dev, gc, dac):
 
     model = L.compile_model(gc, dac, outC=1).to(dev)
     model.bev_layout = args.bev_layout
-    model.inverse = args.inverse
     model.fuse_depthnet = bool(args.fuse_depthnet)
-    model.plan_side_stream = bool(args.plan_side_stream)
-    from lss_carla_amd import ops
-    ops.SORTED_DEPTH = bool(args.sorted_depth)
     if args.bev_layout == "nhwc":
         model.bevencode.to(memory_format=torch.channels_last)
     if args.trunk_channels_last:
@@ -488,7 +520,7 @@ def main():
     inputs = (imgs, rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"])
 
     pre_step = None
-    if args.graph and args.inverse == "host":
+    if args.graph:
         # host torch.inverse of the (host) rig before every step, staged into the graph's static inputs
         hinv = ops.HostInverses(B * N, dev)
         model.static_inverses = (hinv.pinv, hinv.kinv)
@@ -623,11 +655,10 @@ def main():
             "config": {"workload": f"{args.config}: B={B}/GPU x {N} cams x {fd[0]}x{fd[1]}, D={D}, {X}x{Y} BEV, "
                                    + what,
                        "global_batch": world * B, "parallelism": f"dp{world}", "bev_layout": args.bev_layout,
-                       "inverse": args.inverse, "fuse_depthnet": bool(args.fuse_depthnet),
+                       "inverse": "host torch.inverse", "fuse_depthnet": bool(args.fuse_depthnet),
                        "depthwise": args.dw_impl, "batchnorm": "hip" if args.hip_bn else "miopen",
                        "step": "hipgraph" if args.graph else "eager", "flat_params": bool(args.flat_params),
                        "param_groups": bool(args.flat_params and args.param_groups),
-                       "plan_side_stream": bool(args.plan_side_stream), "sorted_depth": bool(args.sorted_depth),
                        "all_reduce": ("overlapped with backward (3 groups, captured)" if getattr(step, "overlap", False)
                                       else "one flat all-reduce between the graphs" if (world > 1 or FORCE_PG)
                                       else None)},

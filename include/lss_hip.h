@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 16
+#define LSS_ABI_VERSION 17
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -45,7 +45,6 @@ typedef struct lss_grid {
 enum { LSS_F32 = 0, LSS_BF16 = 1 };          /* element types */
 enum { LSS_NCHW = 0, LSS_NHWC = 1 };         /* BEV memory layouts of a (B, Z*C, X, Y) tensor */
 enum { LSS_EINVAL = -1, LSS_EUNSUPPORTED = -2 };
-enum { LSS_SPLAT_EMPTY_FILLED = 1, LSS_SPLAT_UNORDERED = 2 };  /* lss_splat_fwd flags */
 
 typedef void* lss_stream_t; /* a hipStream_t */
 typedef void* lss_event_t;  /* a hipEvent_t */
@@ -80,12 +79,6 @@ int lss_ceiling_store(void* dst, size_t bytes, int32_t per_thread, int32_t flavo
                       lss_event_t ev_start, lss_event_t ev_stop);
 int lss_ceiling_read(const void* src, size_t bytes, void* sink, lss_stream_t stream);
 
-/* Device 3x3 inverses of post_rots and intrins (fp64 adjugate, rounded to fp32).
- * Replaces torch.inverse(post_rots.cpu()) / torch.inverse(intrins.cpu())
- * of src/models.py:180,186 without a device->host round trip. */
-int lss_camera_inverse(const float* post_rots, const float* intrins, int32_t n_cams,
-                       float* pinv, float* kinv, lss_stream_t stream);
-
 /* get_geometry (src/models.py:170-190) fused with quantise + bounds filter
  * (src/models.py:211-223). fp32, sequential non-FMA mat-vecs, IEEE division,
  * truncation toward zero. out_geom (Nprime*3) may be NULL. cell_of (Nprime)
@@ -97,15 +90,6 @@ int lss_geometry_cells(const float* frustum, const float* rots, const float* tra
                        const lss_dims_t* dims, const lss_grid_t* grid,
                        float* out_geom, int32_t* cell_of, int32_t* cell_count, int32_t* slot_of,
                        lss_stream_t stream);
-
-/* lss_geometry_cells with the frustum given by its axes: axes = [xs (W) | ys (H) | ds (D)] fp32,
- * the 1-D tensors create_frustum broadcasts (src/models.py:157-168: frustum[d, h, w] =
- * (xs[w], ys[h], ds[d])). Same outputs, bit for bit, as lss_geometry_cells on that frustum. */
-int lss_geometry_cells_axes(const float* axes, const float* rots, const float* trans,
-                            const float* kinv, const float* pinv, const float* post_trans,
-                            const lss_dims_t* dims, const lss_grid_t* grid, float* out_geom,
-                            int32_t* cell_of, int32_t* cell_count, int32_t* slot_of,
-                            lss_stream_t stream);
 
 /* Quantise a given (Nprime, 3) fp32 geometry (voxel_pooling(geom_feats, x) boundary,
  * src/models.py:204-223). Same outputs as lss_geometry_cells; points_per_batch =
@@ -121,13 +105,12 @@ int lss_cells_from_geom(const float* geom, int32_t nprime, int32_t points_per_ba
  * (cell << 32) | p, followed by the sentinel key -1 in every slot from cell_start[ncells] to
  * Nprime; sorted_row (Nprime capacity) = the row each entry's features are read from: the pixel
  * q(p) when dims is given (fused lift), p itself when dims is NULL (per-point rows); defined for
- * the first cell_start[ncells] entries. pos_of (Nprime, nullable) = the inverse permutation: the
- * sorted position of point p, -1 for a dropped point (lets the lift write its depth weights in CSR
- * order, see lss_lift_prep). scratch: lss_csr_scratch_bytes bytes. */
+ * the first cell_start[ncells] entries. scratch: lss_csr_scratch_bytes bytes.
+ * Replaces: ranks = ...; sorts = ranks.argsort(); x, geom_feats, ranks = x[sorts], ... (src/models.py:225-231). */
 size_t lss_csr_scratch_bytes(int32_t ncells, int32_t nprime);
 int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime,
                   const int32_t* cell_count, int32_t ncells, const lss_dims_t* dims,
-                  int32_t* cell_start, long long* sorted_key, int32_t* sorted_row, int32_t* pos_of,
+                  int32_t* cell_start, long long* sorted_key, int32_t* sorted_row,
                   void* scratch, lss_stream_t stream);
 
 /* lss_csr_build with a persistent workspace: the same outputs, bit for bit, in three kernels
@@ -137,49 +120,23 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
  * use; cell_count is zero-filled before the first lss_geometry_cells / lss_cells_from_geom that
  * counts into it; every call leaves both zero-filled again. One call at a time per workspace (the
  * caller orders calls that share one: ops.py records the stream and event of its last use).
- * Workspace header, 4 uint32: [0] scan ticket, [1] sticky count of look-back timeouts (a block that
+ * Workspace header, 4 uint32: [0] unused, [1] sticky count of look-back timeouts (a block that
  * waited its spin limit for a predecessor sums that predecessor's counts itself: the output is exact
  * either way), [2] spin-limit override (0: the built-in limit; s > 0: s - 1 polls -- tests of the
- * timeout path), [3] unused.
- * sorted_row == NULL (pos_of must then be NULL too): no canonical pass -- sorted_key is grouped by
- * ascending cell with the sentinel tail as above, but the entries of a cell are in the order the
- * counting sort's atomics gave them (one kernel fewer; lss_splat_fwd with LSS_SPLAT_UNORDERED puts
- * every cell in canonical order itself, with identical results). */
+ * timeout path), [3] unused. */
 size_t lss_csr_workspace_bytes(int32_t ncells);
 int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime,
                      int32_t* cell_count, int32_t ncells, const lss_dims_t* dims,
-                     int32_t* cell_start, long long* sorted_key, int32_t* sorted_row, int32_t* pos_of,
+                     int32_t* cell_start, long long* sorted_key, int32_t* sorted_row,
                      void* scratch, void* workspace, lss_stream_t stream);
-
-/* The whole plan in one call, on the persistent workspace of lss_csr_build_ws: lss_geometry_cells
- * (counting into cell_count; slot_of is scratch, Nprime ints) that also sums the counts of every
- * group of 4096 cells into the workspace, a scan that reads each group's prefix from those sums
- * (no look-back between blocks), the scatter and the canonical pass. Outputs -- cell_of,
- * cell_start, sorted_key, sorted_row, pos_of (nullable) -- bit-identical to lss_geometry_cells +
- * lss_csr_build_ws; same workspace contract (zero-filled, left zero-filled). */
-int lss_plan_ws(const float* frustum, const float* rots, const float* trans, const float* kinv,
-                const float* pinv, const float* post_trans, const lss_dims_t* dims, const lss_grid_t* grid,
-                int32_t* cell_of, int32_t* slot_of, int32_t* cell_count, int32_t* cell_start,
-                long long* sorted_key, int32_t* sorted_row, int32_t* pos_of, void* scratch, void* workspace,
-                lss_stream_t stream);
 
 /* Lift, part 1 (CamEncode.get_depth_dist + layout, src/models.py:49-59, 192-202):
  * depth (B*N, D, H, W) fp32 = softmax over D of depthnet_out[:, :D];
  * ctx_t (B*N*H*W, C), element type ctx_dtype = depthnet_out[:, D:D+C] moved to pixel-major rows
  * (bf16 rows are exact when depthnet_out is bf16, as under autocast).
- * depthnet_out is (B*N, D+C, H, W) contiguous, element type in_dtype. With pos_of (from
- * lss_csr_build; nullable) every kept point's weight is also written to sorted_depth[pos_of[p]]
- * (Nprime fp32): the splat then reads its weights contiguously, in CSR order, instead of
- * gathering depth[p] per entry.
- * Empty-row fill (bev nullable): bev is the channels-last (B, Z*C, X, Y) BEV of element type
- * bev_dtype that lss_splat_fwd will write; blocks of this launch beside the lift's own write zeros
- * into the rows of the cells that are empty by cell_start (of the plan, on bev_grid) -- work that
- * needs no lift output, done on CUs the lift leaves idle. Pass LSS_SPLAT_EMPTY_FILLED to the
- * splat then: it writes the occupied rows only. */
+ * depthnet_out is (B*N, D+C, H, W) contiguous, element type in_dtype. */
 int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims,
-                  float* depth, void* ctx_t, int32_t ctx_dtype, const int32_t* pos_of,
-                  float* sorted_depth, const int32_t* cell_start, const lss_grid_t* bev_grid, void* bev,
-                  int32_t bev_dtype, lss_stream_t stream);
+                  float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream);
 
 /* Depthnet + lift, part 1, fused (CamEncode.depthnet 1x1 conv + get_depth_dist + layout,
  * src/models.py:47, 55-59, 192-202): logits = weight . feat + bias on MFMA (bf16 in, fp32
@@ -188,21 +145,16 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
  * depthnet output (B*N, D+C, H, W) is never written. feat (B*N, K, H, W) contiguous, weight
  * (D+C, K) row-major, bias (D+C); dtype and ctx_dtype must be LSS_BF16; K % 16 == 0, K <= 512,
  * D + C <= 128 (else LSS_EUNSUPPORTED). The backward stays the conv's: d(logits) from
- * lss_splat_bwd feeds the 1x1 conv's weight / input gradients. pos_of / sorted_depth and the
- * empty-row fill (cell_start, bev_grid, bev, bev_dtype) as in lss_lift_prep. */
+ * lss_splat_bwd feeds the 1x1 conv's weight / input gradients. */
 int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
-                      const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype,
-                      const int32_t* pos_of, float* sorted_depth, const int32_t* cell_start,
-                      const lss_grid_t* bev_grid, void* bev, int32_t bev_dtype, lss_stream_t stream);
+                      const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream);
 
 /* As lss_depthnet_lift, with feat channels-last: (B*N, H, W, K) = pixel-major rows of K bf16 (the
  * memory of a torch.channels_last (B*N, K, H, W) tensor, as a channels-last Up stage produces it).
- * K must be 512. One block per compute unit, each on one contiguous run of pixel rows; identical
- * results to lss_depthnet_lift on the same values. */
+ * K must be 512; feat and weight 16-B aligned (else LSS_EINVAL). One block per compute unit, each
+ * on one contiguous run of pixel rows; identical results to lss_depthnet_lift on the same values. */
 int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
-                           const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype,
-                           const int32_t* pos_of, float* sorted_depth, const int32_t* cell_start,
-                           const lss_grid_t* bev_grid, void* bev, int32_t bev_dtype, lss_stream_t stream);
+                           const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream);
 
 /* Splat forward: segmented per-cell sum written as the dense (B, Z*C, X, Y) BEV
  * (voxel_pooling + QuickCumsum.forward + griddify, src/models.py:233-246,
@@ -215,22 +167,13 @@ int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bia
  * 64-entry chunk of the CSR (one gather round trip, LDS-staged ordered sums, rows stored
  * directly) plus zero-fill waves; LSS_NCHW: a BEV-row tile kernel (<= 128 cells per tile along Y)
  * with an LDS transpose. sorted_key / sorted_row as lss_csr_build wrote them (sorted_row is
- * unused in lifted mode, where the rows are the point ids). sorted_depth (nullable, fused mode):
- * the depth weights in CSR order as lss_lift_prep / lss_depthnet_lift wrote them; LSS_NHWC then
- * reads them with the keys instead of gathering depth[p] (the same values: identical results).
- * flags: LSS_SPLAT_EMPTY_FILLED (LSS_NHWC only): the empty cells' rows are already zero (the
- * lift's fill, lss_lift_prep / lss_depthnet_lift with bev), only the occupied rows are written.
- * LSS_SPLAT_UNORDERED (LSS_NHWC only, sorted_depth NULL, sorted_row unused): sorted_key comes from
- * lss_csr_build_ws without sorted_row -- arrival order inside each cell; each chunk wave ranks the
- * entries of every cell by point id before summing, so the result is bit-identical to the
- * canonical CSR's. Fused mode needs Nprime < 2^24 (rows from point ids), else LSS_EUNSUPPORTED.
+ * unused in lifted mode, where the rows are the point ids).
  * ev_start / ev_stop (nullable) are stamped with the kernel's own start / end
  * (hipExtLaunchKernel), so their elapsed time is the kernel alone, never launch latency. */
 int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
                   const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
-                  const float* sorted_depth, const lss_dims_t* dims, const lss_grid_t* grid,
-                  void* out, int32_t out_dtype, int32_t out_layout, int32_t flags, lss_stream_t stream,
-                  lss_event_t ev_start, lss_event_t ev_stop);
+                  const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype,
+                  int32_t out_layout, lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop);
 
 /* Backward helpers. A "row" is the C gradient values of one cell.
  * lss_bev_rows: NCHW dbev -> rows[cell*C + c] for every occupied cell (others untouched). */

@@ -18,9 +18,7 @@ DEBUG_LIB_PATH = os.path.join(_HERE, "liblss_hip_debug.so")  # LSS_DEBUG=1: devi
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 16
-SPLAT_EMPTY_FILLED = 1
-SPLAT_UNORDERED = 2
+ABI_VERSION = 17
 
 
 class Dims(ctypes.Structure):
@@ -57,22 +55,16 @@ SIGNATURES = {
     "lss_event_record": (ctypes.c_int, [_p, _p]),
     "lss_ceiling_store": (ctypes.c_int, [_p, ctypes.c_size_t, _i32, _i32, _p, _p, _p]),
     "lss_ceiling_read": (ctypes.c_int, [_p, ctypes.c_size_t, _p, _p]),
-    "lss_camera_inverse": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p]),
     "lss_geometry_cells": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _p, _p, _p, _p]),
-    "lss_geometry_cells_axes": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _p, _p, _p, _p]),
     "lss_cells_from_geom": (ctypes.c_int, [_p, _i32, _i32, _GRID, _p, _p, _p, _p]),
     "lss_csr_scratch_bytes": (ctypes.c_size_t, [_i32, _i32]),
-    "lss_csr_build": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p, _p]),
+    "lss_csr_build": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p]),
     "lss_csr_workspace_bytes": (ctypes.c_size_t, [_i32]),
-    "lss_csr_build_ws": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p, _p, _p]),
-    "lss_plan_ws": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID] + [_p] * 10),
-    "lss_lift_prep": (ctypes.c_int, [_p, _i32, _DIMS, _p, _p, _i32, _p, _p, _p, _GRID, _p, _i32, _p]),
-    "lss_depthnet_lift": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p, _p, _p, _GRID, _p, _i32,
-                                         _p]),
-    "lss_depthnet_lift_nhwc": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p, _p, _p, _GRID, _p,
-                                              _i32, _p]),
-    "lss_splat_fwd": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _i32, _p, _p,
-                                     _p]),
+    "lss_csr_build_ws": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p, _p]),
+    "lss_lift_prep": (ctypes.c_int, [_p, _i32, _DIMS, _p, _p, _i32, _p]),
+    "lss_depthnet_lift": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p]),
+    "lss_depthnet_lift_nhwc": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p]),
+    "lss_splat_fwd": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _p, _p, _p]),
     "lss_bev_rows": (ctypes.c_int, [_p, _i32, _p, _DIMS, _GRID, _p, _p]),
     "lss_splat_bwd": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p, _i32, _DIMS, _GRID, _p, _i32, _p]),
     "lss_splat_bwd_lifted": (ctypes.c_int, [_p, _i32, _i32, _p, _i32, _DIMS, _GRID, _p, _p]),

@@ -66,8 +66,8 @@ int lss_ceiling_store(void* dst, size_t bytes, int32_t per_thread, int32_t flavo
 int lss_ceiling_read(const void* src, size_t bytes, void* sink, lss_stream_t stream) {
     if (!src || (bytes & 15) || ((uintptr_t)src & 15)) return LSS_EINVAL;
     int dev = 0, cus = 256;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
     hipLaunchKernelGGL(k_ceiling_read, dim3(cus * 8), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src,
                        (long)(bytes / 16), (unsigned*)sink);
     return (int)hipGetLastError();

@@ -78,6 +78,11 @@ __device__ __forceinline__ float wave_sum(float v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
     return v;
 }
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
 __device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, kWave));
@@ -104,11 +109,8 @@ __device__ unsigned long long g_lss_trace[16384][5];
 // each other with the same mapping hand data over through the same XCD's L2: the lift writes a
 // sample's context rows / depth weights, the CSR build its keys, the scan its cell starts, from the
 // XCD whose splat blocks read them. The grid must be xcd_grid(nb) blocks; logical ids >= nb idle.
-#ifndef LSS_XCD_MAP
-#define LSS_XCD_MAP 1  // 0: plain block order everywhere (timing comparisons)
-#endif
 __device__ __forceinline__ int xcd_block() {
-    return LSS_XCD_MAP ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    return (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
 }
 inline int xcd_grid(long nb) { return (int)(8 * ((nb + 7) / 8)); }
 
@@ -161,30 +163,6 @@ __device__ __forceinline__ float dot3_seq(float m0, float m1, float m2, float v0
     return __fadd_rn(acc, __fmul_rn(m2, v2));
 }
 
-// ----------------------------------------------------------------------------- camera inverse
-__global__ __launch_bounds__(kBlock) void k_camera_inverse(const float* __restrict__ post_rots,
-                                                           const float* __restrict__ intrins, int n_cams,
-                                                           float* __restrict__ pinv, float* __restrict__ kinv) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= 2 * n_cams) return;
-    const float* M = i < n_cams ? post_rots + 9 * i : intrins + 9 * (i - n_cams);
-    float* O = i < n_cams ? pinv + 9 * i : kinv + 9 * (i - n_cams);
-    double a[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) a[k] = (double)M[k];
-    const double c00 = a[4] * a[8] - a[5] * a[7];
-    const double c01 = a[5] * a[6] - a[3] * a[8];
-    const double c02 = a[3] * a[7] - a[4] * a[6];
-    const double det = a[0] * c00 + a[1] * c01 + a[2] * c02;
-    const double inv[9] = {
-        c00, a[2] * a[7] - a[1] * a[8], a[1] * a[5] - a[2] * a[4],
-        c01, a[0] * a[8] - a[2] * a[6], a[2] * a[3] - a[0] * a[5],
-        c02, a[1] * a[6] - a[0] * a[7], a[0] * a[4] - a[1] * a[3],
-    };
-#pragma unroll
-    for (int k = 0; k < 9; ++k) O[k] = (float)(inv[k] / det);
-}
-
 // ----------------------------------------------------------------------------- geometry -> cells
 __device__ __forceinline__ int quantize_cell(float ex, float ey, float ez, const lss_grid_t& g, int b) {
     // ((geom - (bx - dx/2)) / dx).long() + bounds filter (src/models.py:212-223).
@@ -199,13 +177,7 @@ __device__ __forceinline__ int quantize_cell(float ex, float ey, float ez, const
     return ((b * g.nx[2] + iz) * g.nx[0] + ix) * g.nx[1] + iy;
 }
 
-#ifndef LSS_GEOM_AGG
-#define LSS_GEOM_AGG 3  // 3: one atomic per distinct cell of a block (LDS hash), 1: of a wave (ballots), 0: per point
-#endif
-#ifndef LSS_GEO_BLOCK
-#define LSS_GEO_BLOCK 256  // threads (points) per block of the geometry / cell kernels
-#endif
-constexpr int kGeoBlock = LSS_GEO_BLOCK;
+constexpr int kGeoBlock = 256;  // threads (points) per block of the geometry / cell kernels
 constexpr int kGeoHashBits = kGeoBlock <= 256 ? 9 : kGeoBlock <= 512 ? 10 : 11;
 constexpr int kGeoHash = 1 << kGeoHashBits;  // >= 2 entries per point of the block: short probe chains
 static_assert(kGeoHash >= 2 * kGeoBlock, "hash table at most half full");
@@ -216,38 +188,21 @@ struct GeoHash {
     int cnt[kGeoHash];
 };
 
-// LSS_GEOM_AGG 3: slots grouped per block. Every kept point inserts its cell into the block's LDS
-// table (multiplicative hash, linear probing) and takes a rank among the block's points of that cell
-// from an LDS atomic; then ONE returning device atomic per distinct cell of the block adds the
-// group's size to the count, and a point's slot is that old count plus its rank. At c3 a block of 256
-// points holds 67 k distinct (block, cell) pairs in all against 141 k (wave, cell) pairs; at c5 171 k
-// against 535 k -- and the device atomics, executed at the memory side, are what the kernel waits on.
+// Slots grouped per block. Every kept point inserts its cell into the block's LDS table
+// (multiplicative hash, linear probing) and takes a rank among the block's points of that cell from an
+// LDS atomic; then ONE returning device atomic per distinct cell of the block adds the group's size to
+// the count, and a point's slot is that old count plus its rank (arrival order; k_csr_canon fixes the
+// order later). At c3 a block of 256 points holds 67 k distinct (block, cell) pairs in all against
+// 141 k (wave, cell) pairs; at c5 171 k against 535 k -- and the device atomics, executed at the memory
+// side, are what the kernel waits on (per-wave groups: 11.8 vs 7.3 us at c3, profiles/r02).
 // Must be called by every thread of the block (cell = -1 for dropped / out-of-range points).
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
-}
-
-// agg (nullable): the counts are also summed per group of kScanItems cells into agg[cell / kScanItems]
-// (the block's groups -- one or two -- first in a small LDS table, then one atomic each), so the scan
-// reads every block's prefix directly (k_scan_agg) instead of looking back.
-constexpr int kGeoGroups = 16;
-constexpr int kAggRep = 16;  // replicas of every group sum (agg[g * kAggRep + block % kAggRep]): device
-                             // atomics on one address serialise at the memory side
-template <bool AGG = false>
 __device__ __forceinline__ void emit_cell_block(int p, int cell, int32_t* cell_of, int32_t* cell_count,
-                                                int32_t* slot_of, bool live, GeoHash& h, int32_t* agg = nullptr) {
+                                                int32_t* slot_of, bool live, GeoHash& h) {
     if (live) cell_of[p] = cell;
     if (cell_count == nullptr) return;  // block-uniform
-    __shared__ int s_gkey[kGeoGroups], s_gval[kGeoGroups];
     for (int i = threadIdx.x; i < kGeoHash; i += kGeoBlock) {
         h.key[i] = -1;
         h.cnt[i] = 0;
-    }
-    if (AGG && threadIdx.x < kGeoGroups) {
-        s_gkey[threadIdx.x] = -1;
-        s_gval[threadIdx.x] = 0;
     }
     __syncthreads();
     const bool kept = live && cell >= 0;
@@ -262,91 +217,12 @@ __device__ __forceinline__ void emit_cell_block(int p, int cell, int32_t* cell_o
         rank = atomicAdd(&h.cnt[at], 1);
     }
     __syncthreads();
-    // (every thread runs the same number of iterations: the group sums below use wave-wide ballots)
     for (int i = threadIdx.x; i < kGeoHash; i += kGeoBlock) {
         const int c = h.key[i];
-        const int n = c >= 0 ? h.cnt[i] : 0;
-        if (c >= 0) h.cnt[i] = atomicAdd(cell_count + c, n);
-        if (AGG) {
-            // per wave: one sum per distinct group (usually one), then one LDS atomic by its leader
-            const int gk = c >= 0 ? c / kScanItems : -1;
-            unsigned long long rem = __ballot(c >= 0);
-            while (rem) {
-                const int l0 = __builtin_ctzll(rem);
-                const int g0 = __builtin_amdgcn_readlane(gk, l0);
-                const unsigned long long peers = __ballot(gk == g0) & rem;
-                rem &= ~peers;
-                const int sum = wave_sum_i(((peers >> (threadIdx.x & 63)) & 1ull) ? n : 0);
-                if ((int)(threadIdx.x & 63) == l0) {
-                    int at2 = g0 & (kGeoGroups - 1), probes = 0;
-                    for (; probes < kGeoGroups; ++probes) {
-                        const int prev = atomicCAS(&s_gkey[at2], -1, g0);
-                        if (prev == -1 || prev == g0) break;
-                        at2 = (at2 + 1) & (kGeoGroups - 1);
-                    }
-                    if (probes < kGeoGroups) atomicAdd(&s_gval[at2], sum);
-                    else atomicAdd(agg + g0 * kAggRep + (blockIdx.x % kAggRep), sum);  // (table full)
-                }
-            }
-        }
+        if (c >= 0) h.cnt[i] = atomicAdd(cell_count + c, h.cnt[i]);
     }
     __syncthreads();
-    if (AGG && threadIdx.x < kGeoGroups && s_gkey[threadIdx.x] >= 0)
-        atomicAdd(agg + s_gkey[threadIdx.x] * kAggRep + (blockIdx.x % kAggRep), s_gval[threadIdx.x]);
     if (live) slot_of[p] = kept ? h.cnt[at] + rank : -1;
-}
-
-// Slot of point p inside its cell (arrival order; k_csr_canon fixes the order later). Atomics on
-// the counts execute at the memory side, so a wave first groups its lanes by cell (a ballot per
-// distinct cell, no memory traffic), then ONE atomic instruction adds each group's size from its
-// leader lane; a lane's slot is its leader's old count plus its rank in the group.
-// Must be called by every lane of the wave (cell = -1 for dropped / out-of-range points).
-__device__ __forceinline__ void emit_cell(int p, int cell, int32_t* cell_of, int32_t* cell_count, int32_t* slot_of,
-                                          bool live = true) {
-    if (live) cell_of[p] = cell;
-    if (cell_count == nullptr) return;
-    if (!LSS_GEOM_AGG) {
-        int slot = -1;
-        if (live && cell >= 0) slot = atomicAdd(cell_count + cell, 1);
-        if (live) slot_of[p] = slot;
-        return;
-    }
-    const int lane = threadIdx.x & 63;
-    if (LSS_GEOM_AGG == 2) {
-        // runs of equal cells in adjacent lanes (neighbouring pixels at one depth mostly share a cell):
-        // one atomic per run from its first lane; the bit operations replace the per-cell ballot loop
-        const bool kept = live && cell >= 0;
-        const int up = __shfl(cell, (lane + 63) & 63, kWave);
-        const unsigned long long keptm = __ballot(kept);
-        const unsigned long long starts = __ballot(kept && (lane == 0 || up != cell || !((keptm >> (lane - 1)) & 1ull)));
-        const unsigned long long below = starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-        const int lead = below ? 63 - __builtin_clzll(below) : lane;
-        const unsigned long long after = lead == 63 ? 0ull : (~0ull << (lead + 1));
-        const unsigned long long nxt = (starts | ~keptm) & after;  // next run start or dropped lane
-        const int stop = nxt ? __builtin_ctzll(nxt) : 64;
-        int base = 0;
-        if (kept && lead == lane) base = atomicAdd(cell_count + cell, stop - lane);
-        base = __shfl(base, lead, kWave);
-        if (live) slot_of[p] = kept ? base + (lane - lead) : -1;
-        return;
-    }
-    unsigned long long rem = __ballot(live && cell >= 0);
-    int leader = -1, rank = 0, size = 0;
-    while (rem) {
-        const int l0 = __builtin_ctzll(rem);
-        const int c = __builtin_amdgcn_readlane(cell, l0);
-        const unsigned long long peers = __ballot(cell == c) & rem;
-        rem &= ~peers;
-        if ((peers >> lane) & 1ull) {
-            leader = l0;
-            rank = __builtin_popcountll(peers & ((1ull << lane) - 1));
-            size = __builtin_popcountll(peers);
-        }
-    }
-    int base = 0;
-    if (leader == lane) base = atomicAdd(cell_count + cell, size);
-    base = __shfl(base, leader < 0 ? lane : leader, kWave);
-    if (live) slot_of[p] = leader < 0 ? -1 : base + rank;
 }
 
 // One frustum point through one camera (src/models.py:172-190), fp32, each op rounded in the
@@ -378,18 +254,11 @@ __device__ __forceinline__ void geometry_point(const float* __restrict__ frustum
     }
 }
 
-// AXES: the frustum given as its three axes -- xs[W], ys[H], ds[D] -- instead of the (D, H, W, 3)
-// tensor: create_frustum builds it as the broadcast of exactly these 1-D tensors (src/models.py:
-// 157-168), so point (d, h, w) = (xs[w], ys[h], ds[d]) bit for bit; 71 floats read through the
-// caches instead of 12 B per point from HBM.
-template <bool AXES, bool AGG = false>  // AGG: also the per-group count sums (lss_plan_ws)
 __global__ __launch_bounds__(kGeoBlock) void k_geometry_cells(
     const float* __restrict__ frustum, const float* __restrict__ rots, const float* __restrict__ trans,
     const float* __restrict__ kinv, const float* __restrict__ pinv, const float* __restrict__ post_trans,
-    int N, int DHW, int HW, int W, int nprime, lss_grid_t g, float* __restrict__ out_geom,
-    int32_t* __restrict__ cell_of, int32_t* __restrict__ cell_count, int32_t* __restrict__ slot_of,
-    int32_t* __restrict__ agg = nullptr) {
-    LSS_STAMP(blockIdx.x * (kGeoBlock / kWave) + (threadIdx.x >> 6), 0);
+    int N, int DHW, int nprime, lss_grid_t g, float* __restrict__ out_geom,
+    int32_t* __restrict__ cell_of, int32_t* __restrict__ cell_count, int32_t* __restrict__ slot_of) {
     const int p0 = blockIdx.x * kGeoBlock + threadIdx.x;
     const bool live = p0 < nprime;
     const int p = live ? p0 : nprime - 1;  // dead lanes recompute the last point, then write nothing
@@ -397,32 +266,15 @@ __global__ __launch_bounds__(kGeoBlock) void k_geometry_cells(
     const int f = p - cam * DHW;
     const int b = cam / N;
     float e[3];
-    if (AXES) {
-        const int d = f / HW, r = f - d * HW, h = r / W, w = r - h * W;
-        const float* xs = frustum;
-        const float* ys = frustum + W;
-        const float* ds = ys + HW / W;
-        const float fr[3] = {xs[w], ys[h], ds[d]};
-        geometry_point(fr, rots, trans, kinv, pinv, post_trans, cam, 0, e);
-    } else {
-        geometry_point(frustum, rots, trans, kinv, pinv, post_trans, cam, f, e);
-    }
+    geometry_point(frustum, rots, trans, kinv, pinv, post_trans, cam, f, e);
     if (out_geom != nullptr && live) {
         out_geom[3 * (size_t)p + 0] = e[0];
         out_geom[3 * (size_t)p + 1] = e[1];
         out_geom[3 * (size_t)p + 2] = e[2];
     }
-    [[maybe_unused]] const int tslot = blockIdx.x * (kGeoBlock / kWave) + (threadIdx.x >> 6);  // LSS_TRACE builds
-    LSS_STAMP(tslot, 1);
     const int cell = live ? quantize_cell(e[0], e[1], e[2], g, b) : -1;
-    LSS_STAMP(tslot, 2);
-    if (LSS_GEOM_AGG == 3) {
-        __shared__ GeoHash hash;
-        emit_cell_block<AGG>(p, cell, cell_of, cell_count, slot_of, live, hash, agg);
-    } else {
-        emit_cell(p, cell, cell_of, cell_count, slot_of, live);
-    }
-    LSS_STAMP(tslot, 3);
+    __shared__ GeoHash hash;
+    emit_cell_block(p, cell, cell_of, cell_count, slot_of, live, hash);
 }
 
 __global__ __launch_bounds__(kGeoBlock) void k_cells_from_geom(const float* __restrict__ geom, int nprime, int ppb,
@@ -434,12 +286,8 @@ __global__ __launch_bounds__(kGeoBlock) void k_cells_from_geom(const float* __re
     const int p = live ? p0 : nprime - 1;  // dead lanes stay for the block barriers, write nothing
     const int cell =
         live ? quantize_cell(geom[3 * (size_t)p], geom[3 * (size_t)p + 1], geom[3 * (size_t)p + 2], g, p / ppb) : -1;
-    if (LSS_GEOM_AGG == 3) {
-        __shared__ GeoHash hash;
-        emit_cell_block(p, cell, cell_of, cell_count, slot_of, live, hash);
-    } else {
-        emit_cell(p, cell, cell_of, cell_count, slot_of, live);
-    }
+    __shared__ GeoHash hash;
+    emit_cell_block(p, cell, cell_of, cell_count, slot_of, live, hash);
 }
 
 // ----------------------------------------------------------------------------- CSR (counting sort)
@@ -555,11 +403,8 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ 
 // timeout only costs time; the sticky timeout word counts them. The scatter re-zeroes the ticket and
 // the granules after the scan, so every call starts from zeros.
 constexpr unsigned kScanSpinLimit = 1u << 22;
-#ifndef LSS_SCAN_TICKET
-#define LSS_SCAN_TICKET 0  // 1: logical index from a ticket counter (one more atomic round trip)
-#endif
-struct ScanWs {  // lss_csr_workspace_bytes: [ticket, timeouts, spin_limit_override, pad][granule x nb]
-    unsigned ticket, timeouts;
+struct ScanWs {  // lss_csr_workspace_bytes: [unused, timeouts, spin_limit_override, pad][granule x nb]
+    unsigned unused, timeouts;
     unsigned spin_override;  // 0: kScanSpinLimit polls; s > 0: s - 1 polls (tests of the timeout path)
     unsigned pad;
 };
@@ -598,16 +443,8 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
     unsigned long long* gran = reinterpret_cast<unsigned long long*>(ws + 1);
     // Logical index = blockIdx: workgroups of a launch are dispatched in index order, so block k only
     // waits for blocks that were dispatched before it (at worst delayed while another kernel holds
-    // their XCD's CUs). LSS_SCAN_TICKET=1 takes the index from a ticket counter instead.
-    LSS_STAMP(blockIdx.x * 16 + (threadIdx.x >> 6), 0);
-    int lb = blockIdx.x;
-    if (LSS_SCAN_TICKET) {
-        __shared__ int s_blk;
-        if (threadIdx.x == 0) s_blk = (int)atomicAdd(&ws->ticket, 1u);
-        __syncthreads();
-        lb = s_blk;
-    }
-    LSS_STAMP(blockIdx.x * 16 + (threadIdx.x >> 6), 1);
+    // their XCD's CUs).
+    const int lb = blockIdx.x;
     const int nb = (ncells + kScanItems - 1) / kScanItems;
     const int base = lb * kScanItems + threadIdx.x * 4;
     // 16-byte count loads / cell_start stores when both arrays allow it (uniform over the launch)
@@ -622,7 +459,6 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
         if (base + 3 < ncells) c4.w = cnt[base + 3];
     }
     const int excl = block_exclusive_scan_1024(c4.x + c4.y + c4.z + c4.w, s_wave, &s_total);
-    LSS_STAMP(blockIdx.x * 16 + (threadIdx.x >> 6), 2);
     if (threadIdx.x < kWave) {
         const int lane = threadIdx.x;
         const int agg = s_total;
@@ -679,72 +515,23 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
         if (base + 3 < ncells) cell_start[base + 3] = o4.w;
     }
     if (lb == nb - 1 && threadIdx.x == 0) cell_start[ncells] = s_prefix + s_total;
-    LSS_STAMP(blockIdx.x * 16 + (threadIdx.x >> 6), 3);
 }
 
-// ---- scan from per-group aggregates (lss_plan_ws): the geometry summed the counts of every group of
-// kScanItems cells into agg[], so block lb's prefix is agg[0] + ... + agg[lb - 1] -- read in the same
-// round trip as its counts, no look-back, no waiting on other blocks.
-__global__ __launch_bounds__(1024) void k_scan_agg(const int32_t* __restrict__ cnt, int ncells,
-                                                   const int32_t* __restrict__ agg, int32_t* __restrict__ cell_start) {
-    __shared__ int s_wave[32];
-    __shared__ int s_total;
-    __shared__ int s_red[16];
-    const int lb = blockIdx.x;
-    const int nb = (ncells + kScanItems - 1) / kScanItems;
-    const int base = lb * kScanItems + threadIdx.x * 4;
-    const bool vec = ((reinterpret_cast<uintptr_t>(cnt) | reinterpret_cast<uintptr_t>(cell_start)) & 15) == 0;
-    int4 c4 = make_int4(0, 0, 0, 0);
-    if (vec && base + 4 <= ncells) {
-        c4 = *reinterpret_cast<const int4*>(cnt + base);
-    } else if (base < ncells) {
-        c4.x = cnt[base];
-        if (base + 1 < ncells) c4.y = cnt[base + 1];
-        if (base + 2 < ncells) c4.z = cnt[base + 2];
-        if (base + 3 < ncells) c4.w = cnt[base + 3];
-    }
-    int pre = 0;
-    for (int i = threadIdx.x; i < lb * kAggRep; i += 1024) pre += agg[i];
-    pre = wave_sum_i(pre);
-    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = pre;
-    const int excl = block_exclusive_scan_1024(c4.x + c4.y + c4.z + c4.w, s_wave, &s_total);  // (barriers)
-    int prefix = 0;
-#pragma unroll
-    for (int w = 0; w < 16; ++w) prefix += s_red[w];
-    const int r0 = prefix + excl;
-    const int4 o4 = make_int4(r0, r0 + c4.x, r0 + c4.x + c4.y, r0 + c4.x + c4.y + c4.z);
-    if (vec && base + 4 <= ncells) {
-        *reinterpret_cast<int4*>(cell_start + base) = o4;
-    } else if (base < ncells) {
-        cell_start[base] = o4.x;
-        if (base + 1 < ncells) cell_start[base + 1] = o4.y;
-        if (base + 2 < ncells) cell_start[base + 2] = o4.z;
-        if (base + 3 < ncells) cell_start[base + 3] = o4.w;
-    }
-    if (lb == nb - 1 && threadIdx.x == 0) cell_start[ncells] = prefix + s_total;
-}
-
-// k_scatter plus the reset for the next call: the scan's ticket and granules and the cell counts
-// (nothing reads them after the scan). The grid covers max(nprime, ncells) threads.
-// tail: key_out is the final CSR (no k_csr_canon after this: arrival order inside a cell), so the
-// scatter also writes its sentinel tail (key -1 at entries [cell_start[ncells], nprime)).
+// k_scatter plus the reset for the next call: the scan's granules and the cell counts (nothing reads
+// them after the scan). The grid covers max(nprime, ncells) threads.
 __global__ __launch_bounds__(kBlock) void k_scatter_ws(const int32_t* __restrict__ cell_of,
                                                        const int32_t* __restrict__ slot_of, int nprime,
                                                        const int32_t* __restrict__ cell_start,
                                                        long long* __restrict__ key_out, int32_t* __restrict__ cnt,
-                                                       int ncells, ScanWs* __restrict__ ws, int tail,
-                                                       int32_t* __restrict__ agg = nullptr) {
+                                                       int ncells, ScanWs* __restrict__ ws) {
     const int t = blockIdx.x * kBlock + threadIdx.x;
     if (t < nprime) {
         const int cell = cell_of[t];
         if (cell >= 0) key_out[scatter_pos(cell, slot_of[t], cell_start, nprime)] = ((long long)cell << 32) | (unsigned)t;
-        if (tail && t >= cell_start[ncells]) key_out[t] = -1ll;
     }
     if (t < ncells) cnt[t] = 0;
     const int nb = (ncells + kScanItems - 1) / kScanItems;
     if (t < nb) reinterpret_cast<unsigned long long*>(ws + 1)[t] = 0ull;
-    if (agg != nullptr && t < nb * kAggRep) agg[t] = 0;
-    if (t == 0) ws->ticket = 0u;
 }
 
 // The sorted list is cut into 64-entry chunks; the wave of chunk w owns the cells that START
@@ -793,10 +580,6 @@ __device__ __forceinline__ int point_row(int p, int DHW, int HW) {
     return cam * HW + (p - cam * DHW) % HW;  // pixel of point p = its context row
 }
 
-#ifndef LSS_CANON_LDS
-#define LSS_CANON_LDS 1  // k_csr_canon ranks: 1 per-lane scan of its own cell in LDS, 0 wave-wide readlane loop
-#endif
-
 // Canonical CSR order: inside every cell the entries are sorted by point id (so every later
 // reduction over a cell is deterministic without sorting again), and each entry's context-row
 // index (its pixel) is stored beside it. One wave per 64-entry chunk, cells owned as above.
@@ -804,9 +587,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
                                                       const int32_t* __restrict__ total_ptr, int nchunks, int nprime,
                                                       int DHW,
                                                       int HW, long long* __restrict__ key_out,
-                                                      int32_t* __restrict__ row_out,
-                                                      const int32_t* __restrict__ cell_of,
-                                                      int32_t* __restrict__ pos_out) {
+                                                      int32_t* __restrict__ row_out) {
     const int lane = threadIdx.x & 63;
     const int w = xcd_block() * (kBlock / kWave) + uniform(threadIdx.x >> 6);
     if (w >= nchunks) return;
@@ -822,11 +603,8 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
     int prev_at = max(base - 1, 0);
     asm("" : "+v"(prev_at));  // a vector load issued with the others, not a scalar one sunk past the stores
     const long long kpr = key_in[prev_at];
-    const int cofe = pos_out ? cell_of[min(e0, nprime - 1)] : 0;
     // sentinel tail: entries [total, nprime) hold key -1 (cell -1), so a reader needs no entry count
     if (e0 >= total && e0 < nprime) key_out[e0] = -1ll;
-    // sorted position of every point (pos_out[p], -1 = dropped): dropped points here, kept ones below
-    if (pos_out && e0 < nprime && cofe < 0) pos_out[e0] = -1;
     if (base >= total) return;
     const long long k0 = e0 < total ? k0r : -1ll;
     const long long k1 = e1 < total ? k1r : -1ll;
@@ -845,43 +623,32 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
     const int cs0 = base + 63 - __builtin_clzll((st0 & le) | 1ull);  // bit 0 guard: owned entries have a start
     const int cs1 = (st1 & le) ? base + kWave + 63 - __builtin_clzll(st1 & le)
                                : base + 63 - __builtin_clzll(st0 | 1ull);
+    // rank inside the cell from the window's point ids staged in LDS: each lane scans only its own
+    // cell's run [cell start, next start) -- at most 64 entries, 8.5 on average at c3
     int r0 = 0, r1 = 0;
-    if (LSS_CANON_LDS) {
-        // rank inside the cell from the window's point ids staged in LDS: each lane scans only its
-        // own cell's run [cell start, next start) -- at most 64 entries, 8.5 on average at c3 --
-        // instead of every owned entry of the chunk through cross-lane reads
-        __shared__ int s_pid[kBlock / kWave][2 * kWave];
-        int* sp = s_pid[threadIdx.x >> 6];
-        sp[lane] = p0;
-        sp[kWave + lane] = p1;
-        __builtin_amdgcn_wave_barrier();
-        const int lim = cc.end - base;
-        const unsigned long long after = lane == 63 ? 0ull : (~0ull << (lane + 1));
-        const unsigned long long n0 = st0 & after, n1 = st1 & after;
-        const int ce0 = min(n0 ? (int)__builtin_ctzll(n0) : (st1 ? kWave + (int)__builtin_ctzll(st1) : 2 * kWave), lim);
-        const int ce1 = min(n1 ? kWave + (int)__builtin_ctzll(n1) : 2 * kWave, lim);
-        if (e0 >= cc.s && e0 < cc.end)
-            for (int j = cs0 - base; j < ce0; ++j) r0 += sp[j] < p0 ? 1 : 0;
-        if (e1 >= cc.s && e1 < cc.end)
-            for (int j = cs1 - base; j < ce1; ++j) r1 += sp[j] < p1 ? 1 : 0;
-    } else {
-        for (int j = cc.s; j < cc.end; ++j) {
-            const int cj = pick(c0, c1, j - base), pj = pick(p0, p1, j - base);
-            r0 += (cj == c0 && pj < p0) ? 1 : 0;
-            r1 += (cj == c1 && pj < p1) ? 1 : 0;
-        }
-    }
+    __shared__ int s_pid[kBlock / kWave][2 * kWave];
+    int* sp = s_pid[threadIdx.x >> 6];
+    sp[lane] = p0;
+    sp[kWave + lane] = p1;
+    __builtin_amdgcn_wave_barrier();
+    const int lim = cc.end - base;
+    const unsigned long long after = lane == 63 ? 0ull : (~0ull << (lane + 1));
+    const unsigned long long n0 = st0 & after, n1 = st1 & after;
+    const int ce0 = min(n0 ? (int)__builtin_ctzll(n0) : (st1 ? kWave + (int)__builtin_ctzll(st1) : 2 * kWave), lim);
+    const int ce1 = min(n1 ? kWave + (int)__builtin_ctzll(n1) : 2 * kWave, lim);
+    if (e0 >= cc.s && e0 < cc.end)
+        for (int j = cs0 - base; j < ce0; ++j) r0 += sp[j] < p0 ? 1 : 0;
+    if (e1 >= cc.s && e1 < cc.end)
+        for (int j = cs1 - base; j < ce1; ++j) r1 += sp[j] < p1 ? 1 : 0;
     if (e0 >= cc.s && e0 < cc.end) {
         const int at = dchk(cs0 + r0, total, kDbgCanonPos);
         key_out[at] = k0;
         row_out[at] = point_row(dchk(p0, nprime, kDbgSplatPoint), DHW, HW);
-        if (pos_out) pos_out[p0] = at;
     }
     if (e1 >= cc.s && e1 < cc.end) {
         const int at = dchk(cs1 + r1, total, kDbgCanonPos);
         key_out[at] = k1;
         row_out[at] = point_row(dchk(p1, nprime, kDbgSplatPoint), DHW, HW);
-        if (pos_out) pos_out[p1] = at;
     }
     if (cc.big_start >= 0) {
         // one cell with more than 64 entries: ordered selection straight from memory (rare)
@@ -899,7 +666,6 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
             if (lane == 0) {
                 key_out[cc.big_start + k] = ((long long)cell << 32) | (unsigned)best;
                 row_out[cc.big_start + k] = point_row(best, DHW, HW);
-                if (pos_out) pos_out[best] = cc.big_start + k;
             }
             last = best;
         }
@@ -921,8 +687,6 @@ __global__ __launch_bounds__(kBlock) void k_debug_csr(const int32_t* __restrict_
 struct BevGeo {
     int X, Y, Z;
     int ncells;
-    int dhw, hw;            // points per camera, pixels per camera (context row of point p)
-    float inv_dhw, inv_hw;  // their reciprocals (row_of_point; exact for p < 2^24)
     int nrows;              // feature rows (LSS_DEBUG bound of the gathered row index)
 };
 
@@ -940,43 +704,6 @@ __device__ __forceinline__ OutT* cell_row(OutT* out, int cell, const BevGeo& g) 
     return out + cell_row_offset(cell, g);
 }
 
-// Empty cells' BEV rows (channels-last, (B, X, Y, Z*C)) written as zeros, 64-cell units. The fill is
-// independent of the lift's data (it needs only cell_start), so the lift kernels run it in blocks of
-// their own on the CUs the lift leaves idle, and the splat then writes the occupied rows only
-// (lss_splat_fwd flag LSS_SPLAT_EMPTY_FILLED). Wave `w` of `nw` takes a contiguous run of units; all its
-// cell_start loads are issued before any store. Row bytes = 64 elements of `esize` bytes, 16-B
-// non-temporal stores.
-constexpr int kFillUnits = 8;  // units per wave per batch (their loads in flight together)
-__device__ void fill_empty_rows(int w, int nw, const int32_t* __restrict__ cell_start, const BevGeo& g,
-                                unsigned char* __restrict__ out, int esize, int lane) {
-    const int nunits = (g.ncells + kWave - 1) / kWave;
-    const int per = (nunits + nw - 1) / nw;
-    const int u_begin = w * per, u_end = min(nunits, u_begin + per);
-    const int lpr = kC * esize / 16, rps = kWave / lpr;  // lanes per row, rows per store instruction
-    for (int u0 = u_begin; u0 < u_end; u0 += kFillUnits) {
-        int a[kFillUnits], b[kFillUnits];
-#pragma unroll
-        for (int i = 0; i < kFillUnits; ++i) {  // clamped, unconditional: every load in flight at once
-            const int k = min((u0 + i) * kWave + lane, g.ncells - 1);
-            a[i] = cell_start[k];
-            b[i] = cell_start[k + 1];
-        }
-#pragma unroll
-        for (int i = 0; i < kFillUnits; ++i) {
-            const int u = u0 + i;
-            if (u >= u_end) break;  // wave-uniform
-            const unsigned long long em = __ballot(u * kWave + lane < g.ncells && a[i] == b[i]);
-            for (int r0 = 0; r0 < kWave; r0 += rps) {
-                const int r = r0 + lane / lpr;
-                if ((em >> r) & 1ull) {
-                    const size_t off = cell_row_offset(u * kWave + r, g) * esize + (lane % lpr) * 16;
-                    __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, reinterpret_cast<u32x4*>(out + off));
-                }
-            }
-        }
-    }
-}
-
 // ----------------------------------------------------------------------------- lift prep
 // One block = 64 consecutive pixels x 4 waves. Wave w owns depth bins d = w, w+4, ... and
 // context channels 16w..16w+15 of every pixel, so all of a thread's loads are issued back to
@@ -985,21 +712,10 @@ __device__ void fill_empty_rows(int w, int nw, const int32_t* __restrict__ cell_
 // pixel-major rows ctx_t[q*64 + c] (coalesced 256-B rows).
 template <typename InT, typename CT, int NI>  // NI = depth bins per wave part: D <= 4 * NI
 __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn, int D, int HW, int npix,
-                                                      float* __restrict__ depth, CT* __restrict__ ctx_t,
-                                                      const int32_t* __restrict__ pos_of,
-                                                      float* __restrict__ sorted_depth, int nlift_groups,
-                                                      int nfill_groups, const int32_t* __restrict__ cell_start,
-                                                      BevGeo bg, unsigned char* __restrict__ bev, int esize) {
+                                                      float* __restrict__ depth, CT* __restrict__ ctx_t) {
     __shared__ float s_ctx[kC][65];
     __shared__ float s_red[2][4][64];
-    const int gi = blockIdx.x >> 3, xcd = blockIdx.x & 7;  // as k_depthnet_lift2: lift groups, then fill groups
-    if (gi >= nlift_groups) {
-        const int fb = xcd * nfill_groups + (gi - nlift_groups);
-        fill_empty_rows(fb * (kBlock / kWave) + (int)(threadIdx.x >> 6), nfill_groups * 8 * (kBlock / kWave),
-                        cell_start, bg, bev, esize, threadIdx.x & 63);
-        return;
-    }
-    const int q0 = (xcd * nlift_groups + gi) * 64;
+    const int q0 = xcd_block() * 64;  // XCD x: one contiguous run of pixel tiles (the splat's CSR order)
     if (q0 >= npix) return;  // block-uniform
     const int px = threadIdx.x & 63, part = threadIdx.x >> 6;
     const int q = q0 + px;
@@ -1010,15 +726,10 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
     const int bn = qc / HW, hw = qc - bn * HW;
     const InT* src = dn + (size_t)bn * (D + kC) * HW + hw;
     float cv[16], l[NI];
-    int at[NI];
 #pragma unroll
     for (int i = 0; i < 16; ++i) cv[i] = to_f32(src[(size_t)(D + part * 16 + i) * HW]);
 #pragma unroll
     for (int i = 0; i < NI; ++i) l[i] = to_f32(src[(size_t)min(part + 4 * i, D - 1) * HW]);
-    if (pos_of) {
-#pragma unroll
-        for (int i = 0; i < NI; ++i) at[i] = pos_of[(bn * D + min(part + 4 * i, D - 1)) * HW + hw];
-    }
     float m = -INFINITY;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -1044,11 +755,7 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int d = part + 4 * i;
-            if (d < D) {
-                const float v = e[i] / sum;
-                dst[(size_t)d * HW] = v;
-                if (pos_of && at[i] >= 0) sorted_depth[at[i]] = v;  // the weight at its CSR position
-            }
+            if (d < D) dst[(size_t)d * HW] = e[i] / sum;
         }
     }
     for (int i = threadIdx.x; i < 64 * kC; i += kBlock) {
@@ -1057,13 +764,8 @@ __global__ __launch_bounds__(kBlock) void k_lift_prep(const InT* __restrict__ dn
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_fill_empty(const int32_t* __restrict__ cell_start, BevGeo bg,
-                                                       unsigned char* __restrict__ bev, int esize) {
-    fill_empty_rows(blockIdx.x * (kBlock / kWave) + (int)(threadIdx.x >> 6), gridDim.x * (kBlock / kWave), cell_start,
-                    bg, bev, esize, threadIdx.x & 63);
-}
-
 // ----------------------------------------------------------------------------- depthnet + lift prep (fused)
+// General shapes (any K <= 512 with K % 16 == 0, any H*W; k_depthnet_lift2 / 3 take up1's K = 512).
 // CamEncode's depthnet 1x1 conv (K -> D + C channels, with bias) fused with the lift's first half
 // (src/models.py:47, 55-59): logits = W.x + b on MFMA (v_mfma_f32_32x32x16_bf16: bf16 in, fp32
 // accumulate), rounded to bf16 as the autocast conv's output is, then depth = softmax over the D
@@ -1078,9 +780,7 @@ constexpr int kDnMaxO = 128;  // D + C <= 4 waves x 32 output channels
 
 __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict__ feat, const bf16* __restrict__ weight,
                                                           const bf16* __restrict__ bias, int K, int D, int HW,
-                                                          int npix, float* __restrict__ depth, bf16* __restrict__ ctx_t,
-                                                          const int32_t* __restrict__ pos_of,
-                                                          float* __restrict__ sorted_depth) {
+                                                          int npix, float* __restrict__ depth, bf16* __restrict__ ctx_t) {
     using bf16x8 = __attribute__((ext_vector_type(8))) short;
     using f32x16 = __attribute__((ext_vector_type(16))) float;
     __shared__ __attribute__((aligned(16))) bf16 s_x[kDnPix][kDnMaxK + 8];  // [pixel][k]; +8: spread the banks
@@ -1177,14 +877,7 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
     if (q < npix) {
         const int bn = q / HW, hw = q - bn * HW;
         float* dst = depth + (size_t)bn * D * HW + hw;
-        for (int d = part; d < D; d += kParts) {
-            const float v = expf(s_lg[d][p] - m) / sum;
-            dst[(size_t)d * HW] = v;
-            if (pos_of) {
-                const int at = pos_of[(bn * D + d) * HW + hw];
-                if (at >= 0) sorted_depth[at] = v;
-            }
-        }
+        for (int d = part; d < D; d += kParts) dst[(size_t)d * HW] = expf(s_lg[d][p] - m) / sum;
     }
     // context rows: 64 consecutive channels of a pixel = one 128-B row
     for (int i = threadIdx.x; i < kDnPix * kC; i += kBlock) {
@@ -1201,33 +894,17 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
 // of it transposed by ds_read_b64_tr_b16 (gfx950: 4 rows x 16 columns of 16-bit elements, delivered
 // column-major), two per K step. Then logits + bias rounded to bf16 (the autocast conv's output), depth
 // softmax over the first D rows, context rows -- as k_depthnet_lift.
-#ifndef LSS_DN_PIX
-#define LSS_DN_PIX 48  // pixels per block: 48 -> 176 blocks at B=8 (32 -> 264 blocks, 8 CUs run two)
-#endif
-constexpr int kDn2Pix = LSS_DN_PIX;             // pixels per block (16-pixel MFMA column tiles)
+// pixels per block (16-pixel MFMA column tiles): 48 -> 176 blocks at B=8 (32 -> 264 blocks, 8 CUs run two)
+constexpr int kDn2Pix = 48;
 constexpr int kDn2Waves = 8;                   // 8 x 16 = 128 output rows >= D + C
 constexpr int kDn2Block = kDn2Waves * kWave;
-#ifndef LSS_DN_ROT
-#define LSS_DN_ROT 0  // 1: rotate the K-step order per block (spreads the weight requests; changes fp32 sum order)
-#endif
-#ifndef LSS_DN_SKIP
-#define LSS_DN_SKIP 0  // timing experiments only (wrong output): 1 skips the weight loads, 2 the feature loads
-#endif
-#ifndef LSS_DN_IMPL
-#define LSS_DN_IMPL 2  // 1: k_depthnet_lift (32x32x16, weights streamed from L2), 2: k_depthnet_lift2
-#endif
 
-template <int K, int PX, bool SD>  // input channels (compile-time: straight-line code, every load up front),
-                                   // pixels per block, SD: also write the weights in CSR order (pos_of)
+template <int K, int PX>  // input channels (compile-time: straight-line code, every load up front), pixels per block
 __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __restrict__ feat,
                                                               const bf16* __restrict__ weight,
                                                               const bf16* __restrict__ bias, int D, int HW,
                                                               int npix, float* __restrict__ depth,
-                                                              bf16* __restrict__ ctx_t,
-                                                              const int32_t* __restrict__ pos_of,
-                                                              float* __restrict__ sorted_depth, int nlift_groups,
-                                                              int nfill_groups, const int32_t* __restrict__ cell_start,
-                                                              BevGeo bg, unsigned char* __restrict__ bev, int esize) {
+                                                              bf16* __restrict__ ctx_t) {
     static_assert(K % 32 == 0 && K <= kDnMaxK, "K steps of 32 staged in LDS");
     static_assert(PX % 16 == 0, "16-pixel MFMA column tiles");
     constexpr int kRow = PX * 2 + 8;  // LDS bytes per channel row (+8: spread the banks, 8-B aligned)
@@ -1239,33 +916,13 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
     __shared__ float s_lg[kDnMaxO][PX + 1];                                  // bf16-rounded logits
     __shared__ float s_red[2][kDn2Block / PX][PX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // blocks come in groups of 8 (one per XCD): nlift_groups of lift blocks (XCD x takes a contiguous
-    // run of pixel tiles), then nfill_groups of blocks that zero the BEV rows of the empty cells
-    const int gi = blockIdx.x >> 3, xcd = blockIdx.x & 7;
-    if (gi >= nlift_groups) {
-        const int fb = xcd * nfill_groups + (gi - nlift_groups);
-        fill_empty_rows(fb * kDn2Waves + wave, nfill_groups * 8 * kDn2Waves, cell_start, bg, bev, esize, lane);
-        return;
-    }
-    const int q0 = (xcd * nlift_groups + gi) * PX;
+    const int q0 = xcd_block() * PX;  // XCD x takes a contiguous run of pixel tiles
     if (q0 >= npix) return;  // block-uniform
     const int O = D + kC;
-    [[maybe_unused]] const int tslot = blockIdx.x * kDn2Waves + wave;  // LSS_TRACE builds only
-    LSS_STAMP(tslot, 0);
-    // the CSR positions of this thread's softmax outputs (SD), in flight with everything else
     constexpr int kParts = kDn2Block / PX;  // threads past kParts * PX sit the softmax out
     constexpr int kPerPart = (64 + kParts - 1) / kParts;  // D <= 64 (D + C <= kDnMaxO)
     const int p = threadIdx.x % PX, part = threadIdx.x / PX;
     const bool sm = part < kParts;
-    int at[SD ? kPerPart : 1];
-    if (SD) {
-        const int qc = min(q0 + p, npix - 1), bnc = qc / HW, hwc = qc - bnc * HW;
-#pragma unroll
-        for (int i = 0; i < kPerPart; ++i) {
-            const int d = min(part + kParts * i, D - 1);
-            at[i] = pos_of[((size_t)bnc * D + d) * HW + hwc];
-        }
-    }
     // ---- loads: this wave's weight rows (A fragments) and the block's feature tile, all in flight
     const int arow = wave * 16 + (lane & 15);
     const int kq = 8 * (lane >> 4);  // k offset of the lane's 8 elements inside a 32-wide K step
@@ -1276,13 +933,8 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
     const int g = lane >> 4, c16 = lane & 15;
     const bf16* wrow = weight + (size_t)min(arow, O - 1) * K + kq;
     bf16x8 a[kSteps];
-    // LSS_DN_ROT: block b walks the K steps starting at b mod kSteps, so the blocks' weight requests
-    // are spread over the matrix instead of all hitting the same lines at once
-    const int rot = LSS_DN_ROT ? (int)(blockIdx.x % kSteps) : 0;
 #pragma unroll
-    for (int s = 0; s < kSteps; ++s)
-        a[s] = (LSS_DN_SKIP & 1) ? bf16x8{(short)lane, 1, 2, 3, 4, 5, 6, (short)s}
-                                 : *reinterpret_cast<const bf16x8*>(wrow + 32 * ((s + rot) & (kSteps - 1)));
+    for (int s = 0; s < kSteps; ++s) a[s] = *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
     float bv[4];  // the bias of this lane's 4 output rows, in flight with the rest
 #pragma unroll
     for (int i = 0; i < 4; ++i) bv[i] = __bfloat162float(bias[min(wave * 16 + 4 * g + i, O - 1)]);
@@ -1294,8 +946,7 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
         const int i = threadIdx.x + t * kDn2Block;
         const int k = i / (PX / 8), q = min(q0 + (i % (PX / 8)) * 8, npix - 8);
         const int bn = q / HW, hw = q - bn * HW;  // HW % 8 == 0: 8 pixels never straddle an image
-        fv[t] = (LSS_DN_SKIP & 2) ? make_uint4(k, q, t, 1u)
-                                  : *reinterpret_cast<const uint4*>(feat + ((size_t)bn * K + k) * HW + hw);
+        fv[t] = *reinterpret_cast<const uint4*>(feat + ((size_t)bn * K + k) * HW + hw);
     }
 #pragma unroll
     for (int t = 0; t < kFeatIt; ++t) {
@@ -1304,7 +955,6 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
         *reinterpret_cast<uint4*>(s_x + k * kRow + p8 * 2) = fv[t];
     }
     __syncthreads();
-    LSS_STAMP(tslot, 1);
     // ---- MFMA: two 16-pixel column tiles, K/32 steps; B fragments by transposed LDS reads
     f32x4 acc[kTiles];
 #pragma unroll
@@ -1316,8 +966,7 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
         for (int t = 0; t < kTiles; ++t) {
             // lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3 of a 4 x 16 block; lane c of
             // the group receives column c (pixel 16t + c), rows 0..3 (4 consecutive channels)
-            const int ss = (s + rot) & (kSteps - 1);
-            const unsigned char* base = s_x + (32 * ss + 8 * g + tq) * kRow + (16 * t + 4 * tp) * 2;
+            const unsigned char* base = s_x + (32 * s + 8 * g + tq) * kRow + (16 * t + 4 * tp) * 2;
             const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                 (__attribute__((address_space(3))) v4s*)(base));
             const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -1335,7 +984,6 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
             if (o < O) s_lg[o][16 * t + c16] = __bfloat162float(__float2bfloat16(acc[t][i] + bv[i]));
         }
     __syncthreads();
-    LSS_STAMP(tslot, 2);
     // ---- softmax over the D bins of each pixel: thread (part, p) covers bins part, part + 16, ...
     float m = -INFINITY;
     for (int d = part; sm && d < D; d += kParts) m = fmaxf(m, s_lg[d][p]);
@@ -1358,18 +1006,13 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
 #pragma unroll
         for (int i = 0; i < kPerPart; ++i) {
             const int d = part + kParts * i;
-            if (d < D) {
-                const float v = expf(s_lg[d][p] - m) / sum;
-                dst[(size_t)d * HW] = v;
-                if (SD && at[SD ? i : 0] >= 0) sorted_depth[at[SD ? i : 0]] = v;  // the weight at its CSR position
-            }
+            if (d < D) dst[(size_t)d * HW] = expf(s_lg[d][p] - m) / sum;
         }
     }
     for (int i = threadIdx.x; i < PX * kC; i += kDn2Block) {
         const int pp = i / kC, c = i - pp * kC;
         if (q0 + pp < npix) ctx_t[(size_t)(q0 + pp) * kC + c] = __float2bfloat16(s_lg[D + c][pp]);
     }
-    LSS_STAMP(tslot, 3);
 }
 
 // ---- depthnet + lift, version 3: pixel-major (channels-last) features, one block per CU.
@@ -1382,30 +1025,21 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
 // block reads (from L2). The tile is staged in LDS as [pixel][k] (row stride K*2 + 16 B: the 16 rows
 // of a B fragment fall on different banks) and the B fragments (8 channels of one pixel per lane) are
 // plain 16-B LDS reads. Rows past the tile's pixel count are clamped copies of its last row and only
-// feed output columns that are never written. A fragments, epilogue (bias, bf16 rounding, softmax,
-// context rows) and the empty-row fill role as k_depthnet_lift2; identical results.
+// feed output columns that are never written. A fragments and epilogue (bias, bf16 rounding, softmax,
+// context rows) as k_depthnet_lift2; identical results.
 constexpr int kDn3Waves = 8;             // 8 x 16 = 128 output rows >= D + C
 constexpr int kDn3Block = kDn3Waves * kWave;
 constexpr int kDn3MaxPix = 48;           // pixels per block at most: three 16-column MFMA tiles
-#ifndef LSS_DN3_PIX
-#define LSS_DN3_PIX 0  // pixels per block of k_depthnet_lift3: 0 one block per CU (at most 48 pixels each), else this many
-#endif
+// K slices of k_depthnet_lift3's loads: slice 0 multiplied while the rest arrive (c3 in-step 11.3 -> 10.9 us;
+// 4 slices no better, profiles/r03/s3/trace_lift3_slices*.txt)
+constexpr int kDn3Slices = 2;
 
-#ifndef LSS_DN3_SLICES
-#define LSS_DN3_SLICES 2  // K slices of k_depthnet_lift3's loads: slice 0 multiplied while the rest arrive
-#endif
-
-template <int K, bool SD>
+template <int K>
 __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __restrict__ feat,
                                                               const bf16* __restrict__ weight,
                                                               const bf16* __restrict__ bias, int D, int HW,
-                                                              int npix, int nlift, int nlgrid,
-                                                              float* __restrict__ depth,
-                                                              bf16* __restrict__ ctx_t,
-                                                              const int32_t* __restrict__ pos_of,
-                                                              float* __restrict__ sorted_depth, int nfill,
-                                                              const int32_t* __restrict__ cell_start, BevGeo bg,
-                                                              unsigned char* __restrict__ bev, int esize) {
+                                                              int npix, int nlift, float* __restrict__ depth,
+                                                              bf16* __restrict__ ctx_t) {
     static_assert(K % 32 == 0 && K <= kDnMaxK, "K steps of 32");
     constexpr int PX = kDn3MaxPix;
     constexpr int kTiles = PX / 16;
@@ -1416,14 +1050,9 @@ __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __rest
     __shared__ float s_lg[kDnMaxO][PX + 1];                                // bf16-rounded logits
     __shared__ float s_red[2][kDn3Block / PX][PX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if ((int)blockIdx.x >= nlgrid) {  // block-uniform: the empty-row fill role
-        fill_empty_rows(((int)blockIdx.x - nlgrid) * kDn3Waves + wave, nfill * kDn3Waves, cell_start, bg, bev, esize,
-                        lane);
-        return;
-    }
     // XCD x takes one contiguous run of pixel tiles (c3: sample x), as the splat's chunk blocks take
     // the CSR: the context rows a splat gathers were written through its own XCD's L2
-    const int blk = LSS_XCD_MAP ? ((int)blockIdx.x & 7) * (nlgrid >> 3) + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
+    const int blk = xcd_block();
     if (blk >= nlift) return;
     // pixel tile [q0, q1): the pixels split as evenly as possible over the nlift blocks
     const int q0 = (int)(((long)npix * blk) / nlift), q1 = (int)(((long)npix * (blk + 1)) / nlift);
@@ -1435,21 +1064,12 @@ __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __rest
     constexpr int kPerPart = (64 + kParts - 1) / kParts;   // D <= 64 (D + C <= kDnMaxO)
     const int p = threadIdx.x % PX, part = threadIdx.x / PX;
     const bool sm = part < kParts;
-    int at[SD ? kPerPart : 1];
-    if (SD) {
-        const int qc = q0 + min(p, np - 1), bnc = qc / HW, hwc = qc - bnc * HW;
-#pragma unroll
-        for (int i = 0; i < kPerPart; ++i) {
-            const int d = min(part + kParts * i, D - 1);
-            at[i] = pos_of[((size_t)bnc * D + d) * HW + hwc];
-        }
-    }
     // ---- loads, all in flight together, in kParts K slices: slice h of the tile (channels
     // [h K/kParts, (h+1) K/kParts) of every pixel row, 16 B per thread and load), then this wave's
     // weight A fragments for the slice's K steps; then the bias values (clamped addresses, no
     // branches). Loads complete in order, so slice 0 is staged and multiplied while the later slices
     // are still arriving (the per-CU intake, ~161 KB at c3, is the stage's bound).
-    constexpr int kSlices = LSS_DN3_SLICES;
+    constexpr int kSlices = kDn3Slices;
     constexpr int kCPR = K * 2 / 16;                     // 16-B pieces per pixel row
     constexpr int kSCPR = kCPR / kSlices;                // ... per pixel row and slice
     constexpr int kSChunks = PX * kSCPR;                 // 16-B pieces of a slice
@@ -1473,13 +1093,10 @@ __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __rest
         for (int t = 0; t < kSIt; ++t) {
             const int i = threadIdx.x + t * kDn3Block;
             const int r = min(i / kSCPR, np - 1), c = h * kSCPR + i % kSCPR;
-            fv[h][t] = (LSS_DN_SKIP & 2) ? make_uint4(r, c, t, 1u)
-                                         : *reinterpret_cast<const uint4*>(tile + (size_t)r * K * 2 + c * 16);
+            fv[h][t] = *reinterpret_cast<const uint4*>(tile + (size_t)r * K * 2 + c * 16);
         }
 #pragma unroll
-        for (int s = h * kSSteps; s < (h + 1) * kSSteps; ++s)
-            a[s] = (LSS_DN_SKIP & 1) ? bf16x8{(short)lane, 1, 2, 3, 4, 5, 6, (short)s}
-                                     : *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
+        for (int s = h * kSSteps; s < (h + 1) * kSSteps; ++s) a[s] = *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
     }
     float bv[4];
 #pragma unroll
@@ -1547,11 +1164,7 @@ __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __rest
 #pragma unroll
         for (int i = 0; i < kPerPart; ++i) {
             const int d = part + kParts * i;
-            if (d < D) {
-                const float v = expf(s_lg[d][p] - m) / sum;
-                dst[(size_t)d * HW] = v;
-                if (SD && at[SD ? i : 0] >= 0) sorted_depth[at[SD ? i : 0]] = v;
-            }
+            if (d < D) dst[(size_t)d * HW] = expf(s_lg[d][p] - m) / sum;
         }
     }
     // context rows: the tile's np rows of 64 bf16 are one contiguous run; 8 channels per 16-B store
@@ -1584,37 +1197,9 @@ struct SplatGeo {
     int ncells, nprime, nrows;  // bounds of the data-derived indices (LSS_DEBUG checks): cells, points, feature rows
 };
 
-#ifndef LSS_PREFETCH
-#define LSS_PREFETCH 16
-#endif
-#ifndef LSS_YT_MAX
-#define LSS_YT_MAX 128
-#endif
-#ifndef LSS_MIN_WAVES
-#define LSS_MIN_WAVES 7  // occupancy floor of the channels-last splat (waves per SIMD; VGPR budget 512 / this)
-#endif
-#ifndef LSS_INTERLEAVE
-#define LSS_INTERLEAVE 0  // dispatch order of the block groups: 0 chunks first, 1 interleaved, 2 zero fill first, -1 by slots
-#endif
-#ifndef LSS_CHUNK_STOP
-#define LSS_CHUNK_STOP 0  // timing experiments only: chunk waves stop after round trip 1 (1) or 2 (2)
-#endif
-#ifndef LSS_NO_DEPTH
-#define LSS_NO_DEPTH 0  // timing experiments only: 1 skips the depth-weight gathers (wrong output)
-#endif
-#ifndef LSS_FWD_SKIP
-#define LSS_FWD_SKIP 0  // timing experiments only: 1 skips the chunks, 2 the zero fill (wrong output)
-#endif
-constexpr int kMaxYT = LSS_YT_MAX > 128 ? LSS_YT_MAX : 128;  // cells per NCHW tile (LDS sizing)
-constexpr int kFwdWaves = 8;           // waves per NCHW tile
-constexpr int kFwdBlock = kFwdWaves * kWave;
-constexpr int kPrefetch = LSS_PREFETCH;  // context-row loads in flight per wave
+constexpr int kYtMax = 128;  // cells per NCHW tile at most (LDS sizing)
 
 // 16-byte vector stores of 16/sizeof(T) elements.
-template <typename T> struct Vec;
-template <> struct Vec<float> { static constexpr int n = 4; };
-template <> struct Vec<bf16> { static constexpr int n = 8; };
-
 __device__ __forceinline__ void store_vec(float* dst, const float* src) {
     *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
 }
@@ -1625,44 +1210,8 @@ __device__ __forceinline__ void store_vec(bf16* dst, const float* src) {
                  __float2bfloat16(b.x), __float2bfloat16(b.y), __float2bfloat16(b.z), __float2bfloat16(b.w)};
     *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(v);
 }
-__device__ __forceinline__ void store_zero_vec(float* dst) { *reinterpret_cast<float4*>(dst) = make_float4(0.f, 0.f, 0.f, 0.f); }
-__device__ __forceinline__ void store_zero_vec(bf16* dst) { *reinterpret_cast<uint4*>(dst) = make_uint4(0u, 0u, 0u, 0u); }
 
-// Ordered reduction of canonical CSR entries [s, end) held in registers (entry base+l in lane l of
-// (key0, row0, w0), base+64+l in (key1, row1, w1)); lane = channel. `flush(cell, sum)` is called
-// once per cell, cells in order, points of a cell in ascending point id.
-template <typename RT, typename Flush>
-__device__ __forceinline__ void reduce_entries(int base, int s, int end, int c0, int c1, int row0, int row1, float w0,
-                                               float w1, const RT* __restrict__ rows_base, bool weighted,
-                                               int lane, Flush&& flush) {
-    float acc = 0.f;
-    int cur = s < end ? pick(c0, c1, s - base) : 0;
-    for (int k0 = s; k0 < end; k0 += kPrefetch) {
-        float v[kPrefetch];
-#pragma unroll
-        for (int u = 0; u < kPrefetch; ++u) {
-            const int k = min(k0 + u, end - 1) - base;
-            v[u] = to_f32(rows_base[(size_t)pick(row0, row1, k) * kC + lane]);
-        }
-#pragma unroll
-        for (int u = 0; u < kPrefetch; ++u) {
-            const int k = k0 + u;
-            if (k < end) {
-                const int c = pick(c0, c1, k - base);
-                if (c != cur) {
-                    flush(cur, acc);
-                    acc = 0.f;
-                    cur = c;
-                }
-                const float wk = __int_as_float(pick(__float_as_int(w0), __float_as_int(w1), k - base));
-                acc = weighted ? fmaf(wk, v[u], acc) : __fadd_rn(acc, v[u]);
-            }
-        }
-    }
-    if (s < end) flush(cur, acc);
-}
-
-// A cell with more than 64 entries, canonical order: streamed 64 at a time (rare).
+// A cell with more than 64 entries, canonical order: streamed 64 at a time (rare), lane = channel.
 template <bool FUSED, typename RT>
 __device__ float reduce_big_cell(int start, int nprime, const long long* __restrict__ key,
                                  const int32_t* __restrict__ row, const float* __restrict__ depth,
@@ -1687,125 +1236,6 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
     return acc;
 }
 
-// ---- NCHW (the reference layout): one block = one tile of YT consecutive cells (b, z, x, y0..)
-// of a BEV row, 8 waves; the tile's canonical entries are split over the waves at cell
-// boundaries; sums go to an LDS tile that is written transposed (channel-major) with 16-B
-// stores, zero rows included.
-__device__ __forceinline__ int tile_lower_bound(const int* s, int ny, int t, int lane) {
-    for (int base = 0; base <= ny; base += kWave) {
-        const int c = base + lane;
-        const unsigned long long hit = __ballot(c <= ny && s[min(c, ny)] >= t);
-        if (hit) return base + __builtin_ctzll(hit);
-    }
-    return ny;
-}
-
-template <bool FUSED, typename RT, typename OutT, bool NHWC>
-__global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict__ depth,
-                                                         const RT* __restrict__ rows_base,
-                                                         const int32_t* __restrict__ cell_start,
-                                                         const long long* __restrict__ sorted_key,
-                                                         const int32_t* __restrict__ sorted_row,
-                                                         SplatGeo sg, int nprime, OutT* __restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ int s_start[kMaxYT + 1];
-    const int tile = blockIdx.x;
-    const int bzx = tile / sg.ntiles_y;
-    const int y0 = (tile - bzx * sg.ntiles_y) * sg.YT;
-    const int ny = min(sg.YT, sg.Y - y0);
-    const int x = bzx % sg.X;
-    const int bz = bzx / sg.X;
-    const int z = bz % sg.Z, b = bz / sg.Z;
-    const int cell0 = bzx * sg.Y + y0;
-    const int lane = threadIdx.x & 63;
-    const int wave = uniform(threadIdx.x >> 6);
-    const int S = NHWC ? kC : sg.YT + 4;  // LDS row stride (floats)
-
-    for (int i = threadIdx.x; i <= ny; i += kFwdBlock) s_start[i] = cell_start[cell0 + i];
-    __syncthreads();
-    const int s0 = s_start[0], s1 = s_start[ny];
-    const bool empty = s0 == s1;
-
-    if (!empty) {
-        const int lds_elems = NHWC ? ny * kC : kC * S;
-        for (int i = threadIdx.x * 4; i < lds_elems; i += kFwdBlock * 4)
-            *reinterpret_cast<float4*>(lds + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int span = s1 - s0;
-        const int cb = wave == 0 ? 0 : tile_lower_bound(s_start, ny, s0 + (wave * span) / kFwdWaves, lane);
-        const int ce = wave == kFwdWaves - 1 ? ny
-                                             : tile_lower_bound(s_start, ny, s0 + ((wave + 1) * span) / kFwdWaves, lane);
-        __syncthreads();  // accumulator zeroed before any flush
-        auto flush = [&](int cell, float acc) {
-            const int t = cell - cell0;
-            if (NHWC) lds[t * kC + lane] = acc;
-            else lds[lane * S + t] = acc;
-        };
-        int e = s_start[cb];
-        const int eend = s_start[ce];
-        while (e < eend) {
-            // up to 128 entries of whole cells: [e, stop)
-            const int e0 = e + lane, e1 = e + kWave + lane;
-            const long long k0 = e0 < eend ? sorted_key[e0] : -1ll;
-            const long long k1 = e1 < eend ? sorted_key[e1] : -1ll;
-            const int c0 = (int)(k0 >> 32), c1 = (int)(k1 >> 32);
-            int stop = min(eend, e + 2 * kWave);
-            if (stop < eend) {  // do not split the cell holding entry e + 128: stop at its first entry
-                const int cl = __builtin_amdgcn_readlane(c1, 63);
-                const unsigned long long m0 = __ballot(c0 == cl), m1 = __ballot(c1 == cl);
-                stop = m0 ? e + __builtin_ctzll(m0) : e + kWave + __builtin_ctzll(m1);
-                if (stop == e) {  // one cell longer than 128 entries
-                    int cell;
-                    const float acc = reduce_big_cell<FUSED, RT>(e, nprime, sorted_key, sorted_row, depth, rows_base,
-                                                                 lane, &cell, sg.nrows);
-                    flush(cell, acc);
-                    e = s_start[min(cell - cell0 + 1, ny)];
-                    continue;
-                }
-            }
-            const int p0 = (int)(k0 & 0xFFFFFFFF), p1 = (int)(k1 & 0xFFFFFFFF);
-            const int row0 = FUSED ? (e0 < eend ? sorted_row[e0] : 0) : p0;
-            const int row1 = FUSED ? (e1 < eend ? sorted_row[e1] : 0) : p1;
-            const float w0 = (FUSED && e0 < stop) ? depth[p0] : 1.f;
-            const float w1 = (FUSED && e1 < stop) ? depth[p1] : 1.f;
-            reduce_entries(e, e, stop, c0, c1, row0, row1, w0, w1, rows_base, FUSED, lane, flush);
-            e = stop;
-        }
-        __syncthreads();
-    }
-
-    constexpr int VN = Vec<OutT>::n;
-    if (NHWC) {
-        const size_t zc = (size_t)sg.Z * kC;
-        OutT* obase = out + (((size_t)b * sg.X + x) * sg.Y + y0) * zc + (size_t)z * kC;
-        constexpr int per_row = kC / VN;
-        for (int i = threadIdx.x; i < ny * per_row; i += kFwdBlock) {
-            const int yy = i / per_row, j = (i - yy * per_row) * VN;
-            if (empty) store_zero_vec(obase + yy * zc + j);
-            else store_vec(obase + yy * zc + j, lds + yy * kC + j);
-        }
-    } else {
-        const size_t XY = (size_t)sg.X * sg.Y;
-        OutT* obase = out + (size_t)bz * kC * XY + (size_t)x * sg.Y + y0;
-        if ((sg.Y & 3) == 0 && (ny & 3) == 0) {
-            const int nq = ny >> 2;
-            for (int i = threadIdx.x; i < kC * nq; i += kFwdBlock) {
-                const int c = i / nq, j = (i - c * nq) * 4;
-                if (empty) {
-                    store4(obase + c * XY + j, 0.f, 0.f, 0.f, 0.f);
-                } else {
-                    const float4 v = *reinterpret_cast<const float4*>(lds + c * S + j);
-                    store4(obase + c * XY + j, v.x, v.y, v.z, v.w);
-                }
-            }
-        } else {
-            for (int i = threadIdx.x; i < kC * ny; i += kFwdBlock) {
-                const int c = i / ny, yy = i - c * ny;
-                obase[c * XY + yy] = from_f32<OutT>(empty ? 0.f : lds[c * S + yy]);
-            }
-        }
-    }
-}
-
 // ----------------------------------------------------------------------------- splat forward, channels-last
 // The production layout (BevEncode runs channels-last): every BEV cell is one contiguous row of C
 // values. One launch, two block roles, four independent waves per block, no block barriers:
@@ -1813,76 +1243,34 @@ __global__ __launch_bounds__(kFwdBlock) void k_splat_fwd(const float* __restrict
 //     [64w, 64w + 64) and reads the window [64w - 1, 64w + 128) (cells have <= 64 entries there;
 //     a longer one is streamed by reduce_big_cell). Round trip 1: keys and context-row indices.
 //     Round trip 2: the depth weights and every owned entry's context row, 16-B lane slices, all in
-//     flight at once. The rows are staged in the wave's LDS slice and summed lane = channel in
-//     canonical order (ascending point id per cell, the NCHW tile kernel's order, so both layouts
-//     agree bit for bit); each finished cell's row is stored straight to the BEV. No global load
-//     follows a store, so stores never sit in front of a load's wait.
-//   zero waves: 64 consecutive cells each; the rows of the empty cells are written as zeros with
-//     16-B stores, so every BEV element is written exactly once.
+//     flight at once. The rows are summed lane group by lane group in canonical order (ascending
+//     point id per cell, the NCHW tile kernel's order, so both layouts agree bit for bit); each
+//     finished cell's row is stored straight to the BEV. No global load follows a store, so stores
+//     never sit in front of a load's wait.
+//   zero waves: kZeroUnits x 64 consecutive cells each; the rows of the empty cells are written as
+//     zeros with 16-B non-temporal stores, so every BEV element is written exactly once.
 // The CSR's sentinel tail (key -1 past the last entry, lss_csr_build) spares a load of the count.
-#ifndef LSS_ROW_FROM_P
-#define LSS_ROW_FROM_P 0  // 1: chunk waves compute each entry's context row from its point id (no sorted_row read; measured: no gain)
-#endif
-// Context row (pixel) of point p = ((bn*D + d)*H + h)*W + w: bn*HW + (h*W + w). Divisions by the
-// runtime D*H*W and H*W through the fp32 reciprocal plus one correction step each.
-__device__ __forceinline__ int row_of_point(int p, const BevGeo& g) {
-    int cam = (int)((float)p * g.inv_dhw);
-    int r = p - cam * g.dhw;
-    if (r < 0) { --cam; r += g.dhw; }
-    if (r >= g.dhw) { ++cam; r -= g.dhw; }
-    int q = (int)((float)r * g.inv_hw);
-    int hw = r - q * g.hw;
-    if (hw < 0) hw += g.hw;
-    if (hw >= g.hw) hw -= g.hw;
-    return cam * g.hw + hw;
-}
-
-#ifndef LSS_ZERO_STORE
-#define LSS_ZERO_STORE 1  // zero-fill stores: 0 plain, 1 non-temporal
-#endif
 #ifndef LSS_ZERO_UNITS
 #define LSS_ZERO_UNITS 1  // 64-cell zero-fill units per wave (their cell_start loads in flight together)
 #endif
+#ifndef LSS_INTERLEAVE
+#define LSS_INTERLEAVE 0  // dispatch order of the block groups: 0 chunks first, 1 interleaved, 2 zero fill first
+#endif
 constexpr int kZeroUnits = LSS_ZERO_UNITS;
-#ifndef LSS_SPLAT_WAVES
-#define LSS_SPLAT_WAVES 4  // waves per block of the channels-last splat kernels (waves are independent)
-#endif
-constexpr int kSplatWaves = LSS_SPLAT_WAVES;
+constexpr int kSplatWaves = 4;  // waves per block of the channels-last splat (waves are independent)
 constexpr int kSplatBlock = kSplatWaves * kWave;
-#ifndef LSS_CHUNK_GAP
-#define LSS_CHUNK_GAP 0  // >0: each chunk wave also zeroes the first G empty cells after each cell it owns
-#endif
-constexpr int kChunkGap = LSS_CHUNK_GAP;
-
-// Empty cells [lo, hi) written as zero rows (non-temporal 16-B stores), RPS rows per instruction.
-template <typename OutT>
-__device__ __forceinline__ void zero_gap_rows(int lo, int hi, const BevGeo& g, OutT* __restrict__ out, int lane) {
-    constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
-    for (int r0 = lo; r0 < hi; r0 += RPS) {
-        const int r = r0 + lane / LPR;
-        if (r < hi)
-            __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u},
-                                        reinterpret_cast<u32x4*>(cell_row(out, r, g) + (lane % LPR) * EPL));
-    }
-}
+constexpr int kSplatMinWaves = 7;  // occupancy floor (waves per SIMD): 72 VGPRs, 16 KB LDS per block
 
 // Zero-fill units [u0, u0 + kZeroUnits): cells [64u, 64u + 64) each; empty cells' rows written as zeros.
-// With kChunkGap > 0, an empty cell k at most kChunkGap cells past the previous occupied cell (the
-// cell of entry cell_start[k] - 1) is left to that cell's chunk wave.
 template <typename OutT>
-__device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start,
-                                const long long* __restrict__ sorted_key, const BevGeo& g,
+__device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start, const BevGeo& g,
                                 OutT* __restrict__ out, int lane) {
     unsigned long long emask[kZeroUnits];
 #pragma unroll
     for (int i = 0; i < kZeroUnits; ++i) {
         const int k = (u0 + i) * kWave + lane;
         bool empty = false;
-        if (k < g.ncells) {
-            const int a = cell_start[k];
-            empty = a == cell_start[k + 1];
-            if (kChunkGap > 0 && empty && a > 0 && k - (int)(sorted_key[a - 1] >> 32) <= kChunkGap) empty = false;
-        }
+        if (k < g.ncells) empty = cell_start[k] == cell_start[k + 1];
         emask[i] = __ballot(empty);
     }
     constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
@@ -1891,14 +1279,9 @@ __device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start,
         const int k0 = (u0 + i) * kWave;
         for (int r0 = 0; r0 < kWave; r0 += RPS) {
             const int r = r0 + lane / LPR;
-            if ((emask[i] >> r) & 1ull) {
-                OutT* dst = cell_row(out, k0 + r, g) + (lane % LPR) * EPL;
-                if (LSS_ZERO_STORE == 1) {
-                    __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, reinterpret_cast<u32x4*>(dst));
-                } else {
-                    store_zero_vec(dst);
-                }
-            }
+            if ((emask[i] >> r) & 1ull)
+                __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u},
+                                            reinterpret_cast<u32x4*>(cell_row(out, k0 + r, g) + (lane % LPR) * EPL));
         }
     }
 }
@@ -1929,57 +1312,34 @@ template <typename RT> struct RowSlice {
     static constexpr int NG = kWave / LPR;       // groups per wave: 4, 8
 };
 
-#ifndef LSS_ROW_NT
-#define LSS_ROW_NT 0  // 1: the chunk waves' row stores are non-temporal too (rocprof in the c3 graph replays: 12.7-13.0 vs 12.0-12.3 us plain)
-#endif
 template <int EPL>
 __device__ __forceinline__ void store_slice(float* dst, const float* a) {
 #pragma unroll
-    for (int i = 0; i < EPL; i += 4) {
-        if (LSS_ROW_NT) {
-            const u32x4 v = {__float_as_uint(a[i]), __float_as_uint(a[i + 1]), __float_as_uint(a[i + 2]),
-                             __float_as_uint(a[i + 3])};
-            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + i));
-        } else {
-            *reinterpret_cast<float4*>(dst + i) = make_float4(a[i], a[i + 1], a[i + 2], a[i + 3]);
-        }
-    }
+    for (int i = 0; i < EPL; i += 4) *reinterpret_cast<float4*>(dst + i) = make_float4(a[i], a[i + 1], a[i + 2], a[i + 3]);
 }
 template <int EPL>
 __device__ __forceinline__ void store_slice(bf16* dst, const float* a) {
     bf16 v[EPL];
 #pragma unroll
     for (int i = 0; i < EPL; ++i) v[i] = __float2bfloat16(a[i]);
-    if constexpr (EPL == 4) {
-        if (LSS_ROW_NT) __builtin_nontemporal_store(*reinterpret_cast<const u32x2*>(v), reinterpret_cast<u32x2*>(dst));
-        else *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(v);
-    } else {
-        if (LSS_ROW_NT) __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(v), reinterpret_cast<u32x4*>(dst));
-        else *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(v);
-    }
+    if constexpr (EPL == 4) *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(v);
+    else *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(v);
 }
 
-#ifndef LSS_UNROLL
-#define LSS_UNROLL 8
-#endif
 // Entries in flight per lane group. A group holds at most ceil(128 / NG) entries (16 with bf16 rows),
 // so with 16 every group issues all its gathers before its first row store: a load issued after a
 // store would wait for that store too (vmcnt counts both, in order), and stores are slow while the
 // zero fill saturates the write path.
-constexpr int kUnroll = LSS_UNROLL;
+constexpr int kUnroll = 8;
 
 // Entry metadata of a chunk's 128-entry window, staged once in LDS: (row, point, cell).
 struct alignas(16) EntryMeta {
-    int row, p, cell, wbits;  // wbits: the depth weight (float bits) when the CSR-ordered copy is given
+    int row, p, cell, pad;
 };
 
 // Depth weights of a lane group's next entries [e, e + KU): lane j of the group loads the weight of
-// entry e + j, so ONE wave-wide gather serves all groups (the group's lanes used to load one shared
-// address per entry: KU gathers, each a full texture-unit pass over 64 lanes for 8 useful values),
-// then each weight is broadcast inside the group through the LDS crossbar (ds_bpermute).
-#ifndef LSS_DEPTH_BCAST
-#define LSS_DEPTH_BCAST 1
-#endif
+// entry e + j, so ONE wave-wide gather serves all groups, then each weight is broadcast inside the
+// group through the LDS crossbar (ds_bpermute).
 template <int LPR, int KU>
 __device__ __forceinline__ float group_weight_load(const EntryMeta* __restrict__ meta,
                                                    const float* __restrict__ depth, int e, int last, int lane,
@@ -1993,65 +1353,13 @@ __device__ __forceinline__ float group_weight(float wd, int u, int lane) {
     return __shfl(wd, lane - lane % LPR + u, kWave);
 }
 
-// A cell with more than 64 entries of an unordered CSR (arrival order inside the cell): its point ids
-// staged in LDS (the wave's meta and piece slots: up to `cap` entries), sorted by rank, then summed in
-// canonical order exactly as reduce_big_cell (one channel per lane). A larger cell takes the canonical
-// order by repeated minimum selection straight from memory (slow; never seen at the BASELINE configs,
-// whose largest cell holds 64 points).
-template <bool FUSED, typename RT>
-__device__ float reduce_big_cell_unordered(int start, int nprime, const long long* __restrict__ key,
-                                           const int32_t* __restrict__ cell_start, const float* __restrict__ depth,
-                                           const RT* __restrict__ rows_base, const BevGeo& g, int* __restrict__ s_in,
-                                           int* __restrict__ s_sorted, int cap, int lane, int* cell_out) {
-    const int cell = (int)(key[start] >> 32);
-    *cell_out = cell;
-    const int n = uniform(min(cell_start[cell + 1], nprime) - start);
-    auto entry = [&](int p, float& acc) {
-        const int r = FUSED ? row_of_point(p, g) : p;
-        const float w = FUSED ? depth[dchk(p, nprime, kDbgSplatPoint)] : 1.f;
-        const float v = to_f32(rows_base[(size_t)dchk(r, g.nrows, kDbgSplatRow) * kC + lane]);
-        acc = FUSED ? fmaf(w, v, acc) : __fadd_rn(acc, v);
-    };
-    float acc = 0.f;
-    if (n <= cap) {
-        for (int i = lane; i < n; i += kWave) s_in[i] = (int)(key[start + i] & 0xFFFFFFFF);
-        __builtin_amdgcn_wave_barrier();
-        for (int i = lane; i < n; i += kWave) {
-            const int p = s_in[i];
-            int r = 0;
-            for (int j = 0; j < n; ++j) r += s_in[j] < p ? 1 : 0;  // point ids are distinct inside a cell
-            s_sorted[r] = p;
-        }
-        __builtin_amdgcn_wave_barrier();
-        for (int k = 0; k < n; ++k) entry(s_sorted[k], acc);
-        return acc;
-    }
-    int last = -1;
-    for (int k = 0; k < n; ++k) {
-        int best = INT_MAX;
-        for (int i = lane; i < n; i += kWave) {
-            const int v = (int)(key[start + i] & 0xFFFFFFFF);
-            if (v > last && v < best) best = v;
-        }
-        best = uniform(wave_min(best));
-        entry(best, acc);
-        last = best;
-    }
-    return acc;
-}
-
-#ifndef LSS_SPLAT_UNORDERED_CODE
-#define LSS_SPLAT_UNORDERED_CODE 1  // 0: the chunk waves' in-cell ranking (LSS_SPLAT_UNORDERED) compiled out
-#endif
 template <bool FUSED, typename RT, typename OutT>
 __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __restrict__ depth,
-                                            const float* __restrict__ sorted_depth,
                                             const RT* __restrict__ rows_base,
                                             const long long* __restrict__ sorted_key,
-                                            const int32_t* __restrict__ sorted_row,
-                                            const int32_t* __restrict__ cell_start, const BevGeo& g,
+                                            const int32_t* __restrict__ sorted_row, const BevGeo& g,
                                             OutT* __restrict__ out, EntryMeta* __restrict__ meta,
-                                            float* __restrict__ part, int lane, bool unordered) {
+                                            float* __restrict__ part, int lane) {
     using RS = RowSlice<RT>;
     // round trip 1: keys (cell << 32 | point), context rows, the previous entry's cell
     const int base = w * kWave;
@@ -2059,107 +1367,24 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     const long long k0 = e0 < nprime ? sorted_key[e0] : -1ll;
     const long long k1 = e1 < nprime ? sorted_key[e1] : -1ll;
     int rs0 = 0, rs1 = 0;
-    const bool row_from_p = (LSS_ROW_FROM_P || unordered) && g.dhw > 0;
-    if (FUSED && !row_from_p) {
+    if (FUSED) {
         rs0 = e0 < nprime ? sorted_row[e0] : 0;
         rs1 = e1 < nprime ? sorted_row[e1] : 0;
     }
     const int prevcell = base > 0 ? (int)(sorted_key[base - 1] >> 32) : -2;
-    // depth weights in CSR order (coalesced, same round trip) when the lift wrote them
-    const bool sorted_w = FUSED && sorted_depth != nullptr;
-    float sw0 = 0.f, sw1 = 0.f;
-    if (sorted_w) {
-        sw0 = e0 < nprime ? sorted_depth[e0] : 0.f;
-        sw1 = e1 < nprime ? sorted_depth[e1] : 0.f;
-    }
     const int c0 = (int)(k0 >> 32), c1 = (int)(k1 >> 32);
     const int p0 = (int)(k0 & 0xFFFFFFFF), p1 = (int)(k1 & 0xFFFFFFFF);
     if (!FUSED) {
         rs0 = p0;
         rs1 = p1;
-    } else if (row_from_p) {  // the sentinel (-1) and out-of-range entries get row 0 (never summed)
-        rs0 = p0 >= 0 ? row_of_point(p0, g) : 0;
-        rs1 = p1 >= 0 ? row_of_point(p1, g) : 0;
     }
     LSS_STAMP(w, 1);
     const Span sp = chunk_span(c0, c1, prevcell, lane);
     const int s = uniform(sp.s), end = uniform(sp.end), big = uniform(sp.big);
-    if (LSS_CHUNK_STOP == 1) {
-        if (s == 12345 && end == 777 && (rs0 ^ rs1) == 99) out[0] = from_f32<OutT>(1.f);
-        return;
-    }
     if (end > 0) {
-        int d0 = lane, d1 = kWave + lane;  // the entries' positions in the window
-        if (LSS_SPLAT_UNORDERED_CODE && unordered) {
-            // The CSR's entries are grouped by cell but in arrival order inside a cell (the plan ran
-            // without k_csr_canon): put every cell of the window into canonical order (ascending point
-            // id) here, so the sums below -- and their bits -- are those of the canonical CSR. Rank of
-            // an entry inside its run of equal cells: the run's point ids staged in LDS (this wave's
-            // piece slots, free until the sums), ties (the sentinel's -1) broken by position.
-            int* sp = reinterpret_cast<int*>(part);
-            sp[lane] = p0;
-            sp[kWave + lane] = p1;
-            __builtin_amdgcn_wave_barrier();
-            const int up0 = __shfl(c0, (lane + 63) & 63, kWave), up1 = __shfl(c1, (lane + 63) & 63, kWave);
-            const int c0_last = __builtin_amdgcn_readlane(c0, 63);
-            const unsigned long long st0 = __ballot(c0 != (lane == 0 ? prevcell : up0));
-            const unsigned long long st1 = __ballot(c1 != (lane == 0 ? c0_last : up1));
-            const unsigned long long le = ~0ull >> (63 - lane);
-            const unsigned long long after = lane == 63 ? 0ull : (~0ull << (lane + 1));
-            // run [cs, ce) of each held entry (a run cut by the window's start begins at 0)
-            const int cs0 = 63 - __builtin_clzll((st0 & le) | 1ull);
-            const int cs1 = (st1 & le) ? kWave + 63 - __builtin_clzll(st1 & le) : 63 - __builtin_clzll(st0 | 1ull);
-            const unsigned long long n0 = st0 & after, n1 = st1 & after;
-            const int ce0 = n0 ? (int)__builtin_ctzll(n0) : (st1 ? kWave + (int)__builtin_ctzll(st1) : 2 * kWave);
-            const int ce1 = n1 ? kWave + (int)__builtin_ctzll(n1) : 2 * kWave;
-            // one uniform loop over the longest run of the window, both entries at once, 4 steps
-            // unrolled: 8 independent LDS reads in flight (a per-lane loop waited for each read)
-            // only the owned cells [s, end) are ranked (the others keep their positions: a cell cut
-            // by the window's end is long and never summed from here)
-            const int ws0 = s, we0 = end;  // (window positions)
-            const int l0 = (lane >= ws0 && lane < we0) ? ce0 - cs0 : 0;
-            const int l1 = (kWave + lane >= ws0 && kWave + lane < we0) ? ce1 - cs1 : 0;
-            int lmax = 0;  // the longest owned run: gaps between the run starts, on the scalar unit
-            {
-                unsigned long long a = st0, b = st1;
-                int last = ws0;  // the first owned cell starts at s
-                a &= (ws0 >= kWave - 1) ? 0ull : (~0ull << (ws0 + 1));
-                while (a) {
-                    const int j = (int)__builtin_ctzll(a);
-                    a &= a - 1;
-                    if (j > we0) break;
-                    lmax = max(lmax, j - last);
-                    last = j;
-                }
-                while (b && last < we0) {
-                    const int j = kWave + (int)__builtin_ctzll(b);
-                    b &= b - 1;
-                    if (j > we0) break;
-                    lmax = max(lmax, j - last);
-                    last = j;
-                }
-                lmax = uniform(max(lmax, we0 - last));
-            }
-            int r0 = 0, r1 = 0;
-            for (int k = 0; k < lmax; k += 4) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int j0 = cs0 + k + u, j1 = cs1 + k + u;
-                    const int q0 = sp[min(j0, 2 * kWave - 1)], q1 = sp[min(j1, 2 * kWave - 1)];
-                    r0 += (k + u < l0 && (q0 < p0 || (q0 == p0 && j0 < lane))) ? 1 : 0;
-                    r1 += (k + u < l1 && (q1 < p1 || (q1 == p1 && j1 < kWave + lane))) ? 1 : 0;
-                }
-            }
-            if (l0 > 0) d0 = cs0 + r0;
-            if (l1 > 0) d1 = cs1 + r1;
-            __builtin_amdgcn_wave_barrier();
-        }
-        meta[d0] = EntryMeta{rs0, p0, c0, __float_as_int(sw0)};
-        meta[d1] = EntryMeta{rs1, p1, c1, __float_as_int(sw1)};
+        meta[lane] = EntryMeta{rs0, p0, c0, 0};
+        meta[kWave + lane] = EntryMeta{rs1, p1, c1, 0};
         __builtin_amdgcn_wave_barrier();
-        const int up = __shfl(c0, (lane + 63) & 63, kWave);
-        const unsigned long long starts = __ballot(c0 != (lane == 0 ? prevcell : up)) &
-                                          (~0ull << s) & (end >= kWave ? ~0ull : ((1ull << end) - 1));
         // The owned entries [s, end) (n <= 128) are split evenly over the NG groups of LPR lanes:
         // group q sums entries [s + n*q/NG, s + n*(q+1)/NG) cell by cell; lane j of a group owns row
         // elements [EPL*j, EPL*j + EPL). A cell cut by group boundaries is summed in pieces: every
@@ -2191,28 +1416,14 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
             // else: the first piece of a cut cell stays in acc (combined after the barrier)
         };
         // round trip 2 (one per kUnroll entries of a group): row slices and depth weights in flight together
-#ifndef LSS_TRAP_EXP
-#define LSS_TRAP_EXP 0  // timing experiments only: 1 drops every entry past the first batch (wrong output)
-#endif
-        for (int e = gs; e < (LSS_TRAP_EXP ? min(ge, gs + kUnroll) : ge); e += kUnroll) {
+        for (int e = gs; e < ge; e += kUnroll) {
             uint4 v[kUnroll];
-            float wt[LSS_DEPTH_BCAST ? 1 : kUnroll];  // per-entry weight gathers (LSS_DEPTH_BCAST=0 only)
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
-                const int4 m = *reinterpret_cast<const int4*>(&meta[min(e + u, ge - 1)]);  // (row, p, cell, w)
+                const int4 m = *reinterpret_cast<const int4*>(&meta[min(e + u, ge - 1)]);  // (row, p, cell, -)
                 v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)dchk(m.x, g.nrows, kDbgSplatRow) * kC + col);
-                if (!LSS_DEPTH_BCAST) wt[u] = (FUSED && !LSS_NO_DEPTH && !sorted_w) ? depth[dchk(m.y, nprime, kDbgSplatPoint)] : 1.f;
             }
-            // depth weights: CSR-ordered copy (staged in meta), or one wave-wide gather + group broadcast
-            const bool bcast = FUSED && !LSS_NO_DEPTH && !sorted_w && LSS_DEPTH_BCAST;
-            const float wd = bcast ? group_weight_load<RS::LPR, kUnroll>(meta, depth, e, ge - 1, lane, nprime) : 0.f;
-            if (LSS_CHUNK_STOP == 2) {
-                unsigned x = 0;
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) x ^= v[u].x ^ v[u].w ^ __float_as_uint(wd);
-                if (x == 0x12345u) out[0] = from_f32<OutT>(1.f);
-                continue;
-            }
+            const float wd = FUSED ? group_weight_load<RS::LPR, kUnroll>(meta, depth, e, ge - 1, lane, nprime) : 0.f;
             if (LSS_TRACE && e == gs && grp == 0) LSS_STAMP(w, 2);
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
@@ -2226,20 +1437,18 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                     }
                     float x[RS::EPL];
                     unpack16(v[u], (const RT*)nullptr, x);
-                    const float wu = (!FUSED || LSS_NO_DEPTH) ? 1.f
-                                     : sorted_w ? __int_as_float(meta[e + u].wbits)
-                                     : LSS_DEPTH_BCAST ? group_weight<RS::LPR>(wd, u, lane) : wt[LSS_DEPTH_BCAST ? 0 : u];
+                    const float wu = FUSED ? group_weight<RS::LPR>(wd, u, lane) : 1.f;
 #pragma unroll
                     for (int i = 0; i < RS::EPL; ++i) acc[i] = FUSED ? fmaf(wu, x[i], acc[i]) : __fadd_rn(acc[i], x[i]);
                 }
             }
         }
-        if (cur >= 0 && LSS_CHUNK_STOP != 2) finish(true);
+        if (cur >= 0) finish(true);
         __builtin_amdgcn_wave_barrier();
         // the cell cut at this group's end, if it starts in this group: its first piece (acc) plus
         // the later groups' pieces in group order (empty groups skipped; the cell ends where a
         // group's first cell is another one)
-        if (tail_split && !(head_split && cur == first_cell) && LSS_CHUNK_STOP != 2) {
+        if (tail_split && !(head_split && cur == first_cell)) {
             for (int q = grp + 1; q < RS::NG; ++q) {
                 const int qs = gbeg(q);
                 if (qs == gbeg(q + 1)) continue;  // empty group
@@ -2249,37 +1458,72 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
             }
             store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + col, acc);
         }
-        if (kChunkGap > 0) {
-            // empty cells after each owned cell, up to kChunkGap of them (the next occupied cell is
-            // the cell of the next start, or of entry `end`: the big cell, the next chunk's, or -1)
-            unsigned long long m = starts;
-            while (m) {
-                const int j = __builtin_ctzll(m);
-                m &= m - 1;
-                const int c = __builtin_amdgcn_readlane(c0, j);
-                const int np = m ? (int)__builtin_ctzll(m) : end;
-                int nc = np < kWave ? __builtin_amdgcn_readlane(c0, np) : __builtin_amdgcn_readlane(c1, np - kWave);
-                if (nc < 0) nc = g.ncells;
-                zero_gap_rows<OutT>(c + 1, min(nc, c + 1 + kChunkGap), g, out, lane);
-            }
-        }
     }
     if (big >= 0) {
         int cell;
-        const float a2 = (LSS_SPLAT_UNORDERED_CODE && unordered)
-            ? reduce_big_cell_unordered<FUSED, RT>(base + big, nprime, sorted_key, cell_start, depth, rows_base, g,
-                                                   reinterpret_cast<int*>(meta), reinterpret_cast<int*>(part),
-                                                   min(2 * kWave * 4, RS::NG * kC), lane, &cell)
-            : reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base, lane, &cell,
-                                         g.nrows);
+        const float a2 = reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base, lane,
+                                                    &cell, g.nrows);
         cell_row(out, dchk(cell, g.ncells, kDbgSplatCell), g)[lane] = from_f32<OutT>(a2);
-        if (kChunkGap > 0) {
-            const int nx = uniform(cell_start[cell + 1]);
-            int nc = nx < nprime ? (int)(sorted_key[nx] >> 32) : -1;
-            nc = uniform(nc);
-            if (nc < 0) nc = g.ncells;
-            zero_gap_rows<OutT>(cell + 1, min(nc, cell + 1 + kChunkGap), g, out, lane);
-        }
+    }
+}
+
+template <bool FUSED, typename RT, typename OutT>
+__global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(const float* __restrict__ depth,
+                                                           const RT* __restrict__ rows_base,
+                                                           const int32_t* __restrict__ cell_start,
+                                                           const long long* __restrict__ sorted_key,
+                                                           const int32_t* __restrict__ sorted_row, BevGeo g,
+                                                           int nprime, int nchunk_blocks, int nzero_blocks,
+                                                           int order, OutT* __restrict__ out) {
+    __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
+    __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][RowSlice<RT>::NG * kC];
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    // Blocks come in groups of 8, one per XCD (blocks are dealt round-robin over the 8 XCDs). `order`
+    // 0 dispatches the chunk groups first, then the zero-fill groups; 1 interleaves them evenly; 2 puts
+    // the zero fill first. The chunk blocks of XCD x take one contiguous run of chunks, whose context
+    // rows (a few cameras) then stay in that L2.
+    const int ncg = (nchunk_blocks + 7) >> 3, nzg = (nzero_blocks + 7) >> 3;
+    const int gi = blockIdx.x >> 3, x = blockIdx.x & 7;
+    int zgi = gi - ncg, cgi = gi;
+    bool zero_role = gi >= ncg;
+    if (order == 2) {
+        zero_role = gi < nzg;
+        zgi = gi;
+        cgi = gi - nzg;
+    } else if (order == 1) {
+        const int G = ncg + nzg;
+        zgi = (gi * nzg) / G;
+        zero_role = ((gi + 1) * nzg) / G > zgi;
+        cgi = gi - zgi;
+    }
+    if (!zero_role) {
+        const int cb = x * ncg + cgi;
+        if (cb >= nchunk_blocks) return;
+        const int w = cb * kSplatWaves + wave;
+        // the last chunk block's spare waves own no entries (and must not read the entry before their
+        // base, past the end of sorted_key)
+        if (w * kWave >= nprime) return;
+        LSS_STAMP(w, 0);
+        splat_chunk<FUSED, RT, OutT>(w, nprime, depth, rows_base, sorted_key, sorted_row, g, out, s_meta[wave],
+                                     s_part[wave], lane);
+        LSS_STAMP(w, 3);
+#if LSS_TRACE
+        if (lane == 0 && w < 16384) g_lss_trace[w][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
+                                                    (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+#endif
+    } else {
+        const int zb = x * nzg + zgi;
+        if (zb >= nzero_blocks) return;
+        const int u = (zb * kSplatWaves + wave) * kZeroUnits;
+        [[maybe_unused]] const int zslot = nchunk_blocks * kSplatWaves + zb * kSplatWaves + wave;
+        LSS_STAMP(zslot, 0);
+        if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, g, out, lane);
+        LSS_STAMP(zslot, 3);
+#if LSS_TRACE
+        if (lane == 0 && zslot < 16384) g_lss_trace[zslot][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
+                                                        (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+#endif
     }
 }
 
@@ -2291,26 +1535,13 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 // kernels agree bit for bit), KU entries in flight per batch, and leaves each cell's row in an LDS
 // tile [channel][y] zeroed beforehand (empty cells stay zero). The block then writes the tile one
 // channel plane run at a time with 16-B stores.
-#ifndef LSS_NCHW_IMPL
-#define LSS_NCHW_IMPL 2  // NCHW splat: 1 k_splat_fwd (lane = channel), 2 k_splat_fwd_nchw2 (lane groups)
-#endif
-#ifndef LSS_NCHW_WAVES
-#define LSS_NCHW_WAVES 4  // waves per NCHW tile block (more lane groups share a dense tile's entries)
-#endif
-constexpr int kN2Waves = LSS_NCHW_WAVES;
-#ifndef LSS_NCHW_PAD
-#define LSS_NCHW_PAD 0  // 0: row stride YT rounded to 16 B (25.6 KB tiles, 6 blocks per CU; c2 in-step 16.4 -> 15.3 us, profiles/r03/pad0_eval.txt); 1: 4 more floats (27 KB, 5 per CU)
-#endif
+constexpr int kN2Waves = 4;  // waves per NCHW tile block (more lane groups share a dense tile's entries)
 // LDS row stride of the NCHW tile: YT rounded up to 16 B. At YT = 100 the tile is 25.6 KB, so 6 blocks
 // fit a CU (1,536 of c2's 1,600 tiles resident at once instead of 1,280).
-__host__ __device__ constexpr int nchw2_stride(int yt) { return ((yt + 3) & ~3) + 4 * LSS_NCHW_PAD; }
+// (the round-2 stride YT + 4, 27 KB / 5 blocks per CU, was slower: c2 in-step 16.4 vs 15.3 us,
+// profiles/r03/pad0_eval.txt)
+__host__ __device__ constexpr int nchw2_stride(int yt) { return (yt + 3) & ~3; }
 constexpr int kN2Block = kN2Waves * kWave;
-#ifndef LSS_NCHW_SKIP
-#define LSS_NCHW_SKIP 0  // timing experiments only (wrong output): 1 writes every tile as zeros
-#endif
-#ifndef LSS_NCHW_KU
-#define LSS_NCHW_KU 8  // context rows in flight per lane group and batch (the next batch's keys follow them)
-#endif
 
 
 template <bool FUSED, typename RT, typename OutT>
@@ -2321,11 +1552,11 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
                                                              const int32_t* __restrict__ sorted_row, SplatGeo sg,
                                                              int ntiles, OutT* __restrict__ out) {
     using RS = RowSlice<RT>;
-    constexpr int KU = LSS_NCHW_KU;               // entries per batch of a group
+    constexpr int KU = 8;                         // context rows in flight per group and batch
     constexpr int KPL = (KU + RS::LPR - 1) / RS::LPR;  // keys fetched per lane per batch
     constexpr int NGB = kN2Waves * RS::NG;        // lane groups per block
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ int s_start[kMaxYT + 1];
+    __shared__ int s_start[kYtMax + 1];
     const int tile = xcd_block();  // consecutive tiles (one sample's rows) on one XCD, as the CSR build wrote them
     if (tile >= ntiles) return;    // block-uniform (the grid is rounded up to a multiple of 8)
     const int bzx = tile / sg.ntiles_y;
@@ -2340,7 +1571,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
     __syncthreads();
     LSS_STAMP(tslot, 1);
     const int s0 = s_start[0], s1 = s_start[ny];
-    const bool empty = LSS_NCHW_SKIP || s0 == s1;
+    const bool empty = s0 == s1;
     if (!empty) {
         for (int i = threadIdx.x * 4; i < kC * S; i += kN2Block * 4)
             *reinterpret_cast<float4*>(lds + i) = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2462,288 +1693,12 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
     LSS_STAMP(tslot, 3);
 }
 
-template <bool FUSED, typename RT, typename OutT>
-__global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES) void k_splat_fwd_nhwc(const float* __restrict__ depth,
-                                                           const float* __restrict__ sorted_depth,
-                                                           const RT* __restrict__ rows_base,
-                                                           const int32_t* __restrict__ cell_start,
-                                                           const long long* __restrict__ sorted_key,
-                                                           const int32_t* __restrict__ sorted_row, BevGeo g,
-                                                           int nprime, int nchunk_blocks, int nzero_blocks,
-                                                           int order, int unordered, OutT* __restrict__ out) {
-    __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
-    __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][RowSlice<RT>::NG * kC];
-    const int lane = threadIdx.x & 63;
-    const int wave = uniform(threadIdx.x >> 6);
-    // Blocks come in groups of 8, one per XCD (blocks are dealt round-robin over the 8 XCDs). Chunk
-    // groups and zero-fill groups are interleaved evenly in dispatch order, so the HBM-write-bound
-    // zero fill runs beside the L2-bound chunk gathers from the start; the chunk blocks of XCD x
-    // take one contiguous run of chunks, whose context rows (a few cameras) then stay in that L2.
-    const int ncg = (nchunk_blocks + 7) >> 3, nzg = (nzero_blocks + 7) >> 3;
-    const int gi = blockIdx.x >> 3, x = blockIdx.x & 7;
-    int zgi = gi - ncg, cgi = gi;
-    bool zero_role = gi >= ncg;
-    if (order == 2) {
-        zero_role = gi < nzg;
-        zgi = gi;
-        cgi = gi - nzg;
-    } else if (order == 1) {
-        const int G = ncg + nzg;
-        zgi = (gi * nzg) / G;
-        zero_role = ((gi + 1) * nzg) / G > zgi;
-        cgi = gi - zgi;
-    }
-    if (!zero_role) {
-        if (LSS_FWD_SKIP & 1) return;
-        const int cb = LSS_XCD_MAP ? x * ncg + cgi : cgi * 8 + x;
-        if (cb >= nchunk_blocks) return;
-        const int w = cb * (kSplatWaves) + wave;
-        // the last chunk block's spare waves own no entries (and must not read the entry before their
-        // base, past the end of sorted_key)
-        if (w * kWave >= nprime) return;
-        LSS_STAMP(w, 0);
-        splat_chunk<FUSED, RT, OutT>(w, nprime, depth, sorted_depth, rows_base, sorted_key, sorted_row, cell_start, g, out,
-                                     s_meta[wave], s_part[wave], lane, unordered != 0);
-        LSS_STAMP(w, 3);
-#if LSS_TRACE
-        if (lane == 0 && w < 16384) g_lss_trace[w][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
-                                                    (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
-#endif
-    } else {
-        if (LSS_FWD_SKIP & 2) return;
-        const int zb = LSS_XCD_MAP ? x * nzg + zgi : zgi * 8 + x;
-        if (zb >= nzero_blocks) return;
-        const int u = (zb * (kSplatWaves) + wave) * kZeroUnits;
-        [[maybe_unused]] const int zslot = nchunk_blocks * (kSplatWaves) + zb * (kSplatWaves) + wave;
-        LSS_STAMP(zslot, 0);
-        if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, sorted_key, g, out, lane);
-        LSS_STAMP(zslot, 3);
-#if LSS_TRACE
-        if (lane == 0 && zslot < 16384) g_lss_trace[zslot][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
-                                                        (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
-#endif
-    }
-}
-
-// ----------------------------------------------------------------------------- splat forward, channels-last, merged roles
-// Every wave owns one chunk (64 canonical CSR entries, cells owned as in splat_chunk) AND one zero
-// unit (64 consecutive cells), so the grid is max(chunks, units) waves -- all resident at once at
-// c3 -- instead of chunks + units waves in two generations. Order inside a wave:
-//   round trip 1   the chunk's keys / context rows / previous cell and the unit's cell starts, one batch;
-//   gathers        every owned entry's context-row slice and depth weight (lane groups as splat_chunk);
-//   zero stores    the unit's empty rows, issued while the gathers are in flight (a load issued AFTER a
-//                  store would wait for it: vmcnt counts both in issue order, so stores go after loads);
-//   sums           cell by cell in canonical order; rows of cells inside one lane group stored at once;
-//   split cells    a cell cut by lane-group boundaries: the groups' pieces are combined by a segmented
-//                  scan over the groups with cross-lane shuffles (fixed association, no LDS, no barrier).
-#ifndef LSS_SPLAT_IMPL
-#define LSS_SPLAT_IMPL 0  // channels-last splat: 0 two block roles (k_splat_fwd_nhwc), 1 merged roles
-#endif
-#ifndef LSS_MIN_WAVES_M
-#define LSS_MIN_WAVES_M 6  // occupancy floor of the merged kernel (waves per SIMD)
-#endif
-#ifndef LSS_UNROLL_M
-#define LSS_UNROLL_M 8     // entries per lane group gathered in the first batch
-#endif
-#ifndef LSS_MERGED_ZERO_LATE
-#define LSS_MERGED_ZERO_LATE 0  // 1: the zero unit's stores after the chunk's own (no store before a load)
-#endif
-constexpr int kUnrollM = LSS_UNROLL_M;
-
-template <typename OutT>
-__device__ __forceinline__ void zero_unit_rows(int k0, unsigned long long emask, const BevGeo& g,
-                                               OutT* __restrict__ out, int lane) {
-    constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
-    constexpr unsigned long long kRowMask = (RPS == 64) ? ~0ull : ((1ull << RPS) - 1);
-#pragma unroll
-    for (int r0 = 0; r0 < kWave; r0 += RPS) {
-        if (((emask >> r0) & kRowMask) == 0) continue;  // wave-uniform
-        const int r = r0 + lane / LPR;
-        if ((emask >> r) & 1ull) {
-            OutT* dst = cell_row(out, k0 + r, g) + (lane % LPR) * EPL;
-            if (LSS_ZERO_STORE == 1) __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, reinterpret_cast<u32x4*>(dst));
-            else store_zero_vec(dst);
-        }
-    }
-}
-
-template <bool FUSED, typename RT, typename OutT>
-__global__ __launch_bounds__(kSplatBlock, LSS_MIN_WAVES_M) void k_splat_fwd_nhwc_m(
-    const float* __restrict__ depth, const float* __restrict__ sorted_depth, const RT* __restrict__ rows_base,
-    const int32_t* __restrict__ cell_start, const long long* __restrict__ sorted_key,
-    const int32_t* __restrict__ sorted_row, BevGeo g, int nprime, int nchunks, int nunits, OutT* __restrict__ out) {
-    using RS = RowSlice<RT>;
-    constexpr int EPL = RS::EPL, LPR = RS::LPR, NG = RS::NG;
-    __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
-    __shared__ __attribute__((aligned(16))) float s_head[kSplatWaves][NG * kC];  // head pieces, lane-private
-    const int lane = threadIdx.x & 63;
-    const int wave = uniform(threadIdx.x >> 6);
-    EntryMeta* meta = s_meta[wave];
-    // blocks are dealt round-robin over the 8 XCDs: the chunk blocks of one XCD are a contiguous run of
-    // chunks (about one sample's cameras, whose context rows then stay in that L2); gridDim.x % 8 == 0
-    const int per_xcd = gridDim.x >> 3;
-    const int w = ((blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3)) * (kSplatWaves) + wave;  // chunk
-    const int zu = blockIdx.x * (kSplatWaves) + wave;                                        // zero unit
-
-    // ---- round trip 1
-    const bool has_chunk = w < nchunks;  // wave-uniform
-    const int base = w * kWave;
-    const int e0 = base + lane, e1 = base + kWave + lane;
-    long long k0 = -1ll, k1 = -1ll;
-    int rs0 = 0, rs1 = 0, prevcell = -2;
-    float sw0 = 0.f, sw1 = 0.f;
-    const bool sorted_w = FUSED && sorted_depth != nullptr;
-    if (has_chunk) {
-        k0 = e0 < nprime ? sorted_key[e0] : -1ll;
-        k1 = e1 < nprime ? sorted_key[e1] : -1ll;
-        if (FUSED) {
-            rs0 = e0 < nprime ? sorted_row[e0] : 0;
-            rs1 = e1 < nprime ? sorted_row[e1] : 0;
-        }
-        if (sorted_w) {
-            sw0 = e0 < nprime ? sorted_depth[e0] : 0.f;
-            sw1 = e1 < nprime ? sorted_depth[e1] : 0.f;
-        }
-        prevcell = base > 0 ? (int)(sorted_key[base - 1] >> 32) : -2;
-    }
-    const int kz = zu * kWave + lane;
-    int za = 0, zb = 0;
-    if (zu < nunits && kz < g.ncells) {
-        za = cell_start[kz];
-        zb = cell_start[kz + 1];
-    }
-    const unsigned long long emask = __ballot(zu < nunits && kz < g.ncells && za == zb);
-    const int c0 = (int)(k0 >> 32), c1 = (int)(k1 >> 32);
-    const int p0 = (int)(k0 & 0xFFFFFFFF), p1 = (int)(k1 & 0xFFFFFFFF);
-    if (!FUSED) {
-        rs0 = p0;
-        rs1 = p1;
-    }
-    Span sp{0, 0, -1};
-    if (has_chunk) sp = chunk_span(c0, c1, prevcell, lane);
-    const int s = uniform(sp.s), end = uniform(sp.end), big = uniform(sp.big);
-
-    if (end > 0) {
-        meta[lane] = EntryMeta{rs0, p0, c0, __float_as_int(sw0)};
-        meta[kWave + lane] = EntryMeta{rs1, p1, c1, __float_as_int(sw1)};
-        __builtin_amdgcn_wave_barrier();
-        const int n = end - s;
-        const int grp = lane / LPR, col = (lane % LPR) * EPL;
-        const int gs = s + (n * grp) / NG, ge = s + (n * (grp + 1)) / NG;
-        const int first_cell = gs < ge ? meta[gs].cell : -1;
-        const int last_cell = gs < ge ? meta[ge - 1].cell : -1;
-        const bool head_split = gs < ge && gs > s && meta[gs - 1].cell == first_cell;
-        const bool tail_split = gs < ge && ge < end && meta[ge].cell == last_cell;
-        const bool middle = head_split && tail_split && first_cell == last_cell;  // one cell across both cuts
-        // gathers of the first batch: row slices and depth weights, all in flight together
-        uint4 v[kUnrollM];
-        float wt[LSS_DEPTH_BCAST ? 1 : kUnrollM];  // per-entry weight gathers (LSS_DEPTH_BCAST=0 only)
-#pragma unroll
-        for (int u = 0; u < kUnrollM; ++u) {
-            const int4 m = *reinterpret_cast<const int4*>(&meta[gs < ge ? min(gs + u, ge - 1) : s]);
-            v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)m.x * kC + col);
-            if (!LSS_DEPTH_BCAST) wt[u] = (FUSED && !sorted_w) ? depth[m.y] : 1.f;
-        }
-        const bool bcast = FUSED && !sorted_w && LSS_DEPTH_BCAST;
-        const float wd = bcast ? group_weight_load<LPR, kUnrollM>(meta, depth, gs < ge ? gs : s, gs < ge ? ge - 1 : s,
-                                                                  lane, nprime) : 0.f;
-        // the zero unit's rows go out while the gathers are in flight (LSS_MERGED_ZERO_LATE: at the end)
-        if (!LSS_MERGED_ZERO_LATE) zero_unit_rows<OutT>(zu * kWave, emask, g, out, lane);
-        float acc[EPL];
-#pragma unroll
-        for (int i = 0; i < EPL; ++i) acc[i] = 0.f;
-        float* hsum = &s_head[wave][grp * kC + col];  // this lane's slice of its group's head piece
-        int cur = -1;
-        auto finish = [&](bool last) {  // the cell `cur` ends at this point of the group
-            if (cur == first_cell && head_split) {
-#pragma unroll
-                for (int i = 0; i < EPL; i += 4)  // head piece: combined after the scan
-                    *reinterpret_cast<float4*>(hsum + i) = make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
-            } else if (!(last && tail_split)) {
-                store_slice<EPL>(cell_row(out, cur, g) + col, acc);
-            }  // tail piece: stays in acc
-        };
-        auto consume = [&](const uint4& raw, float w_, int cl) {
-            if (cl != cur) {
-                if (cur >= 0) finish(false);
-#pragma unroll
-                for (int i = 0; i < EPL; ++i) acc[i] = 0.f;
-                cur = cl;
-            }
-            float x[EPL];
-            unpack16(raw, (const RT*)nullptr, x);
-#pragma unroll
-            for (int i = 0; i < EPL; ++i) acc[i] = FUSED ? fmaf(w_, x[i], acc[i]) : __fadd_rn(acc[i], x[i]);
-        };
-#pragma unroll
-        for (int u = 0; u < kUnrollM; ++u)
-            if (gs + u < ge)
-                consume(v[u], !FUSED ? 1.f : sorted_w ? __int_as_float(meta[gs + u].wbits)
-                              : LSS_DEPTH_BCAST ? group_weight<LPR>(wd, u, lane) : wt[LSS_DEPTH_BCAST ? 0 : u],
-                        meta[gs + u].cell);
-        // further batches (a group holds more than kUnrollM entries only when the chunk owns > 64)
-        for (int e = gs + kUnrollM; e < ge; e += kUnrollM) {
-#pragma unroll
-            for (int u = 0; u < kUnrollM; ++u) {
-                const int4 m = *reinterpret_cast<const int4*>(&meta[min(e + u, ge - 1)]);
-                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)m.x * kC + col);
-                if (!LSS_DEPTH_BCAST) wt[u] = (FUSED && !sorted_w) ? depth[m.y] : 1.f;
-            }
-            const float wd2 = bcast ? group_weight_load<LPR, kUnrollM>(meta, depth, e, ge - 1, lane, nprime) : 0.f;
-#pragma unroll
-            for (int u = 0; u < kUnrollM; ++u)
-                if (e + u < ge)
-                    consume(v[u], !FUSED ? 1.f : sorted_w ? __int_as_float(meta[e + u].wbits)
-                                  : LSS_DEPTH_BCAST ? group_weight<LPR>(wd2, u, lane) : wt[LSS_DEPTH_BCAST ? 0 : u],
-                            meta[e + u].cell);
-        }
-        if (cur >= 0) finish(true);
-        // split cells: inclusive segmented scan over the groups of (restart flag, exported piece)
-        if (__ballot(head_split)) {
-            float c[EPL];
-            bool f = !tail_split || !middle;  // restart unless the group continues its predecessor's cell
-#pragma unroll
-            for (int i = 0; i < EPL; ++i) c[i] = tail_split ? acc[i] : 0.f;
-#pragma unroll
-            for (int d = 1; d < NG; d <<= 1) {
-                const bool fu = __shfl_up((int)f, d * LPR, kWave) != 0;
-                float up[EPL];
-#pragma unroll
-                for (int i = 0; i < EPL; ++i) up[i] = __shfl_up(c[i], d * LPR, kWave);
-                if (grp >= d && !f) {
-#pragma unroll
-                    for (int i = 0; i < EPL; ++i) c[i] = __fadd_rn(up[i], c[i]);
-                    f = fu;
-                }
-            }
-            float carry[EPL];
-#pragma unroll
-            for (int i = 0; i < EPL; ++i) carry[i] = __shfl_up(c[i], LPR, kWave);
-            if (head_split && !middle) {
-                // the head cell ends in this group: predecessors' pieces (in group order) + this group's
-#pragma unroll
-                for (int i = 0; i < EPL; ++i) carry[i] = __fadd_rn(carry[i], hsum[i]);
-                store_slice<EPL>(cell_row(out, first_cell, g) + col, carry);
-            }
-        }
-    } else if (!LSS_MERGED_ZERO_LATE) {
-        zero_unit_rows<OutT>(zu * kWave, emask, g, out, lane);
-    }
-    if (LSS_MERGED_ZERO_LATE) zero_unit_rows<OutT>(zu * kWave, emask, g, out, lane);
-    if (big >= 0) {
-        int cell;
-        const float a2 = reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base, lane,
-                                                    &cell, g.nrows);
-        cell_row(out, cell, g)[lane] = from_f32<OutT>(a2);
-    }
-}
-
 // ----------------------------------------------------------------------------- backward
 template <typename GT>
 __global__ __launch_bounds__(kBlock) void k_bev_rows(const GT* __restrict__ dbev, const int32_t* __restrict__ cell_start,
                                                      SplatGeo sg, GT* __restrict__ rows) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ int s_start[kMaxYT + 1];
+    __shared__ int s_start[kYtMax + 1];
     const int tile = blockIdx.x;
     const int bzx = tile / sg.ntiles_y;
     const int y0 = (tile - bzx * sg.ntiles_y) * sg.YT;
@@ -2904,16 +1859,10 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd_reg(const GT* __restrict__
         for (int e = 0; e < EPL; ++e) dst[(size_t)(D + col + e) * HW] = from_f32<DT>(dc[e]);
 }
 
-#ifndef LSS_BWD_PPW
-#define LSS_BWD_PPW 1  // pixels per wave of k_splat_bwd_tile for bf16 gradients (2: twice the gathers in flight per
-                       // wave but 105 VGPRs, two blocks per CU: 12.2 us vs 10.3 us at c3)
-#endif
-#ifndef LSS_BWD_MIN_WAVES
-#define LSS_BWD_MIN_WAVES 5  // occupancy floor of k_splat_bwd_tile, bf16 rows (waves per SIMD; 70 VGPRs give 7 anyway)
-#endif
-#ifndef LSS_BWD_TILE
-#define LSS_BWD_TILE 1  // 1: k_splat_bwd_tile (pixel tiles, coalesced loads and stores) where the shape allows
-#endif
+// pixels per wave of k_splat_bwd_tile for bf16 gradients (2: twice the gathers in flight per wave but 105
+// VGPRs, two blocks per CU: 12.2 us vs 10.3 us at c3)
+constexpr int kBwdPpw = 1;
+constexpr int kBwdMinWaves = 5;  // occupancy floor of k_splat_bwd_tile, bf16 rows (70 VGPRs give 7 anyway)
 
 // Pixel-tile form of k_splat_bwd_reg. The per-pixel form reads the D depth weights and cells of its
 // pixel at a stride of H*W (one cache line per value) and writes d_depthnet_out one element per
@@ -2926,7 +1875,7 @@ constexpr int kBwdWaves = 8;
 constexpr int kBwdBlock = kBwdWaves * kWave;
 
 template <typename GT, typename DT, typename CT, bool NHWC, int MAXD>  // MAXD: D <= MAXD (48 or 64)
-__global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? LSS_BWD_MIN_WAVES : 4) void k_splat_bwd_tile(const GT* __restrict__ g,
+__global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? kBwdMinWaves : 4) void k_splat_bwd_tile(const GT* __restrict__ g,
                                                               const int32_t* __restrict__ cell_of,
                                                               const float* __restrict__ depth,
                                                               const CT* __restrict__ ctx_t, int D, int HW, int npix,
@@ -2935,7 +1884,7 @@ __global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? LSS_BWD_MIN_WAVES : 4)
     constexpr int LPR = kC / EPL;         // lanes per row
     constexpr int RPI = kWave / LPR;      // rows per wave-instruction
     constexpr int NI = MAXD / RPI;        // instructions for MAXD rows
-    constexpr int PPW = sizeof(GT) == 2 ? LSS_BWD_PPW : 1;  // pixels per wave, all gathers in flight
+    constexpr int PPW = sizeof(GT) == 2 ? kBwdPpw : 1;  // pixels per wave, all gathers in flight
     constexpr int PX = kBwdWaves * PPW;           // pixels per block
     __shared__ float s_dep[MAXD + 1][PX];  // + a spare row for the lanes past the end
     __shared__ int s_cell[MAXD + 1][PX];
@@ -3174,10 +2123,10 @@ inline int device_cus() {
 }
 
 inline int choose_yt(int Y) {
-    if (Y <= LSS_YT_MAX) return Y;
-    for (int t = LSS_YT_MAX; t >= 16; t -= 4)
+    if (Y <= kYtMax) return Y;
+    for (int t = kYtMax; t >= 16; t -= 4)
         if (Y % t == 0) return t;
-    return LSS_YT_MAX;
+    return kYtMax;
 }
 
 // nrows: rows of the feature / gradient buffer the kernel gathers from (0: the dims' pixels)
@@ -3217,31 +2166,6 @@ inline bool grid_ok(const lss_grid_t* g) {
 
 // The empty-row fill that rides along a lift launch: channels-last BEV geometry and the number of
 // 8-block fill groups. bev == nullptr: no fill (0 groups).
-#ifndef LSS_FILL_WAVES
-#define LSS_FILL_WAVES 640  // fill waves beside the lift (c3: 80 idle CUs x 8 waves of k_depthnet_lift2)
-#endif
-struct FillPlan {
-    int groups = 0;
-    BevGeo bg{};
-    unsigned char* bev = nullptr;
-    int esize = 0;
-};
-inline int fill_plan(const lss_dims_t* dims, const lss_grid_t* grid, const int32_t* cell_start, void* bev,
-                     int32_t bev_dtype, int waves_per_block, FillPlan* fp) {
-    if (!bev) return 0;
-    if (!cell_start || !grid_ok(grid) || (bev_dtype != LSS_F32 && bev_dtype != LSS_BF16)) return LSS_EINVAL;
-    fp->bg = BevGeo{};
-    fp->bg.X = grid->nx[0];
-    fp->bg.Y = grid->nx[1];
-    fp->bg.Z = grid->nx[2];
-    fp->bg.ncells = dims->B * fp->bg.Z * fp->bg.X * fp->bg.Y;
-    fp->bev = static_cast<unsigned char*>(bev);
-    fp->esize = bev_dtype == LSS_F32 ? 4 : 2;
-    fp->groups = std::max(1, LSS_FILL_WAVES / (8 * waves_per_block));
-    return 0;
-}
-
-
 }  // namespace
 
 // ============================================================================= C ABI
@@ -3304,14 +2228,6 @@ const char* lss_error_string(int code) {
     return "lss: unknown error";
 }
 
-int lss_camera_inverse(const float* post_rots, const float* intrins, int32_t n_cams, float* pinv, float* kinv,
-                       lss_stream_t stream) {
-    if (!post_rots || !intrins || !pinv || !kinv || n_cams <= 0) return LSS_EINVAL;
-    hipLaunchKernelGGL(k_camera_inverse, dim3(grid_blocks(2L * n_cams, kBlock)), dim3(kBlock), 0,
-                       (hipStream_t)stream, post_rots, intrins, n_cams, pinv, kinv);
-    return launch_status();
-}
-
 int lss_geometry_cells(const float* frustum, const float* rots, const float* trans, const float* kinv,
                        const float* pinv, const float* post_trans, const lss_dims_t* dims, const lss_grid_t* grid,
                        float* out_geom, int32_t* cell_of, int32_t* cell_count, int32_t* slot_of,
@@ -3322,25 +2238,9 @@ int lss_geometry_cells(const float* frustum, const float* rots, const float* tra
     const long DHW = (long)dims->D * dims->H * dims->W;
     const long nprime = (long)dims->B * dims->N * DHW;
     if (nprime >= INT_MAX) return LSS_EUNSUPPORTED;
-    hipLaunchKernelGGL(k_geometry_cells<false>, dim3(grid_blocks(nprime, kGeoBlock)), dim3(kGeoBlock), 0,
+    hipLaunchKernelGGL(k_geometry_cells, dim3(grid_blocks(nprime, kGeoBlock)), dim3(kGeoBlock), 0,
                        (hipStream_t)stream, frustum, rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW,
-                       dims->H * dims->W, dims->W, (int)nprime, *grid, out_geom, cell_of, cell_count, slot_of);
-    return launch_status();
-}
-
-int lss_geometry_cells_axes(const float* axes, const float* rots, const float* trans, const float* kinv,
-                            const float* pinv, const float* post_trans, const lss_dims_t* dims,
-                            const lss_grid_t* grid, float* out_geom, int32_t* cell_of, int32_t* cell_count,
-                            int32_t* slot_of, lss_stream_t stream) {
-    if (!dims_ok(dims) || !grid_ok(grid) || !axes || !rots || !trans || !kinv || !pinv || !post_trans || !cell_of)
-        return LSS_EINVAL;
-    if (cell_count && !slot_of) return LSS_EINVAL;
-    const long DHW = (long)dims->D * dims->H * dims->W;
-    const long nprime = (long)dims->B * dims->N * DHW;
-    if (nprime >= INT_MAX) return LSS_EUNSUPPORTED;
-    hipLaunchKernelGGL(k_geometry_cells<true>, dim3(grid_blocks(nprime, kGeoBlock)), dim3(kGeoBlock), 0,
-                       (hipStream_t)stream, axes, rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW,
-                       dims->H * dims->W, dims->W, (int)nprime, *grid, out_geom, cell_of, cell_count, slot_of);
+                       (int)nprime, *grid, out_geom, cell_of, cell_count, slot_of);
     return launch_status();
 }
 
@@ -3360,7 +2260,7 @@ size_t lss_csr_scratch_bytes(int32_t ncells, int32_t nprime) {
 
 int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, const int32_t* cell_count,
                   int32_t ncells, const lss_dims_t* dims, int32_t* cell_start, long long* sorted_key,
-                  int32_t* sorted_row, int32_t* pos_of, void* scratch, lss_stream_t stream) {
+                  int32_t* sorted_row, void* scratch, lss_stream_t stream) {
     if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !sorted_row || !scratch || nprime <= 0 ||
         ncells <= 0)
         return LSS_EINVAL;
@@ -3382,58 +2282,21 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
                        cell_start, tmp_key);
     const int nchunks = (nprime + kWave - 1) / kWave;
     hipLaunchKernelGGL(k_csr_canon, dim3(xcd_grid(grid_blocks(nchunks, kBlock / kWave))), dim3(kBlock), 0, s, tmp_key,
-                       cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row, cell_of, pos_of);
+                       cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row);
     debug_check_csr(cell_start, ncells, cell_of, nprime, s);
     return launch_status();
 }
 
 size_t lss_csr_workspace_bytes(int32_t ncells) {
     const size_t nb = (size_t)((ncells + kScanItems - 1) / kScanItems);
-    // header, look-back granules, per-group aggregates (lss_plan_ws)
-    return sizeof(ScanWs) + sizeof(unsigned long long) * nb + sizeof(int32_t) * kAggRep * nb;
-}
-
-int lss_plan_ws(const float* frustum, const float* rots, const float* trans, const float* kinv, const float* pinv,
-                const float* post_trans, const lss_dims_t* dims, const lss_grid_t* grid, int32_t* cell_of,
-                int32_t* slot_of, int32_t* cell_count, int32_t* cell_start, long long* sorted_key, int32_t* sorted_row,
-                int32_t* pos_of, void* scratch, void* workspace, lss_stream_t stream) {
-    if (!dims_ok(dims) || !grid_ok(grid) || !frustum || !rots || !trans || !kinv || !pinv || !post_trans || !cell_of ||
-        !slot_of || !cell_count || !cell_start || !sorted_key || !sorted_row || !scratch || !workspace)
-        return LSS_EINVAL;
-    const long DHW = (long)dims->D * dims->H * dims->W;
-    const long nprime_l = (long)dims->B * dims->N * DHW;
-    const long ncells_l = (long)dims->B * grid->nx[0] * grid->nx[1] * grid->nx[2];
-    if (nprime_l >= INT_MAX || ncells_l >= INT_MAX) return LSS_EUNSUPPORTED;
-    const int nprime = (int)nprime_l, ncells = (int)ncells_l;
-    const int nb = (ncells + kScanItems - 1) / kScanItems;
-    ScanWs* ws = static_cast<ScanWs*>(workspace);
-    int32_t* agg = reinterpret_cast<int32_t*>(reinterpret_cast<unsigned long long*>(ws + 1) + nb);
-    const size_t poff = ((sizeof(int32_t) * (size_t)(nb + 1)) + 255) & ~(size_t)255;  // as lss_csr_build
-    long long* tmp_key = reinterpret_cast<long long*>(static_cast<char*>(scratch) + poff);
-    hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL((k_geometry_cells<false, true>), dim3(grid_blocks(nprime, kGeoBlock)), dim3(kGeoBlock), 0, s, frustum,
-                       rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW, dims->H * dims->W, dims->W, nprime,
-                       *grid, nullptr, cell_of, cell_count, slot_of, agg);
-    hipLaunchKernelGGL(k_scan_agg, dim3(nb), dim3(1024), 0, s, cell_count, ncells, agg, cell_start);
-    hipLaunchKernelGGL(k_scatter_ws, dim3(grid_blocks(std::max(std::max(nprime, ncells), nb * kAggRep), kBlock)),
-                       dim3(kBlock), 0, s, cell_of, slot_of, nprime, cell_start, tmp_key, cell_count, ncells, ws, 0,
-                       agg);
-    const int nchunks = (nprime + kWave - 1) / kWave;
-    hipLaunchKernelGGL(k_csr_canon, dim3(xcd_grid(grid_blocks(nchunks, kBlock / kWave))), dim3(kBlock), 0, s, tmp_key,
-                       cell_start + ncells, nchunks, nprime, (int)DHW, dims->H * dims->W, sorted_key, sorted_row,
-                       cell_of, pos_of);
-    debug_check_csr(cell_start, ncells, cell_of, nprime, s);
-    return launch_status();
+    return sizeof(ScanWs) + sizeof(unsigned long long) * nb;  // header, look-back granules
 }
 
 int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, int32_t* cell_count,
                      int32_t ncells, const lss_dims_t* dims, int32_t* cell_start, long long* sorted_key,
-                     int32_t* sorted_row, int32_t* pos_of, void* scratch, void* workspace, lss_stream_t stream) {
-    // sorted_row == NULL (and pos_of == NULL): the CSR in arrival order inside each cell, no
-    // canonical pass (lss_splat_fwd LSS_SPLAT_UNORDERED puts each cell in order itself)
-    const bool canonical = sorted_row != nullptr;
-    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || (!canonical && pos_of) || !scratch ||
-        !workspace || nprime <= 0 || ncells <= 0)
+                     int32_t* sorted_row, void* scratch, void* workspace, lss_stream_t stream) {
+    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !sorted_row || !scratch || !workspace ||
+        nprime <= 0 || ncells <= 0)
         return LSS_EINVAL;
     int DHW = nprime, HW = nprime;  // no dims: the row of point p is p (per-point rows)
     if (dims != nullptr) {
@@ -3449,15 +2312,10 @@ int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t npr
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(k_scan_lookback, dim3(nb), dim3(1024), 0, s, cell_count, ncells, ws, cell_start);
     hipLaunchKernelGGL(k_scatter_ws, dim3(grid_blocks(std::max(nprime, ncells), kBlock)), dim3(kBlock), 0, s, cell_of,
-                       slot_of, nprime, cell_start, canonical ? tmp_key : sorted_key, cell_count, ncells, ws,
-                       canonical ? 0 : 1);
-    if (!canonical) {
-        debug_check_csr(cell_start, ncells, cell_of, nprime, s);
-        return launch_status();
-    }
+                       slot_of, nprime, cell_start, tmp_key, cell_count, ncells, ws);
     const int nchunks = (nprime + kWave - 1) / kWave;
     hipLaunchKernelGGL(k_csr_canon, dim3(xcd_grid(grid_blocks(nchunks, kBlock / kWave))), dim3(kBlock), 0, s, tmp_key,
-                       cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row, cell_of, pos_of);
+                       cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row);
     debug_check_csr(cell_start, ncells, cell_of, nprime, s);
     return launch_status();
 }
@@ -3476,21 +2334,17 @@ int lss_debug_status(int32_t* out4, int32_t clear) {
 }
 
 int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* dims, float* depth, void* ctx_t,
-                  int32_t ctx_dtype, const int32_t* pos_of, float* sorted_depth, const int32_t* cell_start,
-                  const lss_grid_t* bev_grid, void* bev, int32_t bev_dtype, lss_stream_t stream) {
-    if (!dims_ok(dims) || !depthnet_out || !depth || !ctx_t || (pos_of && !sorted_depth)) return LSS_EINVAL;
+                  int32_t ctx_dtype, lss_stream_t stream) {
+    if (!dims_ok(dims) || !depthnet_out || !depth || !ctx_t) return LSS_EINVAL;
     if (dims->D > 256) return LSS_EUNSUPPORTED;
-    FillPlan fp;
-    if (fill_plan(dims, bev_grid, cell_start, bev, bev_dtype, kBlock / kWave, &fp)) return LSS_EINVAL;
     const int HW = dims->H * dims->W;
     const int npix = dims->B * dims->N * HW;
-    const int nlg = (grid_blocks(npix, 64) + 7) / 8;
-    const dim3 grid(8 * (nlg + fp.groups)), block(kBlock);
+    const dim3 grid(xcd_grid(grid_blocks(npix, 64))), block(kBlock);
     hipStream_t s = (hipStream_t)stream;
     // depth bins per wave part: 16 (D <= 64, the reference's D = 41), 32, 64
 #define LSS_PREP_NI(IT, CT, NI)                                                                                    \
     hipLaunchKernelGGL((k_lift_prep<IT, CT, NI>), grid, block, 0, s, (const IT*)depthnet_out, dims->D, HW, npix,  \
-                       depth, (CT*)ctx_t, pos_of, sorted_depth, nlg, fp.groups, cell_start, fp.bg, fp.bev, fp.esize)
+                       depth, (CT*)ctx_t)
 #define LSS_PREP(IT, CT)                                                                                           \
     do {                                                                                                           \
         if (dims->D <= 64) LSS_PREP_NI(IT, CT, 16);                                                                \
@@ -3508,159 +2362,84 @@ int lss_lift_prep(const void* depthnet_out, int32_t in_dtype, const lss_dims_t* 
 }
 
 int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
-                      const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, const int32_t* pos_of,
-                      float* sorted_depth, const int32_t* cell_start, const lss_grid_t* bev_grid, void* bev,
-                      int32_t bev_dtype, lss_stream_t stream) {
-    if (!dims_ok(dims) || !feat || !weight || !bias || !depth || !ctx_t || (pos_of && !sorted_depth)) return LSS_EINVAL;
+                      const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream) {
+    if (!dims_ok(dims) || !feat || !weight || !bias || !depth || !ctx_t) return LSS_EINVAL;
     if (dtype != LSS_BF16 || ctx_dtype != LSS_BF16) return LSS_EUNSUPPORTED;
     if (K <= 0 || K % 16 != 0 || K > kDnMaxK || dims->D + kC > kDnMaxO) return LSS_EUNSUPPORTED;
     const int HW = dims->H * dims->W;
     const long npix = (long)dims->B * dims->N * HW;
     if (npix >= INT_MAX) return LSS_EUNSUPPORTED;
-    FillPlan fp;
     hipStream_t s = (hipStream_t)stream;
-    if (LSS_DN_IMPL == 2 && K == 512 && HW % 8 == 0) {  // up1's 512 channels
-        // one lift block per CU (its LDS); the fill blocks take the CUs left idle (c3: 176 lift blocks
-        // on 256 CUs), at least LSS_FILL_WAVES waves of them
-        if (fill_plan(dims, bev_grid, cell_start, bev, bev_dtype, kDn2Waves, &fp)) return LSS_EINVAL;
-        const int nlb = grid_blocks(npix, kDn2Pix), nlg = (nlb + 7) / 8;
-        if (fp.bev) fp.groups = std::max(fp.groups, (device_cus() - nlb + 7) / 8);
-        const dim3 gr(8 * (nlg + fp.groups)), bl(kDn2Block);
-        if (pos_of)
-            hipLaunchKernelGGL((k_depthnet_lift2<512, kDn2Pix, true>), gr, bl, 0, s, (const bf16*)feat,
-                               (const bf16*)weight, (const bf16*)bias, dims->D, HW, (int)npix, depth, (bf16*)ctx_t,
-                               pos_of, sorted_depth, nlg, fp.groups, cell_start, fp.bg, fp.bev, fp.esize);
-        else
-            hipLaunchKernelGGL((k_depthnet_lift2<512, kDn2Pix, false>), gr, bl, 0, s, (const bf16*)feat,
-                               (const bf16*)weight, (const bf16*)bias, dims->D, HW, (int)npix, depth, (bf16*)ctx_t,
-                               nullptr, nullptr, nlg, fp.groups, cell_start, fp.bg, fp.bev, fp.esize);
+    if (K == 512 && HW % 8 == 0) {  // up1's 512 channels: k_depthnet_lift2, one block per CU (its LDS)
+        hipLaunchKernelGGL((k_depthnet_lift2<512, kDn2Pix>), dim3(xcd_grid(grid_blocks(npix, kDn2Pix))),
+                           dim3(kDn2Block), 0, s, (const bf16*)feat, (const bf16*)weight, (const bf16*)bias, dims->D,
+                           HW, (int)npix, depth, (bf16*)ctx_t);
         return launch_status();
     }
-    if (fill_plan(dims, bev_grid, cell_start, bev, bev_dtype, kBlock / kWave, &fp)) return LSS_EINVAL;
     hipLaunchKernelGGL(k_depthnet_lift, dim3(xcd_grid(grid_blocks(npix, kDnPix))), dim3(kBlock), 0, s,
                        (const bf16*)feat, (const bf16*)weight, (const bf16*)bias, K, dims->D, HW, (int)npix, depth,
-                       (bf16*)ctx_t, pos_of, sorted_depth);
-    if (fp.bev)  // this lift kernel has no fill role: the fill as a launch of its own
-        hipLaunchKernelGGL(k_fill_empty, dim3(8 * fp.groups), dim3(kBlock), 0, s, cell_start, fp.bg, fp.bev, fp.esize);
+                       (bf16*)ctx_t);
     return launch_status();
 }
 
 int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
-                           const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, const int32_t* pos_of,
-                           float* sorted_depth, const int32_t* cell_start, const lss_grid_t* bev_grid, void* bev,
-                           int32_t bev_dtype, lss_stream_t stream) {
-    if (!dims_ok(dims) || !feat || !weight || !bias || !depth || !ctx_t || (pos_of && !sorted_depth)) return LSS_EINVAL;
+                           const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream) {
+    if (!dims_ok(dims) || !feat || !weight || !bias || !depth || !ctx_t) return LSS_EINVAL;
+    if (((uintptr_t)feat | (uintptr_t)weight) & 15) return LSS_EINVAL;  // 16-B vector loads of the rows
     if (dtype != LSS_BF16 || ctx_dtype != LSS_BF16) return LSS_EUNSUPPORTED;
     if (K != 512 || dims->D + kC > kDnMaxO) return LSS_EUNSUPPORTED;
     const int HW = dims->H * dims->W;
     const long npix = (long)dims->B * dims->N * HW;
     if (npix >= INT_MAX / 2) return LSS_EUNSUPPORTED;
-    FillPlan fp;
-    if (fill_plan(dims, bev_grid, cell_start, bev, bev_dtype, kDn3Waves, &fp)) return LSS_EINVAL;
     // one block per CU, more only when a CU's share would pass kDn3MaxPix pixels; never more than
     // the pixels (every block holds at least one)
-    const long nlift = LSS_DN3_PIX > 0 ? (npix + std::min(LSS_DN3_PIX, kDn3MaxPix) - 1) / std::min(LSS_DN3_PIX, kDn3MaxPix)
-                                       : std::min<long>(npix, std::max<long>(device_cus(), (npix + kDn3MaxPix - 1) / kDn3MaxPix));
-    const int nfill = fp.bev ? 8 * fp.groups : 0;
-    const int nlgrid = xcd_grid(nlift);
+    const long nlift = std::min<long>(npix, std::max<long>(device_cus(), (npix + kDn3MaxPix - 1) / kDn3MaxPix));
     hipStream_t s = (hipStream_t)stream;
-    const dim3 gr((unsigned)(nlgrid + nfill)), bl(kDn3Block);
-    if (pos_of)
-        hipLaunchKernelGGL((k_depthnet_lift3<512, true>), gr, bl, 0, s, (const bf16*)feat, (const bf16*)weight,
-                           (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, nlgrid, depth, (bf16*)ctx_t, pos_of,
-                           sorted_depth, nfill, cell_start, fp.bg, fp.bev, fp.esize);
-    else
-        hipLaunchKernelGGL((k_depthnet_lift3<512, false>), gr, bl, 0, s, (const bf16*)feat, (const bf16*)weight,
-                           (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, nlgrid, depth, (bf16*)ctx_t,
-                           nullptr, nullptr, nfill, cell_start, fp.bg, fp.bev, fp.esize);
+    hipLaunchKernelGGL((k_depthnet_lift3<512>), dim3(xcd_grid(nlift)), dim3(kDn3Block), 0, s, (const bf16*)feat,
+                       (const bf16*)weight, (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, depth,
+                       (bf16*)ctx_t);
     return launch_status();
 }
 
 int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
                   const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
-                  const float* sorted_depth,
                   const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout,
-                  int32_t flags, lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop) {
+                  lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop) {
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
-    if (flags & ~(LSS_SPLAT_EMPTY_FILLED | LSS_SPLAT_UNORDERED)) return LSS_EINVAL;
-    if ((flags & LSS_SPLAT_EMPTY_FILLED) && out_layout != LSS_NHWC) return LSS_EINVAL;
-    const bool unordered = (flags & LSS_SPLAT_UNORDERED) != 0;
-    if (unordered && (out_layout != LSS_NHWC || sorted_depth || LSS_SPLAT_IMPL != 0)) return LSS_EINVAL;
-    if (unordered && !LSS_SPLAT_UNORDERED_CODE) return LSS_EUNSUPPORTED;
     if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_key || !out) return LSS_EINVAL;
     const bool fused = x_rows == nullptr;
-    if (fused && (!depth || !ctx_t || (!sorted_row && !unordered))) return LSS_EINVAL;
+    if (fused && (!depth || !ctx_t || !sorted_row)) return LSS_EINVAL;
     if (fused && ctx_dtype != LSS_F32 && ctx_dtype != LSS_BF16) return LSS_EINVAL;
     if (out_dtype != LSS_F32 && out_dtype != LSS_BF16) return LSS_EINVAL;
+    if (out_layout != LSS_NCHW && out_layout != LSS_NHWC) return LSS_EINVAL;
     const long nprime_l = (long)dims->B * dims->N * dims->D * dims->H * dims->W;
     if (nprime_l >= INT_MAX - 2 * kWave) return LSS_EUNSUPPORTED;
     const int nprime = (int)nprime_l;
     const SplatGeo sg = splat_geo(grid, dims, fused ? 0 : nprime_l);  // lifted mode: one row per point
-    const bool nhwc = out_layout == LSS_NHWC;
     const bool ctx_bf16 = fused && ctx_dtype == LSS_BF16;
     const void* rows = fused ? ctx_t : (const void*)x_rows;
     hipStream_t s = (hipStream_t)stream;
-    if (nhwc) {
+    if (out_layout == LSS_NHWC) {
         BevGeo g;
         g.X = sg.X; g.Y = sg.Y; g.Z = sg.Z;
         g.ncells = dims->B * sg.Z * sg.X * sg.Y;
-        g.hw = dims->H * dims->W;
-        g.dhw = nprime < (1 << 24) ? dims->D * g.hw : 0;  // 0: read sorted_row instead
-        if (unordered && fused && g.dhw == 0) return LSS_EUNSUPPORTED;  // rows from point ids: p < 2^24
-        g.inv_dhw = g.dhw ? 1.0f / (float)g.dhw : 0.f;
-        g.inv_hw = 1.0f / (float)g.hw;
         g.nrows = sg.nrows;
-        const int wpb = kSplatWaves;
-        if (LSS_SPLAT_IMPL == 1) {
-            const int nchunks = grid_blocks(nprime, kWave), nunits = grid_blocks(g.ncells, kWave);
-            const dim3 grm(8 * grid_blocks(grid_blocks(std::max(nchunks, nunits), wpb), 8)), blm(kSplatBlock);
-#define LSS_NHWC_FWD_M(F, RT, T)                                                                                   \
-    do {                                                                                                           \
-        if (e0 || e1)                                                                                              \
-            hipExtLaunchKernelGGL((k_splat_fwd_nhwc_m<F, RT, T>), grm, blm, 0, s, e0, e1, 0, depth, sorted_depth,  \
-                                  (const RT*)rows, cell_start, sorted_key, sorted_row, g, nprime, nchunks, nunits, \
-                                  (T*)out);                                                                        \
-        else                                                                                                       \
-            hipLaunchKernelGGL((k_splat_fwd_nhwc_m<F, RT, T>), grm, blm, 0, s, depth, sorted_depth,                \
-                               (const RT*)rows, cell_start, sorted_key, sorted_row, g, nprime, nchunks, nunits,    \
-                               (T*)out);                                                                           \
-    } while (0)
-            if (out_dtype == LSS_F32) {
-                if (!fused) LSS_NHWC_FWD_M(false, float, float);
-                else if (ctx_bf16) LSS_NHWC_FWD_M(true, bf16, float);
-                else LSS_NHWC_FWD_M(true, float, float);
-            } else {
-                if (!fused) LSS_NHWC_FWD_M(false, float, bf16);
-                else if (ctx_bf16) LSS_NHWC_FWD_M(true, bf16, bf16);
-                else LSS_NHWC_FWD_M(true, float, bf16);
-            }
-#undef LSS_NHWC_FWD_M
-            return launch_status();
-        }
-        const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), wpb);
-        // the empty rows' zero fill: here, or already done beside the lift (LSS_SPLAT_EMPTY_FILLED)
-        const int nzero_blocks = (flags & LSS_SPLAT_EMPTY_FILLED)
-                                     ? 0 : grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), wpb);
+        const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), kSplatWaves);
+        const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), kSplatWaves);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);
-        // Dispatch order of the two roles: chunks first (c3: all 5,386 chunk waves start at t = 0 in
-        // the 7,168 wave slots and the zero waves take the slots left). LSS_INTERLEAVE=-1 interleaves
-        // once the chunk waves outnumber the slots (c5: 12,420): faster in kbench's step order (25.0
-        // -> 23.0 us) but not inside the c5 training step's graph replays (rocprof A/B on one box:
-        // 26.2 / 25.3 us interleaved vs 25.1 / 25.3 chunks first), so it is off.
-        const long slots = (long)device_cus() * 4 * LSS_MIN_WAVES;
-        const int order = LSS_INTERLEAVE >= 0 ? LSS_INTERLEAVE : ((long)nchunk_blocks * wpb > slots ? 1 : 0);
+        // Dispatch order of the two roles (LSS_INTERLEAVE): chunks first by default (c3: all 5,386 chunk
+        // waves start at t = 0 in the 7,168 wave slots and the zero waves take the slots left).
+        const int order = LSS_INTERLEAVE;
 // kernel-stamped events only when asked for: a plain launch is what a hipGraph capture records
 #define LSS_NHWC_FWD(F, RT, T)                                                                                     \
     do {                                                                                                           \
         if (e0 || e1)                                                                                              \
-            hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, sorted_depth,      \
-                                  (const RT*)rows,                                                                 \
+            hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, (const RT*)rows,   \
                                   cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks,      \
-                                  order, (int)unordered, (T*)out);                                                 \
+                                  order, (T*)out);                                                                 \
         else                                                                                                       \
-            hipLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, depth, sorted_depth, (const RT*)rows,   \
-                               cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, order,  \
-                               (int)unordered, (T*)out);                                                           \
+            hipLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, depth, (const RT*)rows, cell_start,     \
+                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, order, (T*)out);    \
     } while (0)
         if (out_dtype == LSS_F32) {
             if (!fused) LSS_NHWC_FWD(false, float, float);
@@ -3674,12 +2453,10 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
 #undef LSS_NHWC_FWD
         return launch_status();
     }
-    if (sg.YT > kMaxYT) return LSS_EUNSUPPORTED;
+    if (sg.YT > kYtMax) return LSS_EUNSUPPORTED;  // (choose_yt never picks more)
     const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
-    const size_t lds = (size_t)kC * (sg.YT + 4) * sizeof(float);
-    if (LSS_NCHW_IMPL == 2 && sg.YT <= 128) {
-        const dim3 gr2(xcd_grid(nblocks)), bl2(kN2Block);
-        const size_t lds2 = (size_t)kC * nchw2_stride(sg.YT) * sizeof(float);
+    const dim3 gr2(xcd_grid(nblocks)), bl2(kN2Block);
+    const size_t lds2 = (size_t)kC * nchw2_stride(sg.YT) * sizeof(float);
 #define LSS_SPLAT2(F, RT, T)                                                                                      \
     do {                                                                                                          \
         if (e0 || e1)                                                                                             \
@@ -3689,38 +2466,16 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
             hipLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T>), gr2, bl2, lds2, s, depth, (const RT*)rows,          \
                                cell_start, sorted_key, sorted_row, sg, nblocks, (T*)out);                         \
     } while (0)
-        if (out_dtype == LSS_F32) {
-            if (!fused) LSS_SPLAT2(false, float, float);
-            else if (ctx_bf16) LSS_SPLAT2(true, bf16, float);
-            else LSS_SPLAT2(true, float, float);
-        } else {
-            if (!fused) LSS_SPLAT2(false, float, bf16);
-            else if (ctx_bf16) LSS_SPLAT2(true, bf16, bf16);
-            else LSS_SPLAT2(true, float, bf16);
-        }
-#undef LSS_SPLAT2
-        return launch_status();
-    }
-#define LSS_SPLAT(F, RT, T)                                                                                       \
-    do {                                                                                                          \
-        if (e0 || e1)                                                                                             \
-            hipExtLaunchKernelGGL((k_splat_fwd<F, RT, T, false>), dim3(nblocks), dim3(kFwdBlock), (uint32_t)lds, \
-                                  s, e0, e1, 0, depth, (const RT*)rows, cell_start, sorted_key, sorted_row, sg,   \
-                                  nprime, (T*)out);                                                               \
-        else                                                                                                      \
-            hipLaunchKernelGGL((k_splat_fwd<F, RT, T, false>), dim3(nblocks), dim3(kFwdBlock), lds, s, depth,     \
-                               (const RT*)rows, cell_start, sorted_key, sorted_row, sg, nprime, (T*)out);         \
-    } while (0)
     if (out_dtype == LSS_F32) {
-        if (!fused) LSS_SPLAT(false, float, float);
-        else if (ctx_bf16) LSS_SPLAT(true, bf16, float);
-        else LSS_SPLAT(true, float, float);
+        if (!fused) LSS_SPLAT2(false, float, float);
+        else if (ctx_bf16) LSS_SPLAT2(true, bf16, float);
+        else LSS_SPLAT2(true, float, float);
     } else {
-        if (!fused) LSS_SPLAT(false, float, bf16);
-        else if (ctx_bf16) LSS_SPLAT(true, bf16, bf16);
-        else LSS_SPLAT(true, float, bf16);
+        if (!fused) LSS_SPLAT2(false, float, bf16);
+        else if (ctx_bf16) LSS_SPLAT2(true, bf16, bf16);
+        else LSS_SPLAT2(true, float, bf16);
     }
-#undef LSS_SPLAT
+#undef LSS_SPLAT2
     return launch_status();
 }
 
@@ -3772,9 +2527,9 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
     } while (0)
 #define LSS_BWD(GT, DT, CT)                                                                                       \
     do {                                                                                                          \
-        constexpr int px = kBwdWaves * (sizeof(GT) == 2 ? LSS_BWD_PPW : 1);                                       \
+        constexpr int px = kBwdWaves * (sizeof(GT) == 2 ? kBwdPpw : 1);                                       \
         const dim3 grt(xcd_grid(npix / px)), blt(kBwdBlock);                                                      \
-        const bool tile = LSS_BWD_TILE && HW % px == 0 && D <= 64;                                                \
+        const bool tile = HW % px == 0 && D <= 64;                                                \
         if (tile && nhwc && D <= 48)                                                                              \
             hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, true, 48>), grt, blt, 0, s, (const GT*)g, cell_of,  \
                                depth, (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                    \

@@ -20,8 +20,8 @@ stock PyTorch-ROCm modules (MIOpen / MFMA). The hot path refuses CPU tensors.
 Extra knobs (not in the reference, defaults reproduce it):
   ``bev_layout``     'nchw' (reference layout) or 'nhwc' (channels-last BEV, feeds a
                      channels-last BevEncode without a transpose)
-  ``inverse``        'host' (torch.inverse on the CPU, as src/models.py:180,186) or
-                     'device' (no host round trip)
+  ``static_inverses`` (pinv, kinv) device buffers staged from the host's torch.inverse before a
+                     captured step (ops.HostInverses); None: computed per forward, as the reference
   ``fuse_depthnet``  under bf16 autocast, run the depthnet 1x1 conv inside the lift kernel
                      (MFMA); off: the conv runs as its own op (MIOpen)
 """
@@ -39,9 +39,9 @@ from . import resample
 from .norm import bn_act
 from .tools import gen_dx_bx
 
-# CamEncode.up1 on channels-last maps under bf16 autocast (see get_eff_depth); LSS_UP1_CL=0: NCHW (A/B)
-UP1_CHANNELS_LAST = os.environ.get("LSS_UP1_CL", "1") != "0"
-UNORDERED_PLAN = False  # channels-last BEV: plans without the canonical pass (the splat orders each cell); measured slower
+# CamEncode.up1 on channels-last maps under bf16 autocast (see get_eff_depth); False: NCHW (the unfused
+# channel-plane lift, k_depthnet_lift2; tests switch it)
+UP1_CHANNELS_LAST = True
 
 
 class Up(nn.Module):
@@ -293,16 +293,6 @@ class BevEncode(nn.Module):
         return conv1x1(u[4], bn_act(u[2], u[1](x), "relu"))
 
 
-_SIDE_STREAMS = {}
-
-
-def _side_stream(device: torch.device) -> torch.cuda.Stream:
-    """One side stream per device for the plan (kept off the module: modules stay deep-copyable)."""
-    if device not in _SIDE_STREAMS:
-        _SIDE_STREAMS[device] = torch.cuda.Stream(device)
-    return _SIDE_STREAMS[device]
-
-
 class LiftSplatShoot(nn.Module):
     def __init__(self, grid_conf, data_aug_conf, outC):
         super().__init__()
@@ -321,15 +311,10 @@ class LiftSplatShoot(nn.Module):
         # toggle kept for API compatibility (src/models.py:155); both settings run the same kernels.
         self.use_quickcumsum = True
         self.bev_layout = "nchw"
-        self.inverse = "host"
         self.fuse_depthnet = True  # bf16 autocast: depthnet conv fused into the lift kernel
         # (pinv, kinv) device buffers filled from host torch.inverse by ops.HostInverses before the
-        # step (captured training step); None: get_voxels computes them per `inverse`
+        # step (captured training step); None: get_voxels computes them (host torch.inverse)
         self.static_inverses = None
-        # True: build the plan (geometry + CSR, which depend only on the rig) on a side stream while
-        # the trunk runs, joined before the lift (the fork/join is captured into the graph too).
-        # Off: in the captured c3 step the two-branch graph ran 16.0 ms/step against 15.1 serial.
-        self.plan_side_stream = False
         self._grid = ops.GridSpec.from_conf(grid_conf)
 
     def create_frustum(self):
@@ -354,12 +339,12 @@ class LiftSplatShoot(nn.Module):
     def plan(self, rots, trans, intrins, post_rots, post_trans, want_geom=False) -> ops.SplatPlan:
         """Geometry + voxel assignment + CSR of points by cell for one batch of rigs."""
         return ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
-                                     inverse=self.inverse, want_geom=want_geom)
+                                     want_geom=want_geom)
 
     def get_geometry(self, rots, trans, intrins, post_rots, post_trans):
         """(B, N, D, fH, fW, 3) ego-frame points (src/models.py:170-190), HIP kernel."""
         p = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
-                                  inverse=self.inverse, want_geom=True, want_csr=False)
+                                  want_geom=True, want_csr=False)
         return p.geom
 
     def get_cam_feats(self, x):
@@ -378,33 +363,18 @@ class LiftSplatShoot(nn.Module):
     def get_voxels(self, x, rots, trans, intrins, post_rots, post_trans):
         """Fused hot path: trunk, geometry/CSR, lift+splat (src/models.py:248-254).
 
-        Schedule: the camera inverses first (inverse='host' copies the rig to the host, which must
-        not wait behind the trunk), then the trunk, then the plan kernels (optionally on a side
-        stream beside the trunk: plan_side_stream), then the fused lift and the splat.
+        Schedule: the camera inverses first (the host's torch.inverse copies the rig to the host,
+        which must not wait behind the trunk), then the trunk, then the plan kernels, then the fused
+        lift and the splat.
         """
         B, N, C, imH, imW = x.shape
         inv = self.static_inverses
         if inv is None:
-            inv = ops.camera_inverses(post_rots, intrins, self.inverse)
+            inv = ops.camera_inverses(post_rots, intrins)
         ce = self.camencode
-        side = None
-        # the channels-last splat ranks each cell's entries itself: its plan skips the canonical pass
-        canonical = not (UNORDERED_PLAN and self._layout() == _lib.NHWC)
-        if self.plan_side_stream and x.is_cuda:
-            side, main = _side_stream(x.device), torch.cuda.current_stream(x.device)
-            side.wait_stream(main)  # the rig and its inverses (staged by pre_step) are ready
-            with torch.cuda.stream(side):
-                plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
-                                             inverses=inv, canonical=canonical)
         feat = ce.dropout(ce.get_eff_depth(x.view(B * N, C, imH, imW)))
-        if side is None:
-            plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
-                                         inverses=inv, canonical=canonical)
-        else:
-            main.wait_stream(side)
-            if not torch.cuda.is_current_stream_capturing():  # (a captured graph's pool is never reused)
-                for t in plan.tensors():
-                    t.record_stream(main)  # allocated on the side stream, read on this one
+        plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
+                                     inverses=inv)
         out_dtype = self._bev_dtype(x.device)
         if self.fuse_depthnet and out_dtype == torch.bfloat16 and self.D + self.camC <= 128:
             # depthnet 1x1 conv + softmax + context layout in one MFMA kernel (SURVEY.md §8f row 1); its

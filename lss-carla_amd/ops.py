@@ -1,9 +1,9 @@
 """Host orchestration of the HIP hot path: geometry, CSR, fused lift+splat autograd.
 
 Every function here takes device tensors, launches on the current HIP stream
-of that device, never synchronises with the host (except the opt-in
-``inverse='host'`` mode, which mirrors the reference's ``torch.inverse(x.cpu())``
-exactly) and never falls back to another implementation.
+of that device, never synchronises with the host (except camera_inverses, which
+mirrors the reference's ``torch.inverse(x.cpu())`` exactly, when the rig carries no
+host copy) and never falls back to another implementation.
 
 Reference boundary replaced (shdragron/LSS-Carla):
   get_geometry            src/models.py:170-190
@@ -15,8 +15,6 @@ Reference boundary replaced (shdragron/LSS-Carla):
 from __future__ import annotations
 
 import ctypes
-import os
-import weakref
 from dataclasses import dataclass
 from typing import Optional, Sequence, Tuple
 
@@ -79,37 +77,25 @@ def _f32c(t: torch.Tensor) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------- cameras
-def camera_inverses(post_rots: torch.Tensor, intrins: torch.Tensor, mode: str = "host"):
-    """inv(post_rots), inv(intrins) as (B*N, 9) fp32 device tensors.
-
-    mode='host'   : torch.inverse on the CPU, exactly as src/models.py:180,186 (one D2H + H2D copy;
-                    no D2H copy when the device tensors carry their host copies, ``t._lss_host``,
-                    as simbev.finish_batch attaches them: then nothing synchronises the host).
-    mode='device' : lss_camera_inverse (fp64 adjugate rounded to fp32), no host round trip.
+def camera_inverses(post_rots: torch.Tensor, intrins: torch.Tensor):
+    """inv(post_rots), inv(intrins) as (B*N, 9) fp32 device tensors: torch.inverse on the CPU, exactly as
+    src/models.py:180,186 (one D2H + H2D copy; no D2H copy when the device tensors carry their host
+    copies, ``t._lss_host``, as simbev.finish_batch attaches them: then nothing synchronises the host).
     """
     dev = _require_cuda(post_rots, intrins)
     ncam = post_rots.shape[0] * post_rots.shape[1]
-    if mode == "host":
-        def host_copy(t):
-            # the attached host copy only while the device tensor is unchanged since it was attached
-            # (an in-place copy_ into a reused batch buffer bumps _version: then read the device tensor)
-            h = getattr(t, "_lss_host", None)
-            if (h is not None and tuple(h.shape) == tuple(t.shape) and not h.is_cuda
-                    and getattr(t, "_lss_host_version", None) == t._version):
-                return h
-            return t.detach().cpu()
-        pinv = torch.inverse(host_copy(post_rots).float()).reshape(ncam, 9).pin_memory()
-        kinv = torch.inverse(host_copy(intrins).float()).reshape(ncam, 9).pin_memory()
-        return pinv.to(dev, non_blocking=True), kinv.to(dev, non_blocking=True)
-    if mode != "device":
-        raise ValueError(f"inverse mode must be 'host' or 'device', got {mode!r}")
-    lib = _lib.load()
-    pr, it = _f32c(post_rots), _f32c(intrins)
-    pinv = torch.empty(ncam, 9, device=dev, dtype=torch.float32)
-    kinv = torch.empty(ncam, 9, device=dev, dtype=torch.float32)
-    _lib.check(lib.lss_camera_inverse(_lib.ptr(pr), _lib.ptr(it), ncam, _lib.ptr(pinv), _lib.ptr(kinv),
-                                      _lib.stream_handle(dev)), "lss_camera_inverse")
-    return pinv, kinv
+
+    def host_copy(t):
+        # the attached host copy only while the device tensor is unchanged since it was attached
+        # (an in-place copy_ into a reused batch buffer bumps _version: then read the device tensor)
+        h = getattr(t, "_lss_host", None)
+        if (h is not None and tuple(h.shape) == tuple(t.shape) and not h.is_cuda
+                and getattr(t, "_lss_host_version", None) == t._version):
+            return h
+        return t.detach().cpu()
+    pinv = torch.inverse(host_copy(post_rots).float()).reshape(ncam, 9).pin_memory()
+    kinv = torch.inverse(host_copy(intrins).float()).reshape(ncam, 9).pin_memory()
+    return pinv.to(dev, non_blocking=True), kinv.to(dev, non_blocking=True)
 
 
 class HostInverses:
@@ -157,13 +143,11 @@ class SplatPlan:
     dims: Tuple[int, int, int, int, int]  # B, N, D, H, W
     grid: GridSpec
     cell_of: torch.Tensor      # (Nprime,) int32, -1 = dropped
-    cell_start: torch.Tensor   # (ncells+1,) int32
-    sorted_key: torch.Tensor   # (Nprime,) int64 (cell << 32 | point): ascending cell, then point id;
-                               # only the first cell_start[-1] entries are meaningful
-    sorted_row: Optional[torch.Tensor]  # (Nprime,) int32 context row (pixel) of each sorted entry; None:
-                               # an unordered plan (arrival order inside each cell, no canonical pass)
+    cell_start: Optional[torch.Tensor]  # (ncells+1,) int32 (None: geometry only, want_csr=False)
+    sorted_key: Optional[torch.Tensor]  # (Nprime,) int64 (cell << 32 | point): ascending cell, then point
+                               # id; key -1 past the first cell_start[-1] entries
+    sorted_row: Optional[torch.Tensor]  # (Nprime,) int32 context row (pixel) of each sorted entry
     geom: Optional[torch.Tensor] = None
-    pos_of: Optional[torch.Tensor] = None  # (Nprime,) int32 sorted position of each point, -1 = dropped
 
     @property
     def c_dims(self) -> _lib.Dims:
@@ -174,13 +158,8 @@ class SplatPlan:
         B, N, D, H, W = self.dims
         return B * N * D * H * W
 
-    @property
-    def canonical(self) -> bool:
-        """Entries inside each cell in ascending point id (else arrival order: see plan_from_cameras)."""
-        return self.sorted_row is not None
-
     def tensors(self):
-        return [t for t in (self.cell_of, self.cell_start, self.sorted_key, self.sorted_row, self.geom, self.pos_of)
+        return [t for t in (self.cell_of, self.cell_start, self.sorted_key, self.sorted_row, self.geom)
                 if t is not None]
 
 
@@ -281,74 +260,34 @@ def _counted_plan(dev: torch.device, ws: Optional[PlanWs], launch_cells, build_c
     return out
 
 
-def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None, canonical: bool = True):
-    """Counting sort into the canonical CSR (lss_csr_build[_ws]): cell_start, sorted_key, sorted_row.
-    canonical=False (with a persistent workspace): no canonical pass, sorted_row None."""
+def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None):
+    """Counting sort into the canonical CSR (lss_csr_build[_ws]): cell_start, sorted_key, sorted_row."""
     lib = _lib.load()
     B, N, D, H, W = dims
     nprime = B * N * D * H * W
-    canonical = canonical or ws is None or SORTED_DEPTH
     cell_start = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
     sorted_key = torch.empty(nprime, device=dev, dtype=torch.int64)
-    sorted_row = torch.empty(nprime, device=dev, dtype=torch.int32) if canonical else None
-    pos_of = torch.empty(nprime, device=dev, dtype=torch.int32) if SORTED_DEPTH else None
+    sorted_row = torch.empty(nprime, device=dev, dtype=torch.int32)
     if ws is not None:
         _lib.check(lib.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
                                         make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key),
-                                        _lib.ptr(sorted_row), _lib.ptr(pos_of), _lib.ptr(ws.scratch),
-                                        _lib.ptr(ws.workspace), _lib.stream_handle(dev)), "lss_csr_build_ws")
-        return cell_start, sorted_key, sorted_row, pos_of
+                                        _lib.ptr(sorted_row), _lib.ptr(ws.scratch), _lib.ptr(ws.workspace),
+                                        _lib.stream_handle(dev)), "lss_csr_build_ws")
+        return cell_start, sorted_key, sorted_row
     scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
     _lib.check(lib.lss_csr_build(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
                                  make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key), _lib.ptr(sorted_row),
-                                 _lib.ptr(pos_of), _lib.ptr(scratch), _lib.stream_handle(dev)), "lss_csr_build")
-    return cell_start, sorted_key, sorted_row, pos_of
-
-
-_AXES_CACHE = {}
-
-
-def frustum_axes(frustum: torch.Tensor) -> Optional[torch.Tensor]:
-    """[xs (W) | ys (H) | ds (D)] if `frustum` (D, H, W, 3) is the broadcast of its three axes -- as
-    create_frustum builds it (src/models.py:157-168) -- else None (lss_geometry_cells_axes reads
-    71 floats instead of the 4 MB tensor). Checked once per tensor version, outside graph capture; a
-    cache entry holds a weak reference to its tensor, so a new tensor at a freed tensor's address (and
-    version 0) never reuses its entry."""
-    key = (frustum.data_ptr(), frustum._version, tuple(frustum.shape), str(frustum.device))
-    hit = _AXES_CACHE.get(key)
-    if hit is not None and hit[0]() is frustum:
-        return hit[1]
-    if frustum.is_cuda and torch.cuda.is_current_stream_capturing():
-        return None
-    with torch.no_grad():
-        fr = frustum.float()
-        xs, ys, ds = fr[0, 0, :, 0], fr[0, :, 0, 1], fr[:, 0, 0, 2]
-        sep = (torch.equal(fr[..., 0], xs.expand_as(fr[..., 0])) and
-               torch.equal(fr[..., 1], ys[:, None].expand_as(fr[..., 1])) and
-               torch.equal(fr[..., 2], ds[:, None, None].expand_as(fr[..., 2])))
-        axes = torch.cat([xs, ys, ds]).contiguous() if sep else None
-    if len(_AXES_CACHE) > 16:
-        _AXES_CACHE.clear()
-    _AXES_CACHE[key] = (weakref.ref(frustum), axes)
-    return axes
-
-
-USE_PLAN_WS_CALL = False  # plans through lss_plan_ws (aggregate scan): measured slower (geometry +4 us for scan -0.7 us)
-USE_FRUSTUM_AXES = False  # measured: the two index divisions cost more than the 4 MB of frustum reads (11.2 vs 10.3 us)
+                                 _lib.ptr(scratch), _lib.stream_handle(dev)), "lss_csr_build")
+    return cell_start, sorted_key, sorted_row
 
 
 def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, post_trans, grid: GridSpec,
-                      inverse: str = "host", want_geom: bool = False, want_csr: bool = True,
-                      inverses: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                      canonical: bool = True) -> SplatPlan:
+                      want_geom: bool = False, want_csr: bool = True,
+                      inverses: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> SplatPlan:
     """get_geometry + quantise + filter + counting sort, all on the device (src/models.py:170-231).
 
-    `inverses` = a (pinv, kinv) pair from camera_inverses, if already computed (models.py computes
-    them before the trunk, so the host round trip of inverse='host' never waits for device work).
-    canonical=False: the CSR without its canonical pass (k_csr_canon) -- grouped by ascending cell,
-    arrival order inside a cell, sorted_row None -- for the channels-last splat, which ranks each
-    cell's entries itself (LSS_SPLAT_UNORDERED; identical BEV bits). Taken only with the persistent
-    workspace (eager warm-up before capture) and without SORTED_DEPTH; else the plan is canonical.
+    `inverses` = a (pinv, kinv) pair from camera_inverses / HostInverses, if already computed
+    (models.py computes them before the trunk, so the host round trip never waits for device work).
     """
     dev = _require_cuda(frustum, rots, trans, intrins, post_rots, post_trans)
     lib = _lib.load()
@@ -356,7 +295,7 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
     D, H, W = frustum.shape[:3]
     nprime = B * N * D * H * W
     ncells = grid.ncells(B)
-    pinv, kinv = inverses if inverses is not None else camera_inverses(post_rots, intrins, inverse)
+    pinv, kinv = inverses if inverses is not None else camera_inverses(post_rots, intrins)
     fr, ro, tr, pt = _f32c(frustum), _f32c(rots), _f32c(trans), _f32c(post_trans)
     cell_of = torch.empty(nprime, device=dev, dtype=torch.int32)
     geom = torch.empty(B, N, D, H, W, 3, device=dev, dtype=torch.float32) if want_geom else None
@@ -366,41 +305,22 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
         slot_of = torch.empty(nprime, device=dev, dtype=torch.int32)
     dims = make_dims(B, N, D, H, W)
     g = grid.c_struct()
-    axes = frustum_axes(frustum) if USE_FRUSTUM_AXES else None
-    geom_fn = lib.lss_geometry_cells_axes if axes is not None else lib.lss_geometry_cells
 
     def launch_cells():
-        _lib.check(geom_fn(_lib.ptr(axes if axes is not None else fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv),
-                           _lib.ptr(pinv), _lib.ptr(pt), dims, g, _lib.ptr(geom), _lib.ptr(cell_of),
-                           _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
+        _lib.check(lib.lss_geometry_cells(_lib.ptr(fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv),
+                                          _lib.ptr(pt), dims, g, _lib.ptr(geom), _lib.ptr(cell_of), _lib.ptr(counts),
+                                          _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
 
     if not want_csr:
         launch_cells()
-        return SplatPlan((B, N, D, H, W), grid, cell_of, None, None, None, geom, None)
-    if USE_PLAN_WS_CALL and ws is not None and canonical and geom is None and axes is None:
-        # the whole plan in one call: the scan reads each block's prefix from group sums the
-        # geometry kernel leaves (no look-back); outputs identical to the calls below
-        def whole_plan():
-            cs = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
-            sk = torch.empty(nprime, device=dev, dtype=torch.int64)
-            sr = torch.empty(nprime, device=dev, dtype=torch.int32)
-            po = torch.empty(nprime, device=dev, dtype=torch.int32) if SORTED_DEPTH else None
-            _lib.check(lib.lss_plan_ws(_lib.ptr(fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv),
-                                       _lib.ptr(pt), dims, g, _lib.ptr(cell_of), _lib.ptr(slot_of), _lib.ptr(counts),
-                                       _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), _lib.ptr(po), _lib.ptr(ws.scratch),
-                                       _lib.ptr(ws.workspace), _lib.stream_handle(dev)), "lss_plan_ws")
-            return cs, sk, sr, po
-        cell_start, sorted_key, sorted_row, pos_of = _counted_plan(dev, ws, lambda: None, whole_plan)
-        return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom, pos_of)
-    cell_start, sorted_key, sorted_row, pos_of = _counted_plan(
-        dev, ws, launch_cells,
-        lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws, canonical))
-    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom, pos_of)
+        return SplatPlan((B, N, D, H, W), grid, cell_of, None, None, None, geom)
+    cell_start, sorted_key, sorted_row = _counted_plan(
+        dev, ws, launch_cells, lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws))
+    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom)
 
 
-def plan_from_geom(geom: torch.Tensor, grid: GridSpec, canonical: bool = True) -> SplatPlan:
-    """Quantise a given (B, N, D, H, W, 3) geometry (voxel_pooling(geom_feats, x) boundary).
-    canonical: as plan_from_cameras."""
+def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
+    """Quantise a given (B, N, D, H, W, 3) geometry (voxel_pooling(geom_feats, x) boundary)."""
     dev = _require_cuda(geom)
     lib = _lib.load()
     B, N, D, H, W, _ = geom.shape
@@ -416,10 +336,9 @@ def plan_from_geom(geom: torch.Tensor, grid: GridSpec, canonical: bool = True) -
                                            _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)),
                    "lss_cells_from_geom")
 
-    cell_start, sorted_key, sorted_row, pos_of = _counted_plan(
-        dev, ws, launch_cells,
-        lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws, canonical))
-    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, None, pos_of)
+    cell_start, sorted_key, sorted_row = _counted_plan(
+        dev, ws, launch_cells, lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws))
+    return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, None)
 
 
 # ----------------------------------------------------------------------------- profiling hook
@@ -475,53 +394,15 @@ def _new_bev(B, Z, X, Y, dtype, layout, dev) -> torch.Tensor:
     return torch.empty(B, Z * C_CAM, X, Y, device=dev, dtype=dtype)
 
 
-# Option: the CSR build also writes each point's sorted position (plan.pos_of) and the lift writes
-# the depth weights in CSR order, so the channels-last splat reads them with the keys instead of
-# gathering depth[p] per entry. Measured at c3 (scripts/kbench.py, training-step cache state): the
-# splat drops 12.35 -> 11.89 us but the lift's scattered writes cost +2.6 us (lss_lift_prep) /
-# +3.4 us (lss_depthnet_lift), so it is off by default.
-SORTED_DEPTH = False
-
-
-def _sorted_depth_buffers(plan: SplatPlan, layout: int, dev):
-    """(pos_of, sorted_depth) for the lift kernels, or (None, None)."""
-    if SORTED_DEPTH and layout == _lib.NHWC and plan.pos_of is not None:
-        return plan.pos_of, torch.empty(plan.nprime, device=dev, dtype=torch.float32)
-    return None, None
-
-
-def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, layout: int, sorted_depth=None,
-                      flags: int = 0):
+def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, layout: int):
     lib = _lib.load()
     dev = out.device
-    if not plan.canonical:
-        if layout != _lib.NHWC or sorted_depth is not None:
-            raise RuntimeError("lss_carla_amd: an unordered plan (canonical=False) feeds the channels-last splat only")
-        flags |= _lib.SPLAT_UNORDERED
     e0, e1 = SPLAT_PROFILE.new_pair() if SPLAT_PROFILE.enabled else (None, None)
     ctx_code = _lib.dtype_code(ctx_t.dtype) if ctx_t is not None else _lib.F32
-    _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), ctx_code, _lib.ptr(x_rows),
-                                 _lib.ptr(plan.cell_start),
-                                 _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), _lib.ptr(sorted_depth),
-                                 plan.c_dims,
-                                 plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype), layout, flags,
+    _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), ctx_code, _lib.ptr(x_rows), _lib.ptr(plan.cell_start),
+                                 _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), plan.c_dims,
+                                 plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype), layout,
                                  _lib.stream_handle(dev), e0, e1), "lss_splat_fwd")
-
-
-# Option (LSS_FILL_IN_LIFT=1): the channels-last BEV's empty rows are zeroed by blocks of the lift launch
-# (on the CUs the lift leaves idle) instead of by the splat, which then writes the occupied rows only
-# (LSS_SPLAT_EMPTY_FILLED). Measured in the c3 training step (rocprof, profiles/r03/fill_in_lift_ab.txt):
-# lift 11.3 -> 13.8 us, splat 11.8 -> 9.7 us -- the splat's chunk gathers alone take 9.7 us, so moving
-# the fill out saves nothing (hot path 58.3 vs 59.0 us). Off by default.
-FILL_IN_LIFT = os.environ.get("LSS_FILL_IN_LIFT", "0") == "1"
-
-
-def _fill_args(plan: SplatPlan, out: torch.Tensor, layout: int):
-    """(cell_start, grid, bev, bev dtype) for the lift's empty-row fill and the splat's flags."""
-    if FILL_IN_LIFT and layout == _lib.NHWC:
-        return (_lib.ptr(plan.cell_start), plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype)), \
-            _lib.SPLAT_EMPTY_FILLED
-    return (None, None, None, 0), 0
 
 
 def _grad_rows(plan: SplatPlan, dbev: torch.Tensor) -> Tuple[torch.Tensor, int]:
@@ -565,15 +446,12 @@ class LiftSplat(torch.autograd.Function):
         # context rows keep the input's element type: bf16 rows are exact for a bf16 depthnet output
         # and halve the splat's gathered bytes
         ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=dn.dtype)
-        pos_of, sorted_depth = _sorted_depth_buffers(plan, layout, dev)
         X, Y, Z = plan.grid.nx
         out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
-        fill, flags = _fill_args(plan, out, layout)
         _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.dtype_code(dn.dtype), plan.c_dims, _lib.ptr(depth),
-                                     _lib.ptr(ctx_t), _lib.dtype_code(ctx_t.dtype), _lib.ptr(pos_of),
-                                     _lib.ptr(sorted_depth), *fill, _lib.stream_handle(dev)),
+                                     _lib.ptr(ctx_t), _lib.dtype_code(ctx_t.dtype), _lib.stream_handle(dev)),
                    "lss_lift_prep")
-        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout, sorted_depth, flags)
+        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout)
         ctx.save_for_backward(depth, ctx_t)
         ctx.plan = plan
         ctx.dn_dtype = depthnet_out.dtype
@@ -635,15 +513,12 @@ class DepthnetLiftSplat(torch.autograd.Function):
         b = bias.detach().contiguous()
         depth = torch.empty(B * N, D, H, W, device=dev, dtype=torch.float32)
         ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=torch.bfloat16)
-        pos_of, sorted_depth = _sorted_depth_buffers(plan, layout, dev)
         X, Y, Z = plan.grid.nx
         out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
-        fill, flags = _fill_args(plan, out, layout)
         lift = lib.lss_depthnet_lift_nhwc if nhwc else lib.lss_depthnet_lift
         _lib.check(lift(_lib.ptr(f), _lib.ptr(w), _lib.ptr(b), _lib.BF16, K, plan.c_dims, _lib.ptr(depth),
-                        _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(pos_of), _lib.ptr(sorted_depth), *fill,
-                        _lib.stream_handle(dev)), "lss_depthnet_lift")
-        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout, sorted_depth, flags)
+                        _lib.ptr(ctx_t), _lib.BF16, _lib.stream_handle(dev)), "lss_depthnet_lift")
+        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout)
         ctx.save_for_backward(f, weight, depth, ctx_t)
         ctx.plan = plan
         return out

@@ -11,7 +11,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   [ -z "$grp" ] && continue
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc/p$i -o run -- \
-      python3 scripts/kbench.py --only "$ONLY" --iters 20 --variants 0 > gpurun_out/pmc/p$i.log 2>&1
+      python3 scripts/kbench.py --only "$ONLY" --iters 20 > gpurun_out/pmc/p$i.log 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/p$i.log; exit $rc; fi
 done

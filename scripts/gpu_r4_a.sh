@@ -4,7 +4,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/r4a
-timeout -k 10 300 python -u scripts/splat_ab.py --config c3 --libs product,o2,zu2_o2,zu4_o2,zu8_o2,zu16_o2,zu8_o1 \
+timeout -k 10 300 python -u scripts/splat_ab.py --config c3 --libs product,skipzero,skipchunk,o2,zu2_o2,zu4_o2,zu8_o2,zu16_o2,zu8_o1 \
   > gpurun_out/r4a/splat_ab_c3.log 2>&1 || { tail -30 gpurun_out/r4a/splat_ab_c3.log; exit 1; }
 grep -v '^{' gpurun_out/r4a/splat_ab_c3.log | grep -v amdgpu.ids
 bash scripts/gpu_prof_ab.sh product zu8_o2 zu16_o2 zu4_o2 2>&1 | tee gpurun_out/r4a/prof_ab.txt

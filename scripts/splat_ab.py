@@ -45,7 +45,8 @@ def main():
     lib = _lib.load()
     st = lambda: _lib.stream_handle(dev)  # noqa: E731
     dn = syn.make_depthnet_out(B, N, D, H, W).to(dev, torch.bfloat16)
-    plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device")
+    inv = ops.camera_inverses(rig["post_rots"], rig["intrins"])
+    plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverses=inv)
     dims, g = plan.c_dims, grid.c_struct()
     kept = int(plan.cell_start[-1])
     odt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
@@ -60,10 +61,10 @@ def main():
 
     def lift():
         _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx),
-                                     _lib.dtype_code(ctx.dtype), None, None, None, None, None, 0, st()), "lift")
+                                     _lib.dtype_code(ctx.dtype), st()), "lift")
 
     def replan():
-        ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device")
+        ops.plan_from_cameras(frustum, **rig, grid=grid, inverses=inv)
 
     def prepare(mode):
         if mode in ("dirty", "step"):
@@ -102,8 +103,8 @@ def main():
         def launch(a, b):
             _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx), _lib.dtype_code(ctx.dtype), None,
                                        _lib.ptr(plan.cell_start), _lib.ptr(plan.sorted_key),
-                                       _lib.ptr(plan.sorted_row), None, dims, g, _lib.ptr(bev),
-                                       _lib.dtype_code(bev.dtype), layout, 0, st(), a, b), "fwd")
+                                       _lib.ptr(plan.sorted_row), dims, g, _lib.ptr(bev),
+                                       _lib.dtype_code(bev.dtype), layout, st(), a, b), "fwd")
         return launch
 
     splat_fn(lib)(None, None)

@@ -39,26 +39,24 @@ def main():
     X, Y, Z = grid.nx
     dn = syn.make_depthnet_out(B, N, D, H, W).to(dev, torch.bfloat16)
     st = _lib.stream_handle(dev)
-    plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device")  # product library's CSR
+    plan = ops.plan_from_cameras(frustum, **rig, grid=grid)  # product library's CSR
     dims, g = plan.c_dims, grid.c_struct()
     depth = torch.empty(B * N, D, H, W, device=dev)
-    sdepth = torch.empty(B * N * D * H * W, device=dev)  # depth weights in CSR order
     ctx = torch.empty(B * N * H * W, 64, device=dev, dtype=torch.bfloat16)
     out = torch.empty(B, Z * 64, X, Y, device=dev, dtype=torch.bfloat16, memory_format=torch.channels_last)
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
     for it in range(4):
         if a.mode == "step":
             flush.zero_()
-            plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device")
-        _lib.check(l.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16,
-                                   _lib.ptr(plan.pos_of), _lib.ptr(sdepth), None, None, None, 0, st), "lift")
+            plan = ops.plan_from_cameras(frustum, **rig, grid=grid)
+        _lib.check(l.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, st),
+                   "lift")
         e0, e1 = ct.c_void_p(), ct.c_void_p()
         l.lss_event_create(ct.byref(e0))
         l.lss_event_create(ct.byref(e1))
         _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, None, _lib.ptr(plan.cell_start),
-                                   _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), _lib.ptr(sdepth), dims, g,
-                                   _lib.ptr(out),
-                                   _lib.BF16, _lib.NHWC, 0, st, e0, e1), "fwd")
+                                   _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), dims, g, _lib.ptr(out),
+                                   _lib.BF16, _lib.NHWC, st, e0, e1), "fwd")
         ms = ct.c_float()
         l.lss_event_elapsed_ms(e0, e1, ct.byref(ms))
     torch.cuda.synchronize()

@@ -38,7 +38,7 @@ def main():
     grid = ops.GridSpec.from_conf(gc)
     X, Y, Z = grid.nx
     st = _lib.stream_handle(dev)
-    plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="device")
+    plan = ops.plan_from_cameras(frustum, **rig, grid=grid)
     dims, g = plan.c_dims, grid.c_struct()
     depth = torch.empty(B * N, D, H, W, device=dev)
     ctx = torch.empty(B * N * H * W, 64, device=dev, dtype=torch.bfloat16)
@@ -52,7 +52,7 @@ def main():
     ctxf = torch.empty(B * N * H * W, 64, device=dev)
     bevf = torch.empty(B, Z * 64, X, Y, device=dev)
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
-    pinv, kinv = ops.camera_inverses(rig["post_rots"], rig["intrins"], "device")
+    pinv, kinv = ops.camera_inverses(rig["post_rots"], rig["intrins"])
     ro, tr, pt = [t.float().contiguous() for t in (rig["rots"], rig["trans"], rig["post_trans"])]
     ms = ct.c_float()
     for it in range(4):
@@ -78,7 +78,7 @@ def main():
                                                _lib.ptr(pinv), _lib.ptr(pt), dims, g, None, _lib.ptr(cell_of),
                                                _lib.ptr(counts), _lib.ptr(slot), st), "geom")
             _lib.check(l.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot), plan.nprime, _lib.ptr(counts), ncells,
-                                          dims, _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), None, _lib.ptr(scr),
+                                          dims, _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), _lib.ptr(scr),
                                           _lib.ptr(wsb), st), "csr")
             if it == 3:
                 assert torch.equal(cs, plan.cell_start), "trace build CSR differs"
@@ -90,18 +90,17 @@ def main():
                                             _lib.ptr(pinv), _lib.ptr(pt), dims, g, None, _lib.ptr(cell_of),
                                             _lib.ptr(counts), _lib.ptr(slot), st), "geom")
         elif a.kernel == "nchw":  # config 2's forward: fp32 context rows, fp32 NCHW BEV
-            _lib.check(l.lss_lift_prep(_lib.ptr(dnf), _lib.F32, dims, _lib.ptr(depth), _lib.ptr(ctxf), _lib.F32,
-                                       None, None, None, None, None, 0, st), "lift")
+            _lib.check(l.lss_lift_prep(_lib.ptr(dnf), _lib.F32, dims, _lib.ptr(depth), _lib.ptr(ctxf), _lib.F32, st),
+                       "lift")
             _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctxf), _lib.F32, None, _lib.ptr(plan.cell_start),
-                                       _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), None, dims, g,
-                                       _lib.ptr(bevf), _lib.F32, _lib.NCHW, 0, st, None, None), "fwd")
+                                       _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), dims, g,
+                                       _lib.ptr(bevf), _lib.F32, _lib.NCHW, st, None, None), "fwd")
         elif a.kernel == "lift3":  # channels-last features (k_depthnet_lift3)
             _lib.check(l.lss_depthnet_lift_nhwc(_lib.ptr(feat_cl), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims,
-                                                _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, None, None, None, None, None,
-                                                0, st), "lift3")
+                                                _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, st), "lift3")
         elif a.kernel == "lift":
             _lib.check(l.lss_depthnet_lift(_lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims,
-                                           _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, None, None, None, None, None, 0, st), "lift")
+                                           _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, st), "lift")
         else:
             _lib.check(l.lss_splat_bwd(_lib.ptr(gbev), _lib.BF16, _lib.NHWC, _lib.ptr(plan.cell_of), _lib.ptr(depth),
                                        _lib.ptr(ctx), _lib.BF16, dims, g, _lib.ptr(d_dn), _lib.BF16, st), "bwd")

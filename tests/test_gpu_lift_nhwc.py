@@ -31,16 +31,14 @@ def _inputs(B, N, H, W, D, seed=0):
     return feat, weight, bias
 
 
-def _run(fn, feat, weight, bias, dims, pos_of=None, nprime=0, fill=(None, None, None, 0)):
+def _run(fn, feat, weight, bias, dims):
     B, N, D, H, W = dims.B, dims.N, dims.D, dims.H, dims.W
     depth = torch.full((B * N, D, H, W), float("nan"), device=DEV)
     ctx_t = torch.full((B * N * H * W, 64), float("nan"), device=DEV, dtype=torch.bfloat16)
-    sd = torch.zeros(nprime, device=DEV) if pos_of is not None else None
     _lib.check(fn(_lib.ptr(feat), _lib.ptr(weight), _lib.ptr(bias), _lib.BF16, 512, dims, _lib.ptr(depth),
-                  _lib.ptr(ctx_t), _lib.BF16, _lib.ptr(pos_of), _lib.ptr(sd), *fill, _lib.stream_handle(DEV)),
-               "depthnet_lift")
+                  _lib.ptr(ctx_t), _lib.BF16, _lib.stream_handle(DEV)), "depthnet_lift")
     torch.cuda.synchronize()
-    return depth, ctx_t, sd
+    return depth, ctx_t
 
 
 @pytest.mark.parametrize("name", ["c1", "c3", "c5"])
@@ -50,34 +48,13 @@ def test_nhwc_kernel_bit_identical_to_nchw_kernel(name):
     rig = {k: v.to(DEV) for k, v in syn.make_rig(B, N, fd, seed=2).items()}
     frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
     D, H, W = frustum.shape[:3]
-    ops.SORTED_DEPTH = True
-    try:
-        plan = ops.plan_from_cameras(frustum, **rig, grid=ops.GridSpec.from_conf(gc))
-    finally:
-        ops.SORTED_DEPTH = False
+    plan = ops.plan_from_cameras(frustum, **rig, grid=ops.GridSpec.from_conf(gc))
     feat, weight, bias = (t.to(DEV) for t in _inputs(B, N, H, W, D, seed=5))
     feat_cl = feat.contiguous(memory_format=torch.channels_last)
     lib = _lib.load()
-    for pos in (None, plan.pos_of):
-        d0, c0, s0 = _run(lib.lss_depthnet_lift, feat, weight, bias, plan.c_dims, pos, plan.nprime)
-        d1, c1, s1 = _run(lib.lss_depthnet_lift_nhwc, feat_cl, weight, bias, plan.c_dims, pos, plan.nprime)
-        assert torch.equal(d0, d1) and torch.equal(c0, c1)
-        if pos is not None:
-            assert torch.equal(s0, s1)
-    # with the empty-row fill riding along: the splat over the filled BEV (occupied rows only) equals
-    # the full splat
-    X, Y, Z = plan.grid.nx
-    bev = torch.empty((B, Z * 64, X, Y), device=DEV, dtype=torch.bfloat16, memory_format=torch.channels_last).fill_(7.0)
-    d1, c1, _ = _run(lib.lss_depthnet_lift_nhwc, feat_cl, weight, bias, plan.c_dims,
-                     fill=(_lib.ptr(plan.cell_start), plan.grid.c_struct(), _lib.ptr(bev), _lib.BF16))
+    d0, c0 = _run(lib.lss_depthnet_lift, feat, weight, bias, plan.c_dims)
+    d1, c1 = _run(lib.lss_depthnet_lift_nhwc, feat_cl, weight, bias, plan.c_dims)
     assert torch.equal(d0, d1) and torch.equal(c0, c1)
-    full = torch.empty_like(bev)
-    for out, flags in ((full, 0), (bev, _lib.SPLAT_EMPTY_FILLED)):
-        _lib.check(lib.lss_splat_fwd(_lib.ptr(d1), _lib.ptr(c1), _lib.BF16, None, _lib.ptr(plan.cell_start),
-                                     _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), None, plan.c_dims,
-                                     plan.grid.c_struct(), _lib.ptr(out), _lib.BF16, _lib.NHWC, flags,
-                                     _lib.stream_handle(DEV), None, None), "splat")
-    assert torch.equal(full, bev)
 
 
 @pytest.mark.parametrize("shape", [(1, 3, 5, 7, 41), (2, 5, 9, 13, 41), (1, 1, 8, 22, 60), (8, 6, 8, 22, 41)])
@@ -88,7 +65,7 @@ def test_nhwc_kernel_vs_fp64_conv(shape):
     feat, weight, bias = _inputs(B, N, H, W, D, seed=11)
     dims = _lib.Dims(B, N, D, H, W, 64)
     lib = _lib.load()
-    depth, ctx_t, _ = _run(lib.lss_depthnet_lift_nhwc, feat.to(DEV).contiguous(memory_format=torch.channels_last),
+    depth, ctx_t = _run(lib.lss_depthnet_lift_nhwc, feat.to(DEV).contiguous(memory_format=torch.channels_last),
                            weight.to(DEV), bias.to(DEV), dims)
     logits = torch.einsum("nkhw,ok->nohw", feat.double(), weight.double()) + bias.double().view(1, -1, 1, 1)
     dn = logits.to(torch.bfloat16)

@@ -345,10 +345,10 @@ def test_single_pass_scan_matches_two_kernel_csr(name):
         rig = _dev(syn.make_rig(B, N, fd, seed=it))
         old, ops.USE_PLAN_WS = ops.USE_PLAN_WS, False
         try:
-            want = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")
+            want = ops.plan_from_cameras(frustum, **rig, grid=grid)
         finally:
             ops.USE_PLAN_WS = old
-        got = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")
+        got = ops.plan_from_cameras(frustum, **rig, grid=grid)
         torch.cuda.synchronize()
         assert torch.equal(got.cell_start, want.cell_start)
         assert torch.equal(got.sorted_key, want.sorted_key)
@@ -375,17 +375,17 @@ def test_lookback_timeout_path_is_exact(name):
     rig = _dev(syn.make_rig(B, N, fd, seed=11))
     old, ops.USE_PLAN_WS = ops.USE_PLAN_WS, False
     try:
-        want = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")
+        want = ops.plan_from_cameras(frustum, **rig, grid=grid)
     finally:
         ops.USE_PLAN_WS = old
-    ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")  # creates the workspace
+    ops.plan_from_cameras(frustum, **rig, grid=grid)  # creates the workspace
     ws = ops.PLAN_WS.get(DEV, ncells, want.nprime, create=False)
     words = ws.workspace.view(torch.int32)
     timeouts = 0
     try:
         words[2] = 1  # spin limit override: 0 polls
         for _ in range(3):
-            got = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")
+            got = ops.plan_from_cameras(frustum, **rig, grid=grid)
             torch.cuda.synchronize()
             assert torch.equal(got.cell_start, want.cell_start)
             assert torch.equal(got.sorted_key, want.sorted_key)
@@ -407,7 +407,7 @@ def test_plan_workspace_is_ordered_across_streams():
     rigs = [_dev(syn.make_rig(B, N, fd, seed=s)) for s in (21, 22)]
     old, ops.USE_PLAN_WS = ops.USE_PLAN_WS, False
     try:
-        want = [ops.plan_from_cameras(frustum, **r, grid=grid, inverse="host") for r in rigs]
+        want = [ops.plan_from_cameras(frustum, **r, grid=grid) for r in rigs]
     finally:
         ops.USE_PLAN_WS = old
     torch.cuda.synchronize()
@@ -416,7 +416,7 @@ def test_plan_workspace_is_ordered_across_streams():
     for _ in range(3):
         for st, r in zip(streams, rigs):
             with torch.cuda.stream(st):
-                p = ops.plan_from_cameras(frustum, **r, grid=grid, inverse="host")
+                p = ops.plan_from_cameras(frustum, **r, grid=grid)
                 for t in p.tensors():
                     t.record_stream(st)
                 got.append(p)
@@ -457,7 +457,7 @@ def test_csr_build_ws_direct(ncells, nprime, offset):
     scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=DEV, dtype=torch.uint8)
     cd, sd = cell.to(DEV), slot.to(DEV)
     _lib.check(lib.lss_csr_build_ws(_lib.ptr(cd), _lib.ptr(sd), nprime, _lib.ptr(counts), ncells, None,
-                                    _lib.ptr(cell_start), _lib.ptr(sorted_key), _lib.ptr(sorted_row), None,
+                                    _lib.ptr(cell_start), _lib.ptr(sorted_key), _lib.ptr(sorted_row),
                                     _lib.ptr(scratch), _lib.ptr(ws), _lib.stream_handle(DEV)), "lss_csr_build_ws")
     torch.cuda.synchronize()
     assert torch.equal(cell_start.cpu().long(), cs_h)
@@ -480,9 +480,9 @@ def test_geometry_slots_are_a_permutation_per_cell(name):
     frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
     grid = ops.GridSpec.from_conf(gc)
     rig = _dev(syn.make_rig(B, N, fd, seed=3))
-    plan = ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host")
+    plan = ops.plan_from_cameras(frustum, **rig, grid=grid)
     ncells, nprime = grid.ncells(B), plan.nprime
-    pinv, kinv = ops.camera_inverses(rig["post_rots"], rig["intrins"], "host")
+    pinv, kinv = ops.camera_inverses(rig["post_rots"], rig["intrins"])
     ro, tr, pt = [rig[k].float().contiguous() for k in ("rots", "trans", "post_trans")]
     counts = torch.zeros(ncells, device=DEV, dtype=torch.int32)
     slot = torch.full((nprime,), -7, device=DEV, dtype=torch.int32)
@@ -503,32 +503,6 @@ def test_geometry_slots_are_a_permutation_per_cell(name):
     assert torch.unique(key).numel() == int(kept.sum())
 
 
-@pytest.mark.parametrize("name", ["c1", "c3", "c5"])
-def test_frustum_axes_geometry_bit_exact(name):
-    """lss_geometry_cells_axes (the frustum's three axes) == lss_geometry_cells (the full tensor):
-    geometry, voxel ids and counts bit for bit."""
-    cfg, gc, _ = syn.config_confs(name)
-    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
-    frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
-    assert ops.frustum_axes(frustum) is not None
-    grid = ops.GridSpec.from_conf(gc)
-    rig = _dev(syn.make_rig(B, N, fd, seed=5))
-    plans = []
-    for use in (False, True):
-        old, ops.USE_FRUSTUM_AXES = ops.USE_FRUSTUM_AXES, use
-        try:
-            plans.append(ops.plan_from_cameras(frustum, **rig, grid=grid, inverse="host", want_geom=True))
-        finally:
-            ops.USE_FRUSTUM_AXES = old
-    a, b = plans
-    assert torch.equal(a.geom, b.geom) and torch.equal(a.cell_of, b.cell_of)
-    assert torch.equal(a.cell_start, b.cell_start) and torch.equal(a.sorted_key, b.sorted_key)
-    # a frustum that is not a broadcast of its axes keeps the full-tensor path
-    bent = frustum.clone()
-    bent[1, 2, 3, 0] += 0.25
-    assert ops.frustum_axes(bent) is None
-
-
 @settings(max_examples=int(os.environ.get("LSS_HYP_EXAMPLES", "25")), deadline=None)
 @given(seed=st.integers(0, 10_000), B=st.integers(1, 3), N=st.integers(1, 6), fH=st.integers(1, 9),
        fW=st.integers(1, 24), D=st.integers(1, 60), half=st.sampled_from([10.0, 25.0, 50.0]),
@@ -545,7 +519,7 @@ def test_random_shapes_fwd_bwd_vs_oracle(seed, B, N, fH, fW, D, half, dx, Z, bf1
     assert frustum.shape[:3] == (D, fH, fW)
     print(f"example seed={seed} B={B} N={N} fH={fH} fW={fW} D={D} half={half} dx={dx} Z={Z} "
           f"bf16_nhwc={bf16_nhwc}", flush=True)
-    plan = ops.plan_from_cameras(frustum.to(DEV), **_dev(rig), grid=grid, inverse="host", want_geom=True)
+    plan = ops.plan_from_cameras(frustum.to(DEV), **_dev(rig), grid=grid, want_geom=True)
     geom = ref.get_geometry(frustum, **rig)
     np.testing.assert_array_equal(plan.geom.cpu().numpy(), geom)
     dx_, bx_, nx_ = ref.gen_dx_bx(gc["xbound"], gc["ybound"], gc["zbound"])
@@ -578,35 +552,3 @@ def test_random_shapes_fwd_bwd_vs_oracle(seed, B, N, fH, fW, D, half, dx, Z, bf1
     want_g = ref.lift_splat_backward_fp64(dn_in.numpy(), geom, gd.float().cpu().numpy(), dx_, bx_, nx_, D, 64)
     tol = ATOL if dtype == torch.float32 else 2e-2
     np.testing.assert_allclose(dnd.grad.float().cpu().numpy(), want_g, rtol=tol, atol=tol)
-
-
-@pytest.mark.parametrize("fused", [False, True])
-def test_fill_in_lift_option_matches_fill_in_splat(fused):
-    """ops.FILL_IN_LIFT (the lift launch zeroes the empty rows, the splat writes occupied rows only):
-    the same channels-last BEV bit for bit as the splat's own fill, on a buffer pre-filled with NaN."""
-    cfg, gc, _ = syn.config_confs("c3")
-    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
-    rig = syn.make_rig(B, N, fd, seed=4)
-    frustum = ref.create_frustum(fd, gc["dbound"])
-    D, H, W = frustum.shape[:3]
-    plan = ops.plan_from_cameras(frustum.to(DEV), **_dev(rig), grid=ops.GridSpec.from_conf(gc))
-    g = torch.Generator().manual_seed(3)
-    feat = torch.randn(B * N, 512, H, W, generator=g).to(DEV, torch.bfloat16)
-    wdn = (torch.randn(D + 64, 512, 1, 1, generator=g) * 0.05).to(DEV, torch.bfloat16)
-    bdn = (torch.randn(D + 64, generator=g) * 0.1).to(DEV, torch.bfloat16)
-    dn = syn.make_depthnet_out(B, N, D, H, W, seed=4).to(DEV, torch.bfloat16)
-    outs = []
-    old = ops.FILL_IN_LIFT
-    try:
-        for fill in (False, True):
-            ops.FILL_IN_LIFT = fill
-            junk = torch.full((B, 64, 200, 200), float("nan"), device=DEV, dtype=torch.bfloat16)
-            del junk  # leaves NaN in the memory the next BEV is likely to get
-            with torch.no_grad():
-                bev = (ops.depthnet_lift_splat(feat, wdn, bdn, plan, torch.bfloat16, _lib.NHWC) if fused
-                       else ops.lift_splat(dn, plan, torch.bfloat16, _lib.NHWC))
-            outs.append(bev.clone())
-    finally:
-        ops.FILL_IN_LIFT = old
-    assert torch.isfinite(outs[1].float()).all()
-    assert torch.equal(outs[0], outs[1])

@@ -32,7 +32,8 @@ def test_library_loads_and_exports_all_symbols():
     assert lib.lss_error_string(0) == b"success"
     assert b"invalid" in lib.lss_error_string(-1)
     # host-side argument validation (no device work): NULL pointers are rejected
-    assert lib.lss_camera_inverse(None, None, 0, None, None, None) == -1
+    assert lib.lss_geometry_cells(None, None, None, None, None, None, None, None, None, None, None, None, None) == -1
+    assert lib.lss_ceiling_store(None, 16, 1, 0, None, None, None) == -1
     assert lib.lss_csr_scratch_bytes(4096, 100) == 256 + 8 * 100  # scan partials (aligned) + unsorted keys
     assert lib.lss_debug_checks() == (1 if os.environ.get("LSS_DEBUG", "0") == "1" else 0)
 
