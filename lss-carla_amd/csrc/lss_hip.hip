@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <limits.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "lss_hip.h"
 
@@ -55,6 +56,14 @@ __device__ __forceinline__ void store4(bf16* dst, float a, float b, float c, flo
 }
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// The lane id recomputed from the exec mask (v_mbcnt) in place: an asm the compiler can neither hoist
+// nor merge with an earlier lane id, so no register has to hold one across a long stretch of code (a
+// value kept live there can be spilled to scratch, one more memory round trip to reload it).
+__device__ __forceinline__ int fresh_lane() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 __device__ __forceinline__ float readlane_f(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
@@ -1034,8 +1043,11 @@ constexpr int kDn3MaxPix = 48;           // pixels per block at most: three 16-c
 // 4 slices no better, profiles/r03/s3/trace_lift3_slices*.txt)
 constexpr int kDn3Slices = 2;
 
+// One block per CU (8 waves, 2 per SIMD): up to 256 VGPRs per lane. Without the waves-per-EU bound
+// the compiler budgets 128 (the 4 waves per SIMD two blocks' LDS would allow) and kept the feature
+// loads in scratch: stores behind vmcnt waits, reloads behind a vmcnt(0) -- the stage serialised.
 template <int K>
-__global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __restrict__ feat,
+__global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_depthnet_lift3(const bf16* __restrict__ feat,
                                                               const bf16* __restrict__ weight,
                                                               const bf16* __restrict__ bias, int D, int HW,
                                                               int npix, int nlift, float* __restrict__ depth,
@@ -1085,7 +1097,7 @@ __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __rest
     // (unconditional even for a wave past the output rows -- its clamped row is one cached line per
     // K step -- so the compiler can count every load: a load under a branch makes it wait for the
     // worst case, and the tile's LDS writes then waited for most of the weights)
-    uint4 fv[kSlices][kSIt];
+    u32x4 fv[kSlices][kSIt];  // (a native vector type: an array of the uint4 struct stayed in scratch)
     bf16x8 a[kSteps];
 #pragma unroll
     for (int h = 0; h < kSlices; ++h) {
@@ -1093,7 +1105,7 @@ __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __rest
         for (int t = 0; t < kSIt; ++t) {
             const int i = threadIdx.x + t * kDn3Block;
             const int r = min(i / kSCPR, np - 1), c = h * kSCPR + i % kSCPR;
-            fv[h][t] = *reinterpret_cast<const uint4*>(tile + (size_t)r * K * 2 + c * 16);
+            fv[h][t] = *reinterpret_cast<const u32x4*>(tile + (size_t)r * K * 2 + c * 16);
         }
 #pragma unroll
         for (int s = h * kSSteps; s < (h + 1) * kSSteps; ++s) a[s] = *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
@@ -1104,17 +1116,18 @@ __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __rest
     // ---- per slice: stage it in LDS, then its MFMA steps over kTiles 16-pixel column tiles. All
     // tiles always (compile-time trip counts: the LDS reads and MFMAs pipeline); columns past the
     // tile's pixels read clamped rows and only feed logits that are never read. Same K order as one
-    // slice: identical results.
+    // slice: identical results. The slice index is a compile-time constant in each call (a loop over
+    // it left fv[h][...] dynamically indexed, and the compiler kept the loaded features in scratch).
     f32x4 acc[kTiles];
 #pragma unroll
     for (int t = 0; t < kTiles; ++t) acc[t] = f32x4{};
-#pragma unroll
-    for (int h = 0; h < kSlices; ++h) {
+    auto slice = [&](auto hc) {
+        constexpr int h = decltype(hc)::value;
 #pragma unroll
         for (int t = 0; t < kSIt; ++t) {
             const int i = threadIdx.x + t * kDn3Block;
             if (kSChunks % kDn3Block == 0 || i < kSChunks)
-                *reinterpret_cast<uint4*>(s_x + (i / kSCPR) * kRow + (h * kSCPR + i % kSCPR) * 16) = fv[h][t];
+                *reinterpret_cast<u32x4*>(s_x + (i / kSCPR) * kRow + (h * kSCPR + i % kSCPR) * 16) = fv[h][t];
         }
         __syncthreads();
         if (h == 0) LSS_STAMP(tslot, 1);
@@ -1130,7 +1143,10 @@ __global__ __launch_bounds__(kDn3Block) void k_depthnet_lift3(const bf16* __rest
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], b, acc[t], 0, 0, 0);
             }
         }
-    }
+    };
+    static_assert(kSlices == 2, "two K slices");
+    slice(std::integral_constant<int, 0>{});
+    slice(std::integral_constant<int, 1>{});
     // C/D: column (pixel) = lane & 15, row (output) = 4 (lane >> 4) + i
 #pragma unroll
     for (int t = 0; t < kTiles; ++t)
@@ -1405,14 +1421,14 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 #pragma unroll
         for (int i = 0; i < RS::EPL; ++i) acc[i] = 0.f;
         int cur = -1;
-        auto put = [&](float* dst) {
+        auto put = [&](float* dst, int c) {
 #pragma unroll
             for (int i = 0; i < RS::EPL; i += 4)
-                *reinterpret_cast<float4*>(dst + col + i) = make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
+                *reinterpret_cast<float4*>(dst + c + i) = make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
         };
-        auto finish = [&](bool last) {  // the cell `cur` ends at this point of the group
-            if (cur == first_cell && head_split) put(part + grp * kC);  // a later piece of a cut cell
-            else if (!(last && tail_split)) store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + col, acc);
+        auto finish = [&](bool last, int c) {  // the cell `cur` ends at this point of the group
+            if (cur == first_cell && head_split) put(part + grp * kC, c);  // a later piece of a cut cell
+            else if (!(last && tail_split)) store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + c, acc);
             // else: the first piece of a cut cell stays in acc (combined after the barrier)
         };
         // round trip 2 (one per kUnroll entries of a group): row slices and depth weights in flight together
@@ -1430,7 +1446,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                 if (e + u < ge) {
                     const int cl = meta[e + u].cell;
                     if (cl != cur) {
-                        if (cur >= 0) finish(false);
+                        if (cur >= 0) finish(false, col);
 #pragma unroll
                         for (int i = 0; i < RS::EPL; ++i) acc[i] = 0.f;
                         cur = cl;
@@ -1443,7 +1459,10 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                 }
             }
         }
-        if (cur >= 0) finish(true);
+        // (the lane's column recomputed after the loop: kept live across it, it was the one VGPR over
+        // the 72 of 7 waves per SIMD and went to scratch -- a reload round trip at every wave's end)
+        const int tcol = (fresh_lane() % RS::LPR) * RS::EPL;
+        if (cur >= 0) finish(true, tcol);
         __builtin_amdgcn_wave_barrier();
         // the cell cut at this group's end, if it starts in this group: its first piece (acc) plus
         // the later groups' pieces in group order (empty groups skipped; the cell ends where a
@@ -1454,9 +1473,9 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                 if (qs == gbeg(q + 1)) continue;  // empty group
                 if (meta[qs].cell != cur) break;
 #pragma unroll
-                for (int i = 0; i < RS::EPL; ++i) acc[i] = __fadd_rn(acc[i], part[q * kC + col + i]);
+                for (int i = 0; i < RS::EPL; ++i) acc[i] = __fadd_rn(acc[i], part[q * kC + tcol + i]);
             }
-            store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + col, acc);
+            store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + tcol, acc);
         }
     }
     if (big >= 0) {
@@ -1542,22 +1561,42 @@ constexpr int kN2Waves = 4;  // waves per NCHW tile block (more lane groups shar
 // profiles/r03/pad0_eval.txt)
 __host__ __device__ constexpr int nchw2_stride(int yt) { return (yt + 3) & ~3; }
 constexpr int kN2Block = kN2Waves * kWave;
+#ifndef LSS_NCHW_SPLIT
+#define LSS_NCHW_SPLIT 1  // channel splits of the NCHW tile kernel (QS: blocks per tile)
+#endif
+constexpr int kNchwSplit = LSS_NCHW_SPLIT;
 
 
-template <bool FUSED, typename RT, typename OutT>
+// QS > 1: the tile's channels are split over QS blocks (block (tile, q) sums channels
+// [q C/QS, (q+1) C/QS) of every entry: LPR = C/QS/EPL lanes per row slice, QS times the lane groups per
+// tile), so a dense tile's entries are spread over QS x more groups -- the dense tiles near the ego
+// were the kernel's tail (trace_splat_fwd_nchw2_c2.txt: sums p50 3.6 us, max 9.4). Same association
+// per channel: identical bits for every QS.
+template <int QS, typename RT> struct TileSlice {
+    static constexpr int CPB = kC / QS;          // channels per block
+    static constexpr int EPL = 16 / sizeof(RT);  // row elements per 16-B lane slice
+    static constexpr int LPR = CPB / EPL;        // lanes per row slice = lanes per group
+    static constexpr int NG = kWave / LPR;       // groups per wave
+    static_assert(CPB % EPL == 0 && LPR >= 1, "whole 16-B slices per block");
+};
+
+template <bool FUSED, typename RT, typename OutT, int QS>
 __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __restrict__ depth,
                                                              const RT* __restrict__ rows_base,
                                                              const int32_t* __restrict__ cell_start,
                                                              const long long* __restrict__ sorted_key,
                                                              const int32_t* __restrict__ sorted_row, SplatGeo sg,
                                                              int ntiles, OutT* __restrict__ out) {
-    using RS = RowSlice<RT>;
+    using RS = TileSlice<QS, RT>;
     constexpr int KU = 8;                         // context rows in flight per group and batch
     constexpr int KPL = (KU + RS::LPR - 1) / RS::LPR;  // keys fetched per lane per batch
     constexpr int NGB = kN2Waves * RS::NG;        // lane groups per block
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_start[kYtMax + 1];
-    const int tile = xcd_block();  // consecutive tiles (one sample's rows) on one XCD, as the CSR build wrote them
+    // consecutive tiles (one sample's rows) on one XCD, as the CSR build wrote them; the QS blocks of a
+    // tile next to each other (its keys read once from that L2)
+    const int lb = xcd_block();
+    const int tile = lb / QS, qs = lb - tile * QS;
     if (tile >= ntiles) return;    // block-uniform (the grid is rounded up to a multiple of 8)
     const int bzx = tile / sg.ntiles_y;
     const int y0 = (tile - bzx * sg.ntiles_y) * sg.YT;
@@ -1573,7 +1612,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
     const int s0 = s_start[0], s1 = s_start[ny];
     const bool empty = s0 == s1;
     if (!empty) {
-        for (int i = threadIdx.x * 4; i < kC * S; i += kN2Block * 4)
+        for (int i = threadIdx.x * 4; i < RS::CPB * S; i += kN2Block * 4)
             *reinterpret_cast<float4*>(lds + i) = make_float4(0.f, 0.f, 0.f, 0.f);
         const int lane = threadIdx.x & 63;
         const int wgrp = lane / RS::LPR;  // the lane's group inside the wave
@@ -1642,7 +1681,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
 #pragma unroll
             for (int u = 0; u < KU; ++u) {
                 const int r = dchk(__shfl(rr[u / RS::LPR], gl0 + u % RS::LPR, kWave), sg.nrows, kDbgSplatRow);
-                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)r * kC + col);
+                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)r * kC + qs * RS::CPB + col);
             }
             if (e + KU < eend) fetch_keys(e + KU);
 #pragma unroll
@@ -1669,11 +1708,11 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
     LSS_STAMP(tslot, 2);
     // the tile, channel plane by channel plane: (B, Z*C, X, Y), channel z*C + c
     const size_t XY = (size_t)sg.X * sg.Y;
-    OutT* obase = out + (size_t)bz * kC * XY + (size_t)x * sg.Y + y0;
+    OutT* obase = out + ((size_t)bz * kC + qs * RS::CPB) * XY + (size_t)x * sg.Y + y0;
     constexpr int VN = 16 / (int)sizeof(OutT);
     if ((sg.Y % VN) == 0 && (ny % VN) == 0 && (y0 % VN) == 0) {
         const int nq = ny / VN;
-        for (int i = threadIdx.x; i < kC * nq; i += kN2Block) {
+        for (int i = threadIdx.x; i < RS::CPB * nq; i += kN2Block) {
             const int c = i / nq, yv = (i - c * nq) * VN;
             float vals[VN];
 #pragma unroll
@@ -1685,7 +1724,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
             store_vec(obase + c * XY + yv, vals);
         }
     } else {
-        for (int i = threadIdx.x; i < kC * ny; i += kN2Block) {
+        for (int i = threadIdx.x; i < RS::CPB * ny; i += kN2Block) {
             const int c = i / ny, yy = i - c * ny;
             obase[c * XY + yy] = from_f32<OutT>(empty ? 0.f : lds[(size_t)c * S + yy]);
         }
@@ -2455,16 +2494,17 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
     }
     if (sg.YT > kYtMax) return LSS_EUNSUPPORTED;  // (choose_yt never picks more)
     const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
-    const dim3 gr2(xcd_grid(nblocks)), bl2(kN2Block);
-    const size_t lds2 = (size_t)kC * nchw2_stride(sg.YT) * sizeof(float);
+    const dim3 gr2(xcd_grid((long)nblocks * kNchwSplit)), bl2(kN2Block);
+    const size_t lds2 = (size_t)(kC / kNchwSplit) * nchw2_stride(sg.YT) * sizeof(float);
 #define LSS_SPLAT2(F, RT, T)                                                                                      \
     do {                                                                                                          \
         if (e0 || e1)                                                                                             \
-            hipExtLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T>), gr2, bl2, (uint32_t)lds2, s, e0, e1, 0, depth,  \
-                                  (const RT*)rows, cell_start, sorted_key, sorted_row, sg, nblocks, (T*)out);     \
+            hipExtLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T, kNchwSplit>), gr2, bl2, (uint32_t)lds2, s, e0, e1, \
+                                  0, depth, (const RT*)rows, cell_start, sorted_key, sorted_row, sg, nblocks,     \
+                                  (T*)out);                                                                       \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T>), gr2, bl2, lds2, s, depth, (const RT*)rows,          \
-                               cell_start, sorted_key, sorted_row, sg, nblocks, (T*)out);                         \
+            hipLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T, kNchwSplit>), gr2, bl2, lds2, s, depth,              \
+                               (const RT*)rows, cell_start, sorted_key, sorted_row, sg, nblocks, (T*)out);        \
     } while (0)
     if (out_dtype == LSS_F32) {
         if (!fused) LSS_SPLAT2(false, float, float);

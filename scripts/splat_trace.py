@@ -1,7 +1,7 @@
 """Per-wave timeline of the channels-last splat from a LSS_TRACE=1 build (diagnostics only).
 
-  python scripts/splat_trace.py --build [-D KNOB=V ...]   # here: builds variants/trace.so
-  python scripts/splat_trace.py                           # GPU box: step-mode launch, prints the timeline
+  python scripts/splat_trace.py --build [--lib NAME] [-D KNOB=V ...]   # here: builds variants/NAME.so
+  python scripts/splat_trace.py [--lib NAME]               # GPU box: step-mode launch, prints the timeline
 """
 import argparse
 import ctypes as ct
@@ -19,15 +19,16 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("-D", action="append", default=[])
     ap.add_argument("--mode", default="step", choices=["warm", "step"])
+    ap.add_argument("--lib", default="trace")
     a = ap.parse_args()
     if a.build:
         from lss_carla_amd import build
-        print(build.build_variant("trace", ["LSS_TRACE=1"] + a.D))
+        print(build.build_variant(a.lib, ["LSS_TRACE=1"] + a.D))
         return
     import torch
     from lss_carla_amd import _lib, ops, synthetic as syn
     from oracle import lss_ref as ref
-    l = _lib.open_library(os.path.join(REPO, "lss-carla_amd", "variants", "trace.so"))
+    l = _lib.open_library(os.path.join(REPO, "lss-carla_amd", "variants", a.lib + ".so"))
     l.lss_debug_trace.argtypes = [ct.c_void_p, ct.c_int]
     dev = torch.device("cuda:0")
     cfg, gc, _ = syn.config_confs("c3")

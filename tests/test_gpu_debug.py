@@ -65,7 +65,7 @@ def test_debug_checks_fire():
     assert _lib.debug_status() == (0, 0, 0, 0)
     for layout, code in ((_lib.NHWC, 6), (_lib.NCHW, 6)):
         bad = ops.SplatPlan(plan.dims, plan.grid, plan.cell_of, plan.cell_start, plan.sorted_key,
-                            plan.sorted_row.clone(), None, None)
+                            plan.sorted_row.clone(), None)
         bad.sorted_row[3] = 10 ** 8  # a context row far outside the buffer
         ops.lift_splat(dn, bad, torch.float32, layout)
         torch.cuda.synchronize()
@@ -73,7 +73,7 @@ def test_debug_checks_fire():
         assert st[0] > 0 and st[1] == code and st[2] == 10 ** 8, st
     # a point id out of range in the keys (the depth-weight gather)
     bad = ops.SplatPlan(plan.dims, plan.grid, plan.cell_of, plan.cell_start, plan.sorted_key.clone(),
-                        plan.sorted_row, None, None)
+                        plan.sorted_row, None)
     bad.sorted_key[5] = (bad.sorted_key[5] >> 32 << 32) | (plan.nprime + 7)
     ops.lift_splat(dn, bad, torch.float32, _lib.NCHW)
     torch.cuda.synchronize()
