@@ -69,8 +69,8 @@ def test_host_inverse_copy_is_not_used_after_an_in_place_update():
     pr, it = rig_a["post_rots"].to(DEV), rig_a["intrins"].to(DEV)
     pr._lss_host, pr._lss_host_version = rig_a["post_rots"], pr._version  # as simbev.finish_batch attaches it
     it._lss_host, it._lss_host_version = rig_a["intrins"], it._version
-    pinv, _ = ops.camera_inverses(pr, it, "host")
+    pinv, _ = ops.camera_inverses(pr, it)
     assert torch.equal(pinv.cpu(), torch.inverse(rig_a["post_rots"]).reshape(-1, 9))
     pr.copy_(rig_b["post_rots"].to(DEV))  # a reused batch buffer: the attached host copy is stale now
-    pinv, _ = ops.camera_inverses(pr, it, "host")
+    pinv, _ = ops.camera_inverses(pr, it)
     assert torch.equal(pinv.cpu(), torch.inverse(rig_b["post_rots"]).reshape(-1, 9))

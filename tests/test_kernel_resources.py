@@ -46,9 +46,9 @@ def _kernel_notes(lib_path):
     return kernels
 
 
-@pytest.mark.parametrize("path", [_lib.LIB_PATH, _lib.DEBUG_LIB_PATH], ids=["product", "debug"])
-def test_hot_path_kernels_use_no_scratch(path):
-    kernels = _kernel_notes(path)
+def test_hot_path_kernels_use_no_scratch():
+    # (the product library only: the debug build's index checks may spill, it is not timed)
+    kernels = _kernel_notes(_lib.LIB_PATH)
     hot = {k: v for k, v in kernels.items() if any(h in k for h in HOT)}
     assert len(hot) >= len(HOT), sorted(hot)
     bad = {k: v for k, v in hot.items()
