@@ -81,12 +81,6 @@ __device__ __forceinline__ uint4 keep_if(bool c, uint4 v) {
     return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
 }
 __device__ __forceinline__ float keep_if(bool c, float v) { return __uint_as_float(__float_as_uint(v) & keep_mask(c)); }
-// c ? a : b, bit for bit, through the laundered mask: both operands stay computed on every path (the
-// loads feeding `a` cannot be sunk into a branch)
-__device__ __forceinline__ float select_bits(bool c, float a, float b) {
-    const unsigned m = keep_mask(c);
-    return __uint_as_float((__float_as_uint(a) & m) | (__float_as_uint(b) & ~m));
-}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -1437,27 +1431,19 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
             else if (!(last && tail_split)) store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + c, acc);
             // else: the first piece of a cut cell stays in acc (combined after the barrier)
         };
-        // round trip 2 (one per kUnroll entries of a group): row slices and depth weights in flight
-        // together. Every entry's weight is broadcast and every row slice consumed by straight-line
-        // code (a select, not a branch, skips the entries past the group's end): with the loads used
-        // only inside the per-entry branches, the compiler sank the first row load behind the depth
-        // gather, and after each cell's row store (inside those branches) it waited vmcnt(0) --
-        // for that store too -- before the next entry's weight: a store round trip per finished cell.
+        // round trip 2 (one per kUnroll entries of a group): row slices and depth weights in flight together
         for (int e = gs; e < ge; e += kUnroll) {
-            u32x4 v[kUnroll];
+            uint4 v[kUnroll];
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
                 const int4 m = *reinterpret_cast<const int4*>(&meta[min(e + u, ge - 1)]);  // (row, p, cell, -)
-                v[u] = *reinterpret_cast<const u32x4*>(rows_base + (size_t)dchk(m.x, g.nrows, kDbgSplatRow) * kC + col);
+                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)dchk(m.x, g.nrows, kDbgSplatRow) * kC + col);
             }
             const float wd = FUSED ? group_weight_load<RS::LPR, kUnroll>(meta, depth, e, ge - 1, lane, nprime) : 0.f;
             if (LSS_TRACE && e == gs && grp == 0) LSS_STAMP(w, 2);
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
-                // (the weight first, on every path: its wait at u = 0 then covers every load of the batch)
-                const float wu = FUSED ? group_weight<RS::LPR>(wd, u, lane) : 1.f;
-                const bool live = e + u < ge;
-                if (live) {
+                if (e + u < ge) {
                     const int cl = meta[e + u].cell;
                     if (cl != cur) {
                         if (cur >= 0) finish(false, col);
@@ -1465,13 +1451,11 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                         for (int i = 0; i < RS::EPL; ++i) acc[i] = 0.f;
                         cur = cl;
                     }
-                }
-                float x[RS::EPL];
-                unpack16(make_uint4(v[u][0], v[u][1], v[u][2], v[u][3]), (const RT*)nullptr, x);
+                    float x[RS::EPL];
+                    unpack16(v[u], (const RT*)nullptr, x);
+                    const float wu = FUSED ? group_weight<RS::LPR>(wd, u, lane) : 1.f;
 #pragma unroll
-                for (int i = 0; i < RS::EPL; ++i) {
-                    const float a = FUSED ? fmaf(wu, x[i], acc[i]) : __fadd_rn(acc[i], x[i]);
-                    acc[i] = select_bits(live, a, acc[i]);
+                    for (int i = 0; i < RS::EPL; ++i) acc[i] = FUSED ? fmaf(wu, x[i], acc[i]) : __fadd_rn(acc[i], x[i]);
                 }
             }
         }
