@@ -214,7 +214,7 @@ def write_ceiling(numel, dtype, dev, reps=10) -> dict:
 
     forms = {}
     for pt in CEILING_PER_THREAD:
-        for fl, fname in ((1, "nt"), (0, "plain")):
+        for fl, fname in ((1, "nt"), (0, "plain"), (2, "sc1")):
             forms[f"pt{pt}_{fname}"] = {"read": round(stamped(pt, fl, "read"), 2),
                                         "dirty": round(stamped(pt, fl, "dirty"), 2)}
     best = min(forms, key=lambda k: forms[k]["read"])

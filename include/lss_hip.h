@@ -71,7 +71,8 @@ int lss_event_record(lss_event_t ev, lss_stream_t stream);
 
 /* Measurement kernels (bench.py's roofline ceiling; not on the model's path).
  * lss_ceiling_store: `bytes` (multiple of 16, dst 16-B aligned) written with 16-B vector stores,
- *   per_thread vectors per lane (grid-strided), flavor 0 plain / 1 non-temporal; optional
+ *   per_thread vectors per lane (grid-strided), flavor 0 plain / 1 non-temporal / 2 device scope
+ *   (sc1: written through the XCD's L2); optional
  *   kernel-stamped events as lss_splat_fwd.
  * lss_ceiling_read: a 16-B-load sweep over `bytes` (sets the cache state before a timed launch);
  *   sink (4 B, device) is never written in practice. */

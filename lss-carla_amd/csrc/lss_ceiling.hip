@@ -16,7 +16,8 @@ namespace {
 
 using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
 
-// flavor 0: plain global_store_dwordx4, 1: non-temporal (nt)
+// flavor 0: plain global_store_dwordx4, 1: non-temporal (nt), 2: device scope (sc1: written through
+// the XCD's L2 and dropped from it, no dirty line left for the end-of-kernel write-back)
 template <int FLAVOR>
 __global__ __launch_bounds__(256) void k_ceiling_store(u32x4* __restrict__ dst, long nvec, int per_thread, unsigned v) {
     const long stride = (long)gridDim.x * blockDim.x;
@@ -25,6 +26,7 @@ __global__ __launch_bounds__(256) void k_ceiling_store(u32x4* __restrict__ dst, 
     for (int k = 0; k < per_thread; ++k, i += stride) {
         if (i < nvec) {
             if (FLAVOR == 1) __builtin_nontemporal_store(x, dst + i);
+            else if (FLAVOR == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst + i), "v"(x) : "memory");
             else dst[i] = x;
         }
     }
@@ -49,14 +51,16 @@ extern "C" {
 
 int lss_ceiling_store(void* dst, size_t bytes, int32_t per_thread, int32_t flavor, lss_stream_t stream,
                       lss_event_t ev_start, lss_event_t ev_stop) {
-    if (!dst || (bytes & 15) || ((uintptr_t)dst & 15) || per_thread < 1 || flavor < 0 || flavor > 1)
+    if (!dst || (bytes & 15) || ((uintptr_t)dst & 15) || per_thread < 1 || flavor < 0 || flavor > 2)
         return LSS_EINVAL;
     const long nvec = (long)(bytes / 16);
     const long threads = (nvec + per_thread - 1) / per_thread;
     const dim3 gr((unsigned)((threads + 255) / 256)), bl(256);
     hipStream_t s = (hipStream_t)stream;
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
-    if (flavor == 1)
+    if (flavor == 2)
+        hipExtLaunchKernelGGL(k_ceiling_store<2>, gr, bl, 0, s, e0, e1, 0, (u32x4*)dst, nvec, (int)per_thread, 0u);
+    else if (flavor == 1)
         hipExtLaunchKernelGGL(k_ceiling_store<1>, gr, bl, 0, s, e0, e1, 0, (u32x4*)dst, nvec, (int)per_thread, 0u);
     else
         hipExtLaunchKernelGGL(k_ceiling_store<0>, gr, bl, 0, s, e0, e1, 0, (u32x4*)dst, nvec, (int)per_thread, 0u);

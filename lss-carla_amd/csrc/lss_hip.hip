@@ -1272,6 +1272,28 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
 #ifndef LSS_INTERLEAVE
 #define LSS_INTERLEAVE 0  // dispatch order of the block groups: 0 chunks first, 1 interleaved, 2 zero fill first
 #endif
+#ifndef LSS_SPLAT_ROLES
+#define LSS_SPLAT_ROLES 0  // experiments only: 1 runs the chunk waves alone, 2 the zero fill alone
+#endif
+#ifndef LSS_SPLAT_SKIP
+#define LSS_SPLAT_SKIP 0  // experiments only (wrong sums): 1 rows from 8 L1-resident rows, 2 one depth line
+#endif
+#ifndef LSS_CHUNK_STORE
+#define LSS_CHUNK_STORE 0  // chunk waves' row stores: 0 plain, 1 non-temporal, 2 device scope (sc1)
+#endif
+#ifndef LSS_ZERO_STORE
+#define LSS_ZERO_STORE 1  // zero rows: 0 plain, 1 non-temporal, 2 device scope (sc1)
+#endif
+// a 16-B vector store of the given flavour (2: sc1, written through the XCD's L2 and dropped from it)
+template <int FLAVOR>
+__device__ __forceinline__ void store16(void* p, u32x4 v) {
+    if constexpr (FLAVOR == 1) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    else if constexpr (FLAVOR == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else *reinterpret_cast<u32x4*>(p) = v;
+}
+#ifndef LSS_CHUNK_PRIO
+#define LSS_CHUNK_PRIO 0  // experiments only: s_setprio of the chunk waves (0: the default priority)
+#endif
 constexpr int kZeroUnits = LSS_ZERO_UNITS;
 constexpr int kSplatWaves = 4;  // waves per block of the channels-last splat (waves are independent)
 constexpr int kSplatBlock = kSplatWaves * kWave;
@@ -1296,8 +1318,7 @@ __device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start, 
         for (int r0 = 0; r0 < kWave; r0 += RPS) {
             const int r = r0 + lane / LPR;
             if ((emask[i] >> r) & 1ull)
-                __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u},
-                                            reinterpret_cast<u32x4*>(cell_row(out, k0 + r, g) + (lane % LPR) * EPL));
+                store16<LSS_ZERO_STORE>(cell_row(out, k0 + r, g) + (lane % LPR) * EPL, u32x4{0u, 0u, 0u, 0u});
         }
     }
 }
@@ -1331,7 +1352,9 @@ template <typename RT> struct RowSlice {
 template <int EPL>
 __device__ __forceinline__ void store_slice(float* dst, const float* a) {
 #pragma unroll
-    for (int i = 0; i < EPL; i += 4) *reinterpret_cast<float4*>(dst + i) = make_float4(a[i], a[i + 1], a[i + 2], a[i + 3]);
+    for (int i = 0; i < EPL; i += 4)
+        store16<LSS_CHUNK_STORE>(dst + i, u32x4{__float_as_uint(a[i]), __float_as_uint(a[i + 1]),
+                                                __float_as_uint(a[i + 2]), __float_as_uint(a[i + 3])});
 }
 template <int EPL>
 __device__ __forceinline__ void store_slice(bf16* dst, const float* a) {
@@ -1339,7 +1362,7 @@ __device__ __forceinline__ void store_slice(bf16* dst, const float* a) {
 #pragma unroll
     for (int i = 0; i < EPL; ++i) v[i] = __float2bfloat16(a[i]);
     if constexpr (EPL == 4) *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(v);
-    else *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(v);
+    else store16<LSS_CHUNK_STORE>(dst, *reinterpret_cast<const u32x4*>(v));
 }
 
 // Entries in flight per lane group. A group holds at most ceil(128 / NG) entries (16 with bf16 rows),
@@ -1361,6 +1384,7 @@ __device__ __forceinline__ float group_weight_load(const EntryMeta* __restrict__
                                                    const float* __restrict__ depth, int e, int last, int lane,
                                                    int nprime) {
     static_assert(LPR >= KU, "one lane per entry of the batch");
+    if (LSS_SPLAT_SKIP & 2) return depth[lane % LPR];
     return depth[dchk(meta[min(e + lane % LPR, last)].p, nprime, kDbgSplatPoint)];
 }
 // weight of entry e + u of the group (broadcast from the group's lane u; one VGPR held across the wait)
@@ -1437,7 +1461,8 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
                 const int4 m = *reinterpret_cast<const int4*>(&meta[min(e + u, ge - 1)]);  // (row, p, cell, -)
-                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)dchk(m.x, g.nrows, kDbgSplatRow) * kC + col);
+                const int mr = (LSS_SPLAT_SKIP & 1) ? (m.x & 7) : m.x;
+                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)dchk(mr, g.nrows, kDbgSplatRow) * kC + col);
             }
             const float wd = FUSED ? group_weight_load<RS::LPR, kUnroll>(meta, depth, e, ge - 1, lane, nprime) : 0.f;
             if (LSS_TRACE && e == gs && grp == 0) LSS_STAMP(w, 2);
@@ -1517,6 +1542,8 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
         cgi = gi - zgi;
     }
     if (!zero_role) {
+        if (LSS_SPLAT_ROLES == 2) return;
+        if (LSS_CHUNK_PRIO) __builtin_amdgcn_s_setprio(LSS_CHUNK_PRIO);
         const int cb = x * ncg + cgi;
         if (cb >= nchunk_blocks) return;
         const int w = cb * kSplatWaves + wave;
@@ -1532,6 +1559,7 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
                                                     (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
 #endif
     } else {
+        if (LSS_SPLAT_ROLES == 1) return;
         const int zb = x * nzg + zgi;
         if (zb >= nzero_blocks) return;
         const int u = (zb * kSplatWaves + wave) * kZeroUnits;

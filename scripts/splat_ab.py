@@ -125,16 +125,16 @@ def main():
         print(f"splat[{name}] {json.dumps(row)}", flush=True)
     if args.ceiling:
         nb = bev.numel() * bev.element_size()
-        for pt in (1, 2, 4, 8, 16):
-            for fl in (0, 1):
+        for pt in (1, 4):
+            for fl in (0, 1, 2):
                 row = {}
                 for m in ("dirty", "read"):
                     t = stamped(lambda a, b: _lib.check(lib.lss_ceiling_store(_lib.ptr(bev), nb, pt, fl, st(), a, b),
                                                         "ceiling"), m)
                     t["GB/s"] = round(nb / (t["avg"] * 1e3), 1)
                     row[m] = t
-                res[f"ceiling[pt={pt},{'nt' if fl else 'plain'}]"] = row
-                print(f"ceiling[pt={pt},{'nt' if fl else 'plain'}] {json.dumps(row)}", flush=True)
+                res[f"ceiling[pt={pt},{('plain', 'nt', 'sc1')[fl]}]"] = row
+                print(f"ceiling[pt={pt},{('plain', 'nt', 'sc1')[fl]}] {json.dumps(row)}", flush=True)
         row = {}
         for m in ("dirty", "read"):
             tot = []
