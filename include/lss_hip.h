@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 17
+#define LSS_ABI_VERSION 18
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -156,6 +156,22 @@ int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, in
  * on one contiguous run of pixel rows; identical results to lss_depthnet_lift on the same values. */
 int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
                            const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream);
+
+/* The depthnet weights for lss_depthnet_lift_nhwc_packed (CamEncode.depthnet.weight / .bias,
+ * src/models.py:47, as the autocast conv would see them): weight (O, K) row-major and bias (O) of
+ * `dtype` (LSS_F32 or LSS_BF16) rounded to bf16 (nearest even, as torch's .to(torch.bfloat16)) into
+ * `packed` (LSS_DN_PACKED_BYTES(K) bytes, 16-B aligned: the lift kernel's MFMA A fragments in the
+ * order one wave-instruction reads them), and, when non-NULL, `plain` (O*K bf16 row-major, 16-B
+ * aligned) and `bias_out` (O bf16). K % 32 == 0, K <= 512, O <= 128 (else LSS_EUNSUPPORTED). */
+#define LSS_DN_PACKED_BYTES(K) ((size_t)(K) * 256)
+int lss_depthnet_pack(const void* weight, const void* bias, int32_t dtype, int32_t O, int32_t K, void* packed,
+                      void* plain, void* bias_out, lss_stream_t stream);
+
+/* lss_depthnet_lift_nhwc with the weights as lss_depthnet_pack wrote them (bias: O bf16);
+ * identical results. */
+int lss_depthnet_lift_nhwc_packed(const void* feat, const void* packed, const void* bias, int32_t K,
+                                  const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype,
+                                  lss_stream_t stream);
 
 /* Splat forward: segmented per-cell sum written as the dense (B, Z*C, X, Y) BEV
  * (voxel_pooling + QuickCumsum.forward + griddify, src/models.py:233-246,

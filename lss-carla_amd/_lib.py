@@ -18,7 +18,7 @@ DEBUG_LIB_PATH = os.path.join(_HERE, "liblss_hip_debug.so")  # LSS_DEBUG=1: devi
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 
 class Dims(ctypes.Structure):
@@ -64,6 +64,8 @@ SIGNATURES = {
     "lss_lift_prep": (ctypes.c_int, [_p, _i32, _DIMS, _p, _p, _i32, _p]),
     "lss_depthnet_lift": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p]),
     "lss_depthnet_lift_nhwc": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p]),
+    "lss_depthnet_pack": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p]),
+    "lss_depthnet_lift_nhwc_packed": (ctypes.c_int, [_p, _p, _p, _i32, _DIMS, _p, _p, _i32, _p]),
     "lss_splat_fwd": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _p, _p, _p]),
     "lss_bev_rows": (ctypes.c_int, [_p, _i32, _p, _DIMS, _GRID, _p, _p]),
     "lss_splat_bwd": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p, _i32, _DIMS, _GRID, _p, _i32, _p]),
@@ -98,6 +100,11 @@ SIGNATURES = {
 }
 
 _lib: Optional[ctypes.CDLL] = None
+
+
+def DN_PACKED_BYTES(K: int) -> int:
+    """LSS_DN_PACKED_BYTES(K) of include/lss_hip.h: bytes of lss_depthnet_pack's fragment buffer."""
+    return K * 256
 
 
 def open_library(path: str) -> ctypes.CDLL:

@@ -1043,10 +1043,36 @@ constexpr int kDn3MaxPix = 48;           // pixels per block at most: three 16-c
 // 4 slices no better, profiles/r03/s3/trace_lift3_slices*.txt)
 constexpr int kDn3Slices = 2;
 
+// The depthnet weights in k_depthnet_lift3's A-fragment order (lss_depthnet_pack): piece (wave w,
+// K step s, lane l) = the 8 bf16 weights of output row min(16 w + (l & 15), O - 1), channels
+// 32 s + 8 (l >> 4) .. + 7, at piece index (w K/32 + s) 64 + l. A wave's fragment load for one K
+// step is then one contiguous 1 KB (eight whole lines) instead of 64 B of each of 16 rows (16 lines,
+// each fetched again by the next K step). Rounded to bf16 as torch's .to(torch.bfloat16) (nearest
+// even); `plain` gets the same values row-major (the backward's GEMM operand), bias_out the bias.
+__device__ __forceinline__ bf16 to_bf16(float x) { return __float2bfloat16(x); }
+__device__ __forceinline__ bf16 to_bf16(bf16 x) { return x; }
+template <typename WT>
+__global__ __launch_bounds__(kBlock) void k_depthnet_pack(const WT* __restrict__ weight, const WT* __restrict__ bias,
+                                                          int O, int K, bf16* __restrict__ packed,
+                                                          bf16* __restrict__ plain, bf16* __restrict__ bias_out) {
+    const int ksteps = K / 32;
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (bias_out && t < O) bias_out[t] = to_bf16(bias[t]);
+    if (t >= kDn3Waves * ksteps * kWave) return;
+    const int l = t % kWave, st = (t / kWave) % ksteps, w = t / (kWave * ksteps);
+    const int r = 16 * w + (l & 15), k0 = 32 * st + 8 * (l >> 4);
+    const WT* src = weight + (size_t)min(r, O - 1) * K + k0;
+    bf16 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = to_bf16(src[j]);
+    *reinterpret_cast<uint4*>(packed + (size_t)t * 8) = *reinterpret_cast<const uint4*>(v);
+    if (plain && r < O) *reinterpret_cast<uint4*>(plain + (size_t)r * K + k0) = *reinterpret_cast<const uint4*>(v);
+}
+
 // One block per CU (8 waves, 2 per SIMD): up to 256 VGPRs per lane. Without the waves-per-EU bound
 // the compiler budgets 128 (the 4 waves per SIMD two blocks' LDS would allow) and kept the feature
 // loads in scratch: stores behind vmcnt waits, reloads behind a vmcnt(0) -- the stage serialised.
-template <int K>
+template <int K, bool PACKED>
 __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_depthnet_lift3(const bf16* __restrict__ feat,
                                                               const bf16* __restrict__ weight,
                                                               const bf16* __restrict__ bias, int D, int HW,
@@ -1108,7 +1134,12 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
             fv[h][t] = *reinterpret_cast<const u32x4*>(tile + (size_t)r * K * 2 + c * 16);
         }
 #pragma unroll
-        for (int s = h * kSSteps; s < (h + 1) * kSSteps; ++s) a[s] = *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
+        for (int s = h * kSSteps; s < (h + 1) * kSSteps; ++s) {
+            if (PACKED)  // lss_depthnet_pack's order: each wave-instruction reads one contiguous 1 KB
+                a[s] = *reinterpret_cast<const bf16x8*>(weight + ((size_t)(wave * kSteps + s) * kWave + lane) * 8);
+            else
+                a[s] = *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
+        }
     }
     float bv[4];
 #pragma unroll
@@ -1167,7 +1198,11 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
 #pragma unroll
     for (int j = 1; j < kParts; ++j) m = fmaxf(m, s_red[0][j][p]);
     float sum = 0.f;
-    for (int d = part; pl && d < D; d += kParts) sum += expf(s_lg[d][p] - m);
+    for (int d = part; pl && d < D; d += kParts) {
+        const float e = expf(s_lg[d][p] - m);
+        s_lg[d][p] = e;  // (this thread's own bins: read back below instead of a second expf)
+        sum += e;
+    }
     if (sm) s_red[1][part][p] = sum;
     __syncthreads();
     sum = 0.f;
@@ -1180,7 +1215,7 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
 #pragma unroll
         for (int i = 0; i < kPerPart; ++i) {
             const int d = part + kParts * i;
-            if (d < D) dst[(size_t)d * HW] = expf(s_lg[d][p] - m) / sum;
+            if (d < D) dst[(size_t)d * HW] = s_lg[d][p] / sum;
         }
     }
     // context rows: the tile's np rows of 64 bf16 are one contiguous run; 8 channels per 16-B store
@@ -1295,7 +1330,10 @@ __device__ __forceinline__ void store16(void* p, u32x4 v) {
 #define LSS_CHUNK_PRIO 0  // experiments only: s_setprio of the chunk waves (0: the default priority)
 #endif
 constexpr int kZeroUnits = LSS_ZERO_UNITS;
-constexpr int kSplatWaves = 4;  // waves per block of the channels-last splat (waves are independent)
+#ifndef LSS_SPLAT_WAVES
+#define LSS_SPLAT_WAVES 4  // waves per block of the channels-last splat (waves are independent)
+#endif
+constexpr int kSplatWaves = LSS_SPLAT_WAVES;
 constexpr int kSplatBlock = kSplatWaves * kWave;
 constexpr int kSplatMinWaves = 7;  // occupancy floor (waves per SIMD): 72 VGPRs, 16 KB LDS per block
 
@@ -1589,42 +1627,24 @@ constexpr int kN2Waves = 4;  // waves per NCHW tile block (more lane groups shar
 // profiles/r03/pad0_eval.txt)
 __host__ __device__ constexpr int nchw2_stride(int yt) { return (yt + 3) & ~3; }
 constexpr int kN2Block = kN2Waves * kWave;
-#ifndef LSS_NCHW_SPLIT
-#define LSS_NCHW_SPLIT 1  // channel splits of the NCHW tile kernel (QS: blocks per tile)
-#endif
-constexpr int kNchwSplit = LSS_NCHW_SPLIT;
 
-
-// QS > 1: the tile's channels are split over QS blocks (block (tile, q) sums channels
-// [q C/QS, (q+1) C/QS) of every entry: LPR = C/QS/EPL lanes per row slice, QS times the lane groups per
-// tile), so a dense tile's entries are spread over QS x more groups -- the dense tiles near the ego
-// were the kernel's tail (trace_splat_fwd_nchw2_c2.txt: sums p50 3.6 us, max 9.4). Same association
-// per channel: identical bits for every QS.
-template <int QS, typename RT> struct TileSlice {
-    static constexpr int CPB = kC / QS;          // channels per block
-    static constexpr int EPL = 16 / sizeof(RT);  // row elements per 16-B lane slice
-    static constexpr int LPR = CPB / EPL;        // lanes per row slice = lanes per group
-    static constexpr int NG = kWave / LPR;       // groups per wave
-    static_assert(CPB % EPL == 0 && LPR >= 1, "whole 16-B slices per block");
-};
-
-template <bool FUSED, typename RT, typename OutT, int QS>
+template <bool FUSED, typename RT, typename OutT>
 __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __restrict__ depth,
                                                              const RT* __restrict__ rows_base,
                                                              const int32_t* __restrict__ cell_start,
                                                              const long long* __restrict__ sorted_key,
                                                              const int32_t* __restrict__ sorted_row, SplatGeo sg,
                                                              int ntiles, OutT* __restrict__ out) {
-    using RS = TileSlice<QS, RT>;
+    using RS = RowSlice<RT>;
     constexpr int KU = 8;                         // context rows in flight per group and batch
     constexpr int KPL = (KU + RS::LPR - 1) / RS::LPR;  // keys fetched per lane per batch
     constexpr int NGB = kN2Waves * RS::NG;        // lane groups per block
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_start[kYtMax + 1];
-    // consecutive tiles (one sample's rows) on one XCD, as the CSR build wrote them; the QS blocks of a
-    // tile next to each other (its keys read once from that L2)
-    const int lb = xcd_block();
-    const int tile = lb / QS, qs = lb - tile * QS;
+    // consecutive tiles (one sample's rows) on one XCD, as the CSR build wrote them
+    // (a tile's channels split over 2 / 4 blocks, for more lane groups per dense tile, was slower:
+    // c2 20.5 / 32.9 vs 18.6 us, round 4)
+    const int tile = xcd_block();
     if (tile >= ntiles) return;    // block-uniform (the grid is rounded up to a multiple of 8)
     const int bzx = tile / sg.ntiles_y;
     const int y0 = (tile - bzx * sg.ntiles_y) * sg.YT;
@@ -1640,7 +1660,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
     const int s0 = s_start[0], s1 = s_start[ny];
     const bool empty = s0 == s1;
     if (!empty) {
-        for (int i = threadIdx.x * 4; i < RS::CPB * S; i += kN2Block * 4)
+        for (int i = threadIdx.x * 4; i < kC * S; i += kN2Block * 4)
             *reinterpret_cast<float4*>(lds + i) = make_float4(0.f, 0.f, 0.f, 0.f);
         const int lane = threadIdx.x & 63;
         const int wgrp = lane / RS::LPR;  // the lane's group inside the wave
@@ -1709,7 +1729,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
 #pragma unroll
             for (int u = 0; u < KU; ++u) {
                 const int r = dchk(__shfl(rr[u / RS::LPR], gl0 + u % RS::LPR, kWave), sg.nrows, kDbgSplatRow);
-                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)r * kC + qs * RS::CPB + col);
+                v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)r * kC + col);
             }
             if (e + KU < eend) fetch_keys(e + KU);
 #pragma unroll
@@ -1736,11 +1756,11 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
     LSS_STAMP(tslot, 2);
     // the tile, channel plane by channel plane: (B, Z*C, X, Y), channel z*C + c
     const size_t XY = (size_t)sg.X * sg.Y;
-    OutT* obase = out + ((size_t)bz * kC + qs * RS::CPB) * XY + (size_t)x * sg.Y + y0;
+    OutT* obase = out + (size_t)bz * kC * XY + (size_t)x * sg.Y + y0;
     constexpr int VN = 16 / (int)sizeof(OutT);
     if ((sg.Y % VN) == 0 && (ny % VN) == 0 && (y0 % VN) == 0) {
         const int nq = ny / VN;
-        for (int i = threadIdx.x; i < RS::CPB * nq; i += kN2Block) {
+        for (int i = threadIdx.x; i < kC * nq; i += kN2Block) {
             const int c = i / nq, yv = (i - c * nq) * VN;
             float vals[VN];
 #pragma unroll
@@ -1752,7 +1772,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
             store_vec(obase + c * XY + yv, vals);
         }
     } else {
-        for (int i = threadIdx.x; i < RS::CPB * ny; i += kN2Block) {
+        for (int i = threadIdx.x; i < kC * ny; i += kN2Block) {
             const int c = i / ny, yy = i - c * ny;
             obase[c * XY + yy] = from_f32<OutT>(empty ? 0.f : lds[(size_t)c * S + yy]);
         }
@@ -2449,8 +2469,9 @@ int lss_depthnet_lift(const void* feat, const void* weight, const void* bias, in
     return launch_status();
 }
 
-int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
-                           const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream) {
+static int depthnet_lift_nhwc(const void* feat, const void* weight, bool packed, const void* bias, int32_t dtype,
+                              int32_t K, const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype,
+                              lss_stream_t stream) {
     if (!dims_ok(dims) || !feat || !weight || !bias || !depth || !ctx_t) return LSS_EINVAL;
     if (((uintptr_t)feat | (uintptr_t)weight) & 15) return LSS_EINVAL;  // 16-B vector loads of the rows
     if (dtype != LSS_BF16 || ctx_dtype != LSS_BF16) return LSS_EUNSUPPORTED;
@@ -2462,9 +2483,43 @@ int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bia
     // the pixels (every block holds at least one)
     const long nlift = std::min<long>(npix, std::max<long>(device_cus(), (npix + kDn3MaxPix - 1) / kDn3MaxPix));
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL((k_depthnet_lift3<512>), dim3(xcd_grid(nlift)), dim3(kDn3Block), 0, s, (const bf16*)feat,
-                       (const bf16*)weight, (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, depth,
-                       (bf16*)ctx_t);
+    if (packed)
+        hipLaunchKernelGGL((k_depthnet_lift3<512, true>), dim3(xcd_grid(nlift)), dim3(kDn3Block), 0, s, (const bf16*)feat,
+                           (const bf16*)weight, (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, depth,
+                           (bf16*)ctx_t);
+    else
+        hipLaunchKernelGGL((k_depthnet_lift3<512, false>), dim3(xcd_grid(nlift)), dim3(kDn3Block), 0, s, (const bf16*)feat,
+                           (const bf16*)weight, (const bf16*)bias, dims->D, HW, (int)npix, (int)nlift, depth,
+                           (bf16*)ctx_t);
+    return launch_status();
+}
+
+int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bias, int32_t dtype, int32_t K,
+                           const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype, lss_stream_t stream) {
+    return depthnet_lift_nhwc(feat, weight, false, bias, dtype, K, dims, depth, ctx_t, ctx_dtype, stream);
+}
+
+int lss_depthnet_lift_nhwc_packed(const void* feat, const void* packed, const void* bias, int32_t K,
+                                  const lss_dims_t* dims, float* depth, void* ctx_t, int32_t ctx_dtype,
+                                  lss_stream_t stream) {
+    return depthnet_lift_nhwc(feat, packed, true, bias, LSS_BF16, K, dims, depth, ctx_t, ctx_dtype, stream);
+}
+
+int lss_depthnet_pack(const void* weight, const void* bias, int32_t dtype, int32_t O, int32_t K, void* packed,
+                      void* plain, void* bias_out, lss_stream_t stream) {
+    if (!weight || !packed || (bias_out && !bias)) return LSS_EINVAL;
+    if (((uintptr_t)packed | (uintptr_t)plain) & 15) return LSS_EINVAL;
+    if (K <= 0 || K % 32 != 0 || K > kDnMaxK || O <= 0 || O > kDn3Waves * 16) return LSS_EUNSUPPORTED;
+    const int n = std::max(kDn3Waves * (K / 32) * kWave, (int)O);
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == LSS_F32)
+        hipLaunchKernelGGL(k_depthnet_pack<float>, dim3(grid_blocks(n, kBlock)), dim3(kBlock), 0, s, (const float*)weight,
+                           (const float*)bias, (int)O, (int)K, (bf16*)packed, (bf16*)plain, (bf16*)bias_out);
+    else if (dtype == LSS_BF16)
+        hipLaunchKernelGGL(k_depthnet_pack<bf16>, dim3(grid_blocks(n, kBlock)), dim3(kBlock), 0, s, (const bf16*)weight,
+                           (const bf16*)bias, (int)O, (int)K, (bf16*)packed, (bf16*)plain, (bf16*)bias_out);
+    else
+        return LSS_EINVAL;
     return launch_status();
 }
 
@@ -2522,16 +2577,16 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
     }
     if (sg.YT > kYtMax) return LSS_EUNSUPPORTED;  // (choose_yt never picks more)
     const int nblocks = dims->B * sg.Z * sg.X * sg.ntiles_y;
-    const dim3 gr2(xcd_grid((long)nblocks * kNchwSplit)), bl2(kN2Block);
-    const size_t lds2 = (size_t)(kC / kNchwSplit) * nchw2_stride(sg.YT) * sizeof(float);
+    const dim3 gr2(xcd_grid((long)nblocks)), bl2(kN2Block);
+    const size_t lds2 = (size_t)kC * nchw2_stride(sg.YT) * sizeof(float);
 #define LSS_SPLAT2(F, RT, T)                                                                                      \
     do {                                                                                                          \
         if (e0 || e1)                                                                                             \
-            hipExtLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T, kNchwSplit>), gr2, bl2, (uint32_t)lds2, s, e0, e1, \
+            hipExtLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T>), gr2, bl2, (uint32_t)lds2, s, e0, e1, \
                                   0, depth, (const RT*)rows, cell_start, sorted_key, sorted_row, sg, nblocks,     \
                                   (T*)out);                                                                       \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T, kNchwSplit>), gr2, bl2, lds2, s, depth,              \
+            hipLaunchKernelGGL((k_splat_fwd_nchw2<F, RT, T>), gr2, bl2, lds2, s, depth,              \
                                (const RT*)rows, cell_start, sorted_key, sorted_row, sg, nblocks, (T*)out);        \
     } while (0)
     if (out_dtype == LSS_F32) {

@@ -484,21 +484,28 @@ class DepthnetLiftSplat(torch.autograd.Function):
     with the depth softmax and the context-row layout, src/models.py:47, 55-59) and lss_splat_fwd.
     The (B*N, D+C, H, W) depthnet output is never materialised in the forward.
 
-    bf16 only (the autocast training path): under autocast the inputs are cast to bf16 as the
-    reference's ``nn.Conv2d`` would be. Backward: lss_splat_bwd gives d(logits); the conv's own
-    backward (MIOpen) turns it into d(feat), d(weight), d(bias).
+    bf16 only (the autocast training path): under autocast the operands are rounded to bf16 as the
+    reference's ``nn.Conv2d`` would see them -- the features by a cast, the weight and bias by
+    lss_depthnet_pack on the channels-last path (one launch: the lift kernel's fragment order, the
+    plain bf16 weight for the backward and the bf16 bias), by casts otherwise. Backward:
+    lss_splat_bwd gives d(logits); the conv's own backward turns it into d(feat), d(weight), d(bias).
     """
 
     @staticmethod
-    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
+    @torch.amp.custom_fwd(device_type="cuda")
     def forward(ctx, feat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, plan: SplatPlan,
                 out_dtype: torch.dtype, layout: int):
         dev = _require_cuda(feat, weight, bias)
         lib = _lib.load()
         B, N, D, H, W = plan.dims
         O, K = weight.shape[0], weight.shape[1]
-        if feat.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16 or bias.dtype != torch.bfloat16:
+        bf = torch.bfloat16
+        if torch.is_autocast_enabled("cuda"):
+            feat = feat.to(bf)
+        elif feat.dtype != bf or weight.dtype != bf or bias.dtype != bf:
             raise RuntimeError("lss_carla_amd: the fused depthnet path is bf16 (run it under torch.autocast)")
+        if weight.dtype not in (torch.float32, bf) or bias.dtype != weight.dtype:
+            raise RuntimeError(f"lss_carla_amd: depthnet weight / bias of dtype {weight.dtype} / {bias.dtype}")
         if feat.shape != (B * N, K, H, W) or O != D + C_CAM or tuple(weight.shape[2:]) != (1, 1):
             raise RuntimeError(f"depthnet shapes feat {tuple(feat.shape)} weight {tuple(weight.shape)} do not match "
                                f"the plan (B*N={B * N}, D+C={D + C_CAM}, H={H}, W={W})")
@@ -509,17 +516,28 @@ class DepthnetLiftSplat(torch.autograd.Function):
         f = feat.detach() if nhwc else feat.detach().contiguous()
         if f.data_ptr() % 16:
             f = f.clone(memory_format=torch.channels_last if nhwc else torch.contiguous_format)
-        w = weight.detach().reshape(O, K).contiguous()
-        b = bias.detach().contiguous()
         depth = torch.empty(B * N, D, H, W, device=dev, dtype=torch.float32)
-        ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=torch.bfloat16)
+        ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=bf)
         X, Y, Z = plan.grid.nx
         out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
-        lift = lib.lss_depthnet_lift_nhwc if nhwc else lib.lss_depthnet_lift
-        _lib.check(lift(_lib.ptr(f), _lib.ptr(w), _lib.ptr(b), _lib.BF16, K, plan.c_dims, _lib.ptr(depth),
-                        _lib.ptr(ctx_t), _lib.BF16, _lib.stream_handle(dev)), "lss_depthnet_lift")
+        st = _lib.stream_handle(dev)
+        if nhwc:
+            packed = torch.empty(_lib.DN_PACKED_BYTES(K) // 2, device=dev, dtype=bf)
+            w = torch.empty(O, K, device=dev, dtype=bf)
+            b = torch.empty(O, device=dev, dtype=bf)
+            _lib.check(lib.lss_depthnet_pack(_lib.ptr(weight.detach().reshape(O, K).contiguous()),
+                                             _lib.ptr(bias.detach().contiguous()), _lib.dtype_code(weight.dtype),
+                                             O, K, _lib.ptr(packed), _lib.ptr(w), _lib.ptr(b), st), "lss_depthnet_pack")
+            _lib.check(lib.lss_depthnet_lift_nhwc_packed(_lib.ptr(f), _lib.ptr(packed), _lib.ptr(b), K, plan.c_dims,
+                                                         _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, st),
+                       "lss_depthnet_lift_nhwc_packed")
+        else:
+            w = weight.detach().to(bf).reshape(O, K).contiguous()
+            b = bias.detach().to(bf).contiguous()
+            _lib.check(lib.lss_depthnet_lift(_lib.ptr(f), _lib.ptr(w), _lib.ptr(b), _lib.BF16, K, plan.c_dims,
+                                             _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, st), "lss_depthnet_lift")
         _splat_fwd_launch(plan, depth, ctx_t, None, out, layout)
-        ctx.save_for_backward(f, weight, depth, ctx_t)
+        ctx.save_for_backward(f, w.view(weight.shape), depth, ctx_t)
         ctx.plan = plan
         return out
 

@@ -131,6 +131,17 @@ def main():
         r["depthnet_lift_nhwc (channels-last feat)"] = timeit("depthnet_lift_nhwc", lambda: _lib.check(
             l.lss_depthnet_lift_nhwc(_lib.ptr(feat_cl), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims,
                                      _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, st()), "lift3"))
+        if hasattr(l, "lss_depthnet_pack"):
+            packed = torch.empty(_lib.DN_PACKED_BYTES(512) // 2, device=dev, dtype=torch.bfloat16)
+            _lib.check(l.lss_depthnet_pack(_lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, D + 64, 512, _lib.ptr(packed),
+                                           None, None, st()), "pack")
+            r["depthnet_lift_nhwc_packed (fragment-order weights)"] = timeit("depthnet_lift_nhwc_packed", lambda: _lib.check(
+                l.lss_depthnet_lift_nhwc_packed(_lib.ptr(feat_cl), _lib.ptr(packed), _lib.ptr(bdn), 512, dims,
+                                                _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, st()), "lift3p"))
+            wf, bfl = wdn.float().contiguous(), bdn.float()
+            r["depthnet_pack (fp32 -> fragments + plain + bias)"] = timeit("depthnet_pack", lambda: _lib.check(
+                l.lss_depthnet_pack(_lib.ptr(wf), _lib.ptr(bfl), _lib.F32, D + 64, 512, _lib.ptr(packed),
+                                    _lib.ptr(wdn), _lib.ptr(bdn), st()), "pack"))
         lift_prep(ctx_t, _lib.BF16)()
         lift_prep(ctx_f, _lib.F32)()
         if not args.only or "splat_fwd" in args.only:

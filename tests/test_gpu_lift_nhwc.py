@@ -1,8 +1,8 @@
 """Fused depthnet lift on channels-last features (lss_depthnet_lift_nhwc, k_depthnet_lift3).
 
 The kernel must give the same bits as the NCHW kernel (k_depthnet_lift2) on the same values -- same
-MFMA operands, same K order, same epilogue -- at every BASELINE config it serves, with and without the
-CSR-ordered depth copy and the empty-row fill; at pixel counts the NCHW kernel does not tile (odd
+MFMA operands, same K order, same epilogue -- at every BASELINE config it serves, with the weights as
+they lie or in lss_depthnet_pack's fragment order; at pixel counts the NCHW kernel does not tile (odd
 feature maps, fewer pixels than CUs) it is checked against the fp64 conv + the oracle's lift
 (src/models.py:47, 52-59).
 """
@@ -55,6 +55,56 @@ def test_nhwc_kernel_bit_identical_to_nchw_kernel(name):
     d0, c0 = _run(lib.lss_depthnet_lift, feat, weight, bias, plan.c_dims)
     d1, c1 = _run(lib.lss_depthnet_lift_nhwc, feat_cl, weight, bias, plan.c_dims)
     assert torch.equal(d0, d1) and torch.equal(c0, c1)
+
+
+def _pack(weight, bias):
+    O, K = weight.shape
+    packed = torch.full((_lib.DN_PACKED_BYTES(K) // 2,), float("nan"), device=DEV, dtype=torch.bfloat16)
+    plain = torch.full((O, K), float("nan"), device=DEV, dtype=torch.bfloat16)
+    b16 = torch.full((O,), float("nan"), device=DEV, dtype=torch.bfloat16)
+    _lib.check(_lib.load().lss_depthnet_pack(_lib.ptr(weight), _lib.ptr(bias), _lib.dtype_code(weight.dtype), O, K,
+                                             _lib.ptr(packed), _lib.ptr(plain), _lib.ptr(b16),
+                                             _lib.stream_handle(DEV)), "pack")
+    torch.cuda.synchronize()
+    return packed, plain, b16
+
+
+@pytest.mark.parametrize("name", ["c1", "c3", "c5"])
+@pytest.mark.parametrize("wdtype", [torch.float32, torch.bfloat16])
+def test_packed_weights_bit_identical(name, wdtype):
+    """lss_depthnet_pack (fp32 master or bf16 weights -> the fragment order, the plain bf16 copy and the
+    bf16 bias: torch's round to nearest even) + lss_depthnet_lift_nhwc_packed give the bits of
+    lss_depthnet_lift_nhwc on the torch-rounded weights."""
+    cfg, gc, _ = syn.config_confs(name)
+    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
+    D, H, W = ref.create_frustum(fd, gc["dbound"]).shape[:3]
+    g = torch.Generator().manual_seed(3)
+    feat = torch.randn(B * N, 512, H, W, generator=g).to(torch.bfloat16).to(DEV)
+    weight = (torch.randn(D + 64, 512, generator=g) * 0.05).to(wdtype).to(DEV)
+    bias = (torch.randn(D + 64, generator=g) * 0.1).to(wdtype).to(DEV)
+    feat_cl = feat.contiguous(memory_format=torch.channels_last)
+    dims = _lib.Dims(B, N, D, H, W, 64)
+    packed, plain, b16 = _pack(weight, bias)
+    assert torch.equal(plain, weight.to(torch.bfloat16)) and torch.equal(b16, bias.to(torch.bfloat16))
+    lib = _lib.load()
+    d0, c0 = _run(lib.lss_depthnet_lift_nhwc, feat_cl, plain, b16, dims)
+    depth = torch.full_like(d0, float("nan"))
+    ctx_t = torch.full_like(c0, float("nan"))
+    _lib.check(lib.lss_depthnet_lift_nhwc_packed(_lib.ptr(feat_cl), _lib.ptr(packed), _lib.ptr(b16), 512, dims,
+                                                 _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16,
+                                                 _lib.stream_handle(DEV)), "lift packed")
+    torch.cuda.synchronize()
+    assert torch.equal(depth, d0) and torch.equal(ctx_t, c0)
+
+
+def test_pack_rejects_bad_arguments():
+    lib = _lib.load()
+    w = torch.zeros(105, 512, device=DEV)
+    buf = torch.empty(_lib.DN_PACKED_BYTES(512) // 2, device=DEV, dtype=torch.bfloat16)
+    st = _lib.stream_handle(DEV)
+    assert lib.lss_depthnet_pack(_lib.ptr(w), _lib.ptr(w), _lib.F32, 105, 500, _lib.ptr(buf), None, None, st) == -2
+    assert lib.lss_depthnet_pack(_lib.ptr(w), _lib.ptr(w), _lib.F32, 129, 512, _lib.ptr(buf), None, None, st) == -2
+    assert lib.lss_depthnet_pack(_lib.ptr(w), None, _lib.F32, 105, 512, _lib.ptr(buf), None, _lib.ptr(buf), st) == -1
 
 
 @pytest.mark.parametrize("shape", [(1, 3, 5, 7, 41), (2, 5, 9, 13, 41), (1, 1, 8, 22, 60), (8, 6, 8, 22, 41)])
