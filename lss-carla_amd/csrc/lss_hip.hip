@@ -1301,39 +1301,17 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
 //   zero waves: kZeroUnits x 64 consecutive cells each; the rows of the empty cells are written as
 //     zeros with 16-B non-temporal stores, so every BEV element is written exactly once.
 // The CSR's sentinel tail (key -1 past the last entry, lss_csr_build) spares a load of the count.
-#ifndef LSS_ZERO_UNITS
-#define LSS_ZERO_UNITS 1  // 64-cell zero-fill units per wave (their cell_start loads in flight together)
-#endif
-#ifndef LSS_INTERLEAVE
-#define LSS_INTERLEAVE 0  // dispatch order of the block groups: 0 chunks first, 1 interleaved, 2 zero fill first
-#endif
 #ifndef LSS_SPLAT_ROLES
 #define LSS_SPLAT_ROLES 0  // experiments only: 1 runs the chunk waves alone, 2 the zero fill alone
 #endif
 #ifndef LSS_SPLAT_SKIP
-#define LSS_SPLAT_SKIP 0  // experiments only (wrong sums): 1 rows from 8 L1-resident rows, 2 one depth line
+#define LSS_SPLAT_SKIP 0  // experiments only (wrong sums): 1 rows from 8 L1-resident rows, 2 one depth line, 4 no row stores
 #endif
-#ifndef LSS_CHUNK_STORE
-#define LSS_CHUNK_STORE 0  // chunk waves' row stores: 0 plain, 1 non-temporal, 2 device scope (sc1)
-#endif
-#ifndef LSS_ZERO_STORE
-#define LSS_ZERO_STORE 1  // zero rows: 0 plain, 1 non-temporal, 2 device scope (sc1)
-#endif
-// a 16-B vector store of the given flavour (2: sc1, written through the XCD's L2 and dropped from it)
-template <int FLAVOR>
-__device__ __forceinline__ void store16(void* p, u32x4 v) {
-    if constexpr (FLAVOR == 1) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-    else if constexpr (FLAVOR == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-    else *reinterpret_cast<u32x4*>(p) = v;
-}
-#ifndef LSS_CHUNK_PRIO
-#define LSS_CHUNK_PRIO 0  // experiments only: s_setprio of the chunk waves (0: the default priority)
-#endif
-constexpr int kZeroUnits = LSS_ZERO_UNITS;
-#ifndef LSS_SPLAT_WAVES
-#define LSS_SPLAT_WAVES 4  // waves per block of the channels-last splat (waves are independent)
-#endif
-constexpr int kSplatWaves = LSS_SPLAT_WAVES;
+// 64-cell zero-fill units per wave: 1 (2-16 with their cell_start loads in flight together measured
+// slower, as did dispatching the zero fill first or interleaved with the chunks: rounds 3-4)
+constexpr int kZeroUnits = 1;
+constexpr int kSplatWaves = 4;  // waves per block of the channels-last splat (waves are independent;
+                                // 2 / 7 / 8 measured slower, round 4)
 constexpr int kSplatBlock = kSplatWaves * kWave;
 constexpr int kSplatMinWaves = 7;  // occupancy floor (waves per SIMD): 72 VGPRs, 16 KB LDS per block
 
@@ -1356,7 +1334,8 @@ __device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start, 
         for (int r0 = 0; r0 < kWave; r0 += RPS) {
             const int r = r0 + lane / LPR;
             if ((emask[i] >> r) & 1ull)
-                store16<LSS_ZERO_STORE>(cell_row(out, k0 + r, g) + (lane % LPR) * EPL, u32x4{0u, 0u, 0u, 0u});
+                __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u},
+                                            reinterpret_cast<u32x4*>(cell_row(out, k0 + r, g) + (lane % LPR) * EPL));
         }
     }
 }
@@ -1390,9 +1369,7 @@ template <typename RT> struct RowSlice {
 template <int EPL>
 __device__ __forceinline__ void store_slice(float* dst, const float* a) {
 #pragma unroll
-    for (int i = 0; i < EPL; i += 4)
-        store16<LSS_CHUNK_STORE>(dst + i, u32x4{__float_as_uint(a[i]), __float_as_uint(a[i + 1]),
-                                                __float_as_uint(a[i + 2]), __float_as_uint(a[i + 3])});
+    for (int i = 0; i < EPL; i += 4) *reinterpret_cast<float4*>(dst + i) = make_float4(a[i], a[i + 1], a[i + 2], a[i + 3]);
 }
 template <int EPL>
 __device__ __forceinline__ void store_slice(bf16* dst, const float* a) {
@@ -1400,7 +1377,7 @@ __device__ __forceinline__ void store_slice(bf16* dst, const float* a) {
 #pragma unroll
     for (int i = 0; i < EPL; ++i) v[i] = __float2bfloat16(a[i]);
     if constexpr (EPL == 4) *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(v);
-    else store16<LSS_CHUNK_STORE>(dst, *reinterpret_cast<const u32x4*>(v));
+    else *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(v);
 }
 
 // Entries in flight per lane group. A group holds at most ceil(128 / NG) entries (16 with bf16 rows),
@@ -1490,7 +1467,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
         };
         auto finish = [&](bool last, int c) {  // the cell `cur` ends at this point of the group
             if (cur == first_cell && head_split) put(part + grp * kC, c);  // a later piece of a cut cell
-            else if (!(last && tail_split)) store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + c, acc);
+            else if (!(last && tail_split) && !(LSS_SPLAT_SKIP & 4)) store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + c, acc);
             // else: the first piece of a cut cell stays in acc (combined after the barrier)
         };
         // round trip 2 (one per kUnroll entries of a group): row slices and depth weights in flight together
@@ -1538,7 +1515,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
 #pragma unroll
                 for (int i = 0; i < RS::EPL; ++i) acc[i] = __fadd_rn(acc[i], part[q * kC + tcol + i]);
             }
-            store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + tcol, acc);
+            if (!(LSS_SPLAT_SKIP & 4)) store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + tcol, acc);
         }
     }
     if (big >= 0) {
@@ -1556,32 +1533,21 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
                                                            const long long* __restrict__ sorted_key,
                                                            const int32_t* __restrict__ sorted_row, BevGeo g,
                                                            int nprime, int nchunk_blocks, int nzero_blocks,
-                                                           int order, OutT* __restrict__ out) {
+                                                           OutT* __restrict__ out) {
     __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
     __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][RowSlice<RT>::NG * kC];
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
-    // Blocks come in groups of 8, one per XCD (blocks are dealt round-robin over the 8 XCDs). `order`
-    // 0 dispatches the chunk groups first, then the zero-fill groups; 1 interleaves them evenly; 2 puts
-    // the zero fill first. The chunk blocks of XCD x take one contiguous run of chunks, whose context
-    // rows (a few cameras) then stay in that L2.
+    // Blocks come in groups of 8, one per XCD (blocks are dealt round-robin over the 8 XCDs): the
+    // chunk groups first, then the zero-fill groups (c3: all 5,386 chunk waves start at t = 0 in the
+    // 7,168 wave slots, the zero waves take the slots left). The chunk blocks of XCD x take one
+    // contiguous run of chunks, whose context rows (a few cameras) then stay in that L2.
     const int ncg = (nchunk_blocks + 7) >> 3, nzg = (nzero_blocks + 7) >> 3;
     const int gi = blockIdx.x >> 3, x = blockIdx.x & 7;
-    int zgi = gi - ncg, cgi = gi;
-    bool zero_role = gi >= ncg;
-    if (order == 2) {
-        zero_role = gi < nzg;
-        zgi = gi;
-        cgi = gi - nzg;
-    } else if (order == 1) {
-        const int G = ncg + nzg;
-        zgi = (gi * nzg) / G;
-        zero_role = ((gi + 1) * nzg) / G > zgi;
-        cgi = gi - zgi;
-    }
+    const int zgi = gi - ncg, cgi = gi;
+    const bool zero_role = gi >= ncg;
     if (!zero_role) {
         if (LSS_SPLAT_ROLES == 2) return;
-        if (LSS_CHUNK_PRIO) __builtin_amdgcn_s_setprio(LSS_CHUNK_PRIO);
         const int cb = x * ncg + cgi;
         if (cb >= nchunk_blocks) return;
         const int w = cb * kSplatWaves + wave;
@@ -2549,19 +2515,16 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), kSplatWaves);
         const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), kSplatWaves);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);
-        // Dispatch order of the two roles (LSS_INTERLEAVE): chunks first by default (c3: all 5,386 chunk
-        // waves start at t = 0 in the 7,168 wave slots and the zero waves take the slots left).
-        const int order = LSS_INTERLEAVE;
 // kernel-stamped events only when asked for: a plain launch is what a hipGraph capture records
 #define LSS_NHWC_FWD(F, RT, T)                                                                                     \
     do {                                                                                                           \
         if (e0 || e1)                                                                                              \
             hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, (const RT*)rows,   \
                                   cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks,      \
-                                  order, (T*)out);                                                                 \
+                                  (T*)out);                                                                 \
         else                                                                                                       \
             hipLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, depth, (const RT*)rows, cell_start,     \
-                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, order, (T*)out);    \
+                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, (T*)out);    \
     } while (0)
         if (out_dtype == LSS_F32) {
             if (!fused) LSS_NHWC_FWD(false, float, float);

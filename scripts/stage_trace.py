@@ -95,9 +95,13 @@ def main():
             _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctxf), _lib.F32, None, _lib.ptr(plan.cell_start),
                                        _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), dims, g,
                                        _lib.ptr(bevf), _lib.F32, _lib.NCHW, st, None, None), "fwd")
-        elif a.kernel == "lift3":  # channels-last features (k_depthnet_lift3)
-            _lib.check(l.lss_depthnet_lift_nhwc(_lib.ptr(feat_cl), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims,
-                                                _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, st), "lift3")
+        elif a.kernel == "lift3":  # channels-last features (k_depthnet_lift3), weights in fragment order
+            if it == 0:
+                packed = torch.empty(_lib.DN_PACKED_BYTES(512) // 2, device=dev, dtype=torch.bfloat16)
+                _lib.check(l.lss_depthnet_pack(_lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, wdn.shape[0], 512,
+                                               _lib.ptr(packed), None, None, st), "pack")
+            _lib.check(l.lss_depthnet_lift_nhwc_packed(_lib.ptr(feat_cl), _lib.ptr(packed), _lib.ptr(bdn), 512, dims,
+                                                       _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, st), "lift3")
         elif a.kernel == "lift":
             _lib.check(l.lss_depthnet_lift(_lib.ptr(feat), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims,
                                            _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, st), "lift")
