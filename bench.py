@@ -74,9 +74,6 @@ def parse():
     ap.add_argument("--miopen-find", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
     ap.add_argument("--hip-bn", type=int, default=1, help="BatchNorm + activation on the lss_bn_* kernels")
     ap.add_argument("--fuse-depthnet", type=int, default=1, help="depthnet 1x1 conv inside the lift kernel (MFMA)")
-    ap.add_argument("--bev-prefill", default="none", choices=["none", "lift", "trunk"],
-                    help="channels-last BEV: empty rows written on a second stream beside the lift / the trunk "
-                         "(lss_splat_zero_empty), the splat writes the occupied rows")
     ap.add_argument("--graph", type=int, default=1,
                     help="replay the step as HIP graphs (fwd+bwd, clip+Adam) with the gradient all-reduce "
                          "between them; 0 = eager (DDP for N>1)")
@@ -290,7 +287,7 @@ def measure_in_graph(args) -> dict | None:
            "--", sys.executable, os.path.abspath(__file__), "--config", args.config, "--batch", str(args.batch),
            "--dtype", args.dtype, "--bev-layout", args.bev_layout, "--steps", str(steps), "--warmup", "3",
            "--profile-steps", "0", "--pmc-traffic", "0", "--cpu-baseline", "0", "--in-graph-prof", "0",
-           "--mode", args.mode, "--bev-prefill", args.bev_prefill]
+           "--mode", args.mode]
     try:
         # the child's progress lines pass through to this process's stderr (no long silence)
         r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL,
@@ -302,13 +299,12 @@ def measure_in_graph(args) -> dict | None:
     if r.returncode != 0 or not files:
         log(f"[bench] in-graph kernel trace failed (rc={r.returncode})")
         return None
-    rows = {"splat": [], "zero": [], "lift": []}
+    rows = {"splat": [], "lift": []}
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row["Kernel_Name"]
-                key = ("splat" if "k_splat_fwd" in k else "zero" if "k_splat_zero" in k
-                       else "lift" if "k_depthnet_lift" in k or "k_lift_prep" in k else None)
+                key = "splat" if "k_splat_fwd" in k else "lift" if ("k_depthnet_lift" in k or "k_lift_prep" in k) else None
                 if key:
                     rows[key].append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
     shutil.rmtree(tmp, ignore_errors=True)
@@ -321,39 +317,13 @@ def measure_in_graph(args) -> dict | None:
     durs = [(e - b) / 1e3 for b, e in sel]
     res = {"us": round(sum(durs) / len(durs), 2), "min_us": round(min(durs), 2), "launches": len(durs),
            "how": "rocprofv3 --kernel-trace of a child run of this script: the 10 timed graph replays"}
-    # the time the splat stage adds after the lift: from the lift kernel's end to the splat's end (with a
-    # prefilled BEV it includes any wait for the zero-fill stream)
-    after, zero = [], []
-    for b, e in sel:
-        lift_end = max((le for lb, le in rows["lift"] if le <= b), default=None)
-        if lift_end is not None:
-            after.append((e - lift_end) / 1e3)
-        z = [(ze - zb) / 1e3 for zb, ze in rows["zero"] if ze <= e]  # this step's zero fill (prefill)
-        if z:
-            zero.append(z[-1])
+    # what the splat adds to the step after the lift: the lift kernel's end to the splat's end (the
+    # kernel plus the launch gap in front of it)
+    after = [(e - max(le for lb, le in rows["lift"] if le <= b)) / 1e3 for b, e in sel
+             if any(le <= b for lb, le in rows["lift"])]
     if after:
         res["after_lift_us"] = round(sum(after) / len(after), 2)
-    if zero:
-        res["zero_fill_us"] = round(sum(zero) / len(zero), 2)
     return res
-
-
-def in_graph_roofline(in_graph, nbytes, prefill, empty_row_bytes):
-    """The splat's in-graph fractions. Without a prefill: algorithmic bytes / the kernel's time. With
-    the empty rows written on a second stream (--bev-prefill): the combined bytes of both kernels / the
-    occupied-row kernel's time (the zero stream runs beside the lift or the trunk), the kernel's own
-    bytes / its time, and in both modes the combined bytes / the time from the lift's end to the
-    splat's end (which includes any wait for the zero stream and the launch gap)."""
-    if not in_graph:
-        return None
-    r = dict(in_graph, frac=round(nbytes / (in_graph["us"] * 1e3) / HBM_PEAK_GBS, 4))
-    if prefill:
-        r["prefill"] = f"empty rows by lss_splat_zero_empty on a second stream beside the {prefill}"
-        r["own_bytes"] = nbytes - empty_row_bytes
-        r["own_frac"] = round((nbytes - empty_row_bytes) / (in_graph["us"] * 1e3) / HBM_PEAK_GBS, 4)
-    if in_graph.get("after_lift_us"):
-        r["after_lift_frac"] = round(nbytes / (in_graph["after_lift_us"] * 1e3) / HBM_PEAK_GBS, 4)
-    return r
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -452,7 +422,6 @@ def build_model(args, dev, gc, dac):
     model = L.compile_model(gc, dac, outC=1).to(dev)
     model.bev_layout = args.bev_layout
     model.fuse_depthnet = bool(args.fuse_depthnet)
-    model.bev_prefill = None if args.bev_prefill == "none" or args.bev_layout != "nhwc" else args.bev_prefill
     if args.bev_layout == "nhwc":
         model.bevencode.to(memory_format=torch.channels_last)
     if args.trunk_channels_last:
@@ -684,11 +653,8 @@ def main():
         with torch.no_grad():
             plan = model.plan(rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"])
             kept = int(plan.cell_start[-1].item())
-            occupied = int((plan.cell_start[1:] != plan.cell_start[:-1]).sum().item())
         out_bytes = 2 if amp_dtype is not None else 4
         nbytes = splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes, ctx_bytes=out_bytes)
-        prefill = model.bev_prefill
-        empty_row_bytes = (B * Z * X * Y - occupied) * 64 * out_bytes
         achieved = nbytes / (splat_ms * 1e-3) / 1e9 if splat_ms else None
         ceiling = write_ceiling(B * Z * 64 * X * Y, amp_dtype or torch.float32, dev)
         frames = world * B * args.steps
@@ -701,7 +667,6 @@ def main():
             "config": {"workload": f"{args.config}: B={B}/GPU x {N} cams x {fd[0]}x{fd[1]}, D={D}, {X}x{Y} BEV, "
                                    + what,
                        "global_batch": world * B, "parallelism": f"dp{world}", "bev_layout": args.bev_layout,
-                       "bev_prefill": prefill,
                        "inverse": "host torch.inverse", "fuse_depthnet": bool(args.fuse_depthnet),
                        "depthwise": args.dw_impl, "batchnorm": "hip" if args.hip_bn else "miopen",
                        "step": "hipgraph" if args.graph else "eager", "flat_params": bool(args.flat_params),
@@ -718,7 +683,8 @@ def main():
                          "traffic_detail": traffic, "algorithmic_bytes": nbytes,
                          "avg_launch_us": round(splat_ms * 1e3, 2) if splat_ms else None,
                          "timed_in": "eager steps after the timed region, kernel-stamped hipEvents",
-                         "in_graph": in_graph_roofline(in_graph, nbytes, prefill, empty_row_bytes),
+                         "in_graph": dict(in_graph, frac=round(nbytes / (in_graph["us"] * 1e3) / HBM_PEAK_GBS, 4))
+                                     if in_graph else None,
                          "write_ceiling": dict(ceiling, splat_frac_of_ceiling=round(achieved / ceiling["GB/s"], 4)
                                                if achieved else None)},
         }

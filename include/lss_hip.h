@@ -192,19 +192,6 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
                   const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype,
                   int32_t out_layout, lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop);
 
-/* The splat forward in two parts, for a caller that overlaps the first with other work on a second
- * stream (channels-last BEV only, else LSS_EUNSUPPORTED):
- * lss_splat_zero_empty: every empty cell's row of `out` (cell_start[k] == cell_start[k+1]) written
- *   as zeros; needs only the CSR's cell starts.
- * lss_splat_fwd_occupied: lss_splat_fwd writing only the occupied cells' rows (the same bits).
- * Both together write every element of `out` once, as lss_splat_fwd does. */
-int lss_splat_zero_empty(const int32_t* cell_start, const lss_dims_t* dims, const lss_grid_t* grid, void* out,
-                         int32_t out_dtype, int32_t out_layout, lss_stream_t stream);
-int lss_splat_fwd_occupied(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
-                           const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
-                           const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype,
-                           int32_t out_layout, lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop);
-
 /* Backward helpers. A "row" is the C gradient values of one cell.
  * lss_bev_rows: NCHW dbev -> rows[cell*C + c] for every occupied cell (others untouched). */
 int lss_bev_rows(const void* dbev, int32_t g_dtype, const int32_t* cell_start,

@@ -67,8 +67,6 @@ SIGNATURES = {
     "lss_depthnet_pack": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p]),
     "lss_depthnet_lift_nhwc_packed": (ctypes.c_int, [_p, _p, _p, _i32, _DIMS, _p, _p, _i32, _p]),
     "lss_splat_fwd": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _p, _p, _p]),
-    "lss_splat_fwd_occupied": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _p, _p, _p]),
-    "lss_splat_zero_empty": (ctypes.c_int, [_p, _DIMS, _GRID, _p, _i32, _i32, _p]),
     "lss_bev_rows": (ctypes.c_int, [_p, _i32, _p, _DIMS, _GRID, _p, _p]),
     "lss_splat_bwd": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p, _i32, _DIMS, _GRID, _p, _i32, _p]),
     "lss_splat_bwd_lifted": (ctypes.c_int, [_p, _i32, _i32, _p, _i32, _DIMS, _GRID, _p, _p]),

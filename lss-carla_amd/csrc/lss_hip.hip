@@ -1578,17 +1578,6 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
     }
 }
 
-// The zero fill alone (lss_splat_zero_empty): the empty rows of a channels-last BEV, one 64-cell unit
-// per wave, XCD-contiguous. It depends only on the CSR's cell starts, so a caller can run it on a
-// second stream beside the lift (or the trunk) and the splat proper (lss_splat_fwd_occupied) then
-// only writes the occupied rows.
-template <typename OutT>
-__global__ __launch_bounds__(kSplatBlock) void k_splat_zero_nhwc(const int32_t* __restrict__ cell_start, BevGeo g,
-                                                               OutT* __restrict__ out) {
-    const int u = (xcd_block() * kSplatWaves + (threadIdx.x >> 6)) * kZeroUnits;
-    if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, g, out, threadIdx.x & 63);
-}
-
 // ---- NCHW (the reference layout), version 2: one block = one tile of YT consecutive cells of a BEV
 // row (b, z, x, y0..y0 + YT), 4 waves = 4 * NG lane groups of LPR lanes (8 lanes x 16 B per context
 // row for bf16 rows, the NHWC chunk's gather shape: 8 rows per wave instruction). The tile's cells are
@@ -2500,13 +2489,12 @@ int lss_depthnet_pack(const void* weight, const void* bias, int32_t dtype, int32
     return launch_status();
 }
 
-static int splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
-                     const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
-                     const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout,
-                     lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop, bool occupied_only) {
+int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
+                  const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
+                  const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout,
+                  lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop) {
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
     if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_key || !out) return LSS_EINVAL;
-    if (occupied_only && out_layout != LSS_NHWC) return LSS_EUNSUPPORTED;
     const bool fused = x_rows == nullptr;
     if (fused && (!depth || !ctx_t || !sorted_row)) return LSS_EINVAL;
     if (fused && ctx_dtype != LSS_F32 && ctx_dtype != LSS_BF16) return LSS_EINVAL;
@@ -2525,9 +2513,7 @@ static int splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, c
         g.ncells = dims->B * sg.Z * sg.X * sg.Y;
         g.nrows = sg.nrows;
         const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), kSplatWaves);
-        // (occupied_only: the chunk groups alone, the empty rows were written by lss_splat_zero_empty)
-        const int nzero_blocks =
-            occupied_only ? 0 : grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), kSplatWaves);
+        const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), kSplatWaves);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);
 // kernel-stamped events only when asked for: a plain launch is what a hipGraph capture records
 #define LSS_NHWC_FWD(F, RT, T)                                                                                     \
@@ -2576,43 +2562,6 @@ static int splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, c
         else LSS_SPLAT2(true, float, bf16);
     }
 #undef LSS_SPLAT2
-    return launch_status();
-}
-
-int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
-                  const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
-                  const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype, int32_t out_layout,
-                  lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop) {
-    return splat_fwd(depth, ctx_t, ctx_dtype, x_rows, cell_start, sorted_key, sorted_row, dims, grid, out, out_dtype,
-                     out_layout, stream, ev_start, ev_stop, false);
-}
-
-int lss_splat_fwd_occupied(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,
-                           const int32_t* cell_start, const long long* sorted_key, const int32_t* sorted_row,
-                           const lss_dims_t* dims, const lss_grid_t* grid, void* out, int32_t out_dtype,
-                           int32_t out_layout, lss_stream_t stream, lss_event_t ev_start, lss_event_t ev_stop) {
-    return splat_fwd(depth, ctx_t, ctx_dtype, x_rows, cell_start, sorted_key, sorted_row, dims, grid, out, out_dtype,
-                     out_layout, stream, ev_start, ev_stop, true);
-}
-
-int lss_splat_zero_empty(const int32_t* cell_start, const lss_dims_t* dims, const lss_grid_t* grid, void* out,
-                         int32_t out_dtype, int32_t out_layout, lss_stream_t stream) {
-    if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !out) return LSS_EINVAL;
-    if (out_dtype != LSS_F32 && out_dtype != LSS_BF16) return LSS_EINVAL;
-    if (out_layout != LSS_NHWC) return LSS_EUNSUPPORTED;
-    const SplatGeo sg = splat_geo(grid, dims);
-    BevGeo g;
-    g.X = sg.X; g.Y = sg.Y; g.Z = sg.Z;
-    g.ncells = dims->B * sg.Z * sg.X * sg.Y;
-    g.nrows = sg.nrows;
-    const int nblocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), kSplatWaves);
-    hipStream_t s = (hipStream_t)stream;
-    if (out_dtype == LSS_F32)
-        hipLaunchKernelGGL(k_splat_zero_nhwc<float>, dim3(xcd_grid(nblocks)), dim3(kSplatBlock), 0, s, cell_start, g,
-                           (float*)out);
-    else
-        hipLaunchKernelGGL(k_splat_zero_nhwc<bf16>, dim3(xcd_grid(nblocks)), dim3(kSplatBlock), 0, s, cell_start, g,
-                           (bf16*)out);
     return launch_status();
 }
 

@@ -315,10 +315,6 @@ class LiftSplatShoot(nn.Module):
         # (pinv, kinv) device buffers filled from host torch.inverse by ops.HostInverses before the
         # step (captured training step); None: get_voxels computes them (host torch.inverse)
         self.static_inverses = None
-        # channels-last BEV on the GPU: where the empty rows are written (ops.prefill_empty_rows):
-        # "lift" -- on a second stream beside the lift (plan after the trunk), "trunk" -- beside the
-        # trunk (plan before it), None -- inside the splat
-        self.bev_prefill = None
         self._grid = ops.GridSpec.from_conf(grid_conf)
 
     def create_frustum(self):
@@ -376,24 +372,16 @@ class LiftSplatShoot(nn.Module):
         if inv is None:
             inv = ops.camera_inverses(post_rots, intrins)
         ce = self.camencode
-        out_dtype = self._bev_dtype(x.device)
-        prefill_at = self.bev_prefill if (self._layout() == _lib.NHWC and x.is_cuda) else None
-
-        def plan_now():
-            p = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
-                                      inverses=inv)
-            return p, (ops.prefill_empty_rows(p, out_dtype) if prefill_at else None)
-        if prefill_at == "trunk":
-            plan, prefill = plan_now()
         feat = ce.dropout(ce.get_eff_depth(x.view(B * N, C, imH, imW)))
-        if prefill_at != "trunk":
-            plan, prefill = plan_now()
+        plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
+                                     inverses=inv)
+        out_dtype = self._bev_dtype(x.device)
         if self.fuse_depthnet and out_dtype == torch.bfloat16 and self.D + self.camC <= 128:
             # depthnet 1x1 conv + softmax + context layout in one MFMA kernel; its
             # tile holds D + C <= 128 output channels (a larger dbound runs the conv as its own op)
             return ops.depthnet_lift_splat(feat, ce.depthnet.weight, ce.depthnet.bias, plan, out_dtype,
-                                           self._layout(), prefill)
-        return ops.lift_splat(ce.depthnet(feat), plan, out_dtype, self._layout(), prefill)
+                                           self._layout())
+        return ops.lift_splat(ce.depthnet(feat), plan, out_dtype, self._layout())
 
     def forward(self, x, rots, trans, intrins, post_rots, post_trans):
         x = self.get_voxels(x, rots, trans, intrins, post_rots, post_trans)

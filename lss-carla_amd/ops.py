@@ -394,67 +394,15 @@ def _new_bev(B, Z, X, Y, dtype, layout, dev) -> torch.Tensor:
     return torch.empty(B, Z * C_CAM, X, Y, device=dev, dtype=dtype)
 
 
-# ----------------------------------------------------------------------------- empty rows on a second stream
-_SIDE_STREAMS = {}
-
-
-def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
-    s = _SIDE_STREAMS.get(dev.index)
-    if s is None:
-        s = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(dev)
-    return s
-
-
-@dataclass
-class BevPrefill:
-    """A channels-last BEV whose empty rows lss_splat_zero_empty writes on a second stream, started
-    right after the plan (they depend only on its cell starts), so the zero stream -- 35.8 of the
-    41 MB at c3 -- runs beside the lift (or the trunk) instead of inside the splat. The splat waits
-    for `done` and writes only the occupied rows (lss_splat_fwd_occupied); same bits. Inside a
-    captured graph the two streams are a fork and a join of the graph."""
-    out: torch.Tensor
-    done: "torch.cuda.Event"
-
-
-def prefill_empty_rows(plan: SplatPlan, out_dtype: torch.dtype) -> BevPrefill:
-    dev = _require_cuda(plan.cell_start)
-    lib = _lib.load()
-    X, Y, Z = plan.grid.nx
-    out = _new_bev(plan.dims[0], Z, X, Y, out_dtype, _lib.NHWC, dev)
-    side = _side_stream(dev)
-    side.wait_stream(torch.cuda.current_stream(dev))  # after the plan and the allocation
-    with torch.cuda.stream(side):
-        _lib.check(lib.lss_splat_zero_empty(_lib.ptr(plan.cell_start), plan.c_dims, plan.grid.c_struct(),
-                                            _lib.ptr(out), _lib.dtype_code(out_dtype), _lib.NHWC,
-                                            _lib.stream_handle(dev)), "lss_splat_zero_empty")
-        done = torch.cuda.Event()
-        done.record(side)
-    return BevPrefill(out, done)
-
-
-def _bev_out(plan: SplatPlan, out_dtype, layout, dev, prefill: Optional[BevPrefill]) -> torch.Tensor:
-    if prefill is None:
-        X, Y, Z = plan.grid.nx
-        return _new_bev(plan.dims[0], Z, X, Y, out_dtype, layout, dev)
-    if layout != _lib.NHWC or prefill.out.dtype != out_dtype:
-        raise RuntimeError("lss_carla_amd: a prefilled BEV is channels-last, of the splat's dtype")
-    return prefill.out
-
-
-def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, layout: int,
-                      prefill: Optional[BevPrefill] = None):
+def _splat_fwd_launch(plan: SplatPlan, depth, ctx_t, x_rows, out: torch.Tensor, layout: int):
     lib = _lib.load()
     dev = out.device
     e0, e1 = SPLAT_PROFILE.new_pair() if SPLAT_PROFILE.enabled else (None, None)
     ctx_code = _lib.dtype_code(ctx_t.dtype) if ctx_t is not None else _lib.F32
-    fwd = lib.lss_splat_fwd
-    if prefill is not None:
-        torch.cuda.current_stream(dev).wait_event(prefill.done)
-        fwd = lib.lss_splat_fwd_occupied
-    _lib.check(fwd(_lib.ptr(depth), _lib.ptr(ctx_t), ctx_code, _lib.ptr(x_rows), _lib.ptr(plan.cell_start),
-                   _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), plan.c_dims,
-                   plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype), layout,
-                   _lib.stream_handle(dev), e0, e1), "lss_splat_fwd")
+    _lib.check(lib.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx_t), ctx_code, _lib.ptr(x_rows), _lib.ptr(plan.cell_start),
+                                 _lib.ptr(plan.sorted_key), _lib.ptr(plan.sorted_row), plan.c_dims,
+                                 plan.grid.c_struct(), _lib.ptr(out), _lib.dtype_code(out.dtype), layout,
+                                 _lib.stream_handle(dev), e0, e1), "lss_splat_fwd")
 
 
 def _grad_rows(plan: SplatPlan, dbev: torch.Tensor) -> Tuple[torch.Tensor, int]:
@@ -484,8 +432,7 @@ class LiftSplat(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, depthnet_out: torch.Tensor, plan: SplatPlan, out_dtype: torch.dtype, layout: int,
-                prefill: Optional[BevPrefill] = None):
+    def forward(ctx, depthnet_out: torch.Tensor, plan: SplatPlan, out_dtype: torch.dtype, layout: int):
         dev = _require_cuda(depthnet_out)
         lib = _lib.load()
         B, N, D, H, W = plan.dims
@@ -499,11 +446,12 @@ class LiftSplat(torch.autograd.Function):
         # context rows keep the input's element type: bf16 rows are exact for a bf16 depthnet output
         # and halve the splat's gathered bytes
         ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=dn.dtype)
-        out = _bev_out(plan, out_dtype, layout, dev, prefill)
+        X, Y, Z = plan.grid.nx
+        out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
         _lib.check(lib.lss_lift_prep(_lib.ptr(dn), _lib.dtype_code(dn.dtype), plan.c_dims, _lib.ptr(depth),
                                      _lib.ptr(ctx_t), _lib.dtype_code(ctx_t.dtype), _lib.stream_handle(dev)),
                    "lss_lift_prep")
-        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout, prefill)
+        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout)
         ctx.save_for_backward(depth, ctx_t)
         ctx.plan = plan
         ctx.dn_dtype = depthnet_out.dtype
@@ -522,12 +470,12 @@ class LiftSplat(torch.autograd.Function):
                                      plan.grid.c_struct(),
                                      _lib.ptr(d_dn), _lib.dtype_code(d_dn.dtype), _lib.stream_handle(depth.device)),
                    "lss_splat_bwd")
-        return d_dn, None, None, None, None
+        return d_dn, None, None, None
 
 
 def lift_splat(depthnet_out: torch.Tensor, plan: SplatPlan, out_dtype: torch.dtype = torch.float32,
-               layout: int = _lib.NCHW, prefill: Optional[BevPrefill] = None) -> torch.Tensor:
-    return LiftSplat.apply(depthnet_out, plan, out_dtype, layout, prefill)
+               layout: int = _lib.NCHW) -> torch.Tensor:
+    return LiftSplat.apply(depthnet_out, plan, out_dtype, layout)
 
 
 # ----------------------------------------------------------------------------- autograd: depthnet + lift + splat
@@ -546,7 +494,7 @@ class DepthnetLiftSplat(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda")
     def forward(ctx, feat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, plan: SplatPlan,
-                out_dtype: torch.dtype, layout: int, prefill: Optional[BevPrefill] = None):
+                out_dtype: torch.dtype, layout: int):
         dev = _require_cuda(feat, weight, bias)
         lib = _lib.load()
         B, N, D, H, W = plan.dims
@@ -570,7 +518,8 @@ class DepthnetLiftSplat(torch.autograd.Function):
             f = f.clone(memory_format=torch.channels_last if nhwc else torch.contiguous_format)
         depth = torch.empty(B * N, D, H, W, device=dev, dtype=torch.float32)
         ctx_t = torch.empty(B * N * H * W, C_CAM, device=dev, dtype=bf)
-        out = _bev_out(plan, out_dtype, layout, dev, prefill)
+        X, Y, Z = plan.grid.nx
+        out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
         st = _lib.stream_handle(dev)
         if nhwc:
             packed = torch.empty(_lib.DN_PACKED_BYTES(K) // 2, device=dev, dtype=bf)
@@ -587,7 +536,7 @@ class DepthnetLiftSplat(torch.autograd.Function):
             b = bias.detach().to(bf).contiguous()
             _lib.check(lib.lss_depthnet_lift(_lib.ptr(f), _lib.ptr(w), _lib.ptr(b), _lib.BF16, K, plan.c_dims,
                                              _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, st), "lss_depthnet_lift")
-        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout, prefill)
+        _splat_fwd_launch(plan, depth, ctx_t, None, out, layout)
         ctx.save_for_backward(f, w.view(weight.shape), depth, ctx_t)
         ctx.plan = plan
         return out
@@ -621,17 +570,16 @@ class DepthnetLiftSplat(torch.autograd.Function):
                 d_w = torch.mm(dd.t(), fm).view(weight.shape).to(weight.dtype)
             if need[2]:
                 d_b = dd.float().sum(0).to(weight.dtype)
-            return d_feat, d_w, d_b, None, None, None, None
+            return d_feat, d_w, d_b, None, None, None
         d_feat, d_w, d_b = torch.ops.aten.convolution_backward(
             d_dn, feat, weight, [weight.shape[0]], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
             [need[0], need[1], need[2]])
-        return d_feat, d_w, d_b, None, None, None, None
+        return d_feat, d_w, d_b, None, None, None
 
 
 def depthnet_lift_splat(feat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, plan: SplatPlan,
-                        out_dtype: torch.dtype = torch.bfloat16, layout: int = _lib.NHWC,
-                        prefill: Optional[BevPrefill] = None) -> torch.Tensor:
-    return DepthnetLiftSplat.apply(feat, weight, bias, plan, out_dtype, layout, prefill)
+                        out_dtype: torch.dtype = torch.bfloat16, layout: int = _lib.NHWC) -> torch.Tensor:
+    return DepthnetLiftSplat.apply(feat, weight, bias, plan, out_dtype, layout)
 
 
 # ----------------------------------------------------------------------------- autograd: unfused voxel pooling
