@@ -904,44 +904,6 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_lift(const bf16* __restrict
 // column-major), two per K step. Then logits + bias rounded to bf16 (the autocast conv's output), depth
 // softmax over the first D rows, context rows -- as k_depthnet_lift.
 // pixels per block (16-pixel MFMA column tiles): 48 -> 176 blocks at B=8 (32 -> 264 blocks, 8 CUs run two)
-// Epilogue of the fused lifts (k_depthnet_lift2 / k_depthnet_lift3; get_depth_dist + the context
-// layout, src/models.py:52-59): s_lg[o][p] holds the bf16-rounded logits of the tile's np pixels
-// [q0, q0 + np). Softmax over the first D rows per pixel with one wave per pixel (wave w takes pixels
-// w, w + NW, ...; lane d holds bin d, D <= 64): max and sum by xor butterflies -- a fixed association,
-// every lane of the wave gets the same bits -- no block barrier between the two reductions; the
-// probabilities go back to s_lg, then depth (B*N, D, H, W) fp32 in runs of consecutive pixels and the
-// context rows (pixel-major, bf16) with 16-B stores. Both kernels share it: identical bits.
-template <int PX, int NW>
-__device__ __forceinline__ void lift_epilogue(float (*s_lg)[PX + 1], int D, int np, int q0, int HW,
-                                              float* __restrict__ depth, bf16* __restrict__ ctx_t) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int p = wave; p < np; p += NW) {
-        const float x = lane < D ? s_lg[lane][p] : -INFINITY;
-        float m = x;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
-        const float e = lane < D ? expf(x - m) : 0.f;
-        float sum = e;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
-        if (lane < D) s_lg[lane][p] = e / sum;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < D * np; i += NW * kWave) {
-        const int d = i / np, pp = i - d * np;
-        const int q = q0 + pp, bn = q / HW, hw = q - bn * HW;
-        depth[((size_t)bn * D + d) * HW + hw] = s_lg[d][pp];
-    }
-    // context rows: the tile's np rows of 64 bf16 are one contiguous run; 8 channels per 16-B store
-    for (int i = threadIdx.x; i < np * (kC / 8); i += NW * kWave) {
-        const int pp = i / (kC / 8), c8 = (i - pp * (kC / 8)) * 8;
-        bf16 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = __float2bfloat16(s_lg[D + c8 + j][pp]);
-        *reinterpret_cast<uint4*>(ctx_t + (size_t)(q0 + pp) * kC + c8) = *reinterpret_cast<const uint4*>(v);
-    }
-}
-
 constexpr int kDn2Pix = 48;
 constexpr int kDn2Waves = 8;                   // 8 x 16 = 128 output rows >= D + C
 constexpr int kDn2Block = kDn2Waves * kWave;
@@ -961,10 +923,15 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     __shared__ __attribute__((aligned(16))) unsigned char s_x[K * kRow];  // [k][pixel] bf16
     __shared__ float s_lg[kDnMaxO][PX + 1];                                  // bf16-rounded logits
+    __shared__ float s_red[2][kDn2Block / PX][PX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int q0 = xcd_block() * PX;  // XCD x takes a contiguous run of pixel tiles
     if (q0 >= npix) return;  // block-uniform
     const int O = D + kC;
+    constexpr int kParts = kDn2Block / PX;  // threads past kParts * PX sit the softmax out
+    constexpr int kPerPart = (64 + kParts - 1) / kParts;  // D <= 64 (D + C <= kDnMaxO)
+    const int p = threadIdx.x % PX, part = threadIdx.x / PX;
+    const bool sm = part < kParts;
     // ---- loads: this wave's weight rows (A fragments) and the block's feature tile, all in flight
     const int arow = wave * 16 + (lane & 15);
     const int kq = 8 * (lane >> 4);  // k offset of the lane's 8 elements inside a 32-wide K step
@@ -1026,7 +993,35 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
             if (o < O) s_lg[o][16 * t + c16] = __bfloat162float(__float2bfloat16(acc[t][i] + bv[i]));
         }
     __syncthreads();
-    lift_epilogue<PX, kDn2Waves>(s_lg, D, min(PX, npix - q0), q0, HW, depth, ctx_t);
+    // ---- softmax over the D bins of each pixel: thread (part, p) covers bins part, part + 16, ...
+    float m = -INFINITY;
+    for (int d = part; sm && d < D; d += kParts) m = fmaxf(m, s_lg[d][p]);
+    if (sm) s_red[0][part][p] = m;
+    __syncthreads();
+    m = s_red[0][0][p];
+#pragma unroll
+    for (int j = 1; j < kParts; ++j) m = fmaxf(m, s_red[0][j][p]);
+    float sum = 0.f;
+    for (int d = part; sm && d < D; d += kParts) sum += expf(s_lg[d][p] - m);
+    if (sm) s_red[1][part][p] = sum;
+    __syncthreads();
+    sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < kParts; ++j) sum += s_red[1][j][p];
+    const int q = q0 + p;
+    if (sm && q < npix) {
+        const int bn = q / HW, hw = q - bn * HW;
+        float* dst = depth + (size_t)bn * D * HW + hw;
+#pragma unroll
+        for (int i = 0; i < kPerPart; ++i) {
+            const int d = part + kParts * i;
+            if (d < D) dst[(size_t)d * HW] = expf(s_lg[d][p] - m) / sum;
+        }
+    }
+    for (int i = threadIdx.x; i < PX * kC; i += kDn2Block) {
+        const int pp = i / kC, c = i - pp * kC;
+        if (q0 + pp < npix) ctx_t[(size_t)(q0 + pp) * kC + c] = __float2bfloat16(s_lg[D + c][pp]);
+    }
 }
 
 // ---- depthnet + lift, version 3: pixel-major (channels-last) features, one block per CU.
@@ -1048,9 +1043,6 @@ constexpr int kDn3MaxPix = 48;           // pixels per block at most: three 16-c
 // 4 slices no better, profiles/r03/s3/trace_lift3_slices*.txt)
 constexpr int kDn3Slices = 2;
 
-#ifndef LSS_DN3_WCOPIES
-#define LSS_DN3_WCOPIES 1  // experiments only: block b reads packed copy b % copies (the caller packs them all)
-#endif
 // The depthnet weights in k_depthnet_lift3's A-fragment order (lss_depthnet_pack): piece (wave w,
 // K step s, lane l) = the 8 bf16 weights of output row min(16 w + (l & 15), O - 1), channels
 // 32 s + 8 (l >> 4) .. + 7, at piece index (w K/32 + s) 64 + l. A wave's fragment load for one K
@@ -1094,6 +1086,7 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     __shared__ __attribute__((aligned(16))) unsigned char s_x[PX * kRow];  // [pixel][k] bf16
     __shared__ float s_lg[kDnMaxO][PX + 1];                                // bf16-rounded logits
+    __shared__ float s_red[2][kDn3Block / PX][PX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // XCD x takes one contiguous run of pixel tiles (c3: sample x), as the splat's chunk blocks take
     // the CSR: the context rows a splat gathers were written through its own XCD's L2
@@ -1105,6 +1098,10 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
     const int O = D + kC;
     [[maybe_unused]] const int tslot = blk * kDn3Waves + wave;  // LSS_TRACE builds only
     LSS_STAMP(tslot, 0);
+    constexpr int kParts = kDn3Block / PX;                 // softmax: threads (part, p) of the block
+    constexpr int kPerPart = (64 + kParts - 1) / kParts;   // D <= 64 (D + C <= kDnMaxO)
+    const int p = threadIdx.x % PX, part = threadIdx.x / PX;
+    const bool sm = part < kParts;
     // ---- loads, all in flight together, in kParts K slices: slice h of the tile (channels
     // [h K/kParts, (h+1) K/kParts) of every pixel row, 16 B per thread and load), then this wave's
     // weight A fragments for the slice's K steps; then the bias values (clamped addresses, no
@@ -1139,8 +1136,7 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
 #pragma unroll
         for (int s = h * kSSteps; s < (h + 1) * kSSteps; ++s) {
             if (PACKED)  // lss_depthnet_pack's order: each wave-instruction reads one contiguous 1 KB
-                a[s] = *reinterpret_cast<const bf16x8*>(weight + (size_t)(blk % LSS_DN3_WCOPIES) * (kDn3Waves * K * 16) +
-                                                        ((size_t)(wave * kSteps + s) * kWave + lane) * 8);
+                a[s] = *reinterpret_cast<const bf16x8*>(weight + ((size_t)(wave * kSteps + s) * kWave + lane) * 8);
             else
                 a[s] = *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
         }
@@ -1192,7 +1188,44 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
         }
     __syncthreads();
     LSS_STAMP(tslot, 2);
-    lift_epilogue<PX, kDn3Waves>(s_lg, D, np, q0, HW, depth, ctx_t);
+    // ---- softmax over the D bins of each pixel: thread (part, p) covers bins part, part + kParts, ...
+    const bool pl = sm && p < np;
+    float m = -INFINITY;
+    for (int d = part; pl && d < D; d += kParts) m = fmaxf(m, s_lg[d][p]);
+    if (sm) s_red[0][part][p] = m;
+    __syncthreads();
+    m = s_red[0][0][p];
+#pragma unroll
+    for (int j = 1; j < kParts; ++j) m = fmaxf(m, s_red[0][j][p]);
+    float sum = 0.f;
+    for (int d = part; pl && d < D; d += kParts) {
+        const float e = expf(s_lg[d][p] - m);
+        s_lg[d][p] = e;  // (this thread's own bins: read back below instead of a second expf)
+        sum += e;
+    }
+    if (sm) s_red[1][part][p] = sum;
+    __syncthreads();
+    sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < kParts; ++j) sum += s_red[1][j][p];
+    if (pl) {
+        const int q = q0 + p;
+        const int bn = q / HW, hw = q - bn * HW;
+        float* dst = depth + (size_t)bn * D * HW + hw;
+#pragma unroll
+        for (int i = 0; i < kPerPart; ++i) {
+            const int d = part + kParts * i;
+            if (d < D) dst[(size_t)d * HW] = s_lg[d][p] / sum;
+        }
+    }
+    // context rows: the tile's np rows of 64 bf16 are one contiguous run; 8 channels per 16-B store
+    for (int i = threadIdx.x; i < np * (kC / 8); i += kDn3Block) {
+        const int pp = i / (kC / 8), c8 = (i - pp * (kC / 8)) * 8;
+        bf16 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = __float2bfloat16(s_lg[D + c8 + j][pp]);
+        *reinterpret_cast<uint4*>(ctx_t + (size_t)(q0 + pp) * kC + c8) = *reinterpret_cast<const uint4*>(v);
+    }
     LSS_STAMP(tslot, 3);
 }
 

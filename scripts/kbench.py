@@ -132,12 +132,9 @@ def main():
             l.lss_depthnet_lift_nhwc(_lib.ptr(feat_cl), _lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, 512, dims,
                                      _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, st()), "lift3"))
         if hasattr(l, "lss_depthnet_pack"):
-            # 8 packed copies back to back (a LSS_DN3_WCOPIES build spreads its blocks over them)
-            packed8 = torch.empty(8, _lib.DN_PACKED_BYTES(512) // 2, device=dev, dtype=torch.bfloat16)
-            for c in range(8):
-                _lib.check(l.lss_depthnet_pack(_lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, D + 64, 512,
-                                               _lib.ptr(packed8[c]), None, None, st()), "pack")
-            packed = packed8[0]
+            packed = torch.empty(_lib.DN_PACKED_BYTES(512) // 2, device=dev, dtype=torch.bfloat16)
+            _lib.check(l.lss_depthnet_pack(_lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, D + 64, 512, _lib.ptr(packed),
+                                           None, None, st()), "pack")
             r["depthnet_lift_nhwc_packed (fragment-order weights)"] = timeit("depthnet_lift_nhwc_packed", lambda: _lib.check(
                 l.lss_depthnet_lift_nhwc_packed(_lib.ptr(feat_cl), _lib.ptr(packed), _lib.ptr(bdn), 512, dims,
                                                 _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, st()), "lift3p"))
