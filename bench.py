@@ -319,8 +319,10 @@ def measure_in_graph(args) -> dict | None:
            "how": "rocprofv3 --kernel-trace of a child run of this script: the 10 timed graph replays"}
     # what the splat adds to the step after the lift: the lift kernel's end to the splat's end (the
     # kernel plus the launch gap in front of it)
-    after = [(e - max(le for lb, le in rows["lift"] if le <= b)) / 1e3 for b, e in sel
-             if any(le <= b for lb, le in rows["lift"])]
+    # (the lift launched last before the splat; trace timestamps of back-to-back kernels can overlap
+    # by a few ns, so the lift is found by its start)
+    after = [(e - max((lb, le) for lb, le in rows["lift"] if lb <= b)[1]) / 1e3 for b, e in sel
+             if any(lb <= b for lb, le in rows["lift"])]
     if after:
         res["after_lift_us"] = round(sum(after) / len(after), 2)
     return res
