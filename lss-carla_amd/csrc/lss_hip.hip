@@ -1042,6 +1042,9 @@ constexpr int kDn3MaxPix = 48;           // pixels per block at most: three 16-c
 // K slices of k_depthnet_lift3's loads: slice 0 multiplied while the rest arrive (c3 in-step 11.3 -> 10.9 us;
 // 4 slices no better, profiles/r03/s3/trace_lift3_slices*.txt)
 constexpr int kDn3Slices = 2;
+#ifndef LSS_DN3_NT
+#define LSS_DN3_NT 0  // experiments only: non-temporal (L1-bypassing) loads, 1 the weights, 2 the features
+#endif
 
 // The depthnet weights in k_depthnet_lift3's A-fragment order (lss_depthnet_pack): piece (wave w,
 // K step s, lane l) = the 8 bf16 weights of output row min(16 w + (l & 15), O - 1), channels
@@ -1131,11 +1134,17 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
         for (int t = 0; t < kSIt; ++t) {
             const int i = threadIdx.x + t * kDn3Block;
             const int r = min(i / kSCPR, np - 1), c = h * kSCPR + i % kSCPR;
-            fv[h][t] = *reinterpret_cast<const u32x4*>(tile + (size_t)r * K * 2 + c * 16);
+            if (LSS_DN3_NT & 2)
+                fv[h][t] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(tile + (size_t)r * K * 2 + c * 16));
+            else
+                fv[h][t] = *reinterpret_cast<const u32x4*>(tile + (size_t)r * K * 2 + c * 16);
         }
 #pragma unroll
         for (int s = h * kSSteps; s < (h + 1) * kSSteps; ++s) {
-            if (PACKED)  // lss_depthnet_pack's order: each wave-instruction reads one contiguous 1 KB
+            if (PACKED && (LSS_DN3_NT & 1))
+                a[s] = __builtin_nontemporal_load(
+                    reinterpret_cast<const bf16x8*>(weight + ((size_t)(wave * kSteps + s) * kWave + lane) * 8));
+            else if (PACKED)  // lss_depthnet_pack's order: each wave-instruction reads one contiguous 1 KB
                 a[s] = *reinterpret_cast<const bf16x8*>(weight + ((size_t)(wave * kSteps + s) * kWave + lane) * 8);
             else
                 a[s] = *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
