@@ -167,6 +167,14 @@ int lss_depthnet_lift_nhwc(const void* feat, const void* weight, const void* bia
 int lss_depthnet_pack(const void* weight, const void* bias, int32_t dtype, int32_t O, int32_t K, void* packed,
                       void* plain, void* bias_out, lss_stream_t stream);
 
+/* Mixed-precision working copy of flat fp32 master parameters (lss_carla_amd.flat_params): dst[i] =
+ * bf16(src[i]) for i < n (nearest even, as torch's .to(torch.bfloat16)); with `packed` non-NULL the
+ * same launch also writes the depthnet weight (O, K) fp32 at dn_weight (a range of src) as
+ * lss_depthnet_pack does -- the plain bf16 copy and the bias are ranges of dst. src, dst, packed
+ * 16-B aligned. */
+int lss_flat_cast_bf16(const float* src, void* dst, int64_t n, const float* dn_weight, int32_t O, int32_t K,
+                       void* packed, lss_stream_t stream);
+
 /* lss_depthnet_lift_nhwc with the weights as lss_depthnet_pack wrote them (bias: O bf16);
  * identical results. */
 int lss_depthnet_lift_nhwc_packed(const void* feat, const void* packed, const void* bias, int32_t K,

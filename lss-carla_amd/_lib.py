@@ -65,6 +65,7 @@ SIGNATURES = {
     "lss_depthnet_lift": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p]),
     "lss_depthnet_lift_nhwc": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p]),
     "lss_depthnet_pack": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p]),
+    "lss_flat_cast_bf16": (ctypes.c_int, [_p, _p, ctypes.c_int64, _p, _i32, _i32, _p, _p]),
     "lss_depthnet_lift_nhwc_packed": (ctypes.c_int, [_p, _p, _p, _i32, _DIMS, _p, _p, _i32, _p]),
     "lss_splat_fwd": (ctypes.c_int, [_p, _p, _i32, _p, _p, _p, _p, _DIMS, _GRID, _p, _i32, _i32, _p, _p, _p]),
     "lss_bev_rows": (ctypes.c_int, [_p, _i32, _p, _DIMS, _GRID, _p, _p]),

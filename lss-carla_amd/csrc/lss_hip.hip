@@ -1042,9 +1042,6 @@ constexpr int kDn3MaxPix = 48;           // pixels per block at most: three 16-c
 // K slices of k_depthnet_lift3's loads: slice 0 multiplied while the rest arrive (c3 in-step 11.3 -> 10.9 us;
 // 4 slices no better, profiles/r03/s3/trace_lift3_slices*.txt)
 constexpr int kDn3Slices = 2;
-#ifndef LSS_DN3_NT
-#define LSS_DN3_NT 0  // experiments only: non-temporal (L1-bypassing) loads, 1 the weights, 2 the features
-#endif
 
 // The depthnet weights in k_depthnet_lift3's A-fragment order (lss_depthnet_pack): piece (wave w,
 // K step s, lane l) = the 8 bf16 weights of output row min(16 w + (l & 15), O - 1), channels
@@ -1134,17 +1131,11 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
         for (int t = 0; t < kSIt; ++t) {
             const int i = threadIdx.x + t * kDn3Block;
             const int r = min(i / kSCPR, np - 1), c = h * kSCPR + i % kSCPR;
-            if (LSS_DN3_NT & 2)
-                fv[h][t] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(tile + (size_t)r * K * 2 + c * 16));
-            else
-                fv[h][t] = *reinterpret_cast<const u32x4*>(tile + (size_t)r * K * 2 + c * 16);
+            fv[h][t] = *reinterpret_cast<const u32x4*>(tile + (size_t)r * K * 2 + c * 16);
         }
 #pragma unroll
         for (int s = h * kSSteps; s < (h + 1) * kSSteps; ++s) {
-            if (PACKED && (LSS_DN3_NT & 1))
-                a[s] = __builtin_nontemporal_load(
-                    reinterpret_cast<const bf16x8*>(weight + ((size_t)(wave * kSteps + s) * kWave + lane) * 8));
-            else if (PACKED)  // lss_depthnet_pack's order: each wave-instruction reads one contiguous 1 KB
+            if (PACKED)  // lss_depthnet_pack's order: each wave-instruction reads one contiguous 1 KB
                 a[s] = *reinterpret_cast<const bf16x8*>(weight + ((size_t)(wave * kSteps + s) * kWave + lane) * 8);
             else
                 a[s] = *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
@@ -1236,6 +1227,36 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
         *reinterpret_cast<uint4*>(ctx_t + (size_t)(q0 + pp) * kC + c8) = *reinterpret_cast<const uint4*>(v);
     }
     LSS_STAMP(tslot, 3);
+}
+
+// Flat fp32 master -> bf16 working copy (flat_params.FlatParams, once per forward), the depthnet weight
+// also written in k_depthnet_lift3's fragment order from the same fp32 values: blocks [0, ncast) round
+// 8 elements per thread (two 16-B loads, one 16-B store; nearest even, as torch's .to(bfloat16)), blocks
+// [ncast, ...) are k_depthnet_pack's pieces. One launch where the step had a cast and a pack.
+__global__ __launch_bounds__(kBlock) void k_flat_cast_bf16(const float* __restrict__ src, bf16* __restrict__ dst,
+                                                          long n, int ncast, const float* __restrict__ dn_weight, int O,
+                                                          int K, bf16* __restrict__ packed) {
+    if ((int)blockIdx.x < ncast) {
+        const long i = ((long)blockIdx.x * kBlock + threadIdx.x) * 8;
+        if (i + 8 <= n) {
+            const float4 a = *reinterpret_cast<const float4*>(src + i), b = *reinterpret_cast<const float4*>(src + i + 4);
+            const bf16 v[8] = {__float2bfloat16(a.x), __float2bfloat16(a.y), __float2bfloat16(a.z), __float2bfloat16(a.w),
+                               __float2bfloat16(b.x), __float2bfloat16(b.y), __float2bfloat16(b.z), __float2bfloat16(b.w)};
+            *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(v);
+        } else {
+            for (long j = i; j < n; ++j) dst[j] = __float2bfloat16(src[j]);
+        }
+        return;
+    }
+    const int ksteps = K / 32;
+    const int t = (blockIdx.x - ncast) * kBlock + threadIdx.x;
+    if (t >= kDn3Waves * ksteps * kWave) return;
+    const int l = t % kWave, st = (t / kWave) % ksteps, w = t / (kWave * ksteps);
+    const float* row = dn_weight + (size_t)min(16 * w + (l & 15), O - 1) * K + 32 * st + 8 * (l >> 4);
+    bf16 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = __float2bfloat16(row[j]);
+    *reinterpret_cast<uint4*>(packed + (size_t)t * 8) = *reinterpret_cast<const uint4*>(v);
 }
 
 // 16 bytes of fp32 or bf16 row elements -> fp32.
@@ -2495,6 +2516,21 @@ int lss_depthnet_pack(const void* weight, const void* bias, int32_t dtype, int32
                            (const bf16*)bias, (int)O, (int)K, (bf16*)packed, (bf16*)plain, (bf16*)bias_out);
     else
         return LSS_EINVAL;
+    return launch_status();
+}
+
+int lss_flat_cast_bf16(const float* src, void* dst, int64_t n, const float* dn_weight, int32_t O, int32_t K,
+                       void* packed, lss_stream_t stream) {
+    if (!src || !dst || n < 0 || (((uintptr_t)src | (uintptr_t)dst) & 15)) return LSS_EINVAL;
+    if (packed && (!dn_weight || ((uintptr_t)packed & 15))) return LSS_EINVAL;
+    if (packed && (K <= 0 || K % 32 != 0 || K > kDnMaxK || O <= 0 || O > kDn3Waves * 16)) return LSS_EUNSUPPORTED;
+    const long ncast_l = (n + 8L * kBlock - 1) / (8L * kBlock);
+    if (ncast_l >= INT_MAX / 2) return LSS_EUNSUPPORTED;
+    const int ncast = (int)ncast_l;
+    const int npack = packed ? grid_blocks(kDn3Waves * (K / 32) * kWave, kBlock) : 0;
+    if (ncast + npack == 0) return 0;
+    hipLaunchKernelGGL(k_flat_cast_bf16, dim3(ncast + npack), dim3(kBlock), 0, (hipStream_t)stream, src, (bf16*)dst,
+                       (long)n, ncast, dn_weight, (int)O, (int)K, (bf16*)packed);
     return launch_status();
 }
 

@@ -56,7 +56,15 @@ class _Materialize(torch.autograd.Function):
     @staticmethod
     def forward(ctx, master: torch.Tensor, fp: "FlatParams"):
         n16 = fp.n16
-        if n16:
+        if n16 and fp.dn is not None:
+            # one launch: the bf16 copy and the depthnet weight in the fused lift's fragment order
+            from . import _lib
+            w_off, O, K = fp.dn
+            _lib.check(_lib.load().lss_flat_cast_bf16(_lib.ptr(master), _lib.ptr(fp.work16), n16,
+                                                      _lib.ptr(master[w_off:w_off + O * K]), O, K,
+                                                      _lib.ptr(fp.dn_packed), _lib.stream_handle(master.device)),
+                       "lss_flat_cast_bf16")
+        elif n16:
             fp.work16.copy_(master[:n16])
         fp.work32.copy_(master[n16:])
         ctx.fp = fp
@@ -116,6 +124,25 @@ class FlatParams:
         self.master = nn.Parameter(master)
         self.work16 = torch.empty(self.n16, device=dev, dtype=cast_dtype or torch.float32)
         self.work32 = torch.empty(self.numel - self.n16, device=dev, dtype=torch.float32)
+        # the depthnet 1x1 conv (CamEncode.depthnet, src/models.py:47) of a fused-lift model: its bf16
+        # weight is also kept in the lift kernel's fragment order, written by the same cast launch
+        # (lss_flat_cast_bf16), and handed to the module through the weight view's storage address
+        self.dn, self.dn_packed = None, None
+        dn = getattr(model, "camencode", None)
+        dn = getattr(dn, "depthnet", None)
+        wname = next((n for n in self.names16 if n.endswith("camencode.depthnet.weight")), None)
+        if (dn is not None and wname is not None and dev.type == "cuda" and cast_dtype == torch.bfloat16
+                and dn.weight.shape[1] % 32 == 0 and dn.weight.shape[1] <= 512 and dn.weight.shape[0] <= 128):
+            from . import _lib
+            off = 0
+            for n, p in zip(self.names16, self.like16):
+                if n == wname:
+                    break
+                off += p.numel()
+            O, K = dn.weight.shape[0], dn.weight.shape[1]
+            self.dn = (off, O, K)
+            self.dn_packed = torch.empty(_lib.DN_PACKED_BYTES(K) // 2, device=dev, dtype=torch.bfloat16)
+            dn.lss_packed_weight = (self.dn_packed, self.work16.data_ptr() + 2 * off)
 
     def tensors(self) -> Dict[str, torch.Tensor]:
         outs = _Materialize.apply(self.master, self)

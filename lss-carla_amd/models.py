@@ -379,8 +379,10 @@ class LiftSplatShoot(nn.Module):
         if self.fuse_depthnet and out_dtype == torch.bfloat16 and self.D + self.camC <= 128:
             # depthnet 1x1 conv + softmax + context layout in one MFMA kernel; its
             # tile holds D + C <= 128 output channels (a larger dbound runs the conv as its own op)
-            return ops.depthnet_lift_splat(feat, ce.depthnet.weight, ce.depthnet.bias, plan, out_dtype,
-                                           self._layout())
+            w = ce.depthnet.weight
+            pk = getattr(ce.depthnet, "lss_packed_weight", None)  # (buffer, the bf16 view's address)
+            packed = pk[0] if pk is not None and w.dtype == torch.bfloat16 and w.data_ptr() == pk[1] else None
+            return ops.depthnet_lift_splat(feat, w, ce.depthnet.bias, plan, out_dtype, self._layout(), packed)
         return ops.lift_splat(ce.depthnet(feat), plan, out_dtype, self._layout())
 
     def forward(self, x, rots, trans, intrins, post_rots, post_trans):

@@ -494,7 +494,7 @@ class DepthnetLiftSplat(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda")
     def forward(ctx, feat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, plan: SplatPlan,
-                out_dtype: torch.dtype, layout: int):
+                out_dtype: torch.dtype, layout: int, packed: Optional[torch.Tensor] = None):
         dev = _require_cuda(feat, weight, bias)
         lib = _lib.load()
         B, N, D, H, W = plan.dims
@@ -521,7 +521,10 @@ class DepthnetLiftSplat(torch.autograd.Function):
         X, Y, Z = plan.grid.nx
         out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
         st = _lib.stream_handle(dev)
-        if nhwc:
+        if nhwc and packed is not None and weight.dtype == bf and bias.dtype == bf:
+            # weights already in fragment order (flat_params: the same launch as their bf16 copy)
+            w, b = weight.detach().reshape(O, K), bias.detach()
+        elif nhwc:
             packed = torch.empty(_lib.DN_PACKED_BYTES(K) // 2, device=dev, dtype=bf)
             w = torch.empty(O, K, device=dev, dtype=bf)
             b = torch.empty(O, device=dev, dtype=bf)
@@ -570,16 +573,19 @@ class DepthnetLiftSplat(torch.autograd.Function):
                 d_w = torch.mm(dd.t(), fm).view(weight.shape).to(weight.dtype)
             if need[2]:
                 d_b = dd.float().sum(0).to(weight.dtype)
-            return d_feat, d_w, d_b, None, None, None
+            return d_feat, d_w, d_b, None, None, None, None
         d_feat, d_w, d_b = torch.ops.aten.convolution_backward(
             d_dn, feat, weight, [weight.shape[0]], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
             [need[0], need[1], need[2]])
-        return d_feat, d_w, d_b, None, None, None
+        return d_feat, d_w, d_b, None, None, None, None
 
 
 def depthnet_lift_splat(feat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, plan: SplatPlan,
-                        out_dtype: torch.dtype = torch.bfloat16, layout: int = _lib.NHWC) -> torch.Tensor:
-    return DepthnetLiftSplat.apply(feat, weight, bias, plan, out_dtype, layout)
+                        out_dtype: torch.dtype = torch.bfloat16, layout: int = _lib.NHWC,
+                        packed: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """packed: the weight in lss_depthnet_pack's order, already written (flat_params.FlatParams);
+    used only with a bf16 weight and bias."""
+    return DepthnetLiftSplat.apply(feat, weight, bias, plan, out_dtype, layout, packed)
 
 
 # ----------------------------------------------------------------------------- autograd: unfused voxel pooling

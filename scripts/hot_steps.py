@@ -10,7 +10,7 @@ import re
 import sys
 
 HOT = ("k_splat_fwd", "k_splat_bwd", "k_depthnet_lift", "k_lift_prep", "k_geometry_cells", "k_scan", "k_scatter",
-       "k_csr_canon", "k_bev_rows", "k_fill_empty")
+       "k_csr_canon", "k_bev_rows", "k_depthnet_pack")
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 geo = [i for i, r in enumerate(rows) if "k_geometry_cells" in r["Kernel_Name"]]

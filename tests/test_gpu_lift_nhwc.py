@@ -160,3 +160,24 @@ def test_module_up1_channels_last_feeds_nhwc_lift():
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=3e-2, atol=3e-2)
     rel = (outs[0][1] - outs[1][1]).norm() / outs[1][1].norm()
     assert rel < 3e-2, rel.item()
+
+
+def test_flat_params_cast_writes_the_packed_depthnet_weight():
+    """flat_params.FlatParams materialises the bf16 working copy and the depthnet weight in fragment
+    order in one launch (lss_flat_cast_bf16): the copy equals torch's .to(bfloat16) of the fp32 master,
+    the packed weight equals lss_depthnet_pack's, and the model's fused lift picks it up."""
+    from lss_carla_amd.flat_params import FlatParams
+    cfg, gc, dac = syn.config_confs("c1")
+    torch.manual_seed(0)
+    m = L.compile_model(gc, dac, 1).to(DEV)
+    fp = FlatParams(m, cast_dtype=torch.bfloat16)
+    assert fp.dn is not None
+    with torch.no_grad():
+        fp.master.add_(torch.randn_like(fp.master) * 1e-3)  # values a stale copy would not have
+    t = fp.tensors()
+    torch.cuda.synchronize()
+    assert torch.equal(fp.work16, fp.master[:fp.n16].to(torch.bfloat16))
+    w, b = t["camencode.depthnet.weight"], t["camencode.depthnet.bias"]
+    packed, plain, b16 = _pack(m.camencode.depthnet.weight.detach().reshape(w.shape[0], -1), m.camencode.depthnet.bias.detach())
+    assert torch.equal(fp.dn_packed, packed) and torch.equal(w.reshape(plain.shape), plain) and torch.equal(b, b16)
+    assert m.camencode.depthnet.lss_packed_weight[1] == w.data_ptr()
