@@ -531,6 +531,7 @@ class DepthnetLiftSplat(torch.autograd.Function):
             _lib.check(lib.lss_depthnet_pack(_lib.ptr(weight.detach().reshape(O, K).contiguous()),
                                              _lib.ptr(bias.detach().contiguous()), _lib.dtype_code(weight.dtype),
                                              O, K, _lib.ptr(packed), _lib.ptr(w), _lib.ptr(b), st), "lss_depthnet_pack")
+        if nhwc:
             _lib.check(lib.lss_depthnet_lift_nhwc_packed(_lib.ptr(f), _lib.ptr(packed), _lib.ptr(b), K, plan.c_dims,
                                                          _lib.ptr(depth), _lib.ptr(ctx_t), _lib.BF16, st),
                        "lss_depthnet_lift_nhwc_packed")

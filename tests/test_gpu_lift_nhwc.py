@@ -181,3 +181,34 @@ def test_flat_params_cast_writes_the_packed_depthnet_weight():
     packed, plain, b16 = _pack(m.camencode.depthnet.weight.detach().reshape(w.shape[0], -1), m.camencode.depthnet.bias.detach())
     assert torch.equal(fp.dn_packed, packed) and torch.equal(w.reshape(plain.shape), plain) and torch.equal(b, b16)
     assert m.camencode.depthnet.lss_packed_weight[1] == w.data_ptr()
+
+
+def test_model_under_flat_params_takes_the_prepacked_weight():
+    """The BEV of the model run on FlatParams' working copies (the prepacked depthnet weight, no pack
+    launch) equals the BEV of the same model under plain autocast (the pack kernel on the fp32 weight)."""
+    from lss_carla_amd.flat_params import FlatParams
+    cfg, gc, dac = syn.config_confs("c2")
+    torch.manual_seed(1)
+    m = L.compile_model(gc, dac, 1).to(DEV).eval()
+    m.bev_layout = "nhwc"
+    fp = FlatParams(m, cast_dtype=torch.bfloat16)
+    rig = {k: v.to(DEV) for k, v in syn.make_rig(cfg["B"], cfg["N"], cfg["final_dim"], seed=2).items()}
+    imgs = syn.make_images(cfg["B"], cfg["N"], cfg["final_dim"], seed=2).to(DEV)
+    seen = []
+    m.bevencode.register_forward_pre_hook(lambda mod, a: seen.append(a[0].detach().clone()))
+    calls = []
+    orig = ops.DepthnetLiftSplat.forward
+
+    def spy(ctx, *a):
+        calls.append(a[-1] is not None)  # the prepacked weight handed over?
+        return orig(ctx, *a)
+    try:
+        ops.DepthnetLiftSplat.forward = staticmethod(spy)
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            m(imgs, **rig)
+            fp.bind(m)(imgs, **rig)
+    finally:
+        ops.DepthnetLiftSplat.forward = orig
+    torch.cuda.synchronize()
+    assert calls == [False, True]
+    assert torch.equal(seen[0], seen[1])
