@@ -1232,12 +1232,13 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
 // Flat fp32 master -> bf16 working copy (flat_params.FlatParams, once per forward), the depthnet weight
 // also written in k_depthnet_lift3's fragment order from the same fp32 values: blocks [0, ncast) round
 // 8 elements per thread (two 16-B loads, one 16-B store; nearest even, as torch's .to(bfloat16)), blocks
-// [ncast, ...) are k_depthnet_pack's pieces. One launch where the step had a cast and a pack.
+// [0, npack) -- dispatched first, beside the cast -- are k_depthnet_pack's pieces. One launch where the
+// step had a cast and a pack.
 __global__ __launch_bounds__(kBlock) void k_flat_cast_bf16(const float* __restrict__ src, bf16* __restrict__ dst,
-                                                          long n, int ncast, const float* __restrict__ dn_weight, int O,
+                                                          long n, int npack, const float* __restrict__ dn_weight, int O,
                                                           int K, bf16* __restrict__ packed) {
-    if ((int)blockIdx.x < ncast) {
-        const long i = ((long)blockIdx.x * kBlock + threadIdx.x) * 8;
+    if ((int)blockIdx.x >= npack) {
+        const long i = ((long)(blockIdx.x - npack) * kBlock + threadIdx.x) * 8;
         if (i + 8 <= n) {
             const float4 a = *reinterpret_cast<const float4*>(src + i), b = *reinterpret_cast<const float4*>(src + i + 4);
             const bf16 v[8] = {__float2bfloat16(a.x), __float2bfloat16(a.y), __float2bfloat16(a.z), __float2bfloat16(a.w),
@@ -1249,7 +1250,7 @@ __global__ __launch_bounds__(kBlock) void k_flat_cast_bf16(const float* __restri
         return;
     }
     const int ksteps = K / 32;
-    const int t = (blockIdx.x - ncast) * kBlock + threadIdx.x;
+    const int t = blockIdx.x * kBlock + threadIdx.x;
     if (t >= kDn3Waves * ksteps * kWave) return;
     const int l = t % kWave, st = (t / kWave) % ksteps, w = t / (kWave * ksteps);
     const float* row = dn_weight + (size_t)min(16 * w + (l & 15), O - 1) * K + 32 * st + 8 * (l >> 4);
@@ -2530,7 +2531,7 @@ int lss_flat_cast_bf16(const float* src, void* dst, int64_t n, const float* dn_w
     const int npack = packed ? grid_blocks(kDn3Waves * (K / 32) * kWave, kBlock) : 0;
     if (ncast + npack == 0) return 0;
     hipLaunchKernelGGL(k_flat_cast_bf16, dim3(ncast + npack), dim3(kBlock), 0, (hipStream_t)stream, src, (bf16*)dst,
-                       (long)n, ncast, dn_weight, (int)O, (int)K, (bf16*)packed);
+                       (long)n, npack, dn_weight, (int)O, (int)K, (bf16*)packed);
     return launch_status();
 }
 
