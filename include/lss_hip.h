@@ -106,8 +106,7 @@ int lss_cells_from_geom(const float* geom, int32_t nprime, int32_t points_per_ba
  * (cell << 32) | p, followed by the sentinel key -1 in every slot from cell_start[ncells] to
  * Nprime; sorted_row (Nprime capacity) = the row each entry's features are read from: the pixel
  * q(p) when dims is given (fused lift), p itself when dims is NULL (per-point rows); defined for
- * the first cell_start[ncells] entries; sorted_row may be NULL (not written: lss_splat_fwd derives
- * the pixel from the point id). scratch: lss_csr_scratch_bytes bytes.
+ * the first cell_start[ncells] entries. scratch: lss_csr_scratch_bytes bytes.
  * Replaces: ranks = ...; sorts = ranks.argsort(); x, geom_feats, ranks = x[sorts], ... (src/models.py:225-231). */
 size_t lss_csr_scratch_bytes(int32_t ncells, int32_t nprime);
 int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime,
@@ -192,9 +191,8 @@ int lss_depthnet_lift_nhwc_packed(const void* feat, const void* packed, const vo
  * cells are written as zeros; every element of out is written once. LSS_NHWC: one wave per
  * 64-entry chunk of the CSR (one gather round trip, LDS-staged ordered sums, rows stored
  * directly) plus zero-fill waves; LSS_NCHW: a BEV-row tile kernel (<= 128 cells per tile along Y)
- * with an LDS transpose. sorted_key / sorted_row as lss_csr_build wrote them; sorted_row may be
- * NULL (each entry's context row is then computed from its point id, the same value), and it is
- * unused in lifted mode, where the rows are the point ids.
+ * with an LDS transpose. sorted_key / sorted_row as lss_csr_build wrote them (sorted_row is
+ * unused in lifted mode, where the rows are the point ids).
  * ev_start / ev_stop (nullable) are stamped with the kernel's own start / end
  * (hipExtLaunchKernel), so their elapsed time is the kernel alone, never launch latency. */
 int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, const float* x_rows,

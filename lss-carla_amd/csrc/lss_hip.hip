@@ -652,12 +652,12 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
     if (e0 >= cc.s && e0 < cc.end) {
         const int at = dchk(cs0 + r0, total, kDbgCanonPos);
         key_out[at] = k0;
-        if (row_out) row_out[at] = point_row(dchk(p0, nprime, kDbgSplatPoint), DHW, HW);
+        row_out[at] = point_row(dchk(p0, nprime, kDbgSplatPoint), DHW, HW);
     }
     if (e1 >= cc.s && e1 < cc.end) {
         const int at = dchk(cs1 + r1, total, kDbgCanonPos);
         key_out[at] = k1;
-        if (row_out) row_out[at] = point_row(dchk(p1, nprime, kDbgSplatPoint), DHW, HW);
+        row_out[at] = point_row(dchk(p1, nprime, kDbgSplatPoint), DHW, HW);
     }
     if (cc.big_start >= 0) {
         // one cell with more than 64 entries: ordered selection straight from memory (rare)
@@ -674,7 +674,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_canon(const long long* __restric
             best = uniform(wave_min(best));
             if (lane == 0) {
                 key_out[cc.big_start + k] = ((long long)cell << 32) | (unsigned)best;
-                if (row_out) row_out[cc.big_start + k] = point_row(best, DHW, HW);
+                row_out[cc.big_start + k] = point_row(best, DHW, HW);
             }
             last = best;
         }
@@ -697,11 +697,7 @@ struct BevGeo {
     int X, Y, Z;
     int ncells;
     int nrows;              // feature rows (LSS_DEBUG bound of the gathered row index)
-    int DHW, HW;            // points and pixels per image: the context row of a point (point_row) when the
-                            // caller passes no sorted_row (one load per entry fewer in the splat's first
-                            // round trip, and the CSR build writes no row array)
 };
-
 
 // Element offset of cell k's row in the channels-last (B, X, Y, Z*C) BEV:
 // cell ((b*Z + z)*X + x)*Y + y -> ((b*X + x)*Y + y)*Z*C + z*C
@@ -1281,7 +1277,6 @@ __device__ __forceinline__ void unpack16(const uint4& u, const bf16*, float* o) 
 struct SplatGeo {
     int X, Y, Z, YT, ntiles_y;
     int ncells, nprime, nrows;  // bounds of the data-derived indices (LSS_DEBUG checks): cells, points, feature rows
-    int DHW, HW;                // point_row
 };
 
 constexpr int kYtMax = 128;  // cells per NCHW tile at most (LDS sizing)
@@ -1302,8 +1297,7 @@ __device__ __forceinline__ void store_vec(bf16* dst, const float* src) {
 template <bool FUSED, typename RT>
 __device__ float reduce_big_cell(int start, int nprime, const long long* __restrict__ key,
                                  const int32_t* __restrict__ row, const float* __restrict__ depth,
-                                 const RT* __restrict__ rows_base, int lane, int* cell_out, int nrows, int DHW,
-                                 int HW) {
+                                 const RT* __restrict__ rows_base, int lane, int* cell_out, int nrows) {
     const int cell = (int)(key[start] >> 32);
     *cell_out = cell;
     float acc = 0.f;
@@ -1313,8 +1307,7 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
         const bool mine = (int)(k >> 32) == cell;
         const unsigned long long m = __ballot(mine);
         const int n = __popcll(m);  // entries of the cell are contiguous from b
-        const int pt = (int)(k & 0xFFFFFFFF);
-        const int r = mine ? dchk(FUSED ? (row ? row[e] : point_row(pt, DHW, HW)) : pt, nrows, kDbgSplatRow) : 0;
+        const int r = mine ? dchk(FUSED ? row[e] : (int)(k & 0xFFFFFFFF), nrows, kDbgSplatRow) : 0;
         const float w = (FUSED && mine) ? depth[dchk((int)(k & 0xFFFFFFFF), nprime, kDbgSplatPoint)] : 1.f;
         for (int i = 0; i < n; ++i) {
             const float v = to_f32(rows_base[(size_t)__builtin_amdgcn_readlane(r, i) * kC + lane]);
@@ -1460,7 +1453,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     const long long k0 = e0 < nprime ? sorted_key[e0] : -1ll;
     const long long k1 = e1 < nprime ? sorted_key[e1] : -1ll;
     int rs0 = 0, rs1 = 0;
-    if (FUSED && sorted_row) {
+    if (FUSED) {
         rs0 = e0 < nprime ? sorted_row[e0] : 0;
         rs1 = e1 < nprime ? sorted_row[e1] : 0;
     }
@@ -1470,9 +1463,6 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     if (!FUSED) {
         rs0 = p0;
         rs1 = p1;
-    } else if (!sorted_row) {
-        rs0 = e0 < nprime ? point_row(p0, g.DHW, g.HW) : 0;
-        rs1 = e1 < nprime ? point_row(p1, g.DHW, g.HW) : 0;
     }
     LSS_STAMP(w, 1);
     const Span sp = chunk_span(c0, c1, prevcell, lane);
@@ -1562,7 +1552,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     if (big >= 0) {
         int cell;
         const float a2 = reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base, lane,
-                                                    &cell, g.nrows, g.DHW, g.HW);
+                                                    &cell, g.nrows);
         cell_row(out, dchk(cell, g.ncells, kDbgSplatCell), g)[lane] = from_f32<OutT>(a2);
     }
 }
@@ -1713,7 +1703,7 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
             for (int t = 0; t < KPL; ++t) {
                 const int ej = min(e + j + RS::LPR * t, eend - 1);
                 kk[t] = sorted_key[ej];
-                rr[t] = FUSED && sorted_row ? sorted_row[ej] : 0;
+                rr[t] = FUSED ? sorted_row[ej] : 0;
             }
         };
         int e = s_start[cb];
@@ -1731,7 +1721,6 @@ __global__ __launch_bounds__(kN2Block) void k_splat_fwd_nchw2(const float* __res
                 cc[t] = (int)(kk[t] >> 32);
                 wt[t] = FUSED ? depth[pt] : 1.f;
                 if (!FUSED) rr[t] = pt;
-                else if (!sorted_row) rr[t] = point_row(pt, sg.DHW, sg.HW);
             }
             uint4 v[KU];
 #pragma unroll
@@ -2236,8 +2225,6 @@ inline SplatGeo splat_geo(const lss_grid_t* g, const lss_dims_t* d, long nrows =
     s.ncells = (int)std::min<long>((long)d->B * s.Z * s.X * s.Y, INT_MAX);
     s.nprime = (int)std::min<long>(pix * d->D, INT_MAX);
     s.nrows = (int)std::min<long>(nrows > 0 ? nrows : pix, INT_MAX);
-    s.DHW = d->D * d->H * d->W;
-    s.HW = d->H * d->W;
     return s;
 }
 
@@ -2358,7 +2345,7 @@ size_t lss_csr_scratch_bytes(int32_t ncells, int32_t nprime) {
 int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, const int32_t* cell_count,
                   int32_t ncells, const lss_dims_t* dims, int32_t* cell_start, long long* sorted_key,
                   int32_t* sorted_row, void* scratch, lss_stream_t stream) {
-    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !scratch || nprime <= 0 ||
+    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !sorted_row || !scratch || nprime <= 0 ||
         ncells <= 0)
         return LSS_EINVAL;
     int DHW = nprime, HW = nprime;  // no dims: the row of point p is p (per-point rows)
@@ -2392,7 +2379,7 @@ size_t lss_csr_workspace_bytes(int32_t ncells) {
 int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime, int32_t* cell_count,
                      int32_t ncells, const lss_dims_t* dims, int32_t* cell_start, long long* sorted_key,
                      int32_t* sorted_row, void* scratch, void* workspace, lss_stream_t stream) {
-    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !scratch || !workspace ||
+    if (!cell_of || !slot_of || !cell_count || !cell_start || !sorted_key || !sorted_row || !scratch || !workspace ||
         nprime <= 0 || ncells <= 0)
         return LSS_EINVAL;
     int DHW = nprime, HW = nprime;  // no dims: the row of point p is p (per-point rows)
@@ -2555,7 +2542,7 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
     if (!dims_ok(dims) || !grid_ok(grid) || !cell_start || !sorted_key || !out) return LSS_EINVAL;
     const bool fused = x_rows == nullptr;
-    if (fused && (!depth || !ctx_t)) return LSS_EINVAL;  // (sorted_row NULL: rows from the point ids)
+    if (fused && (!depth || !ctx_t || !sorted_row)) return LSS_EINVAL;
     if (fused && ctx_dtype != LSS_F32 && ctx_dtype != LSS_BF16) return LSS_EINVAL;
     if (out_dtype != LSS_F32 && out_dtype != LSS_BF16) return LSS_EINVAL;
     if (out_layout != LSS_NCHW && out_layout != LSS_NHWC) return LSS_EINVAL;
@@ -2571,8 +2558,6 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         g.X = sg.X; g.Y = sg.Y; g.Z = sg.Z;
         g.ncells = dims->B * sg.Z * sg.X * sg.Y;
         g.nrows = sg.nrows;
-        g.DHW = sg.DHW;
-        g.HW = sg.HW;
         const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), kSplatWaves);
         const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), kSplatWaves);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);

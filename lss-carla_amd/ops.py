@@ -260,16 +260,14 @@ def _counted_plan(dev: torch.device, ws: Optional[PlanWs], launch_cells, build_c
     return out
 
 
-def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None, want_rows: bool = False):
-    """Counting sort into the canonical CSR (lss_csr_build[_ws]): cell_start, sorted_key, and, if
-    asked for, sorted_row (each entry's context row; the splat derives it from the point id when it
-    is absent -- one load per entry fewer, and 4 B per point less to write)."""
+def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None):
+    """Counting sort into the canonical CSR (lss_csr_build[_ws]): cell_start, sorted_key, sorted_row."""
     lib = _lib.load()
     B, N, D, H, W = dims
     nprime = B * N * D * H * W
     cell_start = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
     sorted_key = torch.empty(nprime, device=dev, dtype=torch.int64)
-    sorted_row = torch.empty(nprime, device=dev, dtype=torch.int32) if want_rows else None
+    sorted_row = torch.empty(nprime, device=dev, dtype=torch.int32)
     if ws is not None:
         _lib.check(lib.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
                                         make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key),
@@ -285,13 +283,11 @@ def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None, want_r
 
 def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, post_trans, grid: GridSpec,
                       want_geom: bool = False, want_csr: bool = True,
-                      inverses: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                      want_rows: bool = False) -> SplatPlan:
+                      inverses: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> SplatPlan:
     """get_geometry + quantise + filter + counting sort, all on the device (src/models.py:170-231).
 
     `inverses` = a (pinv, kinv) pair from camera_inverses / HostInverses, if already computed
     (models.py computes them before the trunk, so the host round trip never waits for device work).
-    want_rows: also materialise sorted_row (the splat does not need it).
     """
     dev = _require_cuda(frustum, rots, trans, intrins, post_rots, post_trans)
     lib = _lib.load()
@@ -319,8 +315,7 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
         launch_cells()
         return SplatPlan((B, N, D, H, W), grid, cell_of, None, None, None, geom)
     cell_start, sorted_key, sorted_row = _counted_plan(
-        dev, ws, launch_cells,
-        lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws, want_rows))
+        dev, ws, launch_cells, lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws))
     return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom)
 
 

@@ -95,12 +95,12 @@ def main():
             return lambda: _lib.check(l.lss_lift_prep(_lib.ptr(dn), _lib.BF16, dims, _lib.ptr(depth), _lib.ptr(ctx),
                                                       code, st()), "lift_prep")
 
-        def splat(out, layout, ctx, a=None, b=None, rows=True):
+        def splat(out, layout, ctx, a=None, b=None):
             _lib.check(l.lss_splat_fwd(_lib.ptr(depth), _lib.ptr(ctx), _lib.dtype_code(ctx.dtype), None,
-                                       _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr) if rows else None, dims, g,
-                                       _lib.ptr(out), _lib.dtype_code(out.dtype), layout, st(), a, b), "fwd")
+                                       _lib.ptr(cs), _lib.ptr(sk), _lib.ptr(sr), dims, g, _lib.ptr(out),
+                                       _lib.dtype_code(out.dtype), layout, st(), a, b), "fwd")
 
-        def stamped(out, layout, ctx, mode, iters=20, rows=True):
+        def stamped(out, layout, ctx, mode, iters=20):
             tot = 0.0
             for i in range(iters + 3):
                 if mode == "step":
@@ -110,7 +110,7 @@ def main():
                 a, b = ct.c_void_p(), ct.c_void_p()
                 l.lss_event_create(ct.byref(a))
                 l.lss_event_create(ct.byref(b))
-                splat(out, layout, ctx, a, b, rows)
+                splat(out, layout, ctx, a, b)
                 ms = ct.c_float()
                 l.lss_event_elapsed_ms(a, b, ct.byref(ms))
                 if i >= 3:
@@ -147,9 +147,7 @@ def main():
         if not args.only or "splat_fwd" in args.only:
             for m in ("warm", "step"):
                 r[f"{m} splat_fwd nhwc bf16"] = stamped(bev_bf, _lib.NHWC, ctx_t, m)
-                r[f"{m} splat_fwd nhwc bf16, rows from ids"] = stamped(bev_bf, _lib.NHWC, ctx_t, m, rows=False)
                 r[f"{m} splat_fwd nchw f32"] = stamped(bev_f, _lib.NCHW, ctx_f, m)
-                r[f"{m} splat_fwd nchw f32, rows from ids"] = stamped(bev_f, _lib.NCHW, ctx_f, m, rows=False)
         r["splat_bwd nhwc bf16"] = timeit("splat_bwd", lambda: _lib.check(l.lss_splat_bwd(
             _lib.ptr(g_bf), _lib.BF16, _lib.NHWC, _lib.ptr(plan.cell_of), _lib.ptr(depth), _lib.ptr(ctx_t),
             _lib.BF16, dims, g, _lib.ptr(d_dn), _lib.BF16, st()), "bwd"))

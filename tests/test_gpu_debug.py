@@ -58,7 +58,7 @@ def test_debug_checks_fire():
     B, N, fd = 2, 6, cfg["final_dim"]
     frustum = ref.create_frustum(fd, gc["dbound"]).to(dev)
     rig = {k: v.to(dev) for k, v in syn.make_rig(B, N, fd, seed=1).items()}
-    plan = ops.plan_from_cameras(frustum, **rig, grid=ops.GridSpec.from_conf(gc), want_rows=True)
+    plan = ops.plan_from_cameras(frustum, **rig, grid=ops.GridSpec.from_conf(gc))
     D, H, W = frustum.shape[:3]
     dn = syn.make_depthnet_out(B, N, D, H, W, seed=1).to(dev)
     torch.cuda.synchronize()

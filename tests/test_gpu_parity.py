@@ -64,7 +64,7 @@ def test_voxel_ids_bit_exact_full_size(name):
     cfg, gc, rig, frustum, _ = _setup(name)
     geom, cell, _ = _oracle_cells(frustum, rig, gc)
     m_grid = ops.GridSpec.from_conf(gc)
-    plan = ops.plan_from_cameras(frustum.to(DEV), **_rig_dev(rig), grid=m_grid, want_geom=True, want_rows=True)
+    plan = ops.plan_from_cameras(frustum.to(DEV), **_rig_dev(rig), grid=m_grid, want_geom=True)
     np.testing.assert_array_equal(plan.cell_of.cpu().numpy(), cell)
     np.testing.assert_array_equal(plan.geom.cpu().numpy(), geom)
     _check_canonical_csr(plan, cell, m_grid.ncells(cfg["B"]))
@@ -85,8 +85,7 @@ def _check_canonical_csr(plan, cell, ncells):
     np.testing.assert_array_equal(sk >> 32, np.repeat(np.arange(counts.size), counts))
     B, N, D, H, W = plan.dims
     cam, rem = np.divmod(want_p, D * H * W)
-    if plan.sorted_row is not None:  # (materialised on request: the splat derives it from the point id)
-        np.testing.assert_array_equal(plan.sorted_row.cpu().numpy()[:total], cam * H * W + rem % (H * W))
+    np.testing.assert_array_equal(plan.sorted_row.cpu().numpy()[:total], cam * H * W + rem % (H * W))
 
 
 def test_splat_chunk_and_tile_kernels_agree():

@@ -345,10 +345,10 @@ def test_single_pass_scan_matches_two_kernel_csr(name):
         rig = _dev(syn.make_rig(B, N, fd, seed=it))
         old, ops.USE_PLAN_WS = ops.USE_PLAN_WS, False
         try:
-            want = ops.plan_from_cameras(frustum, **rig, grid=grid, want_rows=True)
+            want = ops.plan_from_cameras(frustum, **rig, grid=grid)
         finally:
             ops.USE_PLAN_WS = old
-        got = ops.plan_from_cameras(frustum, **rig, grid=grid, want_rows=True)
+        got = ops.plan_from_cameras(frustum, **rig, grid=grid)
         torch.cuda.synchronize()
         assert torch.equal(got.cell_start, want.cell_start)
         assert torch.equal(got.sorted_key, want.sorted_key)
@@ -552,24 +552,3 @@ def test_random_shapes_fwd_bwd_vs_oracle(seed, B, N, fH, fW, D, half, dx, Z, bf1
     want_g = ref.lift_splat_backward_fp64(dn_in.numpy(), geom, gd.float().cpu().numpy(), dx_, bx_, nx_, D, 64)
     tol = ATOL if dtype == torch.float32 else 2e-2
     np.testing.assert_allclose(dnd.grad.float().cpu().numpy(), want_g, rtol=tol, atol=tol)
-
-
-@pytest.mark.parametrize("name", ["c1", "c3", "c5"])
-def test_splat_rows_from_point_ids_bit_identical(name):
-    """A plan without sorted_row (the product's: the splat derives each entry's context row from its
-    point id) gives the BEV of a plan with it, in both layouts and both row types."""
-    cfg, gc, _ = syn.config_confs(name)
-    B, N, fd = cfg["B"], cfg["N"], cfg["final_dim"]
-    frustum = ref.create_frustum(fd, gc["dbound"]).to(DEV)
-    rig = _dev(syn.make_rig(B, N, fd, seed=3))
-    grid = ops.GridSpec.from_conf(gc)
-    with_rows = ops.plan_from_cameras(frustum, **rig, grid=grid, want_rows=True)
-    without = ops.plan_from_cameras(frustum, **rig, grid=grid)
-    assert without.sorted_row is None and with_rows.sorted_row is not None
-    D, H, W = frustum.shape[:3]
-    for dt in (torch.float32, torch.bfloat16):
-        dn = syn.make_depthnet_out(B, N, D, H, W, seed=5).to(DEV, dt)
-        for layout in (_lib.NHWC, _lib.NCHW):
-            a = ops.lift_splat(dn, with_rows, dt, layout)
-            b = ops.lift_splat(dn, without, dt, layout)
-            assert torch.equal(a, b), (dt, layout)
