@@ -1335,6 +1335,12 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
 #ifndef LSS_SPLAT_ROLES
 #define LSS_SPLAT_ROLES 0  // experiments only: 1 runs the chunk waves alone, 2 the zero fill alone
 #endif
+#ifndef LSS_ZERO_SLEEP
+#define LSS_ZERO_SLEEP 0  // experiments only: s_sleep (x 64 cycles) of the first zero groups
+#endif
+#ifndef LSS_ZERO_SLEEP_GROUPS
+#define LSS_ZERO_SLEEP_GROUPS 56  // (8 XCDs x 56 groups x 4 waves = 1,792 waves: those resident at the start, c3)
+#endif
 #ifndef LSS_SPLAT_SKIP
 #define LSS_SPLAT_SKIP 0  // experiments only (wrong sums): 1 rows from 8 L1-resident rows, 2 one depth line, 4 no row stores
 #endif
@@ -1597,6 +1603,8 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
         if (LSS_SPLAT_ROLES == 1) return;
         const int zb = x * nzg + zgi;
         if (zb >= nzero_blocks) return;
+        // experiments only: the first zero groups (resident beside the chunk waves) hold back
+        if (LSS_ZERO_SLEEP && zgi < LSS_ZERO_SLEEP_GROUPS) __builtin_amdgcn_s_sleep(LSS_ZERO_SLEEP);
         const int u = (zb * kSplatWaves + wave) * kZeroUnits;
         [[maybe_unused]] const int zslot = nchunk_blocks * kSplatWaves + zb * kSplatWaves + wave;
         LSS_STAMP(zslot, 0);
