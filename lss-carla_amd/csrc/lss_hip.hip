@@ -1231,19 +1231,29 @@ __global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2)
 
 // Flat fp32 master -> bf16 working copy (flat_params.FlatParams, once per forward), the depthnet weight
 // also written in k_depthnet_lift3's fragment order from the same fp32 values: blocks [0, ncast) round
-// 8 elements per thread (two 16-B loads, one 16-B store; nearest even, as torch's .to(bfloat16)), blocks
+// 16 elements per thread (four 16-B loads, two 16-B stores; nearest even, as torch's .to(bfloat16)), blocks
 // [0, npack) -- dispatched first, beside the cast -- are k_depthnet_pack's pieces. One launch where the
 // step had a cast and a pack.
 __global__ __launch_bounds__(kBlock) void k_flat_cast_bf16(const float* __restrict__ src, bf16* __restrict__ dst,
                                                           long n, int npack, const float* __restrict__ dn_weight, int O,
                                                           int K, bf16* __restrict__ packed) {
     if ((int)blockIdx.x >= npack) {
-        const long i = ((long)(blockIdx.x - npack) * kBlock + threadIdx.x) * 8;
-        if (i + 8 <= n) {
-            const float4 a = *reinterpret_cast<const float4*>(src + i), b = *reinterpret_cast<const float4*>(src + i + 4);
-            const bf16 v[8] = {__float2bfloat16(a.x), __float2bfloat16(a.y), __float2bfloat16(a.z), __float2bfloat16(a.w),
-                               __float2bfloat16(b.x), __float2bfloat16(b.y), __float2bfloat16(b.z), __float2bfloat16(b.w)};
+        // 16 elements per thread: four 16-B loads in flight, then two 16-B stores
+        const long i = ((long)(blockIdx.x - npack) * kBlock + threadIdx.x) * 16;
+        if (i + 16 <= n) {
+            float4 a[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a[q] = *reinterpret_cast<const float4*>(src + i + 4 * q);
+            bf16 v[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                v[4 * q] = __float2bfloat16(a[q].x);
+                v[4 * q + 1] = __float2bfloat16(a[q].y);
+                v[4 * q + 2] = __float2bfloat16(a[q].z);
+                v[4 * q + 3] = __float2bfloat16(a[q].w);
+            }
             *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(v);
+            *reinterpret_cast<uint4*>(dst + i + 8) = *reinterpret_cast<const uint4*>(v + 8);
         } else {
             for (long j = i; j < n; ++j) dst[j] = __float2bfloat16(src[j]);
         }
@@ -2533,7 +2543,7 @@ int lss_flat_cast_bf16(const float* src, void* dst, int64_t n, const float* dn_w
     if (!src || !dst || n < 0 || (((uintptr_t)src | (uintptr_t)dst) & 15)) return LSS_EINVAL;
     if (packed && (!dn_weight || ((uintptr_t)packed & 15))) return LSS_EINVAL;
     if (packed && (K <= 0 || K % 32 != 0 || K > kDnMaxK || O <= 0 || O > kDn3Waves * 16)) return LSS_EUNSUPPORTED;
-    const long ncast_l = (n + 8L * kBlock - 1) / (8L * kBlock);
+    const long ncast_l = (n + 16L * kBlock - 1) / (16L * kBlock);
     if (ncast_l >= INT_MAX / 2) return LSS_EUNSUPPORTED;
     const int ncast = (int)ncast_l;
     const int npack = packed ? grid_blocks(kDn3Waves * (K / 32) * kWave, kBlock) : 0;

@@ -10,7 +10,7 @@ import statistics
 import sys
 
 HOT = ("k_splat_fwd", "k_splat_bwd", "k_depthnet_lift", "k_lift_prep", "k_geometry_cells", "k_scan", "k_scatter",
-       "k_csr_canon", "k_camera_inverse", "k_bev_rows", "k_seg_")
+       "k_csr_canon", "k_camera_inverse", "k_bev_rows", "k_seg_", "k_flat_cast")
 
 
 def short(name):
