@@ -1345,12 +1345,12 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
 #ifndef LSS_SPLAT_ROLES
 #define LSS_SPLAT_ROLES 0  // experiments only: 1 runs the chunk waves alone, 2 the zero fill alone
 #endif
-#ifndef LSS_ZERO_SLEEP
-#define LSS_ZERO_SLEEP 0  // experiments only: s_sleep (x 64 cycles) of the first zero groups
-#endif
-#ifndef LSS_ZERO_SLEEP_GROUPS
-#define LSS_ZERO_SLEEP_GROUPS 56  // (8 XCDs x 56 groups x 4 waves = 1,792 waves: those resident at the start, c3)
-#endif
+// The zero waves dispatched beside the chunk waves (the wave slots the chunk waves leave at the
+// start) hold back for s_sleep(kZeroHoldBack) = 2,048 cycles (~0.85 us) before their stores, so the
+// chunk waves' two round trips meet a quieter memory system; zero waves dispatched later, as slots
+// free up, start at once. In the c3 graph replays 12.46 / 12.33 -> 11.61 us on one box and
+// 13.00 / 13.00 -> 12.86 / 12.73 on another (s_sleep 24: 12.84, 40: 12.53, 64: no gain; round 4).
+constexpr int kZeroHoldBack = 32;
 #ifndef LSS_SPLAT_SKIP
 #define LSS_SPLAT_SKIP 0  // experiments only (wrong sums): 1 rows from 8 L1-resident rows, 2 one depth line, 4 no row stores
 #endif
@@ -1580,7 +1580,7 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
                                                            const long long* __restrict__ sorted_key,
                                                            const int32_t* __restrict__ sorted_row, BevGeo g,
                                                            int nprime, int nchunk_blocks, int nzero_blocks,
-                                                           OutT* __restrict__ out) {
+                                                           int zhold, OutT* __restrict__ out) {
     __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
     __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][RowSlice<RT>::NG * kC];
     const int lane = threadIdx.x & 63;
@@ -1613,8 +1613,7 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
         if (LSS_SPLAT_ROLES == 1) return;
         const int zb = x * nzg + zgi;
         if (zb >= nzero_blocks) return;
-        // experiments only: the first zero groups (resident beside the chunk waves) hold back
-        if (LSS_ZERO_SLEEP && zgi < LSS_ZERO_SLEEP_GROUPS) __builtin_amdgcn_s_sleep(LSS_ZERO_SLEEP);
+        if (zgi < zhold) __builtin_amdgcn_s_sleep(kZeroHoldBack);  // resident beside the chunk waves
         const int u = (zb * kSplatWaves + wave) * kZeroUnits;
         [[maybe_unused]] const int zslot = nchunk_blocks * kSplatWaves + zb * kSplatWaves + wave;
         LSS_STAMP(zslot, 0);
@@ -2579,16 +2578,19 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         const int nchunk_blocks = grid_blocks(grid_blocks(nprime, kWave), kSplatWaves);
         const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), kSplatWaves);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);
+        // zero groups per XCD resident at the start beside all the chunk waves (c3: 55; c5: none)
+        const long slots = (long)device_cus() * 4 * kSplatMinWaves;
+        const int zhold = (int)std::max<long>(0, (slots - (long)nchunk_blocks * kSplatWaves) / (8L * kSplatWaves));
 // kernel-stamped events only when asked for: a plain launch is what a hipGraph capture records
 #define LSS_NHWC_FWD(F, RT, T)                                                                                     \
     do {                                                                                                           \
         if (e0 || e1)                                                                                              \
             hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, (const RT*)rows,   \
                                   cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks,      \
-                                  (T*)out);                                                                 \
+                                  zhold, (T*)out);                                                                 \
         else                                                                                                       \
             hipLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, depth, (const RT*)rows, cell_start,     \
-                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, (T*)out);    \
+                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, zhold, (T*)out);    \
     } while (0)
         if (out_dtype == LSS_F32) {
             if (!fused) LSS_NHWC_FWD(false, float, float);
