@@ -282,7 +282,7 @@ def measure_in_graph(args) -> dict | None:
     if prof is None or not args.graph:
         return None
     tmp = tempfile.mkdtemp(prefix="lss_trace_", dir="/tmp")
-    steps = 10
+    steps = 30  # (10 replays left the average ±1 us from run to run on one box)
     cmd = ["timeout", "-s", "KILL", "280", prof, "--kernel-trace", "--output-format", "csv", "-d", tmp, "-o", "run",
            "--", sys.executable, os.path.abspath(__file__), "--config", args.config, "--batch", str(args.batch),
            "--dtype", args.dtype, "--bev-layout", args.bev_layout, "--steps", str(steps), "--warmup", "3",
@@ -316,7 +316,7 @@ def measure_in_graph(args) -> dict | None:
         return None
     durs = [(e - b) / 1e3 for b, e in sel]
     res = {"us": round(sum(durs) / len(durs), 2), "min_us": round(min(durs), 2), "launches": len(durs),
-           "how": "rocprofv3 --kernel-trace of a child run of this script: the 10 timed graph replays"}
+           "how": f"rocprofv3 --kernel-trace of a child run of this script: the {steps} timed graph replays"}
     # what the splat adds to the step after the lift: the lift kernel's end to the splat's end (the
     # kernel plus the launch gap in front of it)
     # (the lift launched last before the splat; trace timestamps of back-to-back kernels can overlap
