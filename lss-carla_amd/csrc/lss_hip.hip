@@ -1351,12 +1351,8 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
 // free up, start at once. In the c3 graph replays 12.46 / 12.33 -> 11.61 us on one box and
 // 13.00 / 13.00 -> 12.86 / 12.73 on another (s_sleep 24: 12.84, 40: 12.53, 64: no gain; round 4).
 constexpr int kZeroHoldBack = 32;
-#ifndef LSS_ZERO_HOLD_AFTER_LOAD
-#define LSS_ZERO_HOLD_AFTER_LOAD 0  // experiments only: hold back after the cell_start loads instead (s_sleep arg)
-#endif
-#ifndef LSS_ZERO_PACE
-#define LSS_ZERO_PACE 0  // experiments only: s_sleep between a held-back zero wave's stores
-#endif
+// (holding back after the cell_start loads instead, or pacing the held-back waves' stores, measured
+// no better: 11.8-12.6 vs 11.9-12.3 us in one box's replays, profiles/r04/prof_ab_zero_holdback_variants.txt)
 #ifndef LSS_SPLAT_SKIP
 #define LSS_SPLAT_SKIP 0  // experiments only (wrong sums): 1 rows from 8 L1-resident rows, 2 one depth line, 4 no row stores
 #endif
@@ -1371,7 +1367,7 @@ constexpr int kSplatMinWaves = 7;  // occupancy floor (waves per SIMD): 72 VGPRs
 // Zero-fill units [u0, u0 + kZeroUnits): cells [64u, 64u + 64) each; empty cells' rows written as zeros.
 template <typename OutT>
 __device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start, const BevGeo& g,
-                                OutT* __restrict__ out, int lane, bool hold = false) {
+                                OutT* __restrict__ out, int lane) {
     unsigned long long emask[kZeroUnits];
 #pragma unroll
     for (int i = 0; i < kZeroUnits; ++i) {
@@ -1380,7 +1376,6 @@ __device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start, 
         if (k < g.ncells) empty = cell_start[k] == cell_start[k + 1];
         emask[i] = __ballot(empty);
     }
-    if (LSS_ZERO_HOLD_AFTER_LOAD && hold) __builtin_amdgcn_s_sleep(LSS_ZERO_HOLD_AFTER_LOAD);
     constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
 #pragma unroll
     for (int i = 0; i < kZeroUnits; ++i) {
@@ -1390,7 +1385,6 @@ __device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start, 
             if ((emask[i] >> r) & 1ull)
                 __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u},
                                             reinterpret_cast<u32x4*>(cell_row(out, k0 + r, g) + (lane % LPR) * EPL));
-            if (LSS_ZERO_PACE && hold) __builtin_amdgcn_s_sleep(LSS_ZERO_PACE);
         }
     }
 }
@@ -1621,12 +1615,11 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
         if (LSS_SPLAT_ROLES == 1) return;
         const int zb = x * nzg + zgi;
         if (zb >= nzero_blocks) return;
-        const bool hold = zgi < zhold;  // resident beside the chunk waves
-        if (hold && !LSS_ZERO_HOLD_AFTER_LOAD) __builtin_amdgcn_s_sleep(kZeroHoldBack);
+        if (zgi < zhold) __builtin_amdgcn_s_sleep(kZeroHoldBack);  // resident beside the chunk waves
         const int u = (zb * kSplatWaves + wave) * kZeroUnits;
         [[maybe_unused]] const int zslot = nchunk_blocks * kSplatWaves + zb * kSplatWaves + wave;
         LSS_STAMP(zslot, 0);
-        if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, g, out, lane, hold);
+        if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, g, out, lane);
         LSS_STAMP(zslot, 3);
 #if LSS_TRACE
         if (lane == 0 && zslot < 16384) g_lss_trace[zslot][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
