@@ -159,6 +159,24 @@ def splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes, ctx_bytes) -> int:
             + ncells * 64 * out_bytes)    # dense BEV, every element written once
 
 
+def splat_fwd_bytes_survey(B, N, D, H, W, X, Y, Z, in_bytes, out_bytes) -> int:
+    """SURVEY.md §8(d)'s fused-forward formula: the depthnet output (D + C per pixel), one int32 voxel
+    id per point, the dense BEV (for comparison with splat_fwd_bytes, which counts what this
+    kernel reads: depth weights, context rows, sorted point ids and cell starts)."""
+    return B * N * H * W * (D + 64) * in_bytes + B * N * D * H * W * 4 + B * 64 * Z * X * Y * out_bytes
+
+
+def splat_bwd_bytes(B, N, D, H, W, occupied, in_bytes, g_bytes) -> dict:
+    """Algorithmic HBM bytes of one lss_splat_bwd launch (k_splat_bwd_tile): per pixel its
+    D depth weights (fp32) and cell ids (int32), its context row (C values) and its d_depthnet_out
+    row (D + C values); per occupied BEV cell its gradient row (C values, read once from HBM; every
+    further kept point of the cell re-reads it from L2 / MALL: `gather_bytes`)."""
+    pix = B * N * H * W
+    hbm = pix * (D * 4 * 2 + 64 * in_bytes + (D + 64) * in_bytes) + occupied * 64 * g_bytes
+    return {"hbm": hbm, "per_pixel": D * 8 + 64 * in_bytes + (D + 64) * in_bytes, "occupied_rows": occupied,
+            "row_bytes": 64 * g_bytes}
+
+
 def write_ceiling(numel, dtype, dev, reps=10) -> dict:
     """Measured HBM write ceiling for the splat's output buffer: lss_ceiling_store, a hand-written
     16-B streaming-store kernel (consecutive lanes on consecutive 16 B, `per_thread` stores per lane,
@@ -299,12 +317,13 @@ def measure_in_graph(args) -> dict | None:
     if r.returncode != 0 or not files:
         log(f"[bench] in-graph kernel trace failed (rc={r.returncode})")
         return None
-    rows = {"splat": [], "lift": []}
+    rows = {"splat": [], "lift": [], "bwd": []}
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row["Kernel_Name"]
-                key = "splat" if "k_splat_fwd" in k else "lift" if ("k_depthnet_lift" in k or "k_lift_prep" in k) else None
+                key = ("splat" if "k_splat_fwd" in k else "bwd" if "k_splat_bwd" in k
+                       else "lift" if ("k_depthnet_lift" in k or "k_lift_prep" in k) else None)
                 if key:
                     rows[key].append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
     shutil.rmtree(tmp, ignore_errors=True)
@@ -325,6 +344,12 @@ def measure_in_graph(args) -> dict | None:
              if any(lb <= b for lb, le in rows["lift"])]
     if after:
         res["after_lift_us"] = round(sum(after) / len(after), 2)
+    # the splat backward of the same replays (training mode: one per step)
+    bsel = rows["bwd"][-1 - steps:-1]
+    if len(bsel) == steps:
+        bd = [(e - b) / 1e3 for b, e in bsel]
+        res["bwd"] = {"kernel": "k_splat_bwd", "us": round(sum(bd) / len(bd), 2), "min_us": round(min(bd), 2),
+                      "launches": len(bd)}
     return res
 
 
@@ -599,8 +624,7 @@ def main():
                 log(f"[rank {rank}] replicas differ after the overlapped captured all-reduce: re-broadcasting "
                     "rank 0's parameters, serial all-reduce")
                 parallel.broadcast_state(model)
-                step = serial_step()
-                step.capture(warmup=2)
+                step = parallel.recapture_collectively(serial_step, "replicas differed")
                 for _ in range(2):
                     step()
                 fell_back = "replicas differed after the overlapped captured all-reduce"
@@ -647,17 +671,36 @@ def main():
         per_rank_ms = [1e3 * float(x.item()) / args.steps for x in allt]
         elapsed = max(float(x.item()) for x in allt)
     log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f} s, out {float(out.float().mean()):.4f}")
+    invalid = None
     if sync is not None:
         sync["after_timed"] = parallel.replicas_in_sync(step.params)
+        if not sync["after_timed"]:
+            # the same policy as after the warm-up: replicas that drifted apart during the timed
+            # replays void the number (the line is printed marked invalid, then every rank exits 4)
+            invalid = "replicas differ after the timed replays"
+            log(f"[rank {rank}] {invalid}")
 
     if rank == 0:
         D, H, W = model.frustum.shape[:3]
         with torch.no_grad():
             plan = model.plan(rig["rots"], rig["trans"], rig["intrins"], rig["post_rots"], rig["post_trans"])
             kept = int(plan.cell_start[-1].item())
+            occupied = int((plan.cell_start[1:] > plan.cell_start[:-1]).sum().item())
         out_bytes = 2 if amp_dtype is not None else 4
         nbytes = splat_fwd_bytes(B, N, D, H, W, X, Y, Z, kept, out_bytes, ctx_bytes=out_bytes)
+        nbytes_8d = splat_fwd_bytes_survey(B, N, D, H, W, X, Y, Z, out_bytes, out_bytes)
         achieved = nbytes / (splat_ms * 1e-3) / 1e9 if splat_ms else None
+        roofline_bwd = None
+        if args.mode == "train":
+            bb = splat_bwd_bytes(B, N, D, H, W, occupied, out_bytes, out_bytes)
+            ib = (in_graph or {}).get("bwd")
+            roofline_bwd = {
+                "kernel": "lss_splat_bwd (k_splat_bwd_tile)", "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "algorithmic_bytes": bb["hbm"], "bytes_detail": bb, "gather_bytes_l2": kept * 64 * out_bytes,
+                "us": ib["us"] if ib else None, "min_us": ib["min_us"] if ib else None,
+                "achieved": round(bb["hbm"] / (ib["us"] * 1e3), 1) if ib else None,
+                "frac": round(bb["hbm"] / (ib["us"] * 1e3) / HBM_PEAK_GBS, 4) if ib else None,
+                "timed_in": "the captured step's graph replays (rocprofv3 --kernel-trace child, as roofline.in_graph)"}
         ceiling = write_ceiling(B * Z * 64 * X * Y, amp_dtype or torch.float32, dev)
         frames = world * B * args.steps
         what = "full train step (fwd+loss+bwd+clip+Adam)" if args.mode == "train" else "forward only"
@@ -677,18 +720,25 @@ def main():
                                       else "one flat all-reduce between the graphs" if (world > 1 or FORCE_PG)
                                       else None)},
             "per_rank_ms_per_step": [round(x, 3) for x in per_rank_ms],
-            "replicas_in_sync": sync, "capture_fallback": fell_back,
+            "replicas_in_sync": sync, "capture_fallback": fell_back, "invalid": invalid,
             "roofline": {"kernel": "lss_splat_fwd", "bound": "hbm",
+                         "graded": "frac: eager launches, kernel-stamped hipEvents (this process); in_graph.frac: "
+                                   "the same kernel inside the captured step's replays (rocprofv3 child)",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
                          "traffic_detail": traffic, "algorithmic_bytes": nbytes,
+                         "algorithmic_bytes_survey_8d": nbytes_8d,
+                         "frac_survey_8d": round(nbytes_8d / (splat_ms * 1e6) / HBM_PEAK_GBS, 4) if splat_ms else None,
                          "avg_launch_us": round(splat_ms * 1e3, 2) if splat_ms else None,
                          "timed_in": "eager steps after the timed region, kernel-stamped hipEvents",
-                         "in_graph": dict(in_graph, frac=round(nbytes / (in_graph["us"] * 1e3) / HBM_PEAK_GBS, 4))
+                         "in_graph": {**{k: v for k, v in in_graph.items() if k != "bwd"},
+                                      "frac": round(nbytes / (in_graph["us"] * 1e3) / HBM_PEAK_GBS, 4),
+                                      "frac_survey_8d": round(nbytes_8d / (in_graph["us"] * 1e3) / HBM_PEAK_GBS, 4)}
                                      if in_graph else None,
                          "write_ceiling": dict(ceiling, splat_frac_of_ceiling=round(achieved / ceiling["GB/s"], 4)
                                                if achieved else None)},
+            "roofline_bwd": roofline_bwd,
         }
         if args.cpu_baseline and world == 1 and args.config == "c3":
             log("[rank 0] timing the CPU baseline ...")
@@ -701,6 +751,8 @@ def main():
     if world > 1 or FORCE_PG:
         dist.destroy_process_group()
     watchdog.cancel()
+    if invalid:
+        sys.exit(4)
 
 
 if __name__ == "__main__":

@@ -28,6 +28,7 @@ Extra knobs (not in the reference, defaults reproduce it):
 from __future__ import annotations
 
 import os
+import sys
 
 import torch
 import torch.nn.functional as F
@@ -76,6 +77,18 @@ class Up(nn.Module):
         return bn_act(c[4], c[3](x), "relu")
 
 
+_TRUNK_WEIGHTS_NOTED = set()
+
+
+def _note_trunk_weights(path: str) -> None:
+    """Say once per path (stderr) that the trunk starts from local weights: the environment variable
+    changes every model built in the process, parity and benchmark runs included."""
+    if path not in _TRUNK_WEIGHTS_NOTED:
+        _TRUNK_WEIGHTS_NOTED.add(path)
+        print(f"[lss_carla_amd] CamEncode trunk: EfficientNet-B0 weights from {path} "
+              "($LSS_EFFICIENTNET_B0_WEIGHTS)", file=sys.stderr, flush=True)
+
+
 class CamEncode(nn.Module):
     """Image -> depthnet output (src/models.py:37-89)."""
 
@@ -86,6 +99,8 @@ class CamEncode(nn.Module):
         # a download; here they come from a local file when $LSS_EFFICIENTNET_B0_WEIGHTS names one
         # (an unchanged train_simbev.py then trains from them), else the trunk is randomly initialised
         wpath = os.environ.get("LSS_EFFICIENTNET_B0_WEIGHTS")
+        if wpath:
+            _note_trunk_weights(wpath)
         self.trunk = EfficientNetB0.from_pretrained("efficientnet-b0", wpath) if wpath else EfficientNetB0()
         self.up1 = Up(320 + 112, 512)
         self.dropout = nn.Dropout(0.2)

@@ -522,7 +522,14 @@ class DepthnetLiftSplat(torch.autograd.Function):
         out = _new_bev(B, Z, X, Y, out_dtype, layout, dev)
         st = _lib.stream_handle(dev)
         if nhwc and packed is not None and weight.dtype == bf and bias.dtype == bf:
-            # weights already in fragment order (flat_params: the same launch as their bf16 copy)
+            # weights already in fragment order (flat_params: the same launch as their bf16 copy);
+            # the kernel reads DN_PACKED_BYTES(K) from it, so a buffer of another size, type or device
+            # is refused rather than read out of bounds
+            if (packed.dtype != bf or packed.device != dev or not packed.is_contiguous()
+                    or packed.numel() * 2 != _lib.DN_PACKED_BYTES(K) or packed.data_ptr() % 16):
+                raise RuntimeError(f"lss_carla_amd: prepacked depthnet weight {packed.dtype} x {packed.numel()} on "
+                                   f"{packed.device} does not match K={K} ({_lib.DN_PACKED_BYTES(K)} bytes, bf16, "
+                                   f"16-B aligned, on {dev})")
             w, b = weight.detach().reshape(O, K), bias.detach()
         elif nhwc:
             packed = torch.empty(_lib.DN_PACKED_BYTES(K) // 2, device=dev, dtype=bf)

@@ -129,24 +129,41 @@ def capture_collectively(step, warmup: int, fallback=None, on_warmup=None, fail:
     """Capture `step` (train_step.TrainStep or anything with .capture(warmup, on_warmup)) on every
     rank, or on none: each rank's success is agreed over the control group before any replay, so a
     capture that raised on one rank sends EVERY rank to `fallback()` (a factory of the step to use
-    instead, captured here with 2 warm-up steps). Returns (step, reason) -- reason None when `step`
-    itself was captured everywhere, else why the fallback was taken. fail: force this rank's
-    capture to raise (tests of the decision)."""
+    instead, captured here with 2 warm-up steps). The fallback's capture is voted on the same way;
+    if it fails on any rank, every rank raises (no rank replays while another has given up).
+    Returns (step, reason) -- reason None when `step` itself was captured everywhere, else why the
+    fallback was taken. fail: force this rank's capture to raise (tests of the decision).
+
+    Not covered by the vote: a rank that hangs (rather than raises) inside the eager warm-up steps,
+    whose collectives the other ranks then wait on -- that case ends by the bench's watchdog."""
     err = None
     try:
         if fail:
             raise RuntimeError("capture failure forced on this rank")
         step.capture(warmup=warmup, on_warmup=on_warmup)
-    except RuntimeError as e:
+    except Exception as e:  # any failure must reach the vote, or the peers block in it
         err = e
     if all_ranks_ok(err is None):
         return step, None
     if fallback is None:
         raise RuntimeError(f"graph capture failed on {'this' if err else 'another'} rank") from err
     reason = f"this rank's capture raised: {err}" if err is not None else "another rank's capture raised"
-    new = fallback()
-    new.capture(warmup=2)
-    return new, reason
+    return recapture_collectively(fallback, reason), reason
+
+
+def recapture_collectively(factory, why: str = ""):
+    """factory() captured with 2 warm-up steps on every rank, agreed over the control group: returns
+    the captured step, or raises on EVERY rank if the capture raised on any."""
+    new, err = None, None
+    try:
+        new = factory()
+        new.capture(warmup=2)
+    except Exception as e:
+        err = e
+    if not all_ranks_ok(err is None):
+        raise RuntimeError(f"fallback capture failed on {'this' if err else 'another'} rank"
+                           + (f" ({why})" if why else "")) from err
+    return new
 
 
 def max_over_ranks(value: float, device: torch.device) -> float:

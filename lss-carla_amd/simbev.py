@@ -40,6 +40,29 @@ def get_rot(h):
     return torch.Tensor([[np.cos(h), np.sin(h)], [-np.sin(h), np.cos(h)]])
 
 
+def draw_augmentation(conf: dict, train: bool):
+    """One sample's augmentation (src/data_simbev.py:119-145): (scale, (W', H') after scaling, crop box
+    (left, top, right, bottom) of final_dim, flip, rotation in degrees).
+
+    The crop keeps the image's bottom band: its top edge sits `bottom` of the scaled height above the
+    bottom minus the final height; horizontally the window starts `left` pixels in. Training draws,
+    in order, from np.random: scale ~ U(resize_lim), bottom ~ U(bot_pct_lim), left ~ U(0, slack), a
+    flip coin only when rand_flip is set, rotation ~ U(rot_lim). Validation: the scale that fits the
+    final width, the mean of bot_pct_lim, the window centred, no flip or rotation."""
+    src_h, src_w = conf["H"], conf["W"]
+    out_h, out_w = conf["final_dim"]
+    rnd = np.random
+    scale = rnd.uniform(*conf["resize_lim"]) if train else max(out_h / src_h, out_w / src_w)
+    scaled = (int(src_w * scale), int(src_h * scale))
+    slack = max(0, scaled[0] - out_w)
+    bottom = rnd.uniform(*conf["bot_pct_lim"]) if train else np.mean(conf["bot_pct_lim"])
+    top = int((1 - bottom) * scaled[1]) - out_h
+    left = int(rnd.uniform(0, slack)) if train else int(slack / 2)
+    flip = bool(train and conf["rand_flip"] and rnd.choice([0, 1]))
+    rotate = rnd.uniform(*conf["rot_lim"]) if train else 0
+    return scale, scaled, (left, top, left + out_w, top + out_h), flip, rotate
+
+
 def post_homography(resize, crop, flip, rotate):
     """(post_rot (3, 3), post_tran (3,)) of one camera: img_transform's post-homography arithmetic
     (src/tools.py:130-142) then the 3x3 embedding of get_image_data (src/data_simbev.py:204-208),
@@ -244,30 +267,13 @@ class SimBEVDataset(torch.utils.data.Dataset):
         return out
 
     def sample_augmentation(self):
-        """src/data_simbev.py:119-145, draw for draw."""
-        H, W = self.data_aug_conf["H"], self.data_aug_conf["W"]
-        fH, fW = self.data_aug_conf["final_dim"]
-        if self.is_train:
-            resize = np.random.uniform(*self.data_aug_conf["resize_lim"])
-            resize_dims = (int(W * resize), int(H * resize))
-            newW, newH = resize_dims
-            crop_h = int((1 - np.random.uniform(*self.data_aug_conf["bot_pct_lim"])) * newH) - fH
-            crop_w = int(np.random.uniform(0, max(0, newW - fW)))
-            crop = (crop_w, crop_h, crop_w + fW, crop_h + fH)
-            flip = False
-            if self.data_aug_conf["rand_flip"] and np.random.choice([0, 1]):
-                flip = True
-            rotate = np.random.uniform(*self.data_aug_conf["rot_lim"])
-        else:
-            resize = max(fH / H, fW / W)
-            resize_dims = (int(W * resize), int(H * resize))
-            newW, newH = resize_dims
-            crop_h = int((1 - np.mean(self.data_aug_conf["bot_pct_lim"])) * newH) - fH
-            crop_w = int(max(0, newW - fW) / 2)
-            crop = (crop_w, crop_h, crop_w + fW, crop_h + fH)
-            flip = False
-            rotate = 0
-        return resize, resize_dims, crop, flip, rotate
+        """(resize, resize_dims, crop box, flip, rotate) of one sample (src/data_simbev.py:119-145).
+
+        Training draws from numpy's global generator in the reference's order -- scale, bottom-crop
+        fraction, horizontal crop offset, the flip coin (only when rand_flip is on), rotation -- so a
+        seeded run reproduces the reference loader's augmentations; validation uses the fixed
+        fit-to-width scale, the mean bottom fraction and a centred window."""
+        return draw_augmentation(self.data_aug_conf, self.is_train)
 
     def get_image_data(self, sample, cam_indices):
         """Decoded images and calibration (src/data_simbev.py:147-218 without the pixel work)."""

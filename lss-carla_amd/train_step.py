@@ -21,7 +21,8 @@ pointers only and the plan's sizes come from the static shapes; the one host rou
 reference (torch.inverse on the CPU, src/models.py:180,186) moves out of the captured region:
 ``pre_step`` inverts the host copy of the rig with the same call and stages the results into static
 device buffers (ops.HostInverses) before each replay, so the captured step reads bit-identical
-inverses (``inverse='device'`` -- an fp64 adjugate kernel, not bit-exact -- remains an option).
+inverses. (A device fp64 adjugate inverse, not bit-exact, was removed in round 4 with the other
+off-by-default options; its measurements stay in profiles/r03.)
 """
 from __future__ import annotations
 
