@@ -10,7 +10,7 @@ replay (ops.HostInverses). --graph 0 runs the step eagerly (DDP for N>1).
 
   python bench.py                          # N=1, config 3
   python bench.py --gpus 8                 # launches 8 ranks (torchrun) itself, B=8 per rank
-  python bench.py --config c2              # config 2: B=4, fp32, forward only (NCHW BEV)
+  python bench.py --config c2              # config 2: B=4, fp32, forward only
   python bench.py --config c5              # config 5 per-GPU shard: B=4, 256x704, D=60, 400x400
 
 Also reported on the same JSON line:
@@ -103,7 +103,7 @@ def parse():
     if not args.dtype:
         args.dtype = "fp32" if args.mode == "fwd" else "bf16"
     if not args.bev_layout:
-        args.bev_layout = "nhwc" if args.dtype == "bf16" else "nchw"
+        args.bev_layout = "nhwc"  # the module default (models.LiftSplatShoot.bev_layout)
     return args
 
 
@@ -306,6 +306,10 @@ def measure_in_graph(args) -> dict | None:
            "--dtype", args.dtype, "--bev-layout", args.bev_layout, "--steps", str(steps), "--warmup", "3",
            "--profile-steps", "0", "--pmc-traffic", "0", "--cpu-baseline", "0", "--in-graph-prof", "0",
            "--mode", args.mode]
+    # the rest of this run's configuration, so the child measures the same step
+    for flag in ("miopen_find", "hip_bn", "fuse_depthnet", "trunk_channels_last", "param_groups", "flat_params",
+                 "overlap_all_reduce", "dw_impl"):
+        cmd += ["--" + flag.replace("_", "-"), str(getattr(args, flag))]
     try:
         # the child's progress lines pass through to this process's stderr (no long silence)
         r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL,
