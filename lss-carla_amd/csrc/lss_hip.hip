@@ -98,6 +98,47 @@ __device__ __forceinline__ int wave_min(int v) {
     return v;
 }
 
+// Cross-lane sums without the LDS crossbar (each __shfl_xor is a ds_bpermute: ~50 per pixel made the
+// splat backward's reductions its longest phase): DPP quad / row permutes and gfx950's permlane16 /
+// permlane32 swaps. Level O adds the same two operands as the xor butterfly's level O (v_l +
+// v_{l^O}; fp32 addition commutes), so results are bit-identical to the butterfly -- in every lane for
+// O = 1, 2, 8, 16, 32, and for O = 4 (row_shl:4: lane l reads l + 4 of its row) in the lanes with
+// (l & 7) < 4 (scripts/probes/dpp_check.hip checks each primitive against the butterfly, lane by lane).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int O>
+__device__ __forceinline__ float xsum(float v) {
+    if constexpr (O == 1) {
+        return v + dpp_f<0xB1>(v);  // quad_perm [1,0,3,2]
+    } else if constexpr (O == 2) {
+        return v + dpp_f<0x4E>(v);  // quad_perm [2,3,0,1]
+    } else if constexpr (O == 4) {
+        return v + dpp_f<0x104>(v);  // row_shl:4
+    } else if constexpr (O == 8) {
+        return v + dpp_f<0x128>(v);  // row_ror:8 (= l ^ 8 inside a row of 16)
+    } else if constexpr (O == 16) {
+        const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+    } else {
+        static_assert(O == 32, "butterfly level");
+        const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+    }
+}
+// sum over the lanes l ^ o, o = LO, 2 LO, ..., HI (exact as above)
+template <int LO, int HI>
+__device__ __forceinline__ float xsum_range(float v) {
+    if constexpr (LO <= HI) return xsum_range<LO * 2, HI>(xsum<LO>(v));
+    else return v;
+}
+// wave_sum's value (its butterfly levels in its order, 32 down to 1), exact in lane 0, broadcast
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v = xsum<1>(xsum<2>(xsum<4>(xsum<8>(xsum<16>(xsum<32>(v))))));
+    return readlane_f(v, 0);
+}
+
 #ifndef LSS_TRACE
 #define LSS_TRACE 0  // diagnostics build: per-wave s_memrealtime stamps of the channels-last splat
 #endif
@@ -1443,6 +1484,12 @@ __device__ __forceinline__ void store_slice(bf16* dst, const float* a) {
 // store would wait for that store too (vmcnt counts both, in order), and stores are slow while the
 // zero fill saturates the write path.
 constexpr int kUnroll = 8;
+#ifndef LSS_SPLAT_WAITALL
+#define LSS_SPLAT_WAITALL 1
+#endif
+// s_waitcnt vmcnt(0), expcnt and lgkmcnt left at their maxima (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] |
+// lgkmcnt[11:8] | vmcnt_hi[15:14])
+constexpr int kWaitVm0 = 0x0F70;
 
 // Entry metadata of a chunk's 128-entry window, staged once in LDS: (row, point, cell).
 struct alignas(16) EntryMeta {
@@ -1538,6 +1585,18 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                 v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)dchk(mr, g.nrows, kDbgSplatRow) * kC + col);
             }
             const float wd = FUSED ? group_weight_load<RS::LPR, kUnroll>(meta, depth, e, ge - 1, lane, nprime) : 0.f;
+#if LSS_SPLAT_WAITALL
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u)  // (uses here keep the compiler from sinking a gather below the wait)
+                asm volatile("" : : "v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
+            // Every gather of the batch retired here, before the loop below stores a finished cell's row:
+            // vmcnt also counts stores (gfx9), so a wait for a later row issued after such a store --
+            // the compiler's wait for row u, with a conditional store in front, is vmcnt(0) -- would
+            // wait for that store's write to complete, a round trip per finished cell in the busiest
+            // write phase of the kernel. An explicit s_waitcnt is known to the compiler's wait
+            // insertion, so no row use after it waits again.
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+#endif
             if (LSS_TRACE && e == gs && grp == 0) LSS_STAMP(w, 2);
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
@@ -2134,43 +2193,59 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd_reg(const GT* __restrict__
         for (int e = 0; e < EPL; ++e) dst[(size_t)(D + col + e) * HW] = from_f32<DT>(dc[e]);
 }
 
-// pixels per wave of k_splat_bwd_tile for bf16 gradients (2: twice the gathers in flight per wave but 105
-// VGPRs, two blocks per CU: 12.2 us vs 10.3 us at c3)
-constexpr int kBwdPpw = 1;
-constexpr int kBwdMinWaves = 5;  // occupancy floor of k_splat_bwd_tile, bf16 rows (70 VGPRs give 7 anyway)
+// k_splat_bwd_tile shape for bf16 gradient rows, D <= 48 (experiment switches for build_variant)
+#ifndef LSS_BWD_WAVES
+#define LSS_BWD_WAVES 8
+#endif
+#ifndef LSS_BWD_PPW
+#define LSS_BWD_PPW 1
+#endif
+#ifndef LSS_BWD_MINW
+#define LSS_BWD_MINW 5
+#endif
+#ifndef LSS_BWD_DPP
+#define LSS_BWD_DPP 1  // experiment switch: 0 = the reductions as __shfl_xor butterflies (ds_bpermute)
+#endif
+constexpr int kBwdBigWaves = LSS_BWD_WAVES, kBwdBigPpw = LSS_BWD_PPW, kBwdBigMinW = LSS_BWD_MINW;
 
 // Pixel-tile form of k_splat_bwd_reg. The per-pixel form reads the D depth weights and cells of its
 // pixel at a stride of H*W (one cache line per value) and writes d_depthnet_out one element per
-// channel (D + C lines per pixel, 2 bytes each). Here a block (8 waves) takes PX consecutive pixels
-// of one image: their weights, cells and context rows are read as contiguous runs into LDS; each
-// wave takes PPW pixels, issues ALL their gradient-row gathers before any arithmetic (one round trip),
-// reduces each as k_splat_bwd_reg does (fixed association), and leaves d_logits / d_ctx in an LDS
-// tile that the block writes channel by channel, PX consecutive pixels per run.
-constexpr int kBwdWaves = 8;
-constexpr int kBwdBlock = kBwdWaves * kWave;
-
-template <typename GT, typename DT, typename CT, bool NHWC, int MAXD>  // MAXD: D <= MAXD (48 or 64)
-__global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? kBwdMinWaves : 4) void k_splat_bwd_tile(const GT* __restrict__ g,
-                                                              const int32_t* __restrict__ cell_of,
-                                                              const float* __restrict__ depth,
-                                                              const CT* __restrict__ ctx_t, int D, int HW, int npix,
-                                                              SplatGeo sg, DT* __restrict__ d_dn) {
+// channel (D + C lines per pixel, 2 bytes each). Here a block of WAVES waves takes PX = WAVES * PPW
+// consecutive pixels (a tile may straddle two images): their weights, cells and context rows are
+// read as contiguous runs into LDS; each wave takes PPW pixels, issues ALL their gradient-row gathers
+// before any arithmetic (one round trip), reduces each as k_splat_bwd_reg does (fixed association),
+// and leaves d_logits / d_ctx in an LDS tile that the block writes channel by channel in runs of RUN
+// consecutive pixels of one image.
+//
+// Tile shape: 8 waves x 1 pixel (the product). A one-round shape -- 4 waves x 3 pixels, all of c3's
+// 8,448 pixels resident at once (704 blocks for 768 slots) where 8 x 1 needs 1,056 blocks for 768
+// -- measured no faster (in-step 9.7 vs 9.5 us with the DPP reductions, 11.8 vs 11.7 before them;
+// profiles/r05/prof_ab_bwd_*): the per-pixel reduction, not the block rounds, was the long phase.
+// Kept as the LSS_BWD_WAVES / LSS_BWD_PPW / LSS_BWD_MINW experiment switches.
+template <typename GT, typename DT, typename CT, bool NHWC, int MAXD, int WAVES, int PPW, int MINW>
+__global__ __launch_bounds__(WAVES * kWave) __attribute__((amdgpu_waves_per_eu(MINW))) void k_splat_bwd_tile(
+    const GT* __restrict__ g, const int32_t* __restrict__ cell_of, const float* __restrict__ depth,
+    const CT* __restrict__ ctx_t, int D, int HW, int npix, SplatGeo sg, DT* __restrict__ d_dn) {
+    constexpr int kBwdBlock = WAVES * kWave;
     constexpr int EPL = 16 / sizeof(GT);  // row elements per 16-B lane load
     constexpr int LPR = kC / EPL;         // lanes per row
     constexpr int RPI = kWave / LPR;      // rows per wave-instruction
     constexpr int NI = MAXD / RPI;        // instructions for MAXD rows
-    constexpr int PPW = sizeof(GT) == 2 ? kBwdPpw : 1;  // pixels per wave, all gathers in flight
-    constexpr int PX = kBwdWaves * PPW;           // pixels per block
+    constexpr int PX = WAVES * PPW;       // pixels per block
+    constexpr int kOE = 16 / (int)sizeof(DT);
+    constexpr int RUN = PX % kOE == 0 ? kOE : 4;  // pixels per store: 16 B, or 4 pixels
+    static_assert(PX % RUN == 0, "whole store runs per tile");
+    static_assert(PPW * NI <= 32, "validity bits");
     __shared__ float s_dep[MAXD + 1][PX];  // + a spare row for the lanes past the end
     __shared__ int s_cell[MAXD + 1][PX];
     __shared__ float s_ctx[PX + 1][kC];  // + a spare tile for the lanes past the end
     __shared__ float s_out[MAXD + kC][PX + 1];
     const int q0 = xcd_block() * PX;
     if (q0 >= npix) return;  // block-uniform
-    [[maybe_unused]] const int tslot = blockIdx.x * kBwdWaves + (threadIdx.x >> 6);  // LSS_TRACE builds only
+    [[maybe_unused]] const int tslot = blockIdx.x * WAVES + (threadIdx.x >> 6);  // LSS_TRACE builds only
     LSS_STAMP(tslot, 0);
-    const int bn = q0 / HW, hw0 = q0 - bn * HW;  // HW % PX == 0: the tile lies in one image
-    const size_t pb = (size_t)bn * D * HW + hw0;
+    // PX <= HW: the tile lies in image bn0 up to pixel jcut, in image bn0 + 1 after it
+    const int bn0 = q0 / HW, hw0 = q0 - bn0 * HW, jcut = HW - hw0;
     // Every load below is unconditional (clamped index; an out-of-range value is dropped at the LDS
     // write or zeroed by a select), so the compiler issues them back to back: one round trip for the
     // staging, one for the gathers.
@@ -2185,12 +2260,14 @@ __global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? kBwdMinWaves : 4) void
     for (int t = 0; t < kStage; ++t) {
         const int i = min((int)threadIdx.x + t * kBwdBlock, D * PX - 1);
         const int d = i / PX, j = i - d * PX;
-        dv[t] = depth[pb + (size_t)d * HW + j];
-        cv[t] = cell_of[pb + (size_t)d * HW + j];
+        const size_t at = j < jcut ? ((size_t)bn0 * D + d) * HW + hw0 + j : ((size_t)(bn0 + 1) * D + d) * HW + (j - jcut);
+        dv[t] = depth[at];
+        cv[t] = cell_of[at];
     }
+    __builtin_amdgcn_sched_barrier(0);  // every staging load issued before the first wait
 #pragma unroll
     for (int t = 0; t < kStage; ++t) cv[t] = grad_row<NHWC>(cv[t], sg);  // gradient row index, or -1
-    // LDS writes without branches either (a lane past the end writes the spare row 63 / tile PX)
+    // LDS writes without branches either (a lane past the end writes the spare row MAXD)
 #pragma unroll
     for (int t = 0; t < kStage; ++t) {
         const int i = min((int)threadIdx.x + t * kBwdBlock, MAXD * PX - 1);
@@ -2209,21 +2286,29 @@ __global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? kBwdMinWaves : 4) void
     LSS_STAMP(tslot, 1);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = lane / LPR, col = (lane % LPR) * EPL;
+    // all row indices from LDS first, then every gather back to back; validity as one packed word
+    // (a mask register per gather held until its use cost one VGPR each)
+    int rows[PPW][NI];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i)
+#pragma unroll
+        for (int k = 0; k < NI; ++k) rows[i][k] = s_cell[min(k * RPI + sub, D - 1)][wave * PPW + i];
+    __builtin_amdgcn_sched_barrier(0);
     uint4 raw[PPW][NI];
+    unsigned vbits = 0;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-        const int jj = wave * PPW + i;
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
             // rows past D repeat row D - 1 (same line, no extra traffic); their values are zeroed
-            const int r = min(k * RPI + sub, D - 1);
-            const int row = s_cell[r][jj];
-            const uint4 v = *reinterpret_cast<const uint4*>(g + (size_t)dchk(max(row, 0), sg.nrows, kDbgBwdRow) * kC + col);
-            raw[i][k] = keep_if(k * RPI + sub < D && row >= 0, v);
+            const int row = rows[i][k];
+            raw[i][k] = *reinterpret_cast<const uint4*>(g + (size_t)dchk(max(row, 0), sg.nrows, kDbgBwdRow) * kC + col);
+            vbits |= (k * RPI + sub < D && row >= 0 ? 1u : 0u) << (i * NI + k);
         }
     }
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
+        __builtin_amdgcn_sched_barrier(0);  // one pixel's reduction at a time (register pressure)
         const int jj = wave * PPW + i;
         const float my_depth = lane < D ? s_dep[lane][jj] : 0.f;
         float cx[EPL], dc[EPL], part[NI];
@@ -2237,7 +2322,7 @@ __global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? kBwdMinWaves : 4) void
             const int r = k * RPI + sub;
             const float w = r < D ? s_dep[r][jj] : 0.f;
             float f[EPL];
-            unpack16(raw[i][k], (const GT*)nullptr, f);
+            unpack16(keep_if((vbits >> (i * NI + k)) & 1u, raw[i][k]), (const GT*)nullptr, f);
             float t = 0.f;
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
@@ -2246,6 +2331,14 @@ __global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? kBwdMinWaves : 4) void
             }
             part[k] = t;
         }
+#if LSS_BWD_DPP
+        // d_ctx over the RPI row groups, d_depth over the LPR lanes of a row (exact in lane 0 of each
+        // row group, which the select below reads): DPP / permlane levels, the butterfly's association
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) dc[e] = xsum_range<LPR, kWave / 2>(dc[e]);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) part[k] = xsum_range<1, LPR / 2>(part[k]);
+#else
 #pragma unroll
         for (int o = LPR; o < kWave; o <<= 1)
 #pragma unroll
@@ -2254,6 +2347,7 @@ __global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? kBwdMinWaves : 4) void
         for (int k = 0; k < NI; ++k)
 #pragma unroll
             for (int o = 1; o < LPR; o <<= 1) part[k] += __shfl_xor(part[k], o, kWave);
+#endif
         float dd = 0.f;
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
@@ -2261,7 +2355,11 @@ __global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? kBwdMinWaves : 4) void
             if (lane / RPI == k) dd = v;
         }
         if (lane >= D) dd = 0.f;
+#if LSS_BWD_DPP
+        const float s = wave_sum_dpp(my_depth * dd);
+#else
         const float s = wave_sum(my_depth * dd);
+#endif
         if (lane < D) s_out[lane][jj] = my_depth * (dd - s);
         if (sub == 0)
 #pragma unroll
@@ -2269,22 +2367,29 @@ __global__ __launch_bounds__(kBwdBlock, sizeof(GT) == 2 ? kBwdMinWaves : 4) void
     }
     LSS_STAMP(tslot, 2);
     __syncthreads();
-    // d_depthnet_out: 16-B runs of consecutive pixels of one channel (HW % PX == 0 keeps them aligned)
-    constexpr int kOE = 16 / (int)sizeof(DT);  // pixels per 16-B store
-    constexpr int kRuns = PX / kOE;
-    static_assert(PX % kOE == 0 && (MAXD + kC) * kRuns <= 2 * kBwdBlock, "two stores per thread at most");
-    DT* dst = d_dn + (size_t)bn * (D + kC) * HW + hw0;
+    // d_depthnet_out: runs of RUN consecutive pixels of one channel (HW % RUN == 0 and q0 % RUN == 0:
+    // a run never straddles two images)
+    constexpr int kRuns = PX / RUN;
+    constexpr int kSt = ((MAXD + kC) * kRuns + kBwdBlock - 1) / kBwdBlock;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < kSt; ++t) {
         const int i = threadIdx.x + t * kBwdBlock;
         if (i < (D + kC) * kRuns) {
-            const int ch = i / kRuns, j0 = (i - ch * kRuns) * kOE;
-            DT v[kOE];
+            const int ch = i / kRuns, j0 = (i - ch * kRuns) * RUN;
+            const int bn = j0 < jcut ? bn0 : bn0 + 1, hw = j0 < jcut ? hw0 + j0 : j0 - jcut;
+            DT v[RUN];
 #pragma unroll
-            for (int e = 0; e < kOE; ++e) v[e] = from_f32<DT>(s_out[ch][j0 + e]);
-            uint4 u;
-            __builtin_memcpy(&u, v, 16);
-            *reinterpret_cast<uint4*>(dst + (size_t)ch * HW + j0) = u;
+            for (int e = 0; e < RUN; ++e) v[e] = from_f32<DT>(s_out[ch][j0 + e]);
+            DT* dst = d_dn + ((size_t)bn * (D + kC) + ch) * HW + hw;
+            if constexpr (RUN * sizeof(DT) == 16) {
+                uint4 u;
+                __builtin_memcpy(&u, v, 16);
+                *reinterpret_cast<uint4*>(dst) = u;
+            } else {
+                uint2 u;
+                __builtin_memcpy(&u, v, 8);
+                *reinterpret_cast<uint2*>(dst) = u;
+            }
         }
     }
     LSS_STAMP(tslot, 3);
@@ -2845,7 +2950,9 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
     hipStream_t s = (hipStream_t)stream;
     const bool nhwc = rows_layout == LSS_NHWC;
     const int D = dims->D;
-    // pixel tiles (D <= 64, H*W a multiple of the tile) or the register kernel, 64 depth bins per chunk
+    // pixel tiles (D <= 64; whole tiles, at most one image boundary per tile, store runs inside one
+    // image) or the register kernel, 64 depth bins per chunk
+    auto tile_ok = [&](int px) { return npix % px == 0 && px <= HW && HW % 4 == 0 && (px % 8 != 0 || HW % 8 == 0); };
 #define LSS_BWD_REGK(GT, DT, CT, NH)                                                                              \
     do {                                                                                                          \
         if (D <= kWave)                                                                                           \
@@ -2858,28 +2965,25 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
             hipLaunchKernelGGL((k_splat_bwd_reg<GT, DT, CT, NH, 4>), gr, bl, 0, s, (const GT*)g, cell_of, depth,  \
                                (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                           \
     } while (0)
-#define LSS_BWD(GT, DT, CT)                                                                                       \
+#define LSS_BWD_TILE(GT, DT, CT, NH, MAXD, WV, PPW, MINW)                                                        \
+    hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, NH, MAXD, WV, PPW, MINW>), dim3(xcd_grid(npix / ((WV) * (PPW)))), \
+                       dim3((WV) * kWave), 0, s, (const GT*)g, cell_of, depth, (const CT*)ctx_t, D, HW, npix, sg,      \
+                       (DT*)d_depthnet_out)
+#define LSS_BWD_NH(GT, DT, CT, NH)                                                                                \
     do {                                                                                                          \
-        constexpr int px = kBwdWaves * (sizeof(GT) == 2 ? kBwdPpw : 1);                                       \
-        const dim3 grt(xcd_grid(npix / px)), blt(kBwdBlock);                                                      \
-        const bool tile = HW % px == 0 && D <= 64;                                                \
-        if (tile && nhwc && D <= 48)                                                                              \
-            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, true, 48>), grt, blt, 0, s, (const GT*)g, cell_of,  \
-                               depth, (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                    \
-        else if (tile && nhwc)                                                                                    \
-            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, true, 64>), grt, blt, 0, s, (const GT*)g, cell_of,  \
-                               depth, (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                    \
-        else if (tile && D <= 48)                                                                                 \
-            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, false, 48>), grt, blt, 0, s, (const GT*)g, cell_of, \
-                               depth, (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                    \
-        else if (tile)                                                                                            \
-            hipLaunchKernelGGL((k_splat_bwd_tile<GT, DT, CT, false, 64>), grt, blt, 0, s, (const GT*)g, cell_of, \
-                               depth, (const CT*)ctx_t, D, HW, npix, sg, (DT*)d_depthnet_out);                    \
-        else if (nhwc)                                                                                            \
-            LSS_BWD_REGK(GT, DT, CT, true);                                                                       \
+        constexpr bool kB16 = sizeof(GT) == 2;                                                                    \
+        if (kB16 && D <= 48 && tile_ok(kBwdBigWaves * kBwdBigPpw))                                                \
+            LSS_BWD_TILE(GT, DT, CT, NH, 48, kB16 ? kBwdBigWaves : 8, kB16 ? kBwdBigPpw : 1,                     \
+                         kB16 ? kBwdBigMinW : 4);                                                                 \
+        else if (D <= 48 && tile_ok(8))                                                                           \
+            LSS_BWD_TILE(GT, DT, CT, NH, 48, 8, 1, kB16 ? 5 : 4);                                                 \
+        else if (D <= 64 && tile_ok(8))                                                                           \
+            LSS_BWD_TILE(GT, DT, CT, NH, 64, 8, 1, kB16 ? 5 : 4);                                                 \
         else                                                                                                      \
-            LSS_BWD_REGK(GT, DT, CT, false);                                                                      \
+            LSS_BWD_REGK(GT, DT, CT, NH);                                                                         \
     } while (0)
+#define LSS_BWD(GT, DT, CT)                                                                                       \
+    do { if (nhwc) LSS_BWD_NH(GT, DT, CT, true); else LSS_BWD_NH(GT, DT, CT, false); } while (0)
 #define LSS_BWD2(GT, DT) \
     do { if (ctx_dtype == LSS_BF16) LSS_BWD(GT, DT, bf16); else LSS_BWD(GT, DT, float); } while (0)
     if (ctx_dtype != LSS_F32 && ctx_dtype != LSS_BF16) return LSS_EINVAL;
@@ -2890,6 +2994,8 @@ int lss_splat_bwd(const void* g, int32_t g_dtype, int32_t rows_layout, const int
     else return LSS_EINVAL;
 #undef LSS_BWD2
 #undef LSS_BWD
+#undef LSS_BWD_NH
+#undef LSS_BWD_TILE
 #undef LSS_BWD_REGK
     return launch_status();
 }

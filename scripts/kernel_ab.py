@@ -1,8 +1,10 @@
-"""Splat backward A/B across library builds: lss_splat_bwd (channels-last bf16 dBEV -> bf16 d_depthnet_out)
-of one config, outputs compared with the product build's bit for bit, times from events around the
-launch on its stream in two cache states (warm: back to back; read: after a 512 MiB read sweep).
+"""Hot-kernel A/B across library builds, outputs compared with the product build's bit for bit, times
+from events around the launch on its stream in two cache states (warm: back to back; read: after a
+512 MiB read sweep):
+  bwd   lss_splat_bwd (channels-last bf16 dBEV -> bf16 d_depthnet_out)
+  lift  lss_depthnet_lift_nhwc_packed (channels-last bf16 features, fragment-order weights -> depth, context rows)
 
-  python scripts/bwd_ab.py --config c3 --libs product,bwd81,dpp0
+  python scripts/kernel_ab.py --config c3 --libs product,bwd81,dpp0 [--kernel lift]
 """
 import argparse
 import ctypes as ct
@@ -19,6 +21,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--libs", default="product")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--kernel", default="bwd", choices=["bwd", "lift"])
     args = ap.parse_args()
     import torch
     from lss_carla_amd import _lib, ops, synthetic as syn
@@ -47,9 +50,24 @@ def main():
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
     sink = torch.zeros(4, dtype=torch.int32, device=dev)
 
+    feat = torch.randn(B * N, 512, H, W, generator=gen).to(dev, torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    wdn = (torch.randn(D + 64, 512, 1, 1, generator=gen) * 0.05).to(dev, torch.bfloat16)
+    bdn = (torch.randn(D + 64, generator=gen) * 0.1).to(dev, torch.bfloat16)
+    packed = torch.empty(_lib.DN_PACKED_BYTES(512) // 2, device=dev, dtype=torch.bfloat16)
+    _lib.check(lib.lss_depthnet_pack(_lib.ptr(wdn), _lib.ptr(bdn), _lib.BF16, wdn.shape[0], 512, _lib.ptr(packed),
+                                     None, None, st), "pack")
+
     def run(l):
-        _lib.check(l.lss_splat_bwd(_lib.ptr(gbev), _lib.BF16, _lib.NHWC, _lib.ptr(plan.cell_of), _lib.ptr(depth),
-                                   _lib.ptr(ctx), _lib.BF16, dims, g, _lib.ptr(d_dn), _lib.BF16, st), "bwd")
+        if args.kernel == "bwd":
+            _lib.check(l.lss_splat_bwd(_lib.ptr(gbev), _lib.BF16, _lib.NHWC, _lib.ptr(plan.cell_of), _lib.ptr(depth),
+                                       _lib.ptr(ctx), _lib.BF16, dims, g, _lib.ptr(d_dn), _lib.BF16, st), "bwd")
+        else:
+            _lib.check(l.lss_depthnet_lift_nhwc_packed(_lib.ptr(feat), _lib.ptr(packed), _lib.ptr(bdn), 512, dims,
+                                                       _lib.ptr(depth), _lib.ptr(ctx), _lib.BF16, st), "lift3")
+
+    def output():
+        return d_dn if args.kernel == "bwd" else torch.cat([depth.flatten(), ctx.float().flatten()])
 
     def timed(l, mode):
         ts = []
@@ -74,20 +92,25 @@ def main():
 
     run(lib)
     torch.cuda.synchronize()
-    want = d_dn.clone()
-    res = {"config": args.config, "pixels": B * N * H * W, "D": D}
+    want = output().clone()
+    res = {"config": args.config, "kernel": args.kernel, "pixels": B * N * H * W, "D": D}
     for name in args.libs.split(","):
         l = lib if name == "product" else _lib.open_library(
             os.path.join(REPO, "lss-carla_amd", "variants", name + ".so"))
-        d_dn.fill_(7.0)
+        if args.kernel == "bwd":
+            d_dn.fill_(7.0)
+        else:  # (the lift's outputs; for the backward they are inputs)
+            depth.fill_(7.0)
+            ctx.fill_(7.0)
         run(l)
         torch.cuda.synchronize()
-        row = {"equal_to_product": bool(torch.equal(d_dn, want)),
-               "max_abs_diff": float((d_dn.float() - want.float()).abs().max())}
+        got = output()
+        row = {"equal_to_product": bool(torch.equal(got, want)),
+               "max_abs_diff": float((got.float() - want.float()).abs().max())}
         for m in ("warm", "read"):
             row[m] = timed(l, m)
-        res[f"bwd[{name}]"] = row
-        print(f"bwd[{name}] {json.dumps(row)}", flush=True)
+        res[f"{args.kernel}[{name}]"] = row
+        print(f"{args.kernel}[{name}] {json.dumps(row)}", flush=True)
     print(json.dumps(res))
 
 
