@@ -342,24 +342,29 @@ __global__ __launch_bounds__(kGeoBlock) void k_cells_from_geom(const float* __re
 
 // ----------------------------------------------------------------------------- CSR (counting sort)
 // Exclusive scan of 1024 thread totals inside a block; returns the thread's exclusive prefix.
+// Inclusive scan over the 64 lanes on DPP (integer adds: exact in any order): the sum of the 4 lanes up
+// to l in each row (row_shr 1, 2, 3), of 8 and 16 (row_shr 4 / 8 into the upper banks), then the
+// rows' totals carried over by row_bcast 15 / 31 -- VALU only, where the __shfl_up form was six
+// dependent ds_bpermute round trips through the LDS crossbar.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    int t = v + __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    t += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);         // row_shr:2
+    t += __builtin_amdgcn_update_dpp(0, v, 0x113, 0xf, 0xf, false);         // row_shr:3
+    t += __builtin_amdgcn_update_dpp(0, t, 0x114, 0xf, 0xe, false);         // row_shr:4, banks 1-3
+    t += __builtin_amdgcn_update_dpp(0, t, 0x118, 0xf, 0xc, false);         // row_shr:8, banks 2-3
+    t += __builtin_amdgcn_update_dpp(0, t, 0x142, 0xa, 0xf, false);         // row_bcast:15 into rows 1, 3
+    t += __builtin_amdgcn_update_dpp(0, t, 0x143, 0xc, 0xf, false);         // row_bcast:31 into rows 2, 3
+    return t;
+}
+
 __device__ int block_exclusive_scan_1024(int v, int* s_wave, int* total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o, kWave);
-        if (lane >= o) incl += t;
-    }
+    const int incl = wave_incl_scan(v);
     if (lane == 63) s_wave[wave] = incl;
     __syncthreads();
     if (wave == 0) {
         int w = lane < 16 ? s_wave[lane] : 0;
-        int wi = w;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            const int t = __shfl_up(wi, o, kWave);
-            if (lane >= o) wi += t;
-        }
+        const int wi = wave_incl_scan(w);  // (lanes 16.. add zeros)
         if (lane < 16) s_wave[16 + lane] = wi - w;
         if (lane == 15) *total = wi;
     }
@@ -1487,6 +1492,7 @@ constexpr int kUnroll = 8;
 #ifndef LSS_SPLAT_WAITALL
 #define LSS_SPLAT_WAITALL 1
 #endif
+
 // s_waitcnt vmcnt(0), expcnt and lgkmcnt left at their maxima (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] |
 // lgkmcnt[11:8] | vmcnt_hi[15:14])
 constexpr int kWaitVm0 = 0x0F70;
@@ -1508,8 +1514,33 @@ __device__ __forceinline__ float group_weight_load(const EntryMeta* __restrict__
     return depth[dchk(meta[min(e + lane % LPR, last)].p, nprime, kDbgSplatPoint)];
 }
 // weight of entry e + u of the group (broadcast from the group's lane u; one VGPR held across the wait)
+#ifndef LSS_SPLAT_DPPW
+#define LSS_SPLAT_DPPW 1
+#endif
+// 8-lane groups (bf16 rows): lane U of every group by two DPP moves -- a quad broadcast of lane U & 3,
+// then the other quad of each group takes it from its neighbour quad (row_shr:4 into banks 1 / 3, or
+// row_shl:4 into banks 0 / 2) -- instead of a ds_bpermute through the LDS crossbar
+template <int U>
+__device__ __forceinline__ float bcast8(float wd) {
+    constexpr int k = U & 3;
+    const int q = __builtin_amdgcn_update_dpp(0, __float_as_int(wd), k * 0x55, 0xf, 0xf, false);  // quad_perm [k,k,k,k]
+    if constexpr (U < 4) return __int_as_float(__builtin_amdgcn_update_dpp(q, q, 0x114, 0xf, 0xA, false));
+    else return __int_as_float(__builtin_amdgcn_update_dpp(q, q, 0x104, 0xf, 0x5, false));
+}
 template <int LPR>
 __device__ __forceinline__ float group_weight(float wd, int u, int lane) {
+    if constexpr (LPR == 8 && LSS_SPLAT_DPPW) {
+        switch (u) {  // (u is a constant in every unrolled use)
+            case 0: return bcast8<0>(wd);
+            case 1: return bcast8<1>(wd);
+            case 2: return bcast8<2>(wd);
+            case 3: return bcast8<3>(wd);
+            case 4: return bcast8<4>(wd);
+            case 5: return bcast8<5>(wd);
+            case 6: return bcast8<6>(wd);
+            default: return bcast8<7>(wd);
+        }
+    }
     return __shfl(wd, lane - lane % LPR + u, kWave);
 }
 

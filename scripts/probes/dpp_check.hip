@@ -33,6 +33,18 @@ __global__ void k(const float* in, float* out) {
     }
 }
 
+__device__ int wave_incl_scan(int v) {  // as lss_hip.hip
+    int t = v + __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    t += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    t += __builtin_amdgcn_update_dpp(0, v, 0x113, 0xf, 0xf, false);
+    t += __builtin_amdgcn_update_dpp(0, t, 0x114, 0xf, 0xe, false);
+    t += __builtin_amdgcn_update_dpp(0, t, 0x118, 0xf, 0xc, false);
+    t += __builtin_amdgcn_update_dpp(0, t, 0x142, 0xa, 0xf, false);
+    t += __builtin_amdgcn_update_dpp(0, t, 0x143, 0xc, 0xf, false);
+    return t;
+}
+__global__ void kscan(const int* in, int* out) { out[threadIdx.x] = wave_incl_scan(in[threadIdx.x]); }
+
 int main() {
     float h[64], o[14 * 64];
     for (int i = 0; i < 64; ++i) h[i] = 1.0f + i * 1.0f / 1024 + (i * 37 % 11) * 1e-3f;
@@ -52,5 +64,16 @@ int main() {
             if (memcmp(&o[(6 + c) * 64 + l], &o[ref[c] * 64 + l], 4) == 0) ok |= 1ull << l;
         printf("%-28s equal lanes mask %016llx\n", names[c], ok);
     }
-    return 0;
+    int hi[64], ho[64];
+    for (int i = 0; i < 64; ++i) hi[i] = (i * 7919) % 1000 - 300;
+    int *dii, *dio;
+    hipMalloc(&dii, sizeof hi);
+    hipMalloc(&dio, sizeof ho);
+    hipMemcpy(dii, hi, sizeof hi, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(kscan, dim3(1), dim3(64), 0, 0, dii, dio);
+    hipMemcpy(ho, dio, sizeof ho, hipMemcpyDeviceToHost);
+    int run = 0, bad = 0;
+    for (int i = 0; i < 64; ++i) { run += hi[i]; bad += ho[i] != run; }
+    printf("wave_incl_scan (DPP) vs sequential prefix: %d lanes differ\n", bad);
+    return bad != 0;
 }
