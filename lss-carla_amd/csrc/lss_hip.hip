@@ -1674,154 +1674,9 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
     }
 }
 
-// ---- persistent chunk waves: one wave takes kChunksPerWave consecutive chunks, software-pipelined.
-// Consecutive chunks share half their window: chunk w reads entries [64w, 64w + 128), chunk w + 1
-// [64w + 64, 64w + 192). The wave keeps the window in LDS (EntryMeta) and, while chunk w's gathers are
-// in flight, loads only the new half [64w + 128, 64w + 192) of the next window (one coalesced key +
-// row load). The loads are issued BEFORE the gathers, and the first gather batch is unconditional, so
-// the gathers' wait also retires the prefetch (vector memory ops complete in order) and no store of
-// chunk w sits between the prefetch and its use. So a chunk after the first costs one round trip
-// (gathers + depth weights) instead of two, and the launch needs a third of the chunk waves: every
-// zero-fill wave is resident at t = 0 instead of waiting for chunk waves to retire (round 4's trace:
-// the zero fill started at p50 5.7 us). Per-cell association as splat_chunk (bit-identical BEV).
-#ifndef LSS_SPLAT_K
-#define LSS_SPLAT_K 1  // chunks per chunk wave (1: splat_chunk, one chunk, two round trips)
-#endif
-constexpr int kChunksPerWave = LSS_SPLAT_K;
 #ifndef LSS_SPLAT_ZFIRST
 #define LSS_SPLAT_ZFIRST 0  // dispatch order: 0 chunk groups first, 1 zero-fill groups first
 #endif
-
-template <bool FUSED>
-__device__ __forceinline__ void load_half_window(const long long* __restrict__ key, const int32_t* __restrict__ row,
-                                                 int e, int nprime, long long& k, int& r) {
-    // unconditional (clamped) loads; entries past the buffer read as the sentinel
-    const int ec = min(e, nprime - 1);
-    const long long kr = key[ec];
-    const int rr = FUSED ? row[ec] : 0;
-    k = e < nprime ? kr : -1ll;
-    r = rr;
-}
-
-template <bool FUSED, typename RT, typename OutT>
-__device__ __forceinline__ void splat_chunks_pl(int w0, int wend, int nprime, const float* __restrict__ depth,
-                                                const RT* __restrict__ rows_base,
-                                                const long long* __restrict__ sorted_key,
-                                                const int32_t* __restrict__ sorted_row, const BevGeo& g,
-                                                OutT* __restrict__ out, EntryMeta* __restrict__ meta,
-                                                float* __restrict__ part, int lane) {
-    using RS = RowSlice<RT>;
-    // the first window: entries [64 w0, 64 w0 + 128) and the cell of the entry before it
-    long long ka, kb;
-    int ra, rb;
-    load_half_window<FUSED>(sorted_key, sorted_row, w0 * kWave + lane, nprime, ka, ra);
-    load_half_window<FUSED>(sorted_key, sorted_row, w0 * kWave + kWave + lane, nprime, kb, rb);
-    int prevcell = w0 > 0 ? (int)(sorted_key[w0 * kWave - 1] >> 32) : -2;
-    for (int w = w0; w < wend; ++w) {
-        const int base = w * kWave;
-        const int c0 = (int)(ka >> 32), c1 = (int)(kb >> 32);
-        const int p0 = (int)(ka & 0xFFFFFFFF), p1 = (int)(kb & 0xFFFFFFFF);
-        const int rs0 = FUSED ? ra : p0, rs1 = FUSED ? rb : p1;
-        const Span sp = chunk_span(c0, c1, prevcell, lane);
-        const int s = uniform(sp.s), end = uniform(sp.end), big = uniform(sp.big);
-        // the next window's new half, in flight behind this chunk's gathers
-        long long kn;
-        int rn;
-        load_half_window<FUSED>(sorted_key, sorted_row, base + 2 * kWave + lane, nprime, kn, rn);
-        const int nextprev = __builtin_amdgcn_readlane(c0, 63);  // the cell of entry 64(w + 1) - 1
-        meta[lane] = EntryMeta{rs0, p0, c0, 0};
-        meta[kWave + lane] = EntryMeta{rs1, p1, c1, 0};
-        __builtin_amdgcn_wave_barrier();
-        if (end > 0) {
-            const int n = end - s;
-            const int grp = lane / RS::LPR, col = (lane % RS::LPR) * RS::EPL;
-            auto gbeg = [&](int q) { return s + (n * q) / RS::NG; };
-            const int gs = gbeg(grp), ge = gbeg(grp + 1);
-            const int first_cell = gs < ge ? meta[gs].cell : -1;
-            const bool head_split = gs < ge && gs > s && meta[gs - 1].cell == first_cell;
-            const bool tail_split = gs < ge && ge < end && meta[ge].cell == meta[ge - 1].cell;
-            float acc[RS::EPL];
-#pragma unroll
-            for (int i = 0; i < RS::EPL; ++i) acc[i] = 0.f;
-            int cur = -1;
-            auto put = [&](float* dst, int c) {
-#pragma unroll
-                for (int i = 0; i < RS::EPL; i += 4)
-                    *reinterpret_cast<float4*>(dst + c + i) = make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
-            };
-            auto finish = [&](bool last, int c) {
-                if (cur == first_cell && head_split) put(part + grp * kC, c);
-                else if (!(last && tail_split)) store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + c, acc);
-            };
-            const int hi = max(ge - 1, 0);  // (an empty group reads its clamped first entry, never summed)
-            auto batch = [&](int e, bool first) {
-                uint4 v[kUnroll];
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    const int4 m = *reinterpret_cast<const int4*>(&meta[min(e + u, hi)]);
-                    v[u] = *reinterpret_cast<const uint4*>(rows_base + (size_t)dchk(m.x, g.nrows, kDbgSplatRow) * kC + col);
-                }
-                const float wd = FUSED ? depth[dchk(meta[min(e + lane % RS::LPR, hi)].p, nprime, kDbgSplatPoint)] : 0.f;
-                if (first) {
-                    // the prefetched half window retires with this batch (issued before it): tell the
-                    // compiler here, before any store, so no later wait covers this chunk's stores
-                    asm volatile("" ::"v"(kn), "v"(rn));
-                }
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    if (e + u < ge) {
-                        const int cl = meta[e + u].cell;
-                        if (cl != cur) {
-                            if (cur >= 0) finish(false, col);
-#pragma unroll
-                            for (int i = 0; i < RS::EPL; ++i) acc[i] = 0.f;
-                            cur = cl;
-                        }
-                        float x[RS::EPL];
-                        unpack16(v[u], (const RT*)nullptr, x);
-                        const float wu = FUSED ? group_weight<RS::LPR>(wd, u, lane) : 1.f;
-#pragma unroll
-                        for (int i = 0; i < RS::EPL; ++i) acc[i] = FUSED ? fmaf(wu, x[i], acc[i]) : __fadd_rn(acc[i], x[i]);
-                    }
-                }
-            };
-            batch(gs, true);  // every lane group, unconditionally (clamped)
-            for (int e = gs + kUnroll; e < ge; e += kUnroll) batch(e, false);
-            const int tcol = (fresh_lane() % RS::LPR) * RS::EPL;
-            if (cur >= 0) finish(true, tcol);
-            __builtin_amdgcn_wave_barrier();
-            if (tail_split && !(head_split && cur == first_cell)) {
-                for (int q = grp + 1; q < RS::NG; ++q) {
-                    const int qs = gbeg(q);
-                    if (qs == gbeg(q + 1)) continue;
-                    if (meta[qs].cell != cur) break;
-#pragma unroll
-                    for (int i = 0; i < RS::EPL; ++i) acc[i] = __fadd_rn(acc[i], part[q * kC + tcol + i]);
-                }
-                store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + tcol, acc);
-            }
-        } else {
-            asm volatile("" ::"v"(kn), "v"(rn));
-        }
-        if (big >= 0) {
-            int cell;
-            const float a2 = reduce_big_cell<FUSED, RT>(base + big, nprime, sorted_key, sorted_row, depth, rows_base,
-                                                        lane, &cell, g.nrows);
-            cell_row(out, dchk(cell, g.ncells, kDbgSplatCell), g)[lane] = from_f32<OutT>(a2);
-        }
-        // slide: this window's second half is the next one's first (read back from LDS: no registers
-        // held across the chunk), the prefetched half its second
-        __builtin_amdgcn_wave_barrier();
-        const EntryMeta mb = meta[kWave + lane];
-        __builtin_amdgcn_wave_barrier();  // (every lane has read its slot before the next window is staged)
-        ka = ((long long)mb.cell << 32) | (unsigned)mb.p;
-        ra = mb.row;
-        kb = kn;
-        rb = rn;
-        prevcell = nextprev;
-        if (base + kWave >= nprime) break;
-    }
-}
 
 template <bool FUSED, typename RT, typename OutT>
 __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(const float* __restrict__ depth,
@@ -1845,20 +1700,6 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
     const bool zero_role = LSS_SPLAT_ZFIRST ? gi < nzg : gi >= ncg;
     if (!zero_role) {
         if (LSS_SPLAT_ROLES == 2) return;
-        if (kChunksPerWave > 1) {
-            // XCD x: chunks [x cpx, (x + 1) cpx), kChunksPerWave consecutive ones per wave
-            const int nchunks = (nprime + kWave - 1) / kWave;
-            const int cpx = (nchunks + 7) >> 3;
-            const int j = cgi * kSplatWaves + wave;
-            const int w0 = x * cpx + j * kChunksPerWave;
-            const int wend = min(min(w0 + kChunksPerWave, (x + 1) * cpx), nchunks);
-            if (w0 >= wend) return;
-            LSS_STAMP(w0, 0);
-            splat_chunks_pl<FUSED, RT, OutT>(w0, wend, nprime, depth, rows_base, sorted_key, sorted_row, g, out,
-                                             s_meta[wave], s_part[wave], lane);
-            LSS_STAMP(w0, 3);
-            return;
-        }
         const int cb = x * ncg + cgi;
         if (cb >= nchunk_blocks) return;
         const int w = cb * kSplatWaves + wave;
@@ -2886,11 +2727,7 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         g.ncells = dims->B * sg.Z * sg.X * sg.Y;
         g.nrows = sg.nrows;
         const int nchunks = grid_blocks(nprime, kWave);
-        // persistent chunk waves (kChunksPerWave > 1): per XCD ceil(chunks / 8 / K) waves, in blocks
-        // of kSplatWaves, as 8 x (blocks per XCD) blocks
-        const int nchunk_blocks = kChunksPerWave > 1
-                                      ? 8 * grid_blocks(grid_blocks(grid_blocks(nchunks, 8), kChunksPerWave), kSplatWaves)
-                                      : grid_blocks(nchunks, kSplatWaves);
+        const int nchunk_blocks = grid_blocks(nchunks, kSplatWaves);
         const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), kSplatWaves);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);
         // zero groups per XCD resident at the start beside all the chunk waves (c3: 55; c5: none)

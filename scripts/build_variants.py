@@ -1,6 +1,6 @@
 """Build tuning variants of the product library in parallel (lss-carla_amd/variants/<name>.so).
 
-  python scripts/build_variants.py k3o5=LSS_SPLAT_K=3,LSS_SPLAT_OCC=5 zf=LSS_SPLAT_ZFIRST=1
+  python scripts/build_variants.py o6=LSS_SPLAT_OCC=6 zf=LSS_SPLAT_ZFIRST=1
 
 Each argument is name=define[,define...]; the variants carry every source of the product library,
 built with build.command plus the -D knobs (experiment switches of csrc/*.hip).

@@ -1,4 +1,5 @@
 # Round 5: persistent pipelined chunk waves -- splat-only A/B (bit-equal + cache states), then in-step.
+# (the LSS_SPLAT_K switch this script measured was removed after it; results in profiles/r05)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/r5a; mkdir -p $OUT
