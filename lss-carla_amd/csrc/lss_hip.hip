@@ -1391,17 +1391,12 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
 #ifndef LSS_SPLAT_ROLES
 #define LSS_SPLAT_ROLES 0  // experiments only: 1 runs the chunk waves alone, 2 the zero fill alone
 #endif
-// The zero waves dispatched beside the chunk waves (the wave slots the chunk waves leave at the
-// start) hold back for s_sleep(kZeroHoldBack) = 2,048 cycles (~0.85 us) before their stores, so the
-// chunk waves' two round trips meet a quieter memory system; zero waves dispatched later, as slots
-// free up, start at once. In the c3 graph replays 12.46 / 12.33 -> 11.61 us on one box and
-// 13.00 / 13.00 -> 12.86 / 12.73 on another (s_sleep 24: 12.84, 40: 12.53, 64: no gain; round 4).
-constexpr int kZeroHoldBack = 32;
-#ifndef LSS_SPLAT_HOLD
-#define LSS_SPLAT_HOLD 1
-#endif
-// (holding back after the cell_start loads instead, or pacing the held-back waves' stores, measured
-// no better: 11.8-12.6 vs 11.9-12.3 us in one box's replays, profiles/r04/prof_ab_zero_holdback_variants.txt)
+// (Round 4 held the zero waves dispatched beside the chunk waves back for an s_sleep of 2,048 cycles,
+// sized per launch from the wave slots, so the chunk waves' round trips met a quieter memory system:
+// 12.4 -> 11.6 us in-step then. Once the chunk waves retire their gathers before their row stores
+// (LSS_SPLAT_WAITALL) the hold-back cost time instead -- 11.74 / 11.59 without vs 12.53 / 11.86 us
+// with it in-step, 12.7 vs 13.3 us kernel-stamped (profiles/r05/prof_ab_splat_holdback.txt) -- and
+// was removed.)
 #ifndef LSS_SPLAT_SKIP
 #define LSS_SPLAT_SKIP 0  // experiments only (wrong sums): 1 rows from 8 L1-resident rows, 2 one depth line, 4 no row stores
 #endif
@@ -1685,7 +1680,7 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
                                                            const long long* __restrict__ sorted_key,
                                                            const int32_t* __restrict__ sorted_row, BevGeo g,
                                                            int nprime, int nchunk_blocks, int nzero_blocks,
-                                                           int zhold, OutT* __restrict__ out) {
+                                                           OutT* __restrict__ out) {
     __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
     __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][RowSlice<RT>::NG * kC];
     const int lane = threadIdx.x & 63;
@@ -1718,7 +1713,6 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
         if (LSS_SPLAT_ROLES == 1) return;
         const int zb = x * nzg + zgi;
         if (zb >= nzero_blocks) return;
-        if (zgi < zhold) __builtin_amdgcn_s_sleep(kZeroHoldBack);  // resident beside the chunk waves
         const int u = (zb * kSplatWaves + wave) * kZeroUnits;
         [[maybe_unused]] const int zslot = nchunk_blocks * kSplatWaves + zb * kSplatWaves + wave;
         LSS_STAMP(zslot, 0);
@@ -2730,21 +2724,16 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         const int nchunk_blocks = grid_blocks(nchunks, kSplatWaves);
         const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), kSplatWaves);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);
-        // zero groups per XCD resident at the start beside all the chunk waves (c3: 55; c5: none)
-        const long slots = (long)device_cus() * 4 * kSplatMinWaves;
-        const int zhold = (LSS_SPLAT_HOLD && !LSS_SPLAT_ZFIRST)
-                              ? (int)std::max<long>(0, (slots - (long)nchunk_blocks * kSplatWaves) / (8L * kSplatWaves))
-                              : 0;
 // kernel-stamped events only when asked for: a plain launch is what a hipGraph capture records
 #define LSS_NHWC_FWD(F, RT, T)                                                                                     \
     do {                                                                                                           \
         if (e0 || e1)                                                                                              \
             hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, (const RT*)rows,   \
                                   cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks,      \
-                                  zhold, (T*)out);                                                                 \
+                                  (T*)out);                                                                        \
         else                                                                                                       \
             hipLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, depth, (const RT*)rows, cell_start,     \
-                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, zhold, (T*)out);    \
+                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, (T*)out);           \
     } while (0)
         if (out_dtype == LSS_F32) {
             if (!fused) LSS_NHWC_FWD(false, float, float);
