@@ -63,6 +63,17 @@ int lss_head1_bwd(const void* x, const void* dy, const float* w, int32_t P, int3
 int lss_scale_add(const void* x, const void* u, float keep, const void* res, int64_t N, int64_t per, void* y,
                   void* stream);
 
+/* Dropout (CamEncode.dropout = nn.Dropout(0.2), src/models.py:44, 53), training mode: y = x / keep where
+ * a counter-based draw keeps the element (probability keep), else 0; n elements of dtype (fp32 or bf16)
+ * in memory order (any memory format), n * sizeof(dtype) % 16 == 0, 16-B aligned. The mask is a pure
+ * function of (*seed, element index) -- Philox4x32-10, key = the 64-bit seed (device memory, so a
+ * captured graph draws a new one per replay), counter = (16-B vector index, block) -- so the backward is
+ * the same call on dy with the same seed. Blocks write the tensor in 8 XCD-contiguous eighths (the
+ * fused lift's layout) and, when `prefetch` is non-NULL, also read its `prefetch_bytes` (the lift's
+ * packed depthnet weights) into every XCD's L2. */
+int lss_dropout(const void* x, int32_t dtype, int64_t n, const uint64_t* seed, float keep, void* y,
+                const void* prefetch, int64_t prefetch_bytes, void* stream);
+
 /* Training-mode batch norm fused with an activation (and, for ReLU, a residual add), for
  * nn.BatchNorm2d followed by swish (EfficientNet-B0, src/models.py:68 and the MBConv blocks) or
  * ReLU (CamEncode.up1, BevEncode, src/models.py:15-34, 92-130):

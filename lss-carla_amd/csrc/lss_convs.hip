@@ -442,6 +442,90 @@ __global__ __launch_bounds__(kBlock) void k_scale_add(const uint4* __restrict__ 
     y[i] = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
 }
 
+
+// ---- dropout (CamEncode.dropout, src/models.py:44, 53) on a counter-based RNG, laid out for the next kernel
+// Philox4x32-10 (Salmon et al., SC'11): 10 rounds of the two multiplies and key bumps; a pure function of
+// (key, counter), so the backward regenerates the forward's mask from the same seed.
+__device__ __forceinline__ uint4 philox4x32(uint2 key, uint4 c) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const unsigned lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+        const unsigned lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        c = make_uint4(hi1 ^ c.y ^ key.x, lo1, hi0 ^ c.w ^ key.y, lo0);
+        key.x += 0x9E3779B9u;
+        key.y += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// Elements of 16-B vector v (8 bf16 or 4 fp32) kept: bit j = element j; uniform u = top 24 bits / 2^24,
+// kept when u < keep (P = keep). Counter (v, 0, 0, 0): 4 draws, a second block (v, 0, 1, 0) for bf16.
+template <int EPV>
+__device__ __forceinline__ unsigned keep_bits(uint2 key, long long v, unsigned thresh) {
+    unsigned bits = 0;
+#pragma unroll
+    for (int h = 0; h < EPV / 4; ++h) {
+        const uint4 r = philox4x32(key, make_uint4((unsigned)v, (unsigned)(v >> 32), (unsigned)h, 0u));
+        bits |= ((r.x >> 8) < thresh ? 1u : 0u) << (4 * h);
+        bits |= ((r.y >> 8) < thresh ? 1u : 0u) << (4 * h + 1);
+        bits |= ((r.z >> 8) < thresh ? 1u : 0u) << (4 * h + 2);
+        bits |= ((r.w >> 8) < thresh ? 1u : 0u) << (4 * h + 3);
+    }
+    return bits;
+}
+
+constexpr int kDropVpt = 2;  // 16-B vectors per thread
+// XCD x (blockIdx & 7) writes one contiguous eighth of the tensor, the eighth the fused lift's blocks on
+// that XCD read (k_depthnet_lift3: pixel tiles in XCD-contiguous runs), so the lift finds its features
+// in its own L2 instead of another XCD's; the blocks also touch `pf` (the lift's packed weights), one
+// slice per block of each XCD, so every XCD's L2 holds them before the lift starts.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_dropout(const uint4* __restrict__ x, long long nv,
+                                                    const unsigned long long* __restrict__ seed, unsigned thresh,
+                                                    float scale, uint4* __restrict__ y, const uint4* __restrict__ pf,
+                                                    long long pf16) {
+    constexpr int EPV = 16 / (int)sizeof(T);
+    const int bpx = gridDim.x >> 3;                                         // blocks per XCD
+    const long long lb = (long long)(blockIdx.x & 7) * bpx + (blockIdx.x >> 3);  // XCD-contiguous
+    uint4 warm = make_uint4(0u, 0u, 0u, 0u);
+    if (pf) {
+        const long long per = (pf16 + bpx - 1) / bpx;  // 16-B pieces per block
+        const long long i = (long long)(blockIdx.x >> 3) * per + threadIdx.x;
+        if (threadIdx.x < per && i < pf16) warm = pf[i];
+    }
+    const unsigned long long sd = *seed;
+    const uint2 key = make_uint2((unsigned)sd, (unsigned)(sd >> 32));
+    uint4 in[kDropVpt];
+    long long vi[kDropVpt];
+#pragma unroll
+    for (int k = 0; k < kDropVpt; ++k) {
+        vi[k] = (lb * kDropVpt + k) * kBlock + threadIdx.x;
+        in[k] = vi[k] < nv ? x[vi[k]] : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < kDropVpt; ++k) {
+        if (vi[k] >= nv) continue;
+        const unsigned bits = keep_bits<EPV>(key, vi[k], thresh);
+        uint4 o;
+        if constexpr (EPV == 8) {
+            float v[8];
+            unpack8(in[k], v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = ((bits >> j) & 1u) ? v[j] * scale : 0.f;
+            o = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+        } else {
+            const float v[4] = {__uint_as_float(in[k].x), __uint_as_float(in[k].y), __uint_as_float(in[k].z),
+                                __uint_as_float(in[k].w)};
+            o = make_uint4(__float_as_uint((bits & 1u) ? v[0] * scale : 0.f),
+                           __float_as_uint((bits & 2u) ? v[1] * scale : 0.f),
+                           __float_as_uint((bits & 4u) ? v[2] * scale : 0.f),
+                           __float_as_uint((bits & 8u) ? v[3] * scale : 0.f));
+        }
+        y[vi[k]] = o;
+    }
+    asm volatile("" : : "v"(warm.x), "v"(warm.y), "v"(warm.z), "v"(warm.w));  // (the prefetch must land)
+}
+
 }  // namespace
 
 extern "C" {
@@ -524,6 +608,33 @@ int lss_scale_add(const void* x, const void* u, float keep, const void* res, int
     if (nb > INT_MAX) return LSS_CONV_EINVAL;
     hipLaunchKernelGGL(k_scale_add, dim3((unsigned)nb), dim3(kBlock), 0, (hipStream_t)stream, (const uint4*)x, (const bf16*)u,
                        keep, (const uint4*)res, (long long)(per / 8), n8, (uint4*)y);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+
+int lss_dropout(const void* x, int32_t dtype, int64_t n, const uint64_t* seed, float keep, void* y, const void* prefetch,
+                int64_t prefetch_bytes, void* stream) {
+    const int esz = dtype == LSS_CONV_BF16 ? 2 : dtype == LSS_CONV_F32 ? 4 : 0;
+    if (!x || !y || !seed || !esz || n <= 0 || (n * esz) % 16 != 0 || !(keep > 0.f && keep <= 1.f) ||
+        prefetch_bytes < 0 || (prefetch && prefetch_bytes % 16 != 0) ||
+        ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(prefetch)) & 15))
+        return LSS_CONV_EINVAL;
+    const long long nv = n * esz / 16;
+    const long long nb = (nv + (long long)kBlock * kDropVpt - 1) / ((long long)kBlock * kDropVpt);
+    const long long grid = 8 * ((nb + 7) / 8);  // logical blocks past nb write nothing
+    if (grid > INT_MAX) return LSS_CONV_EINVAL;
+    // keep when (24 random bits) < keep * 2^24; the kept elements are scaled by 1 / keep (torch's dropout)
+    const unsigned thresh = (unsigned)fminf(keep * 16777216.0f, 16777216.0f);
+    const float scale = 1.0f / keep;
+    hipStream_t s = (hipStream_t)stream;
+    const uint4* pf = prefetch_bytes > 0 ? (const uint4*)prefetch : nullptr;
+    if (esz == 2)
+        hipLaunchKernelGGL(k_dropout<bf16>, dim3((unsigned)grid), dim3(kBlock), 0, s, (const uint4*)x, nv,
+                           (const unsigned long long*)seed, thresh, scale, (uint4*)y, pf, prefetch_bytes / 16);
+    else
+        hipLaunchKernelGGL(k_dropout<float>, dim3((unsigned)grid), dim3(kBlock), 0, s, (const uint4*)x, nv,
+                           (const unsigned long long*)seed, thresh, scale, (uint4*)y, pf, prefetch_bytes / 16);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }

@@ -90,6 +90,62 @@ def _note_trunk_weights(path: str) -> None:
               "($LSS_EFFICIENTNET_B0_WEIGHTS)", file=sys.stderr, flush=True)
 
 
+class _HipDropout(torch.autograd.Function):
+    """Training-mode dropout on ``lss_dropout`` (include/lss_convs.h): the mask is a function of a 64-bit
+    seed drawn from torch's CUDA generator (graph-capturable) and the element index, so the backward
+    regenerates it instead of saving it."""
+
+    @staticmethod
+    def forward(ctx, x, p, prefetch):
+        lib = _lib.load()
+        seed = torch.randint(0, 2 ** 62, (1,), device=x.device, dtype=torch.int64)
+        y = torch.empty_like(x)
+        keep = 1.0 - p
+        pf_bytes = prefetch.numel() * prefetch.element_size() if prefetch is not None else 0
+        _lib.check(lib.lss_dropout(_lib.ptr(x), _lib.dtype_code(x.dtype), x.numel(), _lib.ptr(seed), keep, _lib.ptr(y),
+                                   _lib.ptr(prefetch) if pf_bytes else None, pf_bytes, _lib.stream_handle(x.device)),
+                   "lss_dropout")
+        ctx.save_for_backward(seed)
+        ctx.keep = keep
+        # the mask follows the elements' memory order: the gradient is read in the input's format
+        ctx.fmt = torch.contiguous_format if x.is_contiguous() else torch.channels_last
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib.load()
+        (seed,) = ctx.saved_tensors
+        fmt = ctx.fmt
+        dy = dy.contiguous(memory_format=fmt)
+        if dy.data_ptr() % 16:
+            dy = dy.clone(memory_format=fmt)
+        dx = torch.empty_like(dy)
+        _lib.check(lib.lss_dropout(_lib.ptr(dy), _lib.dtype_code(dy.dtype), dy.numel(), _lib.ptr(seed), ctx.keep,
+                                   _lib.ptr(dx), None, 0, _lib.stream_handle(dy.device)), "lss_dropout")
+        return dx, None, None
+
+
+USE_HIP_DROPOUT = True
+
+
+class LssDropout(nn.Dropout):
+    """``nn.Dropout`` (same attributes, no state) whose training-mode CUDA forward is ``lss_dropout``:
+    the same Bernoulli(1 - p) mask distribution and 1 / (1 - p) scaling as torch's (not the same draws),
+    written in the XCD-contiguous eighths the fused lift reads, and warming the lift's packed weights
+    (``prefetch``, set by ``LiftSplatShoot.get_voxels``) into every XCD's L2."""
+
+    prefetch = None
+
+    def forward(self, x):
+        if (USE_HIP_DROPOUT and self.training and 0.0 < self.p < 1.0 and x.is_cuda
+                and x.dtype in (torch.float32, torch.bfloat16) and x.data_ptr() % 16 == 0
+                and (x.numel() * x.element_size()) % 16 == 0
+                and (x.is_contiguous() or (x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)))):
+            pf = self.prefetch if self.prefetch is not None and self.prefetch.device == x.device else None
+            return _HipDropout.apply(x, self.p, pf)
+        return super().forward(x)
+
+
 class CamEncode(nn.Module):
     """Image -> depthnet output (src/models.py:37-89)."""
 
@@ -104,7 +160,7 @@ class CamEncode(nn.Module):
             _note_trunk_weights(wpath)
         self.trunk = EfficientNetB0.from_pretrained("efficientnet-b0", wpath) if wpath else EfficientNetB0()
         self.up1 = Up(320 + 112, 512)
-        self.dropout = nn.Dropout(0.2)
+        self.dropout = LssDropout(0.2)
         self.depthnet = nn.Conv2d(512, self.D + self.C, kernel_size=1, padding=0)
 
     def get_eff_depth(self, x):
@@ -386,24 +442,34 @@ class LiftSplatShoot(nn.Module):
         """Fused hot path: trunk, geometry/CSR, lift+splat (src/models.py:248-254).
 
         Schedule: the camera inverses first (the host's torch.inverse copies the rig to the host,
-        which must not wait behind the trunk), then the trunk, then the plan kernels, then the fused
-        lift and the splat.
+        which must not wait behind the trunk), then the plan kernels, then the trunk (its last kernel,
+        the dropout, writes the features where the fused lift's blocks read them), then the fused lift
+        and the splat.
         """
         B, N, C, imH, imW = x.shape
         inv = self.static_inverses
         if inv is None:
             inv = ops.camera_inverses(post_rots, intrins)
         ce = self.camencode
-        feat = ce.dropout(ce.get_eff_depth(x.view(B * N, C, imH, imW)))
+        # the plan first: it needs only the rig, and the lift then follows the trunk's last kernel (the
+        # dropout) with nothing between them to push its features out of the L2s that hold them
         plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
                                      inverses=inv)
         out_dtype = self._bev_dtype(x.device)
-        if self.fuse_depthnet and out_dtype == torch.bfloat16 and self.D + self.camC <= 128:
-            # depthnet 1x1 conv + softmax + context layout in one MFMA kernel (SURVEY.md §8f row 1); its
-            # tile holds D + C <= 128 output channels (a larger dbound runs the conv as its own op)
+        fused = self.fuse_depthnet and out_dtype == torch.bfloat16 and self.D + self.camC <= 128
+        packed = None
+        if fused:
             w = ce.depthnet.weight
             pk = getattr(ce.depthnet, "lss_packed_weight", None)  # (buffer, the bf16 view's address)
             packed = pk[0] if pk is not None and w.dtype == torch.bfloat16 and w.data_ptr() == pk[1] else None
+        ce.dropout.prefetch = packed
+        try:
+            feat = ce.dropout(ce.get_eff_depth(x.view(B * N, C, imH, imW)))
+        finally:
+            ce.dropout.prefetch = None
+        if fused:
+            # depthnet 1x1 conv + softmax + context layout in one MFMA kernel (SURVEY.md §8f row 1); its
+            # tile holds D + C <= 128 output channels (a larger dbound runs the conv as its own op)
             return ops.depthnet_lift_splat(feat, w, ce.depthnet.bias, plan, out_dtype, self._layout(), packed)
         return ops.lift_splat(ce.depthnet(feat), plan, out_dtype, self._layout())
 

@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--libs", default="product")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--kernel", default="bwd", choices=["bwd", "lift"])
+    ap.add_argument("--producer", default="none", choices=["none", "dropout", "torch"],
+                    help="lift: after the read sweep, rewrite the features with lss_dropout (keep 1: an XCD-"
+                         "contiguous copy, + the packed weights warmed) or torch's copy, as a step's last kernel")
     args = ap.parse_args()
     import torch
     from lss_carla_amd import _lib, ops, synthetic as syn
@@ -69,11 +72,23 @@ def main():
     def output():
         return d_dn if args.kernel == "bwd" else torch.cat([depth.flatten(), ctx.float().flatten()])
 
+    feat_src = feat.clone(memory_format=torch.channels_last) if args.kernel == "lift" else None
+    seed = torch.zeros(1, device=dev, dtype=torch.int64)
+
+    def produce():
+        if args.producer == "dropout":
+            _lib.check(lib.lss_dropout(_lib.ptr(feat_src), _lib.BF16, feat.numel(), _lib.ptr(seed), 1.0, _lib.ptr(feat),
+                                       _lib.ptr(packed), packed.numel() * 2, st), "dropout")
+        elif args.producer == "torch":
+            feat.copy_(feat_src)
+
     def timed(l, mode):
         ts = []
         for i in range(args.iters + 3):
             if mode == "read":
                 _lib.check(lib.lss_ceiling_read(_lib.ptr(flush), flush.numel(), _lib.ptr(sink), st), "read")
+            if args.kernel == "lift":
+                produce()
             a, b = ct.c_void_p(), ct.c_void_p()
             lib.lss_event_create(ct.byref(a))
             lib.lss_event_create(ct.byref(b))
@@ -93,7 +108,7 @@ def main():
     run(lib)
     torch.cuda.synchronize()
     want = output().clone()
-    res = {"config": args.config, "kernel": args.kernel, "pixels": B * N * H * W, "D": D}
+    res = {"config": args.config, "kernel": args.kernel, "producer": args.producer, "pixels": B * N * H * W, "D": D}
     for name in args.libs.split(","):
         l = lib if name == "product" else _lib.open_library(
             os.path.join(REPO, "lss-carla_amd", "variants", name + ".so"))
