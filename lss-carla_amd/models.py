@@ -126,6 +126,8 @@ class _HipDropout(torch.autograd.Function):
 
 
 USE_HIP_DROPOUT = True
+# the plan kernels in front of the trunk (True) or between the trunk and the lift (False)
+PLAN_BEFORE_TRUNK = False
 
 
 class LssDropout(nn.Dropout):
@@ -442,8 +444,8 @@ class LiftSplatShoot(nn.Module):
         """Fused hot path: trunk, geometry/CSR, lift+splat (src/models.py:248-254).
 
         Schedule: the camera inverses first (the host's torch.inverse copies the rig to the host,
-        which must not wait behind the trunk), then the plan kernels, then the trunk (its last kernel,
-        the dropout, writes the features where the fused lift's blocks read them), then the fused lift
+        which must not wait behind the trunk), then the trunk (its last kernel, the dropout, writes the
+        features where the fused lift's blocks read them), then the plan kernels, then the fused lift
         and the splat.
         """
         B, N, C, imH, imW = x.shape
@@ -451,10 +453,10 @@ class LiftSplatShoot(nn.Module):
         if inv is None:
             inv = ops.camera_inverses(post_rots, intrins)
         ce = self.camencode
-        # the plan first: it needs only the rig, and the lift then follows the trunk's last kernel (the
-        # dropout) with nothing between them to push its features out of the L2s that hold them
-        plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
-                                     inverses=inv)
+        plan = None
+        if PLAN_BEFORE_TRUNK:
+            plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
+                                         inverses=inv)
         out_dtype = self._bev_dtype(x.device)
         fused = self.fuse_depthnet and out_dtype == torch.bfloat16 and self.D + self.camC <= 128
         packed = None
@@ -467,6 +469,11 @@ class LiftSplatShoot(nn.Module):
             feat = ce.dropout(ce.get_eff_depth(x.view(B * N, C, imH, imW)))
         finally:
             ce.dropout.prefetch = None
+        if plan is None:
+            # the plan between the trunk and the lift: its CSR is still in the L2s when the splat reads it
+            # (the dropout's features for the lift, ~1 MB per XCD, stay there beside it)
+            plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
+                                         inverses=inv)
         if fused:
             # depthnet 1x1 conv + softmax + context layout in one MFMA kernel; its
             # tile holds D + C <= 128 output channels (a larger dbound runs the conv as its own op)
