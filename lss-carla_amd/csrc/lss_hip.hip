@@ -1487,9 +1487,6 @@ constexpr int kUnroll = 8;
 #ifndef LSS_SPLAT_WAITALL
 #define LSS_SPLAT_WAITALL 1
 #endif
-#ifndef LSS_SPLAT_HOLDROW
-#define LSS_SPLAT_HOLDROW 0  // experiment switch: hold one finished row across a group's second batch
-#endif
 
 // s_waitcnt vmcnt(0), expcnt and lgkmcnt left at their maxima (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] |
 // lgkmcnt[11:8] | vmcnt_hi[15:14])
@@ -1548,7 +1545,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                                             const long long* __restrict__ sorted_key,
                                             const int32_t* __restrict__ sorted_row, const BevGeo& g,
                                             OutT* __restrict__ out, EntryMeta* __restrict__ meta,
-                                            float* __restrict__ part, uint4* __restrict__ hold, int lane) {
+                                            float* __restrict__ part, int lane) {
     using RS = RowSlice<RT>;
     // round trip 1: keys (cell << 32 | point), context rows, the previous entry's cell
     const int base = w * kWave;
@@ -1599,29 +1596,10 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
             for (int i = 0; i < RS::EPL; i += 4)
                 *reinterpret_cast<float4*>(dst + c + i) = make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
         };
-        auto finish = [&](bool last, int c, bool more_loads) {  // the cell `cur` ends at this point of the group
+        auto finish = [&](bool last, int c) {  // the cell `cur` ends at this point of the group
             if (cur == first_cell && head_split) put(part + grp * kC, c);  // a later piece of a cut cell
-            else if (!(last && tail_split) && !(LSS_SPLAT_SKIP & 4)) {
-#if LSS_SPLAT_HOLDROW
-                // a bf16 row slice finished while the group still has a batch of gathers to issue is
-                // parked in LDS (hold, one 16-B slot per lane; its cell + 1 in the group's spare meta word)
-                // and stored after the last batch's wait: a store in front of the next batch's gathers
-                // would make their wait a wait for the store's write too (vmcnt counts stores)
-                if constexpr (sizeof(OutT) == 2 && RS::EPL == 8) {
-                    if (more_loads && meta[gs].pad == 0) {
-                        bf16 hv[8];
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) hv[i] = __float2bfloat16(acc[i]);
-                        uint4 hu;
-                        __builtin_memcpy(&hu, hv, 16);
-                        hold[lane] = hu;
-                        meta[gs].pad = cur + 1;
-                        return;
-                    }
-                }
-#endif
+            else if (!(last && tail_split) && !(LSS_SPLAT_SKIP & 4))
                 store_slice<RS::EPL>(cell_row(out, dchk(cur, g.ncells, kDbgSplatCell), g) + c, acc);
-            }
             // else: the first piece of a cut cell stays in acc (combined after the barrier)
         };
         // round trip 2 (one per kUnroll entries of a group): row slices and depth weights in flight together
@@ -1652,7 +1630,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
                 if (e + u < ge) {
                     const int cl = meta[e + u].cell;
                     if (cl != cur) {
-                        if (cur >= 0) finish(false, col, e + kUnroll < ge);
+                        if (cur >= 0) finish(false, col);
 #pragma unroll
                         for (int i = 0; i < RS::EPL; ++i) acc[i] = 0.f;
                         cur = cl;
@@ -1668,15 +1646,7 @@ __device__ __forceinline__ void splat_chunk(int w, int nprime, const float* __re
         // (the lane's column recomputed after the loop: kept live across it, it was the one VGPR over
         // the 72 of 7 waves per SIMD and went to scratch -- a reload round trip at every wave's end)
         const int tcol = (fresh_lane() % RS::LPR) * RS::EPL;
-        if (cur >= 0) finish(true, tcol, false);
-#if LSS_SPLAT_HOLDROW
-        if constexpr (sizeof(OutT) == 2 && RS::EPL == 8) {
-            const int hc = gs < ge ? meta[gs].pad : 0;  // (an empty group's gs is another group's entry)
-            if (hc > 0)
-                *reinterpret_cast<uint4*>(cell_row(out, dchk(hc - 1, g.ncells, kDbgSplatCell), g) + tcol) =
-                    hold[fresh_lane()];
-        }
-#endif
+        if (cur >= 0) finish(true, tcol);
         __builtin_amdgcn_wave_barrier();
         // the cell cut at this group's end, if it starts in this group: its first piece (acc) plus
         // the later groups' pieces in group order (empty groups skipped; the cell ends where a
@@ -1714,9 +1684,6 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
                                                            OutT* __restrict__ out) {
     __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
     __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][RowSlice<RT>::NG * kC];
-#if LSS_SPLAT_HOLDROW
-    __shared__ uint4 s_hold[kSplatWaves][kWave];
-#endif
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     // Blocks come in groups of 8, one per XCD (blocks are dealt round-robin over the 8 XCDs): the
@@ -1737,13 +1704,7 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
         if (w * kWave >= nprime) return;
         LSS_STAMP(w, 0);
         splat_chunk<FUSED, RT, OutT>(w, nprime, depth, rows_base, sorted_key, sorted_row, g, out, s_meta[wave],
-                                     s_part[wave],
-#if LSS_SPLAT_HOLDROW
-                                     s_hold[wave],
-#else
-                                     nullptr,
-#endif
-                                     lane);
+                                     s_part[wave], lane);
         LSS_STAMP(w, 3);
 #if LSS_TRACE
         if (lane == 0 && w < 16384) g_lss_trace[w][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |

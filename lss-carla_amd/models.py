@@ -126,8 +126,9 @@ class _HipDropout(torch.autograd.Function):
 
 
 USE_HIP_DROPOUT = True
-# the plan kernels in front of the trunk (True) or between the trunk and the lift (False)
-PLAN_BEFORE_TRUNK = False
+# where the plan kernels run: "trunk" (in front of the trunk), "dropout" (between the trunk's last conv
+# and the dropout), "lift" (between the dropout and the fused lift)
+PLAN_AT = "dropout"
 
 
 class LssDropout(nn.Dropout):
@@ -444,9 +445,9 @@ class LiftSplatShoot(nn.Module):
         """Fused hot path: trunk, geometry/CSR, lift+splat (src/models.py:248-254).
 
         Schedule: the camera inverses first (the host's torch.inverse copies the rig to the host,
-        which must not wait behind the trunk), then the trunk (its last kernel, the dropout, writes the
-        features where the fused lift's blocks read them), then the plan kernels, then the fused lift
-        and the splat.
+        which must not wait behind the trunk), then the trunk, the plan kernels, the dropout (it writes
+        the features where the fused lift's blocks read them, right before the lift), then the fused
+        lift and the splat (the plan's CSR still in the L2s).
         """
         B, N, C, imH, imW = x.shape
         inv = self.static_inverses
@@ -454,9 +455,13 @@ class LiftSplatShoot(nn.Module):
             inv = ops.camera_inverses(post_rots, intrins)
         ce = self.camencode
         plan = None
-        if PLAN_BEFORE_TRUNK:
-            plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
+
+        def make_plan():
+            return ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
                                          inverses=inv)
+
+        if PLAN_AT == "trunk":
+            plan = make_plan()
         out_dtype = self._bev_dtype(x.device)
         fused = self.fuse_depthnet and out_dtype == torch.bfloat16 and self.D + self.camC <= 128
         packed = None
@@ -466,14 +471,14 @@ class LiftSplatShoot(nn.Module):
             packed = pk[0] if pk is not None and w.dtype == torch.bfloat16 and w.data_ptr() == pk[1] else None
         ce.dropout.prefetch = packed
         try:
-            feat = ce.dropout(ce.get_eff_depth(x.view(B * N, C, imH, imW)))
+            feat = ce.get_eff_depth(x.view(B * N, C, imH, imW))
+            if PLAN_AT == "dropout":
+                plan = make_plan()
+            feat = ce.dropout(feat)
         finally:
             ce.dropout.prefetch = None
         if plan is None:
-            # the plan between the trunk and the lift: its CSR is still in the L2s when the splat reads it
-            # (the dropout's features for the lift, ~1 MB per XCD, stay there beside it)
-            plan = ops.plan_from_cameras(self.frustum, rots, trans, intrins, post_rots, post_trans, self._grid,
-                                         inverses=inv)
+            plan = make_plan()
         if fused:
             # depthnet 1x1 conv + softmax + context layout in one MFMA kernel; its
             # tile holds D + C <= 128 output channels (a larger dbound runs the conv as its own op)

@@ -6,9 +6,9 @@ OUT=gpurun_out/r5l; mkdir -p $OUT
 timeout -k 10 300 python3 -u scripts/splat_ab.py --config c5 --libs product,wa0,dppw0 --modes step --ceiling 0 > $OUT/splat_ab_c5.log 2>&1 || { tail -30 $OUT/splat_ab_c5.log; exit 1; }
 grep -v '^{' $OUT/splat_ab_c5.log | cut -c1-200
 for cfg in c3 c5; do
-  for v in "0 1" "1 1" "0 0"; do
+  for v in "lift 1" "trunk 1" "lift 0"; do
     set -- $v
-    echo "## $cfg plan-first=$1 hip-dropout=$2"
-    BENCH_ARGS="--config $cfg --plan-first $1 --hip-dropout $2" bash scripts/gpu_prof_ab.sh product 2>&1 | tee -a $OUT/prof_ab_order.txt || exit 1
+    echo "## $cfg plan-at=$1 hip-dropout=$2"
+    BENCH_ARGS="--config $cfg --plan-at $1 --hip-dropout $2" bash scripts/gpu_prof_ab.sh product 2>&1 | tee -a $OUT/prof_ab_order.txt || exit 1
   done
 done
