@@ -74,6 +74,7 @@ def parse():
     ap.add_argument("--miopen-find", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
     ap.add_argument("--hip-bn", type=int, default=1, help="BatchNorm + activation on the lss_bn_* kernels")
     ap.add_argument("--fuse-depthnet", type=int, default=1, help="depthnet 1x1 conv inside the lift kernel (MFMA)")
+    ap.add_argument("--hip-pw", type=int, default=1, help="trunk 1x1 conv weight gradients on lss_pw_wrw (1) or MIOpen (0)")
     ap.add_argument("--plan-at", default="dropout", choices=("trunk", "dropout", "lift"),
                     help="plan kernels in front of the trunk, the dropout or the fused lift")
     ap.add_argument("--hip-dropout", type=int, default=1,
@@ -311,7 +312,7 @@ def measure_in_graph(args) -> dict | None:
            "--profile-steps", "0", "--pmc-traffic", "0", "--cpu-baseline", "0", "--in-graph-prof", "0",
            "--mode", args.mode]
     # the rest of this run's configuration, so the child measures the same step
-    for flag in ("miopen_find", "hip_bn", "fuse_depthnet", "hip_dropout", "plan_at", "trunk_channels_last", "param_groups",
+    for flag in ("miopen_find", "hip_bn", "fuse_depthnet", "hip_dropout", "hip_pw", "plan_at", "trunk_channels_last", "param_groups",
                  "flat_params", "overlap_all_reduce", "dw_impl"):
         cmd += ["--" + flag.replace("_", "-"), str(getattr(args, flag))]
     try:
@@ -465,6 +466,8 @@ def build_model(args, dev, gc, dac):
     norm.USE_HIP_BN = bool(args.hip_bn)
     models.USE_HIP_DROPOUT = bool(args.hip_dropout)
     models.PLAN_AT = args.plan_at
+    from lss_carla_amd import efficientnet
+    efficientnet.USE_HIP_PW_WRW = bool(args.hip_pw)
     from lss_carla_amd.efficientnet import set_depthwise_impl
     set_depthwise_impl(model.camencode.trunk, args.dw_impl)
     model.train() if args.mode == "train" else model.eval()

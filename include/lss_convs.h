@@ -52,6 +52,15 @@ int lss_head1_fwd(const void* x, const float* w, const float* bias, int32_t P, i
 int lss_head1_bwd(const void* x, const void* dy, const float* w, int32_t P, int32_t C, void* dx, float* partial,
                   void* stream);
 
+/* Weight gradient of a 1x1 convolution (no bias, stride 1) over NCHW contiguous bf16 activations:
+ * dw (Cout, Cin) = sum over n < N, q < HW of dy[n][co][q] * x[n][ci][q], fp32 accumulation, written as
+ * dw_dtype (LSS_CONV_BF16: rounded once; LSS_CONV_F32). HW % 4 == 0, 8-B aligned x / dy. workspace:
+ * at least lss_pw_wrw_workspace_bytes(N, Cin, Cout, HW) bytes of device memory (per-split fp32
+ * partials, summed in split order: deterministic). Two launches on the stream. */
+int64_t lss_pw_wrw_workspace_bytes(int32_t N, int32_t Cin, int32_t Cout, int32_t HW);
+int lss_pw_wrw(const void* x, const void* dy, int32_t N, int32_t Cin, int32_t Cout, int32_t HW, void* dw,
+               int32_t dw_dtype, void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Per-sample scale (+ residual) over N samples of `per` contiguous bf16 elements each (any memory
  * format that is sample-major: NCHW or channels-last), per % 8 == 0, 16-B aligned pointers:
  * y = bf16(x * scale[n] + res) (res nullable: y = bf16(x * scale[n])), scale[n] = mask[n] / keep with

@@ -18,6 +18,7 @@
 
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
+#include <algorithm>
 #include <limits.h>
 #include <stdint.h>
 
@@ -39,6 +40,21 @@ __device__ __forceinline__ float ld(const float* p) { return *p; }
 __device__ __forceinline__ float ld(const bf16* p) { return __bfloat162float(*p); }
 __device__ __forceinline__ void st(float* p, float v) { *p = v; }
 __device__ __forceinline__ void st(bf16* p, float v) { *p = __float2bfloat16(v); }
+
+// 8 bf16 <-> fp32 (bf16 -> fp32 is exact; fp32 -> bf16 rounds to nearest even)
+__device__ __forceinline__ void unpack8(const uint4& u, float* o) {
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        o[2 * i] = __uint_as_float(w[i] << 16);
+        o[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+}
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+    const bf16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+    return (unsigned)*reinterpret_cast<const unsigned short*>(&x) |
+           ((unsigned)*reinterpret_cast<const unsigned short*>(&y) << 16);
+}
 
 struct DwGeo {
     int C, Hi, Wi, Ho, Wo, pt, pl, nplanes;  // input (Hi, Wi) -> output (Ho, Wo); nplanes = N * C
@@ -254,6 +270,285 @@ inline bool geo_ok(int N, int C, int Hi, int Wi, int K, int S, int Ho, int Wo) {
            (long)N * C * Hi * Wi < INT_MAX && (long)N * C * Ho * Wo < INT_MAX;
 }
 
+// ---- LDS-staged depthwise kernels (round 5). The kernels above read every input element about twice
+// with 2-byte loads whose lanes stride by the thread tile (4 or 8 bytes apart): the load count, not
+// the bytes, bounded them (10-20 % of HBM on the trunk's large planes). Here a block stages a band of
+// rows of PB planes into LDS (fp32, zero-padded so the taps need no bounds checks), with 16-B loads
+// when a row holds a multiple of 8 elements and coalesced 2-B / 4-B loads otherwise; each thread then
+// computes row segments of SEG consecutive outputs (SEG | Wo: one vector store per segment) from LDS.
+#ifndef LSS_DW_LDS
+#define LSS_DW_LDS 1  // experiment switch: 0 = the register-tiled kernels above
+#endif
+constexpr int kDwLdsFloats = 8192;  // staged input per block (32 KB)
+
+struct DwBand {
+    int BHo, PB, LW, LHmax, nbands;  // output rows per band, planes per block, LDS row width / rows
+};
+
+template <typename T>
+__device__ __forceinline__ void dw_stage(const T* __restrict__ xp, int Hi, int Wi, int ih0, int LH, int LW, int pl,
+                                         bool vec8, float* __restrict__ dst) {
+    // LDS rows r = input rows ih0 + r, columns c = input columns c - pl; zero outside the input
+    if (vec8) {  // Wi % 8 == 0: 8-element row chunks, 16-B (bf16) loads; the pad columns separately
+        const int cpr = Wi / 8;
+        for (int i = threadIdx.x; i < LH * cpr; i += kBlock) {
+            const int r = i / cpr, ch = i - r * cpr;
+            const int ih = ih0 + r;
+            float v[8];
+            if (ih >= 0 && ih < Hi) {
+                const T* src = xp + (size_t)ih * Wi + 8 * ch;
+                if constexpr (sizeof(T) == 2) {
+                    unpack8(*reinterpret_cast<const uint4*>(src), v);
+                } else {
+                    const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+                    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = 0.f;
+            }
+            float* d = dst + r * LW + pl + 8 * ch;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d[k] = v[k];
+        }
+        const int npad = LW - Wi;  // pl left + the rest right
+        for (int i = threadIdx.x; i < LH * npad; i += kBlock) {
+            const int r = i / npad, k = i - r * npad;
+            dst[r * LW + (k < pl ? k : Wi + k)] = 0.f;
+        }
+    } else {
+        for (int i = threadIdx.x; i < LH * LW; i += kBlock) {
+            const int r = i / LW, c = i - r * LW;
+            const int ih = ih0 + r, iw = c - pl;
+            dst[i] = (ih >= 0 && ih < Hi && iw >= 0 && iw < Wi) ? ld(xp + (size_t)ih * Wi + iw) : 0.f;
+        }
+    }
+}
+
+template <int SEG, typename T>
+__device__ __forceinline__ void store_seg(T* __restrict__ p, const float* v, int n) {
+    if (n == SEG) {
+        if constexpr (sizeof(T) == 2 && SEG == 8) {
+            *reinterpret_cast<uint4*>(p) = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+            return;
+        } else if constexpr (sizeof(T) == 2 && SEG == 4) {
+            *reinterpret_cast<uint2*>(p) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+            return;
+        } else if constexpr (sizeof(T) == 2 && SEG == 2) {
+            *reinterpret_cast<unsigned*>(p) = pack2(v[0], v[1]);
+            return;
+        } else if constexpr (sizeof(T) == 4 && SEG % 4 == 0) {
+#pragma unroll
+            for (int k = 0; k < SEG; k += 4) *reinterpret_cast<float4*>(p + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+            return;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < SEG; ++k)
+        if (k < n) st(p + k, v[k]);
+}
+
+template <int SEG, typename T>
+__device__ __forceinline__ void load_seg(const T* __restrict__ p, float* v, int n) {
+    if (n == SEG) {
+        if constexpr (sizeof(T) == 2 && SEG == 8) {
+            unpack8(*reinterpret_cast<const uint4*>(p), v);
+            return;
+        } else if constexpr (sizeof(T) == 4 && SEG % 4 == 0) {
+#pragma unroll
+            for (int k = 0; k < SEG; k += 4) {
+                const float4 a = *reinterpret_cast<const float4*>(p + k);
+                v[k] = a.x; v[k + 1] = a.y; v[k + 2] = a.z; v[k + 3] = a.w;
+            }
+            return;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < SEG; ++k) v[k] = k < n ? ld(p + k) : 0.f;
+}
+
+// y (forward or stride-1 backward-data with flip): block = (PB consecutive planes, band of BHo output rows)
+template <int K, int S, int SEG, typename T>
+__global__ __launch_bounds__(kBlock) void k_dw_fwd_lds(const T* __restrict__ x, const float* __restrict__ w, DwGeo g,
+                                                       int flip, DwBand bd, T* __restrict__ y) {
+    extern __shared__ float smem[];
+    float* s_w = smem;                    // [PB][K*K]
+    float* s_x = smem + bd.PB * K * K;    // [PB][LH][LW] (+ slack for the last segment's reads)
+    const int band = blockIdx.x % bd.nbands, pg = blockIdx.x / bd.nbands;
+    const int p0 = pg * bd.PB, np = min(bd.PB, g.nplanes - p0);
+    const int oh0 = band * bd.BHo, nrow = min(bd.BHo, g.Ho - oh0);
+    const int LH = (nrow - 1) * S + K;
+    for (int i = threadIdx.x; i < np * K * K; i += kBlock) {
+        const int pl = i / (K * K), t = i - pl * (K * K);
+        s_w[i] = w[(size_t)((p0 + pl) % g.C) * K * K + (flip ? K * K - 1 - t : t)];
+    }
+    const bool vec8 = g.Wi % 8 == 0;
+    for (int pl = 0; pl < np; ++pl)
+        dw_stage(x + (size_t)(p0 + pl) * g.Hi * g.Wi, g.Hi, g.Wi, oh0 * S - g.pt, LH, bd.LW, g.pl, vec8,
+                 s_x + pl * bd.LHmax * bd.LW);
+    __syncthreads();
+    const int nseg = (g.Wo + SEG - 1) / SEG;
+    const int items = np * nrow * nseg;
+    constexpr int CW = (SEG - 1) * S + K;
+    for (int it = threadIdx.x; it < items; it += kBlock) {
+        const int pl = it / (nrow * nseg), rem = it - pl * (nrow * nseg);
+        const int r = rem / nseg, sg = rem - r * nseg;
+        const int ow0 = sg * SEG;
+        const float* wk = s_w + pl * K * K;
+        const float* xs = s_x + pl * bd.LHmax * bd.LW + (r * S) * bd.LW + ow0 * S;
+        float acc[SEG];
+#pragma unroll
+        for (int j = 0; j < SEG; ++j) acc[j] = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh) {
+            float v[CW];
+#pragma unroll
+            for (int q = 0; q < CW; ++q) v[q] = xs[kh * bd.LW + q];
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) {
+                const float wv = wk[kh * K + kw];
+#pragma unroll
+                for (int j = 0; j < SEG; ++j) acc[j] = fmaf(v[j * S + kw], wv, acc[j]);
+            }
+        }
+        store_seg<SEG>(y + ((size_t)(p0 + pl) * g.Ho + oh0 + r) * g.Wo + ow0, acc, min(SEG, g.Wo - ow0));
+    }
+}
+
+// weight-gradient partials: block (channel c, image group q), PB images of the group staged at a time
+template <int K, int S, int SEG, typename T>
+__global__ __launch_bounds__(kBlock) void k_dw_wgt_lds(const T* __restrict__ x, const T* __restrict__ dy, DwGeo g,
+                                                       int nimg, int ngroups, DwBand bd, float* __restrict__ partial) {
+    extern __shared__ float smem[];
+    float* s_x = smem;  // [PB][LH][LW]
+    __shared__ float s_red[kBlock / kWave][K * K];
+    const int c = blockIdx.x % g.C, q = blockIdx.x / g.C;
+    const int n0 = (int)((long)nimg * q / ngroups), n1 = (int)((long)nimg * (q + 1) / ngroups);
+    const int nseg = (g.Wo + SEG - 1) / SEG;
+    constexpr int CW = (SEG - 1) * S + K;
+    const bool vec8 = g.Wi % 8 == 0;
+    float acc[K * K];
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
+    for (int nb = n0; nb < n1; nb += bd.PB) {
+        const int np = min(bd.PB, n1 - nb);
+        for (int band = 0; band < bd.nbands; ++band) {
+            const int oh0 = band * bd.BHo, nrow = min(bd.BHo, g.Ho - oh0);
+            const int LH = (nrow - 1) * S + K;
+            __syncthreads();  // the previous chunk's readers are done with s_x
+            for (int pl = 0; pl < np; ++pl)
+                dw_stage(x + ((size_t)(nb + pl) * g.C + c) * g.Hi * g.Wi, g.Hi, g.Wi, oh0 * S - g.pt, LH, bd.LW, g.pl,
+                         vec8, s_x + pl * bd.LHmax * bd.LW);
+            __syncthreads();
+            const int items = np * nrow * nseg;
+            for (int it = threadIdx.x; it < items; it += kBlock) {
+                const int pl = it / (nrow * nseg), rem = it - pl * (nrow * nseg);
+                const int r = rem / nseg, sg = rem - r * nseg;
+                const int ow0 = sg * SEG, nv = min(SEG, g.Wo - ow0);
+                float d[SEG];
+                load_seg<SEG>(dy + (((size_t)(nb + pl) * g.C + c) * g.Ho + oh0 + r) * g.Wo + ow0, d, nv);
+                const float* xs = s_x + pl * bd.LHmax * bd.LW + (r * S) * bd.LW + ow0 * S;
+#pragma unroll
+                for (int kh = 0; kh < K; ++kh) {
+                    float v[CW];
+#pragma unroll
+                    for (int qq = 0; qq < CW; ++qq) v[qq] = xs[kh * bd.LW + qq];
+#pragma unroll
+                    for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+                        for (int j = 0; j < SEG; ++j) acc[kh * K + kw] = fmaf(d[j], v[j * S + kw], acc[kh * K + kw]);
+                }
+            }
+        }
+    }
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) {
+        float v = acc[i];
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+        if (lane == 0) s_red[wave][i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < K * K) {
+        float t = 0.f;
+#pragma unroll
+        for (int jw = 0; jw < kBlock / kWave; ++jw) t += s_red[jw][threadIdx.x];
+        partial[((size_t)c * ngroups + q) * K * K + threadIdx.x] = t;
+    }
+}
+
+// bands and planes per block for the LDS kernels: the whole plane when it fits, several planes per
+// block while the block has fewer than ~2 output segments per thread
+template <int K, int S>
+inline DwBand dw_band(const DwGeo& g, int seg, int max_planes) {
+    DwBand b;
+    b.LW = (g.Wo - 1) * S + K;
+    const int full = (g.Ho - 1) * S + K;
+    if (full * b.LW <= kDwLdsFloats) {
+        b.BHo = g.Ho;
+        const int per_plane = g.Ho * ((g.Wo + seg - 1) / seg);
+        int pb = std::max(1, kDwLdsFloats / (full * b.LW));
+        pb = std::min(pb, std::max(1, (2 * kBlock + per_plane - 1) / per_plane));
+        b.PB = std::max(1, std::min(pb, max_planes));
+    } else {
+        b.BHo = std::max(1, (kDwLdsFloats / b.LW - K) / S + 1);
+        b.PB = 1;
+    }
+    b.LHmax = (b.BHo - 1) * S + K;
+    b.nbands = (g.Ho + b.BHo - 1) / b.BHo;
+    return b;
+}
+
+// the LDS kernels' vector accesses need 16-B aligned tensors; the staged row holds the whole input row
+// (the right padding is not negative); and they run only where an output row splits into segments of
+// 4 or 8 (Wo % 4 == 0): on the trunk's narrow planes (Wo = 22, 11) the register-tiled kernels are
+// faster (c3 step, per layer: 15-55 vs 21-98 us), on the wide ones the LDS kernels (23-74 vs 50-181 us)
+template <int K, int S>
+inline bool dw_lds_ok(const DwGeo& g, const void* a, const void* b) {
+    return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0 && g.Wo % 4 == 0 &&
+           (g.Wo - 1) * S + K >= g.pl + g.Wi && (g.Ho - 1) * S + K >= g.pt + g.Hi;
+}
+
+inline int dw_seg(int Wo) { return Wo % 8 == 0 ? 8 : Wo % 4 == 0 ? 4 : Wo % 2 == 0 ? 2 : 1; }
+
+template <int K, int S, typename T>
+int dw_fwd_lds(const void* x, const float* w, DwGeo g, int flip, void* y, hipStream_t s) {
+    const int seg = dw_seg(g.Wo);
+    const DwBand b = dw_band<K, S>(g, seg, g.nplanes);
+    const long blocks = (long)b.nbands * ((g.nplanes + b.PB - 1) / b.PB);
+    // slack past the staged rows: the last segment of a row reads up to (SEG - 1) * S columns past Wo
+    const size_t lds = sizeof(float) * ((size_t)b.PB * K * K + (size_t)b.PB * b.LHmax * b.LW + 8 * S + K);
+    if (blocks > INT_MAX) return LSS_CONV_EINVAL;
+#define LSS_DW_FWD(SG) hipLaunchKernelGGL((k_dw_fwd_lds<K, S, SG, T>), dim3((unsigned)blocks), dim3(kBlock), lds, s, \
+                                          (const T*)x, w, g, flip, b, (T*)y)
+    switch (seg) {
+        case 8: LSS_DW_FWD(8); break;
+        case 4: LSS_DW_FWD(4); break;
+        case 2: LSS_DW_FWD(2); break;
+        default: LSS_DW_FWD(1); break;
+    }
+#undef LSS_DW_FWD
+    return launch_status();
+}
+
+template <int K, int S, typename T>
+int dw_wgt_lds(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, hipStream_t s) {
+    const int seg = dw_seg(g.Wo);
+    const DwBand b = dw_band<K, S>(g, seg, (nimg + ngroups - 1) / ngroups);
+    const size_t lds = sizeof(float) * ((size_t)b.PB * b.LHmax * b.LW + 8 * S + K);
+#define LSS_DW_WGT(SG) hipLaunchKernelGGL((k_dw_wgt_lds<K, S, SG, T>), dim3(g.C * ngroups), dim3(kBlock), lds, s, \
+                                          (const T*)x, (const T*)dy, g, nimg, ngroups, b, partial)
+    switch (seg) {
+        case 8: LSS_DW_WGT(8); break;
+        case 4: LSS_DW_WGT(4); break;
+        case 2: LSS_DW_WGT(2); break;
+        default: LSS_DW_WGT(1); break;
+    }
+#undef LSS_DW_WGT
+    return launch_status();
+}
+
 // dispatch over (K, S, T)
 template <template <int, int, typename> class F, typename... A>
 int dispatch_kst(int K, int S, int dtype, A... a) {
@@ -274,6 +569,7 @@ int dispatch_kst(int K, int S, int dtype, A... a) {
 template <int K, int S, typename T>
 struct Fwd {
     static int run(const void* x, const float* w, DwGeo g, int flip, void* y, hipStream_t s) {
+        if (LSS_DW_LDS && dw_lds_ok<K, S>(g, x, y)) return dw_fwd_lds<K, S, T>(x, w, g, flip, y, s);
         constexpr int TH = Tile<S>::TH, TW = Tile<S>::TW;
         const long n = (long)g.nplanes * ((g.Ho + TH - 1) / TH) * ((g.Wo + TW - 1) / TW);
         hipLaunchKernelGGL((k_dw_fwd<K, S, TH, TW, T>), dim3(blocks_for(n)), dim3(kBlock), 0, s, (const T*)x, w, g,
@@ -302,6 +598,7 @@ struct BwdData {
 template <int K, int S, typename T>
 struct BwdWeight {
     static int run(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, hipStream_t s) {
+        if (LSS_DW_LDS && dw_lds_ok<K, S>(g, x, dy)) return dw_wgt_lds<K, S, T>(x, dy, g, nimg, ngroups, partial, s);
         hipLaunchKernelGGL((k_dw_bwd_weight<K, S, 4, S == 1 ? 4 : 2, T>), dim3(g.C * ngroups), dim3(kBlock), 0, s,
                            (const T*)x, (const T*)dy, g, nimg, ngroups, partial);
         return launch_status();
@@ -402,19 +699,6 @@ __global__ __launch_bounds__(kBlock) void k_head1_bwd(const uint4* __restrict__ 
 // y = bf16(x * scale[n] (+ r)) over sample-major bf16 tensors, scale[n] from the sample's draw, 8 elements (16 B) per thread: the
 // MBConv residual with stochastic depth (efficientnet_pytorch drop_connect, x / keep * mask +
 // inputs) in one pass instead of three; with r == nullptr, its backward dx = bf16(dy * scale[n]).
-__device__ __forceinline__ void unpack8(const uint4& u, float* o) {
-    const unsigned w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        o[2 * i] = __uint_as_float(w[i] << 16);
-        o[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
-    }
-}
-__device__ __forceinline__ unsigned pack2(float a, float b) {
-    const bf16 x = __float2bfloat16(a), y = __float2bfloat16(b);
-    return (unsigned)*reinterpret_cast<const unsigned short*>(&x) |
-           ((unsigned)*reinterpret_cast<const unsigned short*>(&y) << 16);
-}
 
 // the sample's scale from its uniform draw u (bf16): mask = floor(bf16(keep + u)) as torch computes
 // floor(keep + rand(..., dtype=bf16)), scale = mask / keep
@@ -526,6 +810,201 @@ __global__ __launch_bounds__(kBlock) void k_dropout(const uint4* __restrict__ x,
     asm volatile("" : : "v"(warm.x), "v"(warm.y), "v"(warm.z), "v"(warm.w));  // (the prefetch must land)
 }
 
+
+// ---- 1x1 convolution weight gradient over NCHW activations (the MBConv expand / project convs of
+// the trunk, src/models.py:43 via efficientnet_pytorch): dW[co][ci] = sum over images n and pixels q
+// of dy[n][co][q] * x[n][ci][q]. A GEMM whose K index (n, q) runs along q in BOTH operands, so the
+// v_mfma_f32_16x16x32_bf16 fragments (8 consecutive k per lane) load straight from global memory --
+// no LDS staging, no transposes, no fp32 workspace to zero and cast (MIOpen's atomic NHWC solver
+// needs both, plus NCHW <-> NHWC transposes). Block = 64 x 64 dW tile x one K range (a split); its
+// 4 waves take the range's 32-wide K steps in turn, double-buffered (the next step's 8 fragment loads
+// in flight behind the current step's 16 MFMAs), and are summed in LDS in a fixed order; the splits'
+// partials are summed by k_pw_wrw_reduce in split order (deterministic).
+constexpr int kPwWaves = 4;
+constexpr int kPwThreads = kPwWaves * kWave;
+
+using pw_bf16x8 = __attribute__((ext_vector_type(8))) short;
+using pw_f32x4 = __attribute__((ext_vector_type(4))) float;
+
+// A lane's fragment of one K step: KS consecutive k (8 or 16) of one row, as KS / 8 MFMA operands. Any
+// assignment of k to MFMA slots is a valid GEMM as long as A and B use the same one, so with KS = 16
+// a lane's 32 contiguous bytes feed two MFMAs and a row's 4 lanes read one whole 128-B line.
+template <int VEC, int KS>  // VEC 8: 16-B loads (HW % 8 == 0); VEC 4: 8-B loads (HW % 4 == 0)
+struct PwFrag {
+    pw_bf16x8 v[KS / 8];
+};
+
+template <int VEC, int KS>
+__device__ __forceinline__ PwFrag<VEC, KS> pw_frag(const bf16* __restrict__ p, int q, int HW, bool live) {
+    PwFrag<VEC, KS> f;
+#pragma unroll
+    for (int h = 0; h < KS / 8; ++h) {
+        if constexpr (VEC == 8) {
+            const bool ok = live && q + 8 * h < HW;
+            const uint4 v = ok ? *reinterpret_cast<const uint4*>(p + 8 * h) : make_uint4(0u, 0u, 0u, 0u);
+            f.v[h] = __builtin_bit_cast(pw_bf16x8, v);
+        } else {
+            const bool ok0 = live && q + 8 * h < HW, ok1 = live && q + 8 * h + 4 < HW;
+            const uint2 lo = ok0 ? *reinterpret_cast<const uint2*>(p + 8 * h) : make_uint2(0u, 0u);
+            const uint2 hi = ok1 ? *reinterpret_cast<const uint2*>(p + 8 * h + 4) : make_uint2(0u, 0u);
+            f.v[h] = __builtin_bit_cast(pw_bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        }
+    }
+    return f;
+}
+
+template <int VEC, int KS>
+__global__ __launch_bounds__(kPwThreads) void k_pw_wrw(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                      int Cin, int Cout, int HW, int spi, int nsteps, int tiles_n,
+                                                      int ntiles, int nsplit, float* __restrict__ partial) {
+    constexpr int SW = 4 * KS;                // k per step: 4 lane groups x KS
+    __shared__ pw_f32x4 s_red[2][16][kWave];  // two waves' 64 x 64 tiles (16 fragments x 64 lanes)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // XCD-contiguous logical block: consecutive tiles of one split (one K range, whose activation rows
+    // the tiles share) run on one XCD and meet in its L2
+    const int bpx = gridDim.x >> 3;
+    const int lb = (blockIdx.x & 7) * bpx + (blockIdx.x >> 3);
+    const int split = lb / ntiles, tile = lb - split * ntiles;
+    if (split >= nsplit) return;  // block-uniform (grid padded to a multiple of 8)
+    const int m0 = (tile / tiles_n) * 64, n0 = (tile % tiles_n) * 64;
+    const int fm = min(4, (Cout - m0 + 15) >> 4), fn = min(4, (Cin - n0 + 15) >> 4);  // live 16-row fragments
+    const int t0 = (int)((long long)nsteps * split / nsplit), t1 = (int)((long long)nsteps * (split + 1) / nsplit);
+    const int r16 = lane & 15, kq = KS * (lane >> 4);
+    int arow[4], brow[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        arow[i] = min(m0 + 16 * i + r16, Cout - 1);  // clamped rows feed only discarded outputs
+        brow[i] = min(n0 + 16 * i + r16, Cin - 1);
+    }
+    pw_f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = pw_f32x4{0.f, 0.f, 0.f, 0.f};
+    PwFrag<VEC, KS> a[2][4], b[2][4];
+    auto load = [&](int t, PwFrag<VEC, KS>* av, PwFrag<VEC, KS>* bv) {
+        const bool live = t < t1;
+        t = min(t, nsteps - 1);
+        const int n = t / spi;
+        const int q = (t - n * spi) * SW + kq;
+        const int qq = q < HW ? q : 0;  // (masked halves read nothing; the address stays in the tensor)
+        const bf16* ap = dy + (size_t)n * Cout * HW + qq;
+        const bf16* bp = x + (size_t)n * Cin * HW + qq;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (i < fm) av[i] = pw_frag<VEC, KS>(ap + (size_t)arow[i] * HW, q, HW, live);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < fn) bv[j] = pw_frag<VEC, KS>(bp + (size_t)brow[j] * HW, q, HW, live);
+    };
+    auto mma = [&](const PwFrag<VEC, KS>* av, const PwFrag<VEC, KS>* bv) {
+#pragma unroll
+        for (int h = 0; h < KS / 8; ++h)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (i < fm && j < fn)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i].v[h], bv[j].v[h], acc[i][j], 0, 0, 0);
+    };
+    int t = t0 + wave;
+    if (t < t1) load(t, a[0], b[0]);
+    for (; t < t1; t += 2 * kPwWaves) {
+        load(t + kPwWaves, a[1], b[1]);  // (past t1: zeros)
+        mma(a[0], b[0]);
+        if (t + kPwWaves >= t1) break;
+        load(t + 2 * kPwWaves, a[0], b[0]);
+        mma(a[1], b[1]);
+    }
+    // waves (0 + 2) and (1 + 3) in LDS, then every wave sums the two for its 16-row block
+    if (wave >= 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s_red[wave - 2][4 * i + j][lane] = acc[i][j];
+    }
+    __syncthreads();
+    if (wave < 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s_red[wave][4 * i + j][lane] += acc[i][j];
+    }
+    __syncthreads();
+    const int i = wave;  // this wave writes rows m0 + 16 i + 4 (lane >> 4) + r
+    if (i >= fm) return;
+    float* out = partial + (size_t)split * Cout * Cin;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ci = n0 + 16 * j + r16;
+        if (j >= fn || ci >= Cin) continue;
+        const pw_f32x4 v = s_red[0][4 * i + j][lane] + s_red[1][4 * i + j][lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = m0 + 16 * i + 4 * (lane >> 4) + r;
+            if (co < Cout) out[(size_t)co * Cin + ci] = v[r];
+        }
+    }
+}
+
+// dw[e] = sum over splits s (in order) of partial[s][e], nsplit <= kPwMaxSplit. Four consecutive
+// elements per lane (16-B loads); the splits of a lane's elements are shared by G waves of the block
+// (G = 1 for nsplit <= 16, else 16), each summing its run of <= 16 consecutive splits with every
+// load in flight at once, then the G sums in order.
+constexpr int kPwMaxSplit = 256;
+template <typename T, int G>
+__global__ __launch_bounds__(G == 1 ? 256 : 1024) void k_pw_wrw_reduce(const float* __restrict__ partial, int nsplit,
+                                                                       int E, T* __restrict__ dw) {
+    constexpr int kThreads = G == 1 ? 256 : 1024;
+    __shared__ float4 s_sum[G][kWave];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int chunk = G == 1 ? blockIdx.x * (kThreads / kWave) + wave : blockIdx.x;  // 64 lanes x 4 elements
+    const int e = (chunk * kWave + lane) * 4;
+    const int gw = G == 1 ? 0 : wave;
+    const int per = (nsplit + G - 1) / G, s0 = gw * per, s1 = min(s0 + per, nsplit);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < E) {
+        float4 p[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (s0 + k < s1) {
+                const float* src = partial + (size_t)(s0 + k) * E + e;
+                p[k] = (E & 3) == 0 ? *reinterpret_cast<const float4*>(src)  // (16-B aligned rows)
+                                    : make_float4(src[0], e + 1 < E ? src[1] : 0.f, e + 2 < E ? src[2] : 0.f,
+                                                  e + 3 < E ? src[3] : 0.f);
+            } else {
+                p[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            v.x += p[k].x;
+            v.y += p[k].y;
+            v.z += p[k].z;
+            v.w += p[k].w;
+        }
+    }
+    if constexpr (G > 1) {
+        s_sum[wave][lane] = v;
+        __syncthreads();
+        if (wave != 0) return;
+        v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int w = 0; w < G; ++w) {
+            const float4 t = s_sum[w][lane];
+            v.x += t.x;
+            v.y += t.y;
+            v.z += t.z;
+            v.w += t.w;
+        }
+    }
+    if (e >= E) return;
+    const float o[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (e + k < E) st(dw + e + k, o[k]);
+}
+
 }  // namespace
 
 extern "C" {
@@ -571,6 +1050,65 @@ int lss_head1_bwd(const void* x, const void* dy, const float* w, int32_t P, int3
 #undef LSS_HEAD1_BWD
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
+}
+
+// split count of lss_pw_wrw: about 512 blocks (2 per CU) and >= 2 K steps per wave, at most
+// kPwMaxSplit, and the fp32 partials at most half the activation bytes (or one split)
+static void pw_plan(int N, int Cin, int Cout, int HW, int* spi, int* nsteps, int* tiles_n, int* ntiles, int* nsplit) {
+    *spi = (HW + 63) / 64;
+    *nsteps = N * *spi;
+    *tiles_n = (Cin + 63) / 64;
+    *ntiles = ((Cout + 63) / 64) * *tiles_n;
+    long s = (512 + *ntiles - 1) / *ntiles;
+    s = std::min(s, (long)std::max(1, *nsteps / (2 * kPwWaves)));
+    const long in_bytes = 2L * N * HW * (Cin + Cout), per_split = 4L * Cin * Cout;
+    s = std::min(s, std::max(1L, in_bytes / (2 * per_split)));
+    *nsplit = (int)std::max(1L, std::min(s, (long)kPwMaxSplit));
+}
+
+int64_t lss_pw_wrw_workspace_bytes(int32_t N, int32_t Cin, int32_t Cout, int32_t HW) {
+    if (N <= 0 || Cin <= 0 || Cout <= 0 || HW <= 0) return 0;
+    int spi, nsteps, tiles_n, ntiles, nsplit;
+    pw_plan(N, Cin, Cout, HW, &spi, &nsteps, &tiles_n, &ntiles, &nsplit);
+    return (int64_t)nsplit * Cout * Cin * (int64_t)sizeof(float);
+}
+
+int lss_pw_wrw(const void* x, const void* dy, int32_t N, int32_t Cin, int32_t Cout, int32_t HW, void* dw,
+               int32_t dw_dtype, void* workspace, int64_t workspace_bytes, void* stream) {
+    if (!x || !dy || !dw || !workspace || N <= 0 || Cin <= 0 || Cout <= 0 || HW <= 0 || HW % 4 != 0 ||
+        (dw_dtype != LSS_CONV_F32 && dw_dtype != LSS_CONV_BF16) || (long)N * ((HW + 31) / 32) >= INT_MAX ||
+        (long)N * std::max(Cin, Cout) * HW >= INT_MAX ||
+        ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy)) & 7) ||
+        workspace_bytes < lss_pw_wrw_workspace_bytes(N, Cin, Cout, HW))
+        return LSS_CONV_EINVAL;
+    int spi, nsteps, tiles_n, ntiles, nsplit;
+    pw_plan(N, Cin, Cout, HW, &spi, &nsteps, &tiles_n, &ntiles, &nsplit);
+    const long blocks = 8L * (((long)ntiles * nsplit + 7) / 8);
+    hipStream_t s = (hipStream_t)stream;
+    float* part = (float*)workspace;
+    const bool v8 = HW % 8 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy)) & 15) == 0;
+    if (v8)
+        hipLaunchKernelGGL((k_pw_wrw<8, 16>), dim3((unsigned)blocks), dim3(kPwThreads), 0, s, (const bf16*)x,
+                           (const bf16*)dy, Cin, Cout, HW, spi, nsteps, tiles_n, ntiles, nsplit, part);
+    else
+        hipLaunchKernelGGL((k_pw_wrw<4, 16>), dim3((unsigned)blocks), dim3(kPwThreads), 0, s, (const bf16*)x,
+                           (const bf16*)dy, Cin, Cout, HW, spi, nsteps, tiles_n, ntiles, nsplit, part);
+    const int E = Cout * Cin;
+    const int chunks = (E + 4 * kWave - 1) / (4 * kWave);  // 64 lanes x 4 elements
+#define LSS_PW_REDUCE(T)                                                                                          \
+    if (nsplit <= 16)                                                                                             \
+        hipLaunchKernelGGL((k_pw_wrw_reduce<T, 1>), dim3((chunks + 3) / 4), dim3(256), 0, s, (const float*)part,  \
+                           nsplit, E, (T*)dw);                                                                    \
+    else                                                                                                          \
+        hipLaunchKernelGGL((k_pw_wrw_reduce<T, 16>), dim3(chunks), dim3(1024), 0, s, (const float*)part, nsplit, E, \
+                           (T*)dw)
+    if (dw_dtype == LSS_CONV_BF16) {
+        LSS_PW_REDUCE(bf16);
+    } else {
+        LSS_PW_REDUCE(float);
+    }
+#undef LSS_PW_REDUCE
+    return launch_status();
 }
 
 int lss_dwconv_fwd(const void* x, int32_t dtype, const float* w, int32_t N, int32_t C, int32_t Hi, int32_t Wi,

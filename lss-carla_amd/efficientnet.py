@@ -158,6 +158,62 @@ class _HipDepthwise(torch.autograd.Function):
         return dx, dw, None, None
 
 
+class _HipPointwise(torch.autograd.Function):
+    """1x1 conv (stride 1, no bias) over NCHW activations in bf16: forward and backward-data on MIOpen
+    (as ``nn.Conv2d`` under autocast), the weight gradient on ``lss_pw_wrw`` (include/lss_convs.h) --
+    an MFMA GEMM reading both operands in place, written in the weight's dtype, where MIOpen's NCHW
+    path transposes both activations, accumulates atomically in an fp32 workspace it zero-fills, and
+    casts the result."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        xb = x.to(torch.bfloat16).contiguous()
+        wb = weight.to(torch.bfloat16)
+        with torch.autocast("cuda", enabled=False):
+            y = F.conv2d(xb, wb)
+        ctx.save_for_backward(xb, wb)
+        ctx.dtypes = (x.dtype, weight.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+        lib = _lib.load()
+        xb, wb = ctx.saved_tensors
+        xdt, wdt = ctx.dtypes
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            with torch.autocast("cuda", enabled=False):
+                dx = torch.ops.aten.convolution_backward(dy, xb, wb, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                         [True, False, False])[0].to(xdt)
+        if ctx.needs_input_grad[1]:
+            N, Cin, H, W = xb.shape
+            Cout = dy.shape[1]
+            nbytes = int(lib.lss_pw_wrw_workspace_bytes(N, Cin, Cout, H * W))
+            ws = torch.empty(nbytes, device=xb.device, dtype=torch.uint8)
+            dw = torch.empty(Cout, Cin, 1, 1, device=xb.device, dtype=wdt)
+            _lib.check(lib.lss_pw_wrw(_lib.ptr(xb), _lib.ptr(dy), N, Cin, Cout, H * W, _lib.ptr(dw), _lib.dtype_code(wdt),
+                                      _lib.ptr(ws), nbytes, _lib.stream_handle(xb.device)), "lss_pw_wrw")
+        return dx, dw
+
+
+# the trunk's 1x1 convs (MBConv expand / project) take _HipPointwise when their activations are bf16 NCHW
+USE_HIP_PW_WRW = True
+
+
+def pointwise_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    if (USE_HIP_PW_WRW and x.is_cuda and x.dim() == 4 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+            and conv.groups == 1 and conv.bias is None and conv.padding == (0, 0) and conv.dilation == (1, 1)
+            and isinstance(getattr(conv, "static_padding", None), (nn.Identity, type(None)))
+            and x.is_contiguous() and (x.shape[2] * x.shape[3]) % 4 == 0
+            and conv.weight.dtype in (torch.float32, torch.bfloat16)
+            and ((torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+                 or (x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16))):
+        return _HipPointwise.apply(x, conv.weight)
+    return conv(x)
+
+
 def depthwise_same_pads(conv: "Conv2dStaticSamePadding") -> Tuple[int, int, int, int]:
     """(left, right, top, bottom) padding of a static-same conv, whether it pads itself or via ZeroPad2d."""
     if isinstance(conv.static_padding, nn.ZeroPad2d):
@@ -260,7 +316,7 @@ class MBConvBlock(nn.Module):
     def forward(self, inputs: torch.Tensor, drop_connect_rate=None) -> torch.Tensor:
         x = inputs
         if self.expand != 1:
-            x = bn_act(self._bn0, self._expand_conv(x), "swish")
+            x = bn_act(self._bn0, pointwise_conv(self._expand_conv, x), "swish")
         dw = self._depthwise_conv
         if self.depthwise_impl == "hip" and x.is_cuda:
             x = _HipDepthwise.apply(x, dw.weight, dw.stride[0], depthwise_same_pads(dw))
@@ -273,7 +329,7 @@ class MBConvBlock(nn.Module):
             x = self._depthwise_conv(x)
         x = bn_act(self._bn1, x, "swish")
         x = squeeze_excite(x, self._se_reduce, self._se_expand)
-        x = bn_act(self._bn2, self._project_conv(x))
+        x = bn_act(self._bn2, pointwise_conv(self._project_conv, x))
         if self.stride == 1 and self.in_f == self.out_f:
             x = drop_connect_add(x, inputs, drop_connect_rate, self.training)
         return x

@@ -17,7 +17,7 @@ HEADERS = [os.path.join(REPO, "include", h) for h in ("lss_hip.h", "lss_convs.h"
 
 def _declared():
     text = "".join(open(h).read() for h in HEADERS)
-    return set(re.findall(r"^\s*(?:int|int32_t|size_t|const char\*)\s+(lss_\w+)\s*\(", text, re.M))
+    return set(re.findall(r"^\s*(?:int|int32_t|int64_t|size_t|const char\*)\s+(lss_\w+)\s*\(", text, re.M))
 
 
 def test_header_declarations_match_binding():
