@@ -74,7 +74,9 @@ def parse():
     ap.add_argument("--miopen-find", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
     ap.add_argument("--hip-bn", type=int, default=1, help="BatchNorm + activation on the lss_bn_* kernels")
     ap.add_argument("--fuse-depthnet", type=int, default=1, help="depthnet 1x1 conv inside the lift kernel (MFMA)")
-    ap.add_argument("--hip-pw", type=int, default=1, help="trunk 1x1 conv weight gradients on lss_pw_wrw (1) or MIOpen (0)")
+    ap.add_argument("--hip-pw", type=int, default=2,
+                    help="trunk 1x1 convs: 2 = forward/backward-data on lss_pw_conv and weight gradients on lss_pw_wrw, "
+                         "1 = lss_pw_wrw only, 0 = MIOpen")
     ap.add_argument("--plan-at", default="dropout", choices=("trunk", "dropout", "lift"),
                     help="plan kernels in front of the trunk, the dropout or the fused lift")
     ap.add_argument("--hip-dropout", type=int, default=1,
@@ -467,7 +469,8 @@ def build_model(args, dev, gc, dac):
     models.USE_HIP_DROPOUT = bool(args.hip_dropout)
     models.PLAN_AT = args.plan_at
     from lss_carla_amd import efficientnet
-    efficientnet.USE_HIP_PW_WRW = bool(args.hip_pw)
+    efficientnet.USE_HIP_PW_WRW = args.hip_pw >= 1
+    efficientnet.USE_HIP_PW_GEMM = args.hip_pw >= 2
     from lss_carla_amd.efficientnet import set_depthwise_impl
     set_depthwise_impl(model.camencode.trunk, args.dw_impl)
     model.train() if args.mode == "train" else model.eval()

@@ -61,6 +61,14 @@ int64_t lss_pw_wrw_workspace_bytes(int32_t N, int32_t Cin, int32_t Cout, int32_t
 int lss_pw_wrw(const void* x, const void* dy, int32_t N, int32_t Cin, int32_t Cout, int32_t HW, void* dw,
                int32_t dw_dtype, void* workspace, int64_t workspace_bytes, void* stream);
 
+/* 1x1 convolution (no bias, stride 1) over NCHW contiguous bf16 activations, fp32 accumulation:
+ * y[n][m][q] = bf16(sum_k A(m, k) * x[n][k][q]) for n < N, m < M, q < HW, with A(m, k) = a[m * K + k]
+ * (LSS_PW_MK: the conv weight (M, K), the forward) or a[k * M + m] (LSS_PW_KM: the weight (K, M) read
+ * transposed, the backward-data dx = W^T dy). HW % 4 == 0, K % 8 == 0, M % 8 == 0, 16-B aligned pointers. */
+enum { LSS_PW_MK = 0, LSS_PW_KM = 1 };
+int lss_pw_conv(const void* x, const void* a, int32_t a_layout, int32_t N, int32_t K, int32_t M, int32_t HW, void* y,
+                void* stream);
+
 /* Per-sample scale (+ residual) over N samples of `per` contiguous bf16 elements each (any memory
  * format that is sample-major: NCHW or channels-last), per % 8 == 0, 16-B aligned pointers:
  * y = bf16(x * scale[n] + res) (res nullable: y = bf16(x * scale[n])), scale[n] = mask[n] / keep with

@@ -947,6 +947,126 @@ __global__ __launch_bounds__(kPwThreads) void k_pw_wrw(const bf16* __restrict__ 
     }
 }
 
+// ---- 1x1 convolution forward / backward-data over NCHW bf16 activations (the trunk's MBConv expand /
+// project convs): Y[n][m][p] = sum_k A[m][k] X[n][k][p], A = W (forward, [m][k]) or W^T (backward-data,
+// W given as [k][m]). MIOpen runs these as batched GEMMs of one image each (15-50 us per layer at c3).
+// Here the MFMA rows are PIXELS: D[px][m] = sum_k X^T[px][k] A^T[k][m], so a lane's 4 accumulators are 4
+// consecutive pixels of one channel (one 8-B store). Block = 64 pixels (flattened over images) x 64
+// channels, 4 waves of 16 channels; the X tile (KC k x 64 px) is staged in LDS as it lies in memory and
+// read transposed by ds_read_tr16_b64 (8 consecutive k of one pixel per lane); A comes straight from
+// global ([m][k] rows, forward) or through a second LDS tile ([k][m] rows, backward-data). The next
+// stage's global loads are in flight while the current stage's MFMAs run.
+constexpr int kPgPx = 64, kPgM = 64;
+constexpr int kPgRow = kPgPx * 2 + 8;  // LDS bytes per staged k row (+8: spread the banks)
+
+template <int VEC, bool WT, int KC>  // VEC: pixels per X load (8: P % 8 == 0, else 4); WT: A given as [k][m]
+__global__ __launch_bounds__(256) void k_pw_gemm(const bf16* __restrict__ X, const bf16* __restrict__ A, int M, int K,
+                                                 int P, int ncols, int mtiles, bf16* __restrict__ Y) {
+    using v4s = __attribute__((ext_vector_type(4))) short;
+    constexpr int XL = KC * (kPgPx / VEC) / 256;            // X loads per thread per stage
+    constexpr int WL = WT ? KC * (kPgM / 8) / 256 : KC / 32;  // A loads per thread (WT) / per lane (forward)
+    static_assert(XL >= 1 && WL >= 1, "whole loads per thread");
+    __shared__ __attribute__((aligned(16))) unsigned char s_x[KC * kPgRow];
+    __shared__ __attribute__((aligned(16))) unsigned char s_w[WT ? KC * kPgRow : 16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c16 = lane & 15, g = lane >> 4, tq = c16 >> 2, tp = c16 & 3;
+    // XCD-contiguous logical block, m-tiles fastest: the m-tiles of one pixel tile (same X rows) share an L2
+    const int bpx = gridDim.x >> 3;
+    const int lb = (blockIdx.x & 7) * bpx + (blockIdx.x >> 3);
+    const int mt = lb % mtiles, jt = lb / mtiles;
+    const int j0 = jt * kPgPx, m0 = mt * kPgM;
+    if (j0 >= ncols) return;  // block-uniform (grid padded to a multiple of 8)
+    // this thread's X chunks: (row, pixel chunk) -> global address (pixels of a chunk never straddle images)
+    const uint2 z2 = make_uint2(0u, 0u);
+    uint4 xr[XL];
+    uint2 xr2[XL];
+    uint4 wr[WL], wcur[WT ? 1 : WL];
+    auto gload = [&](int kb) {
+#pragma unroll
+        for (int i = 0; i < XL; ++i) {
+            const int c = threadIdx.x + 256 * i;
+            const int row = c / (kPgPx / VEC), ch = c - row * (kPgPx / VEC);
+            const int col = j0 + ch * VEC, k = kb + row;
+            const bool ok = col < ncols && k < K;
+            const int n = ok ? col / P : 0, pp = ok ? col - n * P : 0;
+            const bf16* src = X + ((size_t)n * K + (ok ? k : 0)) * P + pp;
+            if constexpr (VEC == 8) xr[i] = ok ? *reinterpret_cast<const uint4*>(src) : make_uint4(0u, 0u, 0u, 0u);
+            else xr2[i] = ok ? *reinterpret_cast<const uint2*>(src) : z2;
+        }
+        if constexpr (WT) {  // A^T tile rows k, 64 channels each: A[k][m0 .. m0 + 63], 8 per load (M % 8 == 0)
+#pragma unroll
+            for (int i = 0; i < WL; ++i) {
+                const int c = threadIdx.x + 256 * i;
+                const int row = c >> 3, ch = c & 7;
+                const int k = kb + row, m = m0 + 8 * ch;
+                wr[i] = (k < K && m < M) ? *reinterpret_cast<const uint4*>(A + (size_t)k * M + m) : make_uint4(0u, 0u, 0u, 0u);
+            }
+        } else {  // forward: this lane's B fragments straight from A's rows (K % 8 == 0)
+            const int m = m0 + 16 * wave + c16;
+#pragma unroll
+            for (int i = 0; i < WL; ++i) {
+                const int k = kb + 32 * i + 8 * g;
+                wr[i] = (m < M && k < K) ? *reinterpret_cast<const uint4*>(A + (size_t)m * K + k) : make_uint4(0u, 0u, 0u, 0u);
+            }
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < XL; ++i) {
+            const int c = threadIdx.x + 256 * i;
+            const int row = c / (kPgPx / VEC), ch = c - row * (kPgPx / VEC);
+            if constexpr (VEC == 8) *reinterpret_cast<uint4*>(s_x + row * kPgRow + ch * 16) = xr[i];
+            else *reinterpret_cast<uint2*>(s_x + row * kPgRow + ch * 8) = xr2[i];
+        }
+        if constexpr (WT) {
+#pragma unroll
+            for (int i = 0; i < WL; ++i) {
+                const int c = threadIdx.x + 256 * i;
+                *reinterpret_cast<uint4*>(s_w + (c >> 3) * kPgRow + (c & 7) * 16) = wr[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < WL; ++i) wcur[i] = wr[i];
+        }
+    };
+    auto tr8 = [&](const unsigned char* s, int step, int col0) {  // 8 consecutive k (step) of column col0 + c16
+        const unsigned char* base = s + (32 * step + 8 * g + tq) * kPgRow + (col0 + 4 * tp) * 2;
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(base));
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(base + 4 * kPgRow));
+        return pw_bf16x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    };
+    pw_f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = pw_f32x4{0.f, 0.f, 0.f, 0.f};
+    gload(0);
+    for (int kb = 0; kb < K; kb += KC) {
+        __syncthreads();  // the previous stage's reads of s_x / s_w are done
+        lstore();
+        __syncthreads();
+        if (kb + KC < K) gload(kb + KC);  // in flight behind this stage's MFMAs
+#pragma unroll
+        for (int st = 0; st < KC / 32; ++st) {
+            if (kb + 32 * st >= K) break;
+            pw_bf16x8 b;
+            if constexpr (WT) b = tr8(s_w, st, 16 * wave);
+            else b = __builtin_bit_cast(pw_bf16x8, wcur[st]);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr8(s_x, st, 16 * t), b, acc[t], 0, 0, 0);
+        }
+    }
+    // D[px][m]: this lane holds channel m0 + 16 wave + c16, pixels 16 t + 4 g + 0..3
+    const int m = m0 + 16 * wave + c16;
+    if (m >= M) return;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int col = j0 + 16 * t + 4 * g;
+        if (col >= ncols) continue;
+        const int n = col / P, pp = col - n * P;
+        *reinterpret_cast<uint2*>(Y + ((size_t)n * M + m) * P + pp) =
+            make_uint2(pack2(acc[t][0], acc[t][1]), pack2(acc[t][2], acc[t][3]));
+    }
+}
+
 // dw[e] = sum over splits s (in order) of partial[s][e], nsplit <= kPwMaxSplit. Four consecutive
 // elements per lane (16-B loads); the splits of a lane's elements are shared by G waves of the block
 // (G = 1 for nsplit <= 16, else 16), each summing its run of <= 16 consecutive splits with every
@@ -1108,6 +1228,33 @@ int lss_pw_wrw(const void* x, const void* dy, int32_t N, int32_t Cin, int32_t Co
         LSS_PW_REDUCE(float);
     }
 #undef LSS_PW_REDUCE
+    return launch_status();
+}
+
+int lss_pw_conv(const void* x, const void* a, int32_t a_layout, int32_t N, int32_t K, int32_t M, int32_t HW, void* y,
+                void* stream) {
+    if (!x || !a || !y || N <= 0 || K <= 0 || M <= 0 || HW <= 0 || HW % 4 != 0 || K % 8 != 0 || M % 8 != 0 ||
+        (a_layout != LSS_PW_MK && a_layout != LSS_PW_KM) || (long)N * HW >= INT_MAX ||
+        (long)N * std::max(K, M) * HW >= INT_MAX ||
+        ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(a)) & 15))
+        return LSS_CONV_EINVAL;
+    const int ncols = N * HW, mtiles = (M + kPgM - 1) / kPgM;
+    const long tiles = (long)mtiles * ((ncols + kPgPx - 1) / kPgPx);
+    const long blocks = 8L * ((tiles + 7) / 8);
+    if (blocks > INT_MAX) return LSS_CONV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const bool v8 = HW % 8 == 0, wt = a_layout == LSS_PW_KM, small = K <= 64;
+#define LSS_PW_GEMM(V, W, KC)                                                                                      \
+    hipLaunchKernelGGL((k_pw_gemm<V, W, KC>), dim3((unsigned)blocks), dim3(256), 0, s, (const bf16*)x, (const bf16*)a, \
+                       M, K, HW, ncols, mtiles, (bf16*)y)
+    if (v8) {
+        if (wt) { if (small) LSS_PW_GEMM(8, true, 32); else LSS_PW_GEMM(8, true, 128); }
+        else { if (small) LSS_PW_GEMM(8, false, 32); else LSS_PW_GEMM(8, false, 128); }
+    } else {
+        if (wt) { if (small) LSS_PW_GEMM(4, true, 32); else LSS_PW_GEMM(4, true, 128); }
+        else { if (small) LSS_PW_GEMM(4, false, 32); else LSS_PW_GEMM(4, false, 128); }
+    }
+#undef LSS_PW_GEMM
     return launch_status();
 }
 

@@ -159,20 +159,33 @@ class _HipDepthwise(torch.autograd.Function):
 
 
 class _HipPointwise(torch.autograd.Function):
-    """1x1 conv (stride 1, no bias) over NCHW activations in bf16: forward and backward-data on MIOpen
-    (as ``nn.Conv2d`` under autocast), the weight gradient on ``lss_pw_wrw`` (include/lss_convs.h) --
-    an MFMA GEMM reading both operands in place, written in the weight's dtype, where MIOpen's NCHW
-    path transposes both activations, accumulates atomically in an fp32 workspace it zero-fills, and
-    casts the result."""
+    """1x1 conv (stride 1, no bias) over NCHW activations in bf16 (the autocast conv's operands): forward
+    and backward-data on ``lss_pw_conv`` (MFMA, pixels as the GEMM rows; MIOpen's per-image batched
+    GEMMs when USE_HIP_PW_GEMM is off or the shapes do not fit), the weight gradient on ``lss_pw_wrw``
+    (include/lss_convs.h) -- an MFMA GEMM reading both operands in place, written in the weight's
+    dtype, where MIOpen's NCHW path transposes both activations, accumulates atomically in an fp32
+    workspace it zero-fills, and casts the result."""
 
     @staticmethod
     def forward(ctx, x, weight):
+        from . import _lib
         xb = x.to(torch.bfloat16).contiguous()
         wb = weight.to(torch.bfloat16)
-        with torch.autocast("cuda", enabled=False):
-            y = F.conv2d(xb, wb)
+        N, Cin, H, W = xb.shape
+        Cout = wb.shape[0]
+        gemm = USE_HIP_PW_GEMM and Cin % 8 == 0 and Cout % 8 == 0 and xb.data_ptr() % 16 == 0
+        if gemm:
+            if wb.data_ptr() % 16 or not wb.is_contiguous():
+                wb = wb.contiguous().clone()  # (a flat-parameter view need not be 16-B aligned)
+            y = torch.empty(N, Cout, H, W, device=xb.device, dtype=torch.bfloat16)
+            _lib.check(_lib.load().lss_pw_conv(_lib.ptr(xb), _lib.ptr(wb), 0, N, Cin, Cout, H * W, _lib.ptr(y),
+                                               _lib.stream_handle(xb.device)), "lss_pw_conv")
+        else:
+            with torch.autocast("cuda", enabled=False):
+                y = F.conv2d(xb, wb)
         ctx.save_for_backward(xb, wb)
         ctx.dtypes = (x.dtype, weight.dtype)
+        ctx.gemm = gemm
         return y
 
     @staticmethod
@@ -184,9 +197,16 @@ class _HipPointwise(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            with torch.autocast("cuda", enabled=False):
-                dx = torch.ops.aten.convolution_backward(dy, xb, wb, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                                         [True, False, False])[0].to(xdt)
+            if ctx.gemm and dy.data_ptr() % 16 == 0:
+                N, Cin, H, W = xb.shape
+                dx = torch.empty_like(xb)
+                _lib.check(lib.lss_pw_conv(_lib.ptr(dy), _lib.ptr(wb), 1, N, dy.shape[1], Cin, H * W, _lib.ptr(dx),
+                                           _lib.stream_handle(xb.device)), "lss_pw_conv")
+                dx = dx.to(xdt)
+            else:
+                with torch.autocast("cuda", enabled=False):
+                    dx = torch.ops.aten.convolution_backward(dy, xb, wb, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                             [True, False, False])[0].to(xdt)
         if ctx.needs_input_grad[1]:
             N, Cin, H, W = xb.shape
             Cout = dy.shape[1]
@@ -198,8 +218,10 @@ class _HipPointwise(torch.autograd.Function):
         return dx, dw
 
 
-# the trunk's 1x1 convs (MBConv expand / project) take _HipPointwise when their activations are bf16 NCHW
+# the trunk's 1x1 convs (MBConv expand / project) take _HipPointwise when their activations are bf16 NCHW;
+# USE_HIP_PW_GEMM: its forward and backward-data on lss_pw_conv too (else MIOpen)
 USE_HIP_PW_WRW = True
+USE_HIP_PW_GEMM = True
 
 
 def pointwise_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:

@@ -82,8 +82,15 @@ def test_pw_wrw_rejects_bad_arguments():
     assert rc == -1
 
 
+@pytest.fixture
+def miopen_fwd():
+    efficientnet.USE_HIP_PW_GEMM = False  # forward / backward-data on MIOpen: only the weight gradient differs
+    yield
+    efficientnet.USE_HIP_PW_GEMM = True
+
+
 @pytest.mark.parametrize("wdtype", [torch.float32, torch.bfloat16])
-def test_pointwise_conv_autograd_matches_conv2d(wdtype):
+def test_pointwise_conv_autograd_matches_conv2d(wdtype, miopen_fwd):
     torch.manual_seed(0)
     conv = efficientnet.Conv2dStaticSamePadding(96, 24, 1, bias=False, image_size=(32, 88)).to(DEV)
     if wdtype == torch.bfloat16:
@@ -110,3 +117,58 @@ def test_pointwise_conv_autograd_matches_conv2d(wdtype):
     tol = 2e-2 * ref.abs().max().item()
     assert (gw.float().view_as(ref) - ref).abs().max().item() <= tol
     assert (conv.weight.grad.float().view_as(ref) - ref).abs().max().item() <= tol
+
+
+CONV_SHAPES = [
+    (2, 16, 96, 64, 176),    # b1 expand (K 16: one 32-k stage, half of it masked)
+    (3, 96, 24, 32, 88),     # b1 project
+    (4, 40, 240, 16, 44),
+    (4, 672, 112, 8, 22),    # HW 176
+    (5, 192, 1152, 4, 11),   # HW 44: 8-B pixel loads, tiles straddling images
+    (3, 1152, 320, 4, 11),   # K 1152: nine 128-k stages
+    (2, 8, 8, 2, 2),
+    (1, 136, 72, 3, 4),      # ragged tiles in k, m and pixels
+]
+
+
+@pytest.mark.parametrize("layout", [0, 1])
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_pw_conv_vs_fp64(shape, layout):
+    lib = _lib.load()
+    N, Cin, Cout, H, W = shape
+    g = torch.Generator().manual_seed(7)
+    K, M = (Cin, Cout) if layout == 0 else (Cout, Cin)  # layout 1: the backward-data, dx = W^T dy
+    x = torch.randn(N, K, H, W, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(Cout, Cin, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
+    y = torch.full((N, M, H, W), float("nan"), device=DEV, dtype=torch.bfloat16)
+    _lib.check(lib.lss_pw_conv(_lib.ptr(x), _lib.ptr(w), layout, N, K, M, H * W, _lib.ptr(y), _lib.stream_handle(DEV)),
+               "lss_pw_conv")
+    a = w.double() if layout == 0 else w.double().t()  # (M, K)
+    ref = torch.einsum("mk,nkhw->nmhw", a, x.double())
+    assert torch.isfinite(y.float()).all()
+    # fp32 accumulation, one bf16 rounding of the result
+    err = (y.double() - ref).abs() - 2.0 ** -8 * ref.abs()
+    assert err.max().item() <= 1e-4 * K ** 0.5, err.max().item()
+
+
+def test_pointwise_gemm_autograd_matches_miopen():
+    torch.manual_seed(1)
+    conv = efficientnet.Conv2dStaticSamePadding(112, 672, 1, bias=False, image_size=(8, 22)).to(DEV)
+    x = torch.randn(6, 112, 8, 22, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    gy = torch.randn(6, 672, 8, 22, device=DEV).to(torch.bfloat16)
+    outs = []
+    for gemm in (True, False):
+        efficientnet.USE_HIP_PW_GEMM = gemm
+        try:
+            x.grad = None
+            conv.weight.grad = None
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = efficientnet.pointwise_conv(conv, x)
+            y.backward(gy)
+            outs.append((y.detach().float(), x.grad.float(), conv.weight.grad.clone()))
+        finally:
+            efficientnet.USE_HIP_PW_GEMM = True
+    (y1, gx1, gw1), (y2, gx2, gw2) = outs
+    torch.testing.assert_close(y1, y2, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(gx1, gx2, rtol=1e-2, atol=2e-2)
+    assert torch.equal(gw1, gw2)  # the same lss_pw_wrw either way
