@@ -265,7 +265,8 @@ __global__ __launch_bounds__(kBlock) void k_se_dx(const unsigned short* __restri
 }
 
 // The four parameter gradients of the two 1x1 convs in one launch, one thread per output, the N
-// images summed in order (deterministic): dw2[c][j] = sum_n de[n][c] h[n][j] (C, sq),
+// images summed in order (deterministic; the loops unrolled so 16 images' loads are in flight at once,
+// the sums still one dependent chain in image order): dw2[c][j] = sum_n de[n][c] h[n][j] (C, sq),
 // dw1[j][c] = sum_n dr[n][j] m[n][c] (sq, C), db1[j] = sum_n dr[n][j], db2[c] = sum_n de[n][c].
 __global__ __launch_bounds__(kBlock) void k_se_wgrad(const float* __restrict__ de, const float* __restrict__ h,
                                                      const float* __restrict__ dr, const float* __restrict__ m,
@@ -277,18 +278,22 @@ __global__ __launch_bounds__(kBlock) void k_se_wgrad(const float* __restrict__ d
     float a = 0.f;
     if (t < cs) {  // dw2, lanes over j: de broadcast, h coalesced
         const int c = t / sq, j = t - c * sq;
+#pragma unroll 16
         for (int n = 0; n < N; ++n) a = fmaf(de[(size_t)n * C + c], h[(size_t)n * sq + j], a);
         dw2[t] = a;
     } else if (t < 2 * cs) {  // dw1, lanes over c: m coalesced
         const int u = t - cs, j = u / C, c = u - j * C;
+#pragma unroll 16
         for (int n = 0; n < N; ++n) a = fmaf(dr[(size_t)n * sq + j], m[(size_t)n * C + c], a);
         dw1[u] = a;
     } else if (t < 2 * cs + sq) {
         const int j = t - 2 * cs;
+#pragma unroll 16
         for (int n = 0; n < N; ++n) a += dr[(size_t)n * sq + j];
         db1[j] = a;
     } else if (t < 2 * cs + sq + C) {
         const int c = t - 2 * cs - sq;
+#pragma unroll 16
         for (int n = 0; n < N; ++n) a += de[(size_t)n * C + c];
         db2[c] = a;
     }
