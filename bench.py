@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--miopen-find", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
     ap.add_argument("--hip-bn", type=int, default=1, help="BatchNorm + activation on the lss_bn_* kernels")
     ap.add_argument("--fuse-depthnet", type=int, default=1, help="depthnet 1x1 conv inside the lift kernel (MFMA)")
+    ap.add_argument("--bn-relu-y", default="recompute", choices=("recompute", "keep"),
+                    help="channels-last BN + ReLU without a residual: the backward recomputes the output from x "
+                         "or keeps and re-reads it")
     ap.add_argument("--hip-pw", type=int, default=2,
                     help="trunk 1x1 convs: 2 = forward/backward-data on lss_pw_conv and weight gradients on lss_pw_wrw, "
                          "1 = lss_pw_wrw only, 0 = MIOpen")
@@ -314,7 +317,7 @@ def measure_in_graph(args) -> dict | None:
            "--profile-steps", "0", "--pmc-traffic", "0", "--cpu-baseline", "0", "--in-graph-prof", "0",
            "--mode", args.mode]
     # the rest of this run's configuration, so the child measures the same step
-    for flag in ("miopen_find", "hip_bn", "fuse_depthnet", "hip_dropout", "hip_pw", "plan_at", "trunk_channels_last", "param_groups",
+    for flag in ("miopen_find", "hip_bn", "bn_relu_y", "fuse_depthnet", "hip_dropout", "hip_pw", "plan_at", "trunk_channels_last", "param_groups",
                  "flat_params", "overlap_all_reduce", "dw_impl"):
         cmd += ["--" + flag.replace("_", "-"), str(getattr(args, flag))]
     try:
@@ -466,6 +469,7 @@ def build_model(args, dev, gc, dac):
         model.camencode.to(memory_format=torch.channels_last)
     from lss_carla_amd import norm, models
     norm.USE_HIP_BN = bool(args.hip_bn)
+    norm.RECOMPUTE_RELU_Y = args.bn_relu_y == "recompute"
     models.USE_HIP_DROPOUT = bool(args.hip_dropout)
     models.PLAN_AT = args.plan_at
     from lss_carla_amd import efficientnet

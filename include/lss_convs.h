@@ -91,6 +91,20 @@ int lss_scale_add(const void* x, const void* u, float keep, const void* res, int
 int lss_dropout(const void* x, int32_t dtype, int64_t n, const uint64_t* seed, float keep, void* y,
                 const void* prefetch, int64_t prefetch_bytes, void* stream);
 
+/* SimpleLoss (src/tools.py:222-230: BCEWithLogitsLoss(pos_weight=[pos_weight]), reduction mean) and its
+ * input gradient in one pass: loss[0] = mean over the n elements of
+ *   (1 - t) x + (1 + (pw - 1) t) (log1p(exp(-|x|)) + max(-x, 0)),
+ * grad = ((1 + (pw - 1) t) sigmoid(x) - pw t) / n (the gradient for d loss = 1; the caller scales it by
+ * the incoming gradient). x, grad: n logits of dtype (fp32 or bf16), 16-B aligned; target: n fp32,
+ * 16-B aligned; arithmetic fp32. partial: lss_bce_partials(n) fp32 scratch. Deterministic (fixed-order
+ * sums). Two launches, no host synchronisation. */
+int lss_bce_logits(const void* x, int32_t dtype, const float* target, int64_t n, float pos_weight, float* partial,
+                   float* loss, void* grad, void* stream);
+int64_t lss_bce_partials(int64_t n);
+/* Backward of lss_bce_logits: dx = grad * grad_loss[0] (grad_loss: the loss's incoming gradient, one fp32
+ * in device memory), computed in fp32 and rounded once to dtype; grad and dx 16-B aligned. */
+int lss_bce_logits_bwd(const void* grad, int32_t dtype, int64_t n, const float* grad_loss, void* dx, void* stream);
+
 /* Training-mode batch norm fused with an activation (and, for ReLU, a residual add), for
  * nn.BatchNorm2d followed by swish (EfficientNet-B0, src/models.py:68 and the MBConv blocks) or
  * ReLU (CamEncode.up1, BevEncode, src/models.py:15-34, 92-130):
@@ -110,8 +124,10 @@ int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layou
                float* save_mean, float* save_rstd, float* scale, float* shift, void* y, void* stream);
 
 /* Backward of lss_bn_fwd: dx (and dresidual = the gradient of the residual, nullable) of element
- * type dtype; dgamma, dbeta fp32 (nullable). y is the forward output (needed for ReLU). coef:
- * (C, 2) fp32 scratch. */
+ * type dtype; dgamma, dbeta fp32 (nullable). y is the forward output (needed for ReLU). With
+ * LSS_CONV_NHWC and a forward WITHOUT a residual, y may be NULL for ReLU: the kernels then recompute
+ * it from x and the saved scale / shift exactly as the forward rounded it (one tensor read less).
+ * coef: (C, 2) fp32 scratch. */
 int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int32_t layout, int32_t N, int32_t C,
                int32_t HW, const float* scale, const float* shift, const float* save_mean, const float* save_rstd,
                int32_t act, int32_t ngroups, float* partial, float* coef, float* dgamma, float* dbeta, void* dx,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 20
+#define LSS_ABI_VERSION 21
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;

@@ -18,7 +18,7 @@ DEBUG_LIB_PATH = os.path.join(_HERE, "liblss_hip_debug.so")  # LSS_DEBUG=1: devi
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 
 class Dims(ctypes.Structure):
@@ -89,6 +89,9 @@ SIGNATURES = {
     "lss_head1_bwd": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _p, _p]),
     "lss_scale_add": (ctypes.c_int, [_p, _p, ctypes.c_float, _p, ctypes.c_int64, ctypes.c_int64, _p, _p]),
     "lss_dropout": (ctypes.c_int, [_p, _i32, ctypes.c_int64, _p, ctypes.c_float, _p, _p, ctypes.c_int64, _p]),
+    "lss_bce_logits": (ctypes.c_int, [_p, _i32, _p, ctypes.c_int64, ctypes.c_float, _p, _p, _p, _p]),
+    "lss_bce_partials": (ctypes.c_int64, [ctypes.c_int64]),
+    "lss_bce_logits_bwd": (ctypes.c_int, [_p, _i32, ctypes.c_int64, _p, _p, _p]),
     "lss_pw_wrw_workspace_bytes": (ctypes.c_int64, [_i32, _i32, _i32, _i32]),
     "lss_pw_wrw": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _p, _i32, _p, ctypes.c_int64, _p]),
     "lss_pw_conv": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p]),

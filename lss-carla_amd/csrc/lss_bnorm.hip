@@ -38,7 +38,11 @@ namespace {
 using bf16 = __hip_bfloat16;
 constexpr int kBlock = 256;
 constexpr int kWave = 64;
-constexpr int kMaxGroupsNhwc = 4096;
+#ifndef LSS_BN_GMAX
+#define LSS_BN_GMAX 4096
+#endif
+constexpr int kMaxGroupsNhwc = 4096;  // partial groups the ABI accepts (NHWC)
+constexpr int kGroupsNhwc = LSS_BN_GMAX;  // groups lss_bn_groups picks at most (NHWC)
 
 __device__ __forceinline__ float ld(const float* p) { return *p; }
 __device__ __forceinline__ float ld(const bf16* p) { return __bfloat162float(*p); }
@@ -110,6 +114,15 @@ __device__ __forceinline__ float grad_pre(float dy, float y, float z, int act) {
         return dy * s * (1.f + z * (1.f - s));
     }
     return dy;
+}
+
+// the forward's stored ReLU output for a pre-activation z without a residual: relu(z) rounded to T
+// (the NHWC backward's stand-in for y when the caller passes none -- the same value the forward's
+// apply wrote, so the mask y > 0 is the same; one tensor read less in both backward passes)
+template <typename T> __device__ __forceinline__ float relu_out(float z);
+template <> __device__ __forceinline__ float relu_out<float>(float z) { return fmaxf(z, 0.f); }
+template <> __device__ __forceinline__ float relu_out<bf16>(float z) {
+    return __bfloat162float(__float2bfloat16(fmaxf(z, 0.f)));
 }
 
 struct BnGeo {
@@ -669,16 +682,40 @@ __global__ __launch_bounds__(kBlock) void k_bn_stats_nhwc(const T* __restrict__ 
 }
 
 // fold kernels (NHWC): one wave per channel, lanes over groups, fixed order
+// A lane's pairs of one channel's partials (groups lane, lane + 64, ...) added in that order, kFoldBatch
+// loads in flight at a time: the loop that loaded one pair per iteration waited a cache round trip per
+// 64 groups (up to 64 of them in sequence: a 14-19 us fold at 2,500-4,096 groups).
+constexpr int kFoldBatch = 16;
+__device__ __forceinline__ void fold_lane_pairs(const float* __restrict__ p, int G, int lane, float& s1, float& s2) {
+    int q = lane;
+    for (; q + (kFoldBatch - 1) * kWave < G; q += kFoldBatch * kWave) {
+        float2 v[kFoldBatch];
+#pragma unroll
+        for (int i = 0; i < kFoldBatch; ++i) v[i] = *reinterpret_cast<const float2*>(p + 2 * (q + i * kWave));
+#pragma unroll
+        for (int i = 0; i < kFoldBatch; ++i) {
+            s1 += v[i].x;
+            s2 += v[i].y;
+        }
+    }
+    float2 v[kFoldBatch];
+#pragma unroll
+    for (int i = 0; i < kFoldBatch; ++i)
+        v[i] = q + i * kWave < G ? *reinterpret_cast<const float2*>(p + 2 * (q + i * kWave)) : make_float2(0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < kFoldBatch; ++i)
+        if (q + i * kWave < G) {
+            s1 += v[i].x;
+            s2 += v[i].y;
+        }
+}
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_bn_fold_nhwc(const float* __restrict__ partial, int G, const T* __restrict__ x,
                                                          BnGeo g, BnParams P) {
     const int c = blockIdx.x * (kBlock / kWave) + (int)threadIdx.x / kWave;
     if (c >= g.C) return;
     float s1 = 0.f, s2 = 0.f;
-    for (int q = threadIdx.x & (kWave - 1); q < G; q += kWave) {
-        s1 += partial[((size_t)c * G + q) * 2];
-        s2 += partial[((size_t)c * G + q) * 2 + 1];
-    }
+    fold_lane_pairs(partial + (size_t)c * G * 2, G, (int)threadIdx.x & (kWave - 1), s1, s2);
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
         s1 += __shfl_xor(s1, o, kWave);
@@ -694,10 +731,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_fold_nhwc(const float* __rest
     const int c = blockIdx.x * (kBlock / kWave) + (int)threadIdx.x / kWave;
     if (c >= g.C) return;
     float sg = 0.f, sgx = 0.f;
-    for (int q = threadIdx.x & (kWave - 1); q < G; q += kWave) {
-        sg += partial[((size_t)c * G + q) * 2];
-        sgx += partial[((size_t)c * G + q) * 2 + 1];
-    }
+    fold_lane_pairs(partial + (size_t)c * G * 2, G, (int)threadIdx.x & (kWave - 1), sg, sgx);
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
         sg += __shfl_xor(sg, o, kWave);
@@ -765,14 +799,15 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_stats_nhwc(const T* __restric
             if (idx[u] < 0) continue;
             ldv<8>(dy + idx[u], d[u]);
             ldv<8>(x + idx[u], xv[u]);
-            if (relu) ldv<8>(y + idx[u], yv[u]);
+            if (relu && y) ldv<8>(y + idx[u], yv[u]);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (idx[u] < 0) continue;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float gr = grad_pre(d[u][j], relu ? yv[u][j] : 0.f, fmaf(xv[u][j], sc[j], sh[j]), act);
+                const float z = fmaf(xv[u][j], sc[j], sh[j]);
+                const float gr = grad_pre(d[u][j], relu ? (y ? yv[u][j] : relu_out<T>(z)) : 0.f, z, act);
                 a[j] += gr;
                 b[j] = fmaf(gr, (xv[u][j] - mean[j]) * rstd[j], b[j]);
             }
@@ -802,12 +837,13 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_apply_nhwc(const T* __restric
         float d[8], xv[8], yv[8], o[8], gr[8];
         ldv<8>(dy + i, d);
         ldv<8>(x + i, xv);
-        if (act == LSS_ACT_RELU) ldv<8>(y + i, yv);
+        if (act == LSS_ACT_RELU && y) ldv<8>(y + i, yv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int c = c0 + j;
             const float sc = s_dyn[2 * g.C + c];
-            gr[j] = grad_pre(d[j], act == LSS_ACT_RELU ? yv[j] : 0.f, fmaf(xv[j], sc, s_dyn[3 * g.C + c]), act);
+            const float z = fmaf(xv[j], sc, s_dyn[3 * g.C + c]);
+            gr[j] = grad_pre(d[j], act == LSS_ACT_RELU ? (y ? yv[j] : relu_out<T>(z)) : 0.f, z, act);
             o[j] = sc * (gr[j] - s_dyn[4 * g.C + c] - (xv[j] - s_dyn[c]) * s_dyn[g.C + c] * s_dyn[5 * g.C + c]);
         }
         stv<8>(dx + i, o);
@@ -852,7 +888,7 @@ int lss_bn_groups(int32_t N, int32_t C, int32_t HW, int32_t layout) {
     const long per_chan = (long)N * HW;
     if (layout == LSS_CONV_NHWC) {
         const long g = per_chan * C / 8192;  // ~8 K elements (32 per thread) per block
-        return (int)(g < 1 ? 1 : (g > kMaxGroupsNhwc ? kMaxGroupsNhwc : g));
+        return (int)(g < 1 ? 1 : (g > kGroupsNhwc ? kGroupsNhwc : g));
     }
     const long g = per_chan / 8192;  // ~8 K elements of one channel per block
     return (int)(g < 1 ? 1 : (g > N ? N : g));
@@ -934,7 +970,7 @@ int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int3
         !bn_ok(g, layout))
         return LSS_CONV_EINVAL;
     if (save_rstd != save_mean + C || scale != save_mean + 2 * C || shift != save_mean + 3 * C) return LSS_CONV_EINVAL;
-    if (act == LSS_ACT_RELU && !y) return LSS_CONV_EINVAL;
+    if (act == LSS_ACT_RELU && !y && layout != LSS_CONV_NHWC) return LSS_CONV_EINVAL;
     if (act != LSS_ACT_NONE && act != LSS_ACT_RELU && act != LSS_ACT_SWISH) return LSS_CONV_EINVAL;
     if (layout == LSS_CONV_NHWC && ngroups > kMaxGroupsNhwc) return LSS_CONV_EINVAL;
     hipStream_t s = (hipStream_t)stream;

@@ -1125,6 +1125,118 @@ __global__ __launch_bounds__(G == 1 ? 256 : 1024) void k_pw_wrw_reduce(const flo
         if (e + k < E) st(dw + e + k, o[k]);
 }
 
+
+__device__ __forceinline__ void ldv8(const float* p, float* o) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+__device__ __forceinline__ void ldv8(const bf16* p, float* o) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        o[2 * i] = __uint_as_float(w[i] << 16);
+        o[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+}
+__device__ __forceinline__ void stv8(float* p, const float* v) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void stv8(bf16* p, const float* v) {
+    bf16 b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = __float2bfloat16(v[i]);
+    *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(b);
+}
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(bf16* p, float v) { *p = __float2bfloat16(v); }
+
+// ---- SimpleLoss (src/tools.py:222-230): BCEWithLogitsLoss(pos_weight), mean over the n elements,
+// with its input gradient computed in the same pass. Per element (torch's formula for pos_weight):
+//   lw = 1 + (pw - 1) t,  l = (1 - t) x + lw (log1p(exp(-|x|)) + max(-x, 0)),
+//   dl/dx = lw sigmoid(x) - pw t = (1 - t) sigmoid(x) - pw t sigmoid(-x)
+// Thread = 8 consecutive elements; block sums in a fixed order (wave butterflies, then the 4 waves
+// in order) into partial[block]; k_bce_total folds the partials in block order. fp32 arithmetic for
+// fp32 and bf16 logits (a bf16 input is the same as its exact fp32 cast); the gradient (times 1 / n)
+// is written in the logits' type.
+constexpr int kBceVpt = 8;
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_bce_fwd(const T* __restrict__ x, const float* __restrict__ t, long long n,
+                                                    float pw, float inv_n, float* __restrict__ partial,
+                                                    T* __restrict__ grad) {
+    __shared__ float s_w[kBlock / kWave];
+    const long long i0 = ((long long)blockIdx.x * kBlock + threadIdx.x) * kBceVpt;
+    float xv[kBceVpt], tv[kBceVpt], gv[kBceVpt];
+    const bool full = i0 + kBceVpt <= n;
+    if (full) {
+        ldv8(x + i0, xv);
+        const float4 a = *reinterpret_cast<const float4*>(t + i0), b = *reinterpret_cast<const float4*>(t + i0 + 4);
+        tv[0] = a.x; tv[1] = a.y; tv[2] = a.z; tv[3] = a.w; tv[4] = b.x; tv[5] = b.y; tv[6] = b.z; tv[7] = b.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < kBceVpt; ++j) {
+            xv[j] = i0 + j < n ? ld(x + i0 + j) : 0.f;
+            tv[j] = i0 + j < n ? t[i0 + j] : 0.f;
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < kBceVpt; ++j) {
+        const float xx = xv[j], tt = tv[j];
+        const float lw = fmaf(pw - 1.f, tt, 1.f);
+        const float e = expf(-fabsf(xx));
+        const float l = (1.f - tt) * xx + lw * (log1pf(e) + fmaxf(-xx, 0.f));
+        // lw sigmoid(x) - pw t = (1 - t) sigmoid(x) - pw t sigmoid(-x): no cancellation for saturated x
+        const float sp = 1.f / (1.f + e), sn = e / (1.f + e);  // sigmoid(|x|), sigmoid(-|x|)
+        const float sx = xx >= 0.f ? sp : sn, smx = xx >= 0.f ? sn : sp;
+        gv[j] = ((1.f - tt) * sx - pw * tt * smx) * inv_n;
+        if (i0 + j < n) s += l;
+    }
+    if (full) stv8(grad + i0, gv);
+    else {
+#pragma unroll
+        for (int j = 0; j < kBceVpt; ++j)
+            if (i0 + j < n) st1(grad + i0 + j, gv[j]);
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0) s_w[threadIdx.x / kWave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float b = 0.f;
+#pragma unroll
+        for (int w = 0; w < kBlock / kWave; ++w) b += s_w[w];
+        partial[blockIdx.x] = b;
+    }
+}
+
+// dx = grad * gout[0] (the incoming gradient of the loss, read on the device), rounded once to T
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_bce_bwd(const T* __restrict__ grad, long long n, const float* __restrict__ gout,
+                                                    T* __restrict__ dx) {
+    const long long i0 = ((long long)blockIdx.x * kBlock + threadIdx.x) * kBceVpt;
+    const float gs = gout[0];
+    float v[kBceVpt];
+    if (i0 + kBceVpt <= n) {
+        ldv8(grad + i0, v);
+#pragma unroll
+        for (int j = 0; j < kBceVpt; ++j) v[j] *= gs;
+        stv8(dx + i0, v);
+    } else {
+        for (long long i = i0; i < n; ++i) st1(dx + i, ld(grad + i) * gs);
+    }
+}
+
+// loss = (sum of the block partials, lanes strided over blocks then a fixed butterfly) / n
+__global__ __launch_bounds__(kWave) void k_bce_total(const float* __restrict__ partial, int nb, float inv_n,
+                                                     float* __restrict__ loss) {
+    float s = 0.f;
+    for (int b = threadIdx.x; b < nb; b += kWave) s += partial[b];
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
+    if (threadIdx.x == 0) loss[0] = s * inv_n;
+}
 }  // namespace
 
 extern "C" {
@@ -1323,5 +1435,47 @@ int lss_dropout(const void* x, int32_t dtype, int64_t n, const uint64_t* seed, f
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
+
+int lss_bce_logits(const void* x, int32_t dtype, const float* target, int64_t n, float pos_weight, float* partial,
+                   float* loss, void* grad, void* stream) {
+    const int esz = dtype == LSS_CONV_BF16 ? 2 : dtype == LSS_CONV_F32 ? 4 : 0;
+    if (!x || !target || !partial || !loss || !grad || !esz || n <= 0 ||
+        ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad)) & 15) ||
+        (reinterpret_cast<uintptr_t>(target) & 15))
+        return LSS_CONV_EINVAL;
+    const long long nb = (n + (long long)kBlock * kBceVpt - 1) / ((long long)kBlock * kBceVpt);
+    if (nb > INT_MAX) return LSS_CONV_EINVAL;
+    const float inv_n = 1.0f / (float)n;
+    hipStream_t s = (hipStream_t)stream;
+    if (esz == 2)
+        hipLaunchKernelGGL(k_bce_fwd<bf16>, dim3((unsigned)nb), dim3(kBlock), 0, s, (const bf16*)x, target, (long long)n,
+                           pos_weight, inv_n, partial, (bf16*)grad);
+    else
+        hipLaunchKernelGGL(k_bce_fwd<float>, dim3((unsigned)nb), dim3(kBlock), 0, s, (const float*)x, target,
+                           (long long)n, pos_weight, inv_n, partial, (float*)grad);
+    hipLaunchKernelGGL(k_bce_total, dim3(1), dim3(kWave), 0, s, partial, (int)nb, inv_n, loss);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+int lss_bce_logits_bwd(const void* grad, int32_t dtype, int64_t n, const float* grad_loss, void* dx, void* stream) {
+    const int esz = dtype == LSS_CONV_BF16 ? 2 : dtype == LSS_CONV_F32 ? 4 : 0;
+    if (!grad || !grad_loss || !dx || !esz || n <= 0 ||
+        ((reinterpret_cast<uintptr_t>(grad) | reinterpret_cast<uintptr_t>(dx)) & 15))
+        return LSS_CONV_EINVAL;
+    const long long nb = (n + (long long)kBlock * kBceVpt - 1) / ((long long)kBlock * kBceVpt);
+    if (nb > INT_MAX) return LSS_CONV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (esz == 2)
+        hipLaunchKernelGGL(k_bce_bwd<bf16>, dim3((unsigned)nb), dim3(kBlock), 0, s, (const bf16*)grad, (long long)n,
+                           grad_loss, (bf16*)dx);
+    else
+        hipLaunchKernelGGL(k_bce_bwd<float>, dim3((unsigned)nb), dim3(kBlock), 0, s, (const float*)grad, (long long)n,
+                           grad_loss, (float*)dx);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+int64_t lss_bce_partials(int64_t n) { return (n + (int64_t)kBlock * kBceVpt - 1) / ((int64_t)kBlock * kBceVpt); }
 
 }  // extern "C"

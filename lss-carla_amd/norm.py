@@ -17,6 +17,9 @@ from torch import nn
 from . import _lib
 
 USE_HIP_BN = True
+# channels-last ReLU without a residual: the backward recomputes the output from x (lss_bn_bwd with
+# y = NULL) instead of keeping and re-reading it
+RECOMPUTE_RELU_Y = True
 ACT = {"none": 0, "relu": 1, "swish": 2}
 NCHW, NHWC = 0, 1
 
@@ -61,7 +64,10 @@ class _BnAct(torch.autograd.Function):
                                   _lib.ptr(rv), _lib.ptr(counter), act, groups, _lib.ptr(partial), _lib.ptr(stats[0]),
                                   _lib.ptr(stats[1]), _lib.ptr(stats[2]), _lib.ptr(stats[3]), _lib.ptr(y), st),
                    "lss_bn_fwd")
-        ctx.save_for_backward(x, y if act == ACT["relu"] else None, stats)
+        # ReLU's backward needs y; in channels-last without a residual the kernels recompute it from x
+        # (lss_bn_bwd), so y is neither kept nor read again
+        keep_y = act == ACT["relu"] and (layout == NCHW or residual is not None or not RECOMPUTE_RELU_Y)
+        ctx.save_for_backward(x, y if keep_y else None, stats)
         ctx.conf = (act, layout, groups, residual is not None)
         return y
 

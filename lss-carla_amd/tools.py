@@ -68,15 +68,60 @@ def cumsum_trick(x, geom_feats, ranks):
 
 
 # ----------------------------------------------------------------------------- loss / metrics
+class _BceLogits(torch.autograd.Function):
+    """BCEWithLogitsLoss(pos_weight), mean, on ``lss_bce_logits`` (include/lss_convs.h): the loss and
+    its input gradient in one pass plus a fixed-order fold of the block sums -- two launches where
+    torch's decomposition runs about twenty elementwise / reduction kernels per step. The backward
+    scales the stored gradient by the incoming one (``lss_bce_logits_bwd``, read on the device)."""
+
+    @staticmethod
+    def forward(ctx, x, target, pos_weight: float):
+        from . import _lib
+        lib = _lib.load()
+        n = x.numel()
+        partial = torch.empty(int(lib.lss_bce_partials(n)), device=x.device, dtype=torch.float32)
+        loss = torch.empty((), device=x.device, dtype=torch.float32)
+        grad = torch.empty_like(x)
+        _lib.check(lib.lss_bce_logits(_lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(target), n, float(pos_weight),
+                                      _lib.ptr(partial), _lib.ptr(loss), _lib.ptr(grad),
+                                      _lib.stream_handle(x.device)), "lss_bce_logits")
+        ctx.save_for_backward(grad)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import _lib
+        (grad,) = ctx.saved_tensors
+        g = g.float().contiguous()
+        dx = torch.empty_like(grad)
+        _lib.check(_lib.load().lss_bce_logits_bwd(_lib.ptr(grad), _lib.dtype_code(grad.dtype), grad.numel(),
+                                                  _lib.ptr(g), _lib.ptr(dx), _lib.stream_handle(grad.device)),
+                   "lss_bce_logits_bwd")
+        return dx, None, None
+
+
 class SimpleLoss(torch.nn.Module):
-    """BCE-with-logits with a positive-class weight (src/tools.py:222-230)."""
+    """BCE-with-logits with a positive-class weight (src/tools.py:222-230).
+
+    On the GPU (fp32 or bf16 logits, fp32 labels of the same shape, contiguous) the loss and its
+    gradient come from the fused ``lss_bce_logits`` kernel, computed in fp32 (a bf16 input gives the
+    loss of its exact fp32 cast); otherwise ``loss_fn`` (the reference's ``BCEWithLogitsLoss``). The
+    weight is the constructor's value (reading the module's device buffer back would synchronise)."""
+
+    computes_in_fp32 = True  # callers may pass bf16 logits without casting them first (train_step)
 
     def __init__(self, pos_weight: float):
         super().__init__()
         self.loss_fn = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([float(pos_weight)]))
+        self.pos_weight_value = float(pos_weight)
 
     def forward(self, ypred, ytgt):
-        return self.loss_fn(ypred, ytgt)
+        if (ypred.is_cuda and ypred.dtype in (torch.float32, torch.bfloat16) and ytgt.dtype == torch.float32
+                and ytgt.device == ypred.device and ytgt.shape == ypred.shape and ypred.is_contiguous()
+                and ytgt.is_contiguous() and ypred.data_ptr() % 16 == 0 and ytgt.data_ptr() % 16 == 0
+                and ypred.numel() > 0):
+            return _BceLogits.apply(ypred, ytgt, self.pos_weight_value)
+        return self.loss_fn(ypred.float() if ypred.dtype == torch.bfloat16 else ypred, ytgt)
 
 
 def get_batch_iou(preds: torch.Tensor, binimgs: torch.Tensor):

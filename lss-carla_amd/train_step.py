@@ -76,7 +76,8 @@ class TrainStep:
         with torch.autocast(dev_type, dtype=self.amp_dtype or torch.bfloat16, enabled=self.amp_dtype is not None,
                             cache_enabled=not capturing):
             preds = self.forward(*self.inputs)
-        loss = self.loss_fn(preds.float(), self.labels)
+        # (a loss that computes in fp32 itself, tools.SimpleLoss, takes the bf16 logits: no cast kernels)
+        loss = self.loss_fn(preds if getattr(self.loss_fn, "computes_in_fp32", False) else preds.float(), self.labels)
         loss.backward()
         if self.overlap:  # the collectives the hooks started: the update waits for them
             for w in self._works:

@@ -341,3 +341,56 @@ def test_drop_connect_add_eval_is_plain_add():
     r = torch.randn(4, 16, 4, 4, device=DEV).bfloat16()
     assert torch.equal(E.drop_connect_add(x, r, 0.2, False), x + r)
     assert torch.equal(E.drop_connect_add(x, r, None, True), x + r)
+
+
+# ----------------------------------------------------------------------------- BN backward without y
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_relu_nhwc_backward_recomputes_output(dtype):
+    """Channels-last ReLU without a residual: lss_bn_bwd with y = NULL (the output recomputed from x and
+    the saved scale / shift) gives the same bits as with the forward's y; at a shape with 2,500 partial
+    groups per channel (the fold's batched loads and its tail), and against torch's BN on the GPU."""
+    from lss_carla_amd import _lib
+    lib = _lib.load()
+    N, C, H, W = 4, 128, 200, 200
+    g = torch.Generator().manual_seed(11)
+    cl = torch.channels_last
+    x = (torch.randn(N, C, H, W, generator=g) + 0.3).to(dtype).to(DEV).contiguous(memory_format=cl)
+    dy = torch.randn(N, C, H, W, generator=g).to(dtype).to(DEV).contiguous(memory_format=cl)
+    bn = torch.nn.BatchNorm2d(C).to(DEV).train()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, generator=g) * 0.1)
+    xd = x.clone().requires_grad_(True)
+    y = Nm.bn_act(bn, xd, "relu")
+    y.backward(dy)
+    groups = int(lib.lss_bn_groups(N, C, H * W, Nm.NHWC))
+    assert groups > 64 * 16  # the fold's batched loop runs
+    # the same forward again for its saved statistics, then both backward forms through the C ABI
+    stats = torch.empty(4, C, device=DEV)
+    partial = torch.empty(C, groups, 2, device=DEV)
+    y2 = torch.empty_like(x)
+    st = _lib.stream_handle(DEV)
+    _lib.check(lib.lss_bn_fwd(_lib.ptr(x), None, _lib.dtype_code(dtype), Nm.NHWC, N, C, H * W, _lib.ptr(bn.weight),
+                              _lib.ptr(bn.bias), 1e-5, 0.0, None, None, None, Nm.ACT["relu"], groups,
+                              _lib.ptr(partial), _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
+                              _lib.ptr(stats[3]), _lib.ptr(y2), st), "fwd")
+    outs = []
+    for yy in (y2, None):
+        coef = torch.empty(C, 2, device=DEV)
+        dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        dx = torch.empty_like(x)
+        _lib.check(lib.lss_bn_bwd(_lib.ptr(dy), _lib.ptr(x), _lib.ptr(yy), _lib.dtype_code(dtype), Nm.NHWC, N, C, H * W,
+                                  _lib.ptr(stats[2]), _lib.ptr(stats[3]), _lib.ptr(stats[0]), _lib.ptr(stats[1]),
+                                  Nm.ACT["relu"], groups, _lib.ptr(partial), _lib.ptr(coef), _lib.ptr(dg), _lib.ptr(db),
+                                  _lib.ptr(dx), None, st), "bwd")
+        outs.append((dx, dg, db))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert torch.equal(outs[1][0], xd.grad)
+    # torch's fp32 BN + ReLU on the GPU
+    xr = x.float().requires_grad_(True)
+    ref = F.relu(F.batch_norm(xr, None, None, bn.weight.detach(), bn.bias.detach(), training=True, eps=1e-5))
+    ref.backward(dy.float())
+    tol = dict(rtol=1e-3, atol=1e-3) if dtype == torch.float32 else dict(rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(y.float(), ref.detach(), **tol)
+    torch.testing.assert_close(xd.grad.float(), xr.grad, **tol)
