@@ -851,6 +851,118 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_apply_nhwc(const T* __restric
     }
 }
 
+// Row-walking forms of the two apply passes (LSS_BN_ROWS, the default): block q of G takes the pixel rows
+// [M q / G, M (q+1) / G) like the statistics kernels, a thread keeps one channel octet, so its
+// per-channel coefficients sit in registers for all its rows (the grid-stride forms above re-read
+// them from LDS for every vector), and R rows' loads are in flight per iteration.
+#ifndef LSS_BN_ROWS
+#define LSS_BN_ROWS 1
+#endif
+template <int R, typename F>
+__device__ __forceinline__ void for_rows_nhwc(const BnGeo& g, int G, int q, F&& f) {
+    const int M = g.N * g.HW;
+    const int r0 = (int)((long)M * q / G), r1 = (int)((long)M * (q + 1) / G);
+    const int cg = g.C >> 3, step = kBlock / cg;
+    const int c0 = ((int)threadIdx.x % cg) * 8;
+    if ((int)threadIdx.x >= step * cg) return;
+    int r = r0 + (int)threadIdx.x / cg;
+    for (; r + (R - 1) * step < r1; r += R * step) {
+        int idx[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) idx[u] = (r + u * step) * g.C + c0;
+        f(idx, R);
+    }
+    for (; r < r1; r += step) {
+        int idx[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) idx[u] = r * g.C + c0;
+        f(idx, 1);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_apply_rows_nhwc(const T* __restrict__ x, const T* __restrict__ res, BnGeo g,
+                                                               const float* __restrict__ stats, int act,
+                                                               T* __restrict__ y) {
+    constexpr int R = 4;
+    const int c0 = ((int)threadIdx.x % (g.C >> 3)) * 8;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        sc[j] = stats[2 * g.C + c0 + j];
+        sh[j] = stats[3 * g.C + c0 + j];
+    }
+    for_rows_nhwc<R>(g, (int)gridDim.x, (int)blockIdx.x, [&](const int* idx, int n) {
+        float v[R][8], rv[R][8];
+#pragma unroll
+        for (int u = 0; u < R; ++u)
+            if (u < n) {
+                ldv<8>(x + idx[u], v[u]);
+                if (res) ldv<8>(res + idx[u], rv[u]);
+            }
+#pragma unroll
+        for (int u = 0; u < R; ++u)
+            if (u < n) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float z = fmaf(v[u][j], sc[j], sh[j]);
+                    if (res) z += rv[u][j];
+                    v[u][j] = act_fwd(z, act);
+                }
+                stv<8>(y + idx[u], v[u]);
+            }
+    });
+}
+
+// dx = scale g + B x + K with B = -scale rstd mean(g xhat), K = -scale (mean(g) - mean rstd mean(g xhat))
+// (the grid-stride form's scale (g - mean(g) - (x - mean) rstd mean(g xhat)) regrouped: 4 coefficients
+// per channel held in registers)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_bn_bwd_apply_rows_nhwc(const T* __restrict__ dy, const T* __restrict__ x,
+                                                                   const T* __restrict__ y, BnGeo g,
+                                                                   const float* __restrict__ stats,
+                                                                   const float* __restrict__ coef, int act,
+                                                                   T* __restrict__ dx, T* __restrict__ dres) {
+    constexpr int R = 2;
+    const int c0 = ((int)threadIdx.x % (g.C >> 3)) * 8;
+    float sc[8], sh[8], kb[8], kk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        const float mean = stats[c], rstd = stats[g.C + c];
+        sc[j] = stats[2 * g.C + c];
+        sh[j] = stats[3 * g.C + c];
+        const float mg = coef[2 * c], mgx = coef[2 * c + 1];
+        kb[j] = -sc[j] * rstd * mgx;
+        kk[j] = -sc[j] * (mg - mean * rstd * mgx);
+    }
+    const bool relu = act == LSS_ACT_RELU;
+    for_rows_nhwc<R>(g, (int)gridDim.x, (int)blockIdx.x, [&](const int* idx, int n) {
+        float d[R][8], xv[R][8], yv[R][8];
+#pragma unroll
+        for (int u = 0; u < R; ++u)
+            if (u < n) {
+                ldv<8>(dy + idx[u], d[u]);
+                ldv<8>(x + idx[u], xv[u]);
+                if (relu && y) ldv<8>(y + idx[u], yv[u]);
+            }
+#pragma unroll
+        for (int u = 0; u < R; ++u)
+            if (u < n) {
+                float o[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float z = fmaf(xv[u][j], sc[j], sh[j]);
+                    const float gr = grad_pre(d[u][j], relu ? (y ? yv[u][j] : relu_out<T>(z)) : 0.f, z, act);
+                    o[j] = fmaf(sc[j], gr, fmaf(kb[j], xv[u][j], kk[j]));
+                    d[u][j] = gr;
+                }
+                stv<8>(dx + idx[u], o);
+                if (dres) stv<8>(dres + idx[u], d[u]);
+            }
+    });
+}
+
 // ============================================================================= host side
 inline int launch_status() {
     const hipError_t e = hipGetLastError();
@@ -918,8 +1030,12 @@ int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layou
             hipLaunchKernelGGL(k_bn_stats_nhwc<T>, dim3(G), dim3(kBlock), kNhwcStatsLds * C * sizeof(float), s, xx, \
                                g, G, partial);                                                                     \
             hipLaunchKernelGGL(k_bn_fold_nhwc<T>, dim3((C + 3) / 4), dim3(kBlock), 0, s, partial, G, xx, g, P);   \
-            hipLaunchKernelGGL(k_bn_apply_nhwc<T>, dim3(apply_blocks(g)), dim3(kBlock), lds, s, xx, rr, g,        \
-                               save_mean, (int)act, yy);                                                           \
+            if (LSS_BN_ROWS)                                                                                       \
+                hipLaunchKernelGGL(k_bn_apply_rows_nhwc<T>, dim3(apply_blocks(g)), dim3(kBlock), 0, s, xx, rr, g,  \
+                                   save_mean, (int)act, yy);                                                       \
+            else                                                                                                   \
+                hipLaunchKernelGGL(k_bn_apply_nhwc<T>, dim3(apply_blocks(g)), dim3(kBlock), lds, s, xx, rr, g,    \
+                                   save_mean, (int)act, yy);                                                       \
         } else {                                                                                                   \
             const int V = vec_nchw(HW);                                                                            \
             const dim3 gr(C * G), bl(kBlock);                                                                      \
@@ -988,8 +1104,12 @@ int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int3
                                g, G, stats, (int)act, partial);                                                    \
             hipLaunchKernelGGL(k_bn_bwd_fold_nhwc, dim3((C + 3) / 4), dim3(kBlock), 0, s, partial, G, g, dgamma,  \
                                dbeta, coef);                                                                       \
-            hipLaunchKernelGGL(k_bn_bwd_apply_nhwc<T>, dim3(apply_blocks(g)), dim3(kBlock), 6 * C * sizeof(float), \
-                               s, d, xx, yy, g, stats, coef, (int)act, o, orr);                                    \
+            if (LSS_BN_ROWS)                                                                                       \
+                hipLaunchKernelGGL(k_bn_bwd_apply_rows_nhwc<T>, dim3(apply_blocks(g)), dim3(kBlock), 0, s, d, xx, yy, \
+                                   g, stats, coef, (int)act, o, orr);                                              \
+            else                                                                                                   \
+                hipLaunchKernelGGL(k_bn_bwd_apply_nhwc<T>, dim3(apply_blocks(g)), dim3(kBlock), 6 * C * sizeof(float), \
+                                   s, d, xx, yy, g, stats, coef, (int)act, o, orr);                                \
         } else {                                                                                                   \
             const int V = vec_nchw(HW);                                                                            \
             const dim3 gr(C * G), bl(kBlock);                                                                      \
