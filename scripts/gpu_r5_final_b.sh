@@ -1,9 +1,9 @@
-# Round 5 evidence at HEAD (ABI 20: lss_dropout, lss_pw_wrw, lss_pw_conv): GPU suite, smoke, the default
+# Round 5 evidence at HEAD: GPU suite, smoke, the default
 # bench line (c3, CPU baseline, PMC traffic, in-graph splat + backward), and a rocprofv3 --kernel-trace --stats
 # run of the same bench (per-kernel summary, hot path per step, whole step by kernel).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/r5final_b; mkdir -p $OUT
+OUT=gpurun_out/${R5OUT:-r5final_b}; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread \
   > $OUT/gpu_tests.log 2>&1; trc=$?
 tail -3 $OUT/gpu_tests.log; echo "tests rc=$trc"
