@@ -105,6 +105,10 @@ int64_t lss_bce_partials(int64_t n);
  * in device memory), computed in fp32 and rounded once to dtype; grad and dx 16-B aligned. */
 int lss_bce_logits_bwd(const void* grad, int32_t dtype, int64_t n, const float* grad_loss, void* dx, void* stream);
 
+/* out[c] = sum over (n, pixel) of x[n][c][pixel] (fp32, fixed order), x (N, C, HW) NCHW fp32 or bf16: the
+ * bias gradient of the fused lift's depthnet conv (src/models.py:47) from d(logits). One launch. */
+int lss_channel_sums(const void* x, int32_t dtype, int32_t N, int32_t C, int32_t HW, float* out, void* stream);
+
 /* Training-mode batch norm fused with an activation (and, for ReLU, a residual add), for
  * nn.BatchNorm2d followed by swish (EfficientNet-B0, src/models.py:68 and the MBConv blocks) or
  * ReLU (CamEncode.up1, BevEncode, src/models.py:15-34, 92-130):

@@ -1228,6 +1228,42 @@ __global__ __launch_bounds__(kBlock) void k_bce_bwd(const T* __restrict__ grad, 
     }
 }
 
+// Per-channel sums of an NCHW tensor (the depthnet bias gradient from d(logits), src/models.py:47):
+// block = channel, the (image, pixel) elements strided over the threads, 4 loads in flight per thread,
+// then a fixed-order block reduction (deterministic).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_channel_sums(const T* __restrict__ x, int N, int C, int HW,
+                                                         float* __restrict__ out) {
+    __shared__ float s_w[kBlock / kWave];
+    const int c = blockIdx.x;
+    const int total = N * HW;
+    float s = 0.f;
+    int e = threadIdx.x;
+    for (; e + 3 * kBlock < total; e += 4 * kBlock) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = e + u * kBlock, n = i / HW, p = i - n * HW;
+            v[u] = ld(x + ((size_t)n * C + c) * HW + p);
+        }
+        s += (v[0] + v[1]) + (v[2] + v[3]);
+    }
+    for (; e < total; e += kBlock) {
+        const int n = e / HW, p = e - n * HW;
+        s += ld(x + ((size_t)n * C + c) * HW + p);
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0) s_w[threadIdx.x / kWave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float b = 0.f;
+#pragma unroll
+        for (int w = 0; w < kBlock / kWave; ++w) b += s_w[w];
+        out[c] = b;
+    }
+}
+
 // loss = (sum of the block partials, lanes strided over blocks then a fixed butterfly) / n
 __global__ __launch_bounds__(kWave) void k_bce_total(const float* __restrict__ partial, int nb, float inv_n,
                                                      float* __restrict__ loss) {
@@ -1472,6 +1508,19 @@ int lss_bce_logits_bwd(const void* grad, int32_t dtype, int64_t n, const float* 
     else
         hipLaunchKernelGGL(k_bce_bwd<float>, dim3((unsigned)nb), dim3(kBlock), 0, s, (const float*)grad, (long long)n,
                            grad_loss, (float*)dx);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+int lss_channel_sums(const void* x, int32_t dtype, int32_t N, int32_t C, int32_t HW, float* out, void* stream) {
+    if (!x || !out || N <= 0 || C <= 0 || HW <= 0 || (long long)N * C * HW >= INT_MAX ||
+        (dtype != LSS_CONV_BF16 && dtype != LSS_CONV_F32))
+        return LSS_CONV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == LSS_CONV_BF16)
+        hipLaunchKernelGGL(k_channel_sums<bf16>, dim3(C), dim3(kBlock), 0, s, (const bf16*)x, N, C, HW, out);
+    else
+        hipLaunchKernelGGL(k_channel_sums<float>, dim3(C), dim3(kBlock), 0, s, (const float*)x, N, C, HW, out);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }

@@ -478,6 +478,15 @@ def lift_splat(depthnet_out: torch.Tensor, plan: SplatPlan, out_dtype: torch.dty
     return LiftSplat.apply(depthnet_out, plan, out_dtype, layout)
 
 
+def _wgrad_splits(npix: int) -> int:
+    """Slices of the pixel (reduction) axis for the depthnet weight gradient's batched GEMM: up to 16,
+    each a whole number of pixels."""
+    for s in (16, 8, 4, 2):
+        if npix % s == 0 and npix // s >= 256:
+            return s
+    return 1
+
+
 # ----------------------------------------------------------------------------- autograd: depthnet + lift + splat
 class DepthnetLiftSplat(torch.autograd.Function):
     """depthnet(feat) -> lift -> splat in two kernels: lss_depthnet_lift (the 1x1 conv on MFMA fused
@@ -578,9 +587,19 @@ class DepthnetLiftSplat(torch.autograd.Function):
             if need[0]:
                 d_feat = torch.mm(dd, w2).view(B * N, H, W, K).permute(0, 3, 1, 2)  # channels-last
             if need[1]:
-                d_w = torch.mm(dd.t(), fm).view(weight.shape).to(weight.dtype)
+                # split-K as a batched GEMM: one (O x npix) x (npix x K) product gives hipBLASLt only
+                # (O / 64) x (K / 64) = 16 tiles for 8,448-long dot products (76 us at c3); KSPLIT slices of
+                # the pixels fill the chip, their bf16 partials summed in fp32 (slice order)
+                S = _wgrad_splits(npix)
+                part = torch.bmm(dd.view(S, npix // S, O).transpose(1, 2), fm.view(S, npix // S, K))
+                d_w = part.sum(0, dtype=torch.float32).view(weight.shape).to(weight.dtype)
             if need[2]:
-                d_b = dd.float().sum(0).to(weight.dtype)
+                # per-channel sums straight from the NCHW d(logits) (torch's dim-0 reduction of the
+                # pixel-major copy ran on 128 threads: 89 us at c3)
+                d_b32 = torch.empty(O, device=d_dn.device, dtype=torch.float32)
+                _lib.check(lib.lss_channel_sums(_lib.ptr(d_dn), _lib.BF16, B * N, O, H * W, _lib.ptr(d_b32),
+                                                _lib.stream_handle(d_dn.device)), "lss_channel_sums")
+                d_b = d_b32.to(weight.dtype)
             return d_feat, d_w, d_b, None, None, None, None
         d_feat, d_w, d_b = torch.ops.aten.convolution_backward(
             d_dn, feat, weight, [weight.shape[0]], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
