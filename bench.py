@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--bn-relu-y", default="recompute", choices=("recompute", "keep"),
                     help="channels-last BN + ReLU without a residual: the backward recomputes the output from x "
                          "or keeps and re-reads it")
+    ap.add_argument("--hip-adam", type=int, default=1,
+                    help="clip_grad_norm_ + Adam as two lss_clip_adam launches (0: torch's foreach norm and fused Adam)")
     ap.add_argument("--hip-pw", type=int, default=2,
                     help="trunk 1x1 convs: 2 = forward/backward-data on lss_pw_conv and weight gradients on lss_pw_wrw, "
                          "1 = lss_pw_wrw only, 0 = MIOpen")
@@ -317,7 +319,7 @@ def measure_in_graph(args) -> dict | None:
            "--profile-steps", "0", "--pmc-traffic", "0", "--cpu-baseline", "0", "--in-graph-prof", "0",
            "--mode", args.mode]
     # the rest of this run's configuration, so the child measures the same step
-    for flag in ("miopen_find", "hip_bn", "bn_relu_y", "fuse_depthnet", "hip_dropout", "hip_pw", "plan_at", "trunk_channels_last", "param_groups",
+    for flag in ("miopen_find", "hip_bn", "bn_relu_y", "hip_adam", "fuse_depthnet", "hip_dropout", "hip_pw", "plan_at", "trunk_channels_last", "param_groups",
                  "flat_params", "overlap_all_reduce", "dw_impl"):
         cmd += ["--" + flag.replace("_", "-"), str(getattr(args, flag))]
     try:
@@ -470,6 +472,8 @@ def build_model(args, dev, gc, dac):
     from lss_carla_amd import norm, models
     norm.USE_HIP_BN = bool(args.hip_bn)
     norm.RECOMPUTE_RELU_Y = args.bn_relu_y == "recompute"
+    from lss_carla_amd import optim as lss_optim
+    lss_optim.USE_HIP_ADAM = bool(args.hip_adam)
     models.USE_HIP_DROPOUT = bool(args.hip_dropout)
     models.PLAN_AT = args.plan_at
     from lss_carla_amd import efficientnet

@@ -109,6 +109,19 @@ int lss_bce_logits_bwd(const void* grad, int32_t dtype, int64_t n, const float* 
  * bias gradient of the fused lift's depthnet conv (src/models.py:47) from d(logits). One launch. */
 int lss_channel_sums(const void* x, int32_t dtype, int32_t N, int32_t C, int32_t HW, float* out, void* stream);
 
+/* The training step's update (train_simbev.py:245-248): clip_grad_norm_(params, max_norm) fused with
+ * torch.optim.Adam (L2 weight_decay added to the clipped gradient, no amsgrad) over `count` fp32 tensors
+ * (params[k], grads[k], exp_avg[k], exp_avg_sq[k]: numel[k] elements each; step[k]: the tensor's
+ * device-resident fp32 step count, advanced by one; all distinct). The clip factor is
+ * min(max_norm / (||all grads||_2 + 1e-6), 1); the gradients are not modified. partial:
+ * lss_clip_adam_partials() fp32 scratch. Two launches, no host synchronisation (graph-capturable);
+ * deterministic. */
+#define LSS_ADAM_MAX_TENSORS 32
+int lss_clip_adam_partials(void);
+int lss_clip_adam(int32_t count, float* const* params, const float* const* grads, float* const* exp_avg,
+                  float* const* exp_avg_sq, float* const* step, const int64_t* numel, float max_norm, float lr,
+                  float beta1, float beta2, float eps, float weight_decay, float* partial, void* stream);
+
 /* Training-mode batch norm fused with an activation (and, for ReLU, a residual add), for
  * nn.BatchNorm2d followed by swish (EfficientNet-B0, src/models.py:68 and the MBConv blocks) or
  * ReLU (CamEncode.up1, BevEncode, src/models.py:15-34, 92-130):

@@ -92,6 +92,9 @@ SIGNATURES = {
     "lss_bce_logits": (ctypes.c_int, [_p, _i32, _p, ctypes.c_int64, ctypes.c_float, _p, _p, _p, _p]),
     "lss_bce_partials": (ctypes.c_int64, [ctypes.c_int64]),
     "lss_channel_sums": (ctypes.c_int, [_p, _i32, _i32, _i32, _i32, _p, _p]),
+    "lss_clip_adam_partials": (ctypes.c_int, []),
+    "lss_clip_adam": (ctypes.c_int, [_i32, _p, _p, _p, _p, _p, _p, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                     ctypes.c_float, ctypes.c_float, ctypes.c_float, _p, _p]),
     "lss_bce_logits_bwd": (ctypes.c_int, [_p, _i32, ctypes.c_int64, _p, _p, _p]),
     "lss_pw_wrw_workspace_bytes": (ctypes.c_int64, [_i32, _i32, _i32, _i32]),
     "lss_pw_wrw": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _p, _i32, _p, ctypes.c_int64, _p]),

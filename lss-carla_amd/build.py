@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("lss_hip.hip", "lss_convs.hip", "lss_bnorm.hip",
                                                             "lss_resample.hip", "lss_se.hip", "lss_simbev.hip",
-                                                            "lss_ceiling.hip")]
+                                                            "lss_ceiling.hip", "lss_optim.hip")]
 HEADERS = [os.path.join(REPO, "include", h) for h in ("lss_hip.h", "lss_convs.h", "lss_simbev.h")]
 OUT = os.path.join(HERE, "liblss_hip.so")
 # LSS_DEBUG build: every data-derived index checked on the device (include/lss_hip.h, lss_debug_status);

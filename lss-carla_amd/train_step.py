@@ -113,6 +113,12 @@ class TrainStep:
             for p in self.params:
                 if p.grad is not None:
                     p.grad.mul_(1.0 / self.world)
+        from . import optim
+        if optim.supported(self.opt, self.params):  # both in two launches on the GPU (lss_clip_adam)
+            if getattr(self, "_clip_adam", None) is None or self._clip_adam.opt is not self.opt:
+                self._clip_adam = optim.ClipAdam(self.opt)
+            self._clip_adam.step(self.max_grad_norm)
+            return
         torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)
         self.opt.step()
 

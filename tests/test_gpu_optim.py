@@ -1,0 +1,72 @@
+"""lss_clip_adam (optim.ClipAdam) vs torch.nn.utils.clip_grad_norm_ + torch.optim.Adam (train_simbev.py:245-248):
+several steps over tensors of ragged sizes, with and without active clipping, L2 weight decay; the state
+tensors torch would keep; graph capture."""
+import pytest
+import torch
+
+from lss_carla_amd import optim
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+SIZES = [1, 3, 4, 1021, 4096, 70001, 5]
+
+
+def _setup(seed):
+    g = torch.Generator().manual_seed(seed)
+    ps = [torch.randn(n, generator=g).to(DEV).requires_grad_(True) for n in SIZES]
+    return ps, g
+
+
+@pytest.mark.parametrize("scale,max_norm", [(10.0, 5.0), (1e-3, 5.0), (1.0, 0.5)])
+def test_clip_adam_matches_torch(scale, max_norm):
+    ps_a, g = _setup(1)
+    ps_b = [p.detach().clone().requires_grad_(True) for p in ps_a]
+    opt_a = torch.optim.Adam(ps_a, lr=1e-3, weight_decay=1e-7, fused=True, capturable=True)
+    opt_b = torch.optim.Adam(ps_b, lr=1e-3, weight_decay=1e-7, fused=True, capturable=True)
+    ca = optim.ClipAdam(opt_a)
+    for it in range(4):
+        grads = [torch.randn(p.shape, generator=g).to(DEV) * scale for p in ps_a]
+        for p, q, gr in zip(ps_a, ps_b, grads):
+            p.grad, q.grad = gr.clone(), gr.clone()
+        assert optim.supported(opt_a, ps_a)
+        ca.step(max_norm)
+        torch.nn.utils.clip_grad_norm_(ps_b, max_norm)
+        opt_b.step()
+        for p, q in zip(ps_a, ps_b):
+            torch.testing.assert_close(p.detach(), q.detach(), rtol=2e-5, atol=2e-7)
+    for p, q in zip(ps_a, ps_b):
+        sa, sb = opt_a.state[p], opt_b.state[q]
+        assert set(sa) == set(sb) and float(sa["step"]) == float(sb["step"]) == 4.0
+        assert sa["step"].dtype == sb["step"].dtype and sa["step"].device == sb["step"].device
+        torch.testing.assert_close(sa["exp_avg"], sb["exp_avg"], rtol=1e-5, atol=1e-8)
+        torch.testing.assert_close(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-5, atol=1e-10)
+
+
+def test_clip_adam_graph_replay_and_unsupported_cases():
+    ps, g = _setup(2)
+    opt = torch.optim.Adam(ps, lr=1e-3, fused=True, capturable=True)
+    ref = [p.detach().clone().requires_grad_(True) for p in ps]
+    opt_r = torch.optim.Adam(ref, lr=1e-3, fused=True, capturable=True)
+    grads = [torch.randn(p.shape, generator=g).to(DEV) for p in ps]
+    for p, q, gr in zip(ps, ref, grads):
+        p.grad, q.grad = gr.clone(), gr.clone()
+    ca = optim.ClipAdam(opt)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ca.step(5.0)  # state created eagerly before the capture, as TrainStep's warm-up does
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ca.step(5.0)
+    for _ in range(3):
+        graph.replay()
+    for _ in range(4):
+        torch.nn.utils.clip_grad_norm_(ref, 5.0)
+        opt_r.step()
+    for p, q in zip(ps, ref):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=2e-5, atol=2e-7)
+    assert float(opt.state[ps[0]]["step"]) == 4.0
+    assert not optim.supported(torch.optim.Adam(ps, lr=1e-3, amsgrad=True), ps)
+    assert not optim.supported(torch.optim.AdamW(ps, lr=1e-3), ps)
+    assert not optim.supported(opt, ps[:2])
