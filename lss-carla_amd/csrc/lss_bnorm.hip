@@ -592,20 +592,34 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_fused_reg_nchw(const bf16* __
 // A thread keeps one channel octet (kBlock % (C/8) == 0) and walks the block's pixels with a stride
 // of kBlock / (C/8) rows, four rows per iteration so four 16-byte loads are in flight; 32-bit
 // offsets (the host checks N*HW*C < 2^31).
-template <typename T, typename F>
-__device__ __forceinline__ void for_chunk_nhwc(const BnGeo& g, int G, int q, F&& f) {
+
+// f(idx, n) over the block's rows, R rows' loads in flight per iteration (n of the R row offsets valid)
+template <int R, typename F>
+__device__ __forceinline__ void for_rows_nhwc(const BnGeo& g, int G, int q, F&& f) {
     const int M = g.N * g.HW;
     const int r0 = (int)((long)M * q / G), r1 = (int)((long)M * (q + 1) / G);
-    const int cg = g.C >> 3;
-    const int step = kBlock / cg;
+    const int cg = g.C >> 3, step = kBlock / cg;
     const int c0 = ((int)threadIdx.x % cg) * 8;
+    if ((int)threadIdx.x >= step * cg) return;
     int r = r0 + (int)threadIdx.x / cg;
-    for (; r + 3 * step < r1; r += 4 * step) {
-        f(r * g.C + c0, (r + step) * g.C + c0, (r + 2 * step) * g.C + c0, (r + 3 * step) * g.C + c0);
+    for (; r + (R - 1) * step < r1; r += R * step) {
+        int idx[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) idx[u] = (r + u * step) * g.C + c0;
+        f(idx, R);
     }
-    for (; r < r1; r += step) f(r * g.C + c0, -1, -1, -1);
+    for (; r < r1; r += step) {
+        int idx[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) idx[u] = r * g.C + c0;
+        f(idx, 1);
+    }
 }
 
+// rows in flight per thread in the statistics kernels
+#ifndef LSS_BN_STATS_R
+#define LSS_BN_STATS_R 4
+#endif
 // per-thread 8-channel sums -> per-channel block sums -> partial[c][q][2]. The threads sharing a channel
 // octet are lane, lane + cg, ... (cg = C / 8 divides kBlock, a power of two): a butterfly over those
 // lanes inside each wave, then the waves' rows in LDS ([wave][C][2], zero where a wave holds none of
@@ -661,15 +675,15 @@ __global__ __launch_bounds__(kBlock) void k_bn_stats_nhwc(const T* __restrict__ 
     float k[8];
     ldv<8>(x + c0, k);  // first pixel: the shifts
     float a[8] = {}, b[8] = {};
-    for_chunk_nhwc<T>(g, G, blockIdx.x, [&](int i0, int i1, int i2, int i3) {
-        const int idx[4] = {i0, i1, i2, i3};
-        float v[4][8];
+    constexpr int R = LSS_BN_STATS_R;
+    for_rows_nhwc<R>(g, G, blockIdx.x, [&](const int* idx, int n) {
+        float v[R][8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (idx[u] >= 0) ldv<8>(x + idx[u], v[u]);
+        for (int u = 0; u < R; ++u)
+            if (u < n) ldv<8>(x + idx[u], v[u]);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (idx[u] < 0) continue;
+        for (int u = 0; u < R; ++u) {
+            if (u >= n) continue;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float d = v[u][j] - k[j];
@@ -791,19 +805,19 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_stats_nhwc(const T* __restric
     }
     float a[8] = {}, b[8] = {};
     const bool relu = act == LSS_ACT_RELU;
-    for_chunk_nhwc<T>(g, G, blockIdx.x, [&](int i0, int i1, int i2, int i3) {
-        const int idx[4] = {i0, i1, i2, i3};
-        float d[4][8], xv[4][8], yv[4][8];
+    constexpr int R = LSS_BN_STATS_R;
+    for_rows_nhwc<R>(g, G, blockIdx.x, [&](const int* idx, int n) {
+        float d[R][8], xv[R][8], yv[R][8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (idx[u] < 0) continue;
+        for (int u = 0; u < R; ++u) {
+            if (u >= n) continue;
             ldv<8>(dy + idx[u], d[u]);
             ldv<8>(x + idx[u], xv[u]);
             if (relu && y) ldv<8>(y + idx[u], yv[u]);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (idx[u] < 0) continue;
+        for (int u = 0; u < R; ++u) {
+            if (u >= n) continue;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float z = fmaf(xv[u][j], sc[j], sh[j]);
@@ -858,28 +872,6 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_apply_nhwc(const T* __restric
 #ifndef LSS_BN_ROWS
 #define LSS_BN_ROWS 1
 #endif
-template <int R, typename F>
-__device__ __forceinline__ void for_rows_nhwc(const BnGeo& g, int G, int q, F&& f) {
-    const int M = g.N * g.HW;
-    const int r0 = (int)((long)M * q / G), r1 = (int)((long)M * (q + 1) / G);
-    const int cg = g.C >> 3, step = kBlock / cg;
-    const int c0 = ((int)threadIdx.x % cg) * 8;
-    if ((int)threadIdx.x >= step * cg) return;
-    int r = r0 + (int)threadIdx.x / cg;
-    for (; r + (R - 1) * step < r1; r += R * step) {
-        int idx[R];
-#pragma unroll
-        for (int u = 0; u < R; ++u) idx[u] = (r + u * step) * g.C + c0;
-        f(idx, R);
-    }
-    for (; r < r1; r += step) {
-        int idx[R];
-#pragma unroll
-        for (int u = 0; u < R; ++u) idx[u] = r * g.C + c0;
-        f(idx, 1);
-    }
-}
-
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_bn_apply_rows_nhwc(const T* __restrict__ x, const T* __restrict__ res, BnGeo g,
                                                                const float* __restrict__ stats, int act,
