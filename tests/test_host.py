@@ -142,3 +142,14 @@ def test_bench_gpus_flag_launches_one_rank_per_gpu(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "8")  # under torchrun: no second launch
     assert bench.maybe_launch_ranks(args) is None
     assert args.config == "c3" and args.batch == 8 and args.mode == "train" and args.bev_layout == "nhwc"
+
+
+def test_hip_adam_only_for_plain_cuda_adam():
+    """optim.supported: the lss_clip_adam path is never taken for CPU tensors or other optimizers."""
+    import torch
+    from lss_carla_amd import optim
+    ps = [torch.zeros(4, requires_grad=True), torch.zeros(3, requires_grad=True)]
+    for p in ps:
+        p.grad = torch.ones_like(p)
+    assert not optim.supported(torch.optim.Adam(ps, lr=1e-3), ps)  # CPU tensors
+    assert not optim.supported(torch.optim.SGD(ps, lr=1e-3), ps)
