@@ -152,6 +152,82 @@ __global__ __launch_bounds__(kBlock) void k_up_bwd(const u32x4* __restrict__ dy,
     dx[t] = pack8(acc);
 }
 
+// k_up_bwd with every load of an output row's taps in flight: the output lines with a nonzero weight
+// for this input line / column are listed first (at most T per axis: T >= 2 / r + 1), then each output
+// row's T loads are issued unconditionally (clamped addresses, weight 0 past the list) before they are
+// summed -- the loop above waits for each load behind a data-dependent branch. Same order of the
+// nonzero terms (a zero-weight term adds 0), so the same bits for finite values.
+#ifndef LSS_UP_BWD_V2
+#define LSS_UP_BWD_V2 1
+#endif
+template <int T>
+__global__ __launch_bounds__(kBlock) void k_up_bwd_taps(const u32x4* __restrict__ dy, UpGeo g, u32x4* __restrict__ dx) {
+    const int c8s = g.C2 >> 3, c81 = g.C1 >> 3, c8t = c8s + c81;
+    const int total = g.N * g.Hi * g.Wi * c81;
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= total) return;
+    const int c8 = t % c81;
+    const int pix = t / c81;
+    const int j = pix % g.Wi;
+    const int r = pix / g.Wi;
+    const int i = r % g.Hi;
+    const int n = r / g.Hi;
+    int oh0, oh1, ow0, ow1;
+    out_range(g.rh, i, g.Ho, oh0, oh1);
+    out_range(g.rw, j, g.Wo, ow0, ow1);
+    int hl[T], wl[T];
+    float hw[T], ww[T];
+    int nh = 0, nw = 0;
+#pragma unroll
+    for (int q = 0; q < T; ++q) {
+        hl[q] = oh0; hw[q] = 0.f;
+        wl[q] = ow0; ww[q] = 0.f;
+    }
+    for (int oh = oh0; oh <= oh1; ++oh) {
+        const float wy = line_weight(g.rh, oh, g.Hi, i);
+        if (wy != 0.f && nh < T) {
+#pragma unroll
+            for (int q = 0; q < T; ++q)
+                if (q == nh) { hl[q] = oh; hw[q] = wy; }
+            ++nh;
+        }
+    }
+    for (int ow = ow0; ow <= ow1; ++ow) {
+        const float wx = line_weight(g.rw, ow, g.Wi, j);
+        if (wx != 0.f && nw < T) {
+#pragma unroll
+            for (int q = 0; q < T; ++q)
+                if (q == nw) { wl[q] = ow; ww[q] = wx; }
+            ++nw;
+        }
+    }
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    const u32x4* db = dy + (n * g.Ho * g.Wo) * c8t + c8s + c8;
+    for (int a = 0; a < nh; ++a) {
+        int row = 0;
+        float wy = 0.f;
+#pragma unroll
+        for (int q = 0; q < T; ++q)
+            if (q == a) { row = hl[q]; wy = hw[q]; }
+        u32x4 v[T];
+#pragma unroll
+        for (int b = 0; b < T; ++b) v[b] = db[(row * g.Wo + wl[b]) * c8t];
+#pragma unroll
+        for (int b = 0; b < T; ++b) {
+            if (b < nw) {
+                float f[8];
+                unpack8(v[b], f);
+                const float wgt = wy * ww[b];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc[k] += wgt * f[k];
+            }
+        }
+    }
+    dx[t] = pack8(acc);
+}
+
 inline int launch_status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
@@ -194,7 +270,17 @@ int lss_upsample_bwd(const void* dy, int32_t N, int32_t Hi, int32_t Wi, int32_t 
     if (!dy || !dx || !up_ok(N, Hi, Wi, C1, C2, Ho, Wo) || !aligned16(dy) || !aligned16(dx)) return LSS_CONV_EINVAL;
     const UpGeo g = make_geo(N, Hi, Wi, C1, C2, Ho, Wo);
     const int total = N * Hi * Wi * (C1 / 8);
-    hipLaunchKernelGGL(k_up_bwd, dim3((total + kBlock - 1) / kBlock), dim3(kBlock), 0, (hipStream_t)stream,
+    // output lines with a nonzero weight per input line: those with r * o in (i - 1, i + 1), <= 2 / r + 1
+    const int need = (int)(2.f / fminf(g.rh, g.rw)) + 2;
+    const dim3 gr((total + kBlock - 1) / kBlock), bl(kBlock);
+    if (LSS_UP_BWD_V2 && need <= 6)
+        hipLaunchKernelGGL(k_up_bwd_taps<6>, gr, bl, 0, (hipStream_t)stream,
+                       (const u32x4*)dy, g, (u32x4*)dx);
+    else if (LSS_UP_BWD_V2 && need <= 10)
+        hipLaunchKernelGGL(k_up_bwd_taps<10>, gr, bl, 0, (hipStream_t)stream,
+                       (const u32x4*)dy, g, (u32x4*)dx);
+    else
+        hipLaunchKernelGGL(k_up_bwd, gr, bl, 0, (hipStream_t)stream,
                        (const u32x4*)dy, g, (u32x4*)dx);
     return launch_status();
 }
