@@ -107,7 +107,13 @@ def parse():
     ap.add_argument("--pmc-traffic", type=int, default=1, help="rocprofv3 FETCH_SIZE/WRITE_SIZE passes (rank 0, N=1)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-runs", type=int, default=3, help="timed CPU runs per case (median; 1 warm-up before)")
+    ap.add_argument("--caller", default="bench", choices=("bench", "reference"),
+                    help="reference: the unchanged train_simbev.py loop (train_simbev.py:229-248) -- compile_model "
+                         "with the package defaults, fp32, eager, torch Adam + clip_grad_norm_, the host inverse "
+                         "per forward; overrides --dtype/--graph/--flat-params/--hip-adam and the kernel switches")
     args = ap.parse_args()
+    if args.caller == "reference":
+        args.mode, args.dtype, args.graph, args.flat_params, args.hip_adam = "train", "fp32", 0, 0, 0
     cfg_b = {"c1": 1, "c2": 4, "c3": 8, "c4": 8, "c5": 4}[args.config]
     args.batch = args.batch or cfg_b
     if args.mode == "auto":
@@ -485,6 +491,26 @@ def build_model(args, dev, gc, dac):
     return model
 
 
+class ReferenceCallerStep:
+    """One iteration of the reference's training loop as written (train_simbev.py:229-248): zero_grad,
+    forward with `.to(device)` on every input (no-ops: the batch is resident before the timed region),
+    SimpleLoss, backward, clip_grad_norm_(5.0), torch Adam (its default implementation) step."""
+
+    def __init__(self, model, inputs, labels, loss_fn, opt, dev):
+        self.model, self.inputs, self.labels, self.loss_fn, self.opt, self.dev = model, inputs, labels, loss_fn, opt, dev
+
+    def __call__(self):
+        self.opt.zero_grad()
+        preds = self.model(*[t.to(self.dev) for t in self.inputs])
+        loss = self.loss_fn(preds, self.labels.to(self.dev))
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.model.parameters(), 5.0)
+        self.opt.step()
+        return preds
+
+    eager = __call__
+
+
 class FwdStep:
     """Forward only (config 2): the model's forward under no_grad, eager or replayed as one HIP graph."""
 
@@ -573,7 +599,12 @@ def main():
     import lss_carla_amd as L
 
     torch.manual_seed(1234 + rank)
-    model = build_model(args, dev, gc, dac)
+    if args.caller == "reference":
+        # train_simbev.py:184-185: compile_model(...).to(device), nothing else set
+        model = L.compile_model(gc, dac, outC=1).to(dev)
+        model.train()
+    else:
+        model = build_model(args, dev, gc, dac)
     amp_dtype = torch.bfloat16 if args.dtype == "bf16" else None
     rig_host = syn.make_rig(B, N, fd, seed=rank)
     rig = {k: v.to(dev) for k, v in rig_host.items()}
@@ -590,7 +621,11 @@ def main():
         pinned = {k: rig_host[k].pin_memory() for k in ("post_rots", "intrins")}
         pre_step = lambda: hinv.update(pinned["post_rots"], pinned["intrins"])  # noqa: E731
 
-    if args.mode == "train":
+    if args.caller == "reference":
+        loss_fn = L.SimpleLoss(2.13).to(dev)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-7)  # train_simbev.py:192
+        step = ReferenceCallerStep(model, inputs, labels, loss_fn, opt, dev)
+    elif args.mode == "train":
         flat = None
         if args.graph or args.flat_params:
             # one process per GPU without DDP: identical replicas, one flat gradient all-reduce
@@ -738,7 +773,9 @@ def main():
                        "global_batch": world * B, "parallelism": f"dp{world}", "bev_layout": args.bev_layout,
                        "inverse": "host torch.inverse", "fuse_depthnet": bool(args.fuse_depthnet),
                        "depthwise": args.dw_impl, "batchnorm": "hip" if args.hip_bn else "miopen",
-                       "step": "hipgraph" if args.graph else "eager", "flat_params": bool(args.flat_params),
+                       "step": ("train_simbev.py loop, unchanged (eager, torch Adam, host inverse per forward)"
+                                if args.caller == "reference" else "hipgraph" if args.graph else "eager"),
+                       "flat_params": bool(args.flat_params),
                        "param_groups": bool(args.flat_params and args.param_groups),
                        "all_reduce": ("overlapped with backward (3 groups, captured)" if getattr(step, "overlap", False)
                                       else "one flat all-reduce between the graphs" if (world > 1 or FORCE_PG)

@@ -105,7 +105,10 @@ __global__ __launch_bounds__(kBlock) void k_clip_adam(Segs s, const float* __res
     float acc = 0.f;
     for (int i = threadIdx.x; i < npartial; i += kBlock) acc += partial[i];
     const float norm = sqrtf(block_sum(acc, s_w));
-    const float c = fminf(max_norm / (norm + 1e-6f), 1.f);
+    // clip_coef.clamp(max=1) as torch computes it: a NaN / inf norm passes through (fminf would return
+    // 1 for a NaN and leave the step unclipped), so every parameter goes non-finite as with torch
+    const float q = max_norm / (norm + 1e-6f);
+    const float c = q != q ? q : fminf(q, 1.f);
     long long lo, hi;
     block_range(s.start[s.count], lo, hi);
     for_segments(s, lo, hi, [&](int k, long long a, long long b) {

@@ -118,6 +118,27 @@ __device__ __forceinline__ void out_range(float r, int i, int out, int& lo, int&
     hi = min(out - 1, (int)ceilf((float)(i + 1) / r) + 1);
 }
 
+// d x of input pixel (i, j) from every output pixel whose stencil touches it, nonzero weights only,
+// output rows then columns ascending (k_up_bwd's order; k_up_bwd_taps adds the same terms in the same order)
+__device__ __forceinline__ void up_bwd_sum(const u32x4* __restrict__ db, const UpGeo& g, int i, int j, int oh0,
+                                           int oh1, int ow0, int ow1, int c8t, float acc[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    for (int oh = oh0; oh <= oh1; ++oh) {
+        const float wy = line_weight(g.rh, oh, g.Hi, i);
+        if (wy == 0.f) continue;
+        for (int ow = ow0; ow <= ow1; ++ow) {
+            const float wx = line_weight(g.rw, ow, g.Wi, j);
+            if (wx == 0.f) continue;
+            const float wgt = wy * wx;
+            float v[8];
+            unpack8(db[(oh * g.Wo + ow) * c8t], v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += wgt * v[k];
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_up_bwd(const u32x4* __restrict__ dy, UpGeo g, u32x4* __restrict__ dx) {
     const int c8s = g.C2 >> 3, c81 = g.C1 >> 3, c8t = c8s + c81;
     const int total = g.N * g.Hi * g.Wi * c81;
@@ -133,22 +154,7 @@ __global__ __launch_bounds__(kBlock) void k_up_bwd(const u32x4* __restrict__ dy,
     out_range(g.rh, i, g.Ho, oh0, oh1);
     out_range(g.rw, j, g.Wo, ow0, ow1);
     float acc[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-    const u32x4* db = dy + (n * g.Ho * g.Wo) * c8t + c8s + c8;
-    for (int oh = oh0; oh <= oh1; ++oh) {
-        const float wy = line_weight(g.rh, oh, g.Hi, i);
-        if (wy == 0.f) continue;
-        for (int ow = ow0; ow <= ow1; ++ow) {
-            const float wx = line_weight(g.rw, ow, g.Wi, j);
-            if (wx == 0.f) continue;
-            const float wgt = wy * wx;
-            float v[8];
-            unpack8(db[(oh * g.Wo + ow) * c8t], v);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) acc[k] += wgt * v[k];
-        }
-    }
+    up_bwd_sum(dy + (n * g.Ho * g.Wo) * c8t + c8s + c8, g, i, j, oh0, oh1, ow0, ow1, c8t, acc);
     dx[t] = pack8(acc);
 }
 
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(kBlock) void k_up_bwd_taps(const u32x4* __restrict_
     }
     for (int oh = oh0; oh <= oh1; ++oh) {
         const float wy = line_weight(g.rh, oh, g.Hi, i);
-        if (wy != 0.f && nh < T) {
+        if (wy != 0.f) {
 #pragma unroll
             for (int q = 0; q < T; ++q)
                 if (q == nh) { hl[q] = oh; hw[q] = wy; }
@@ -194,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void k_up_bwd_taps(const u32x4* __restrict_
     }
     for (int ow = ow0; ow <= ow1; ++ow) {
         const float wx = line_weight(g.rw, ow, g.Wi, j);
-        if (wx != 0.f && nw < T) {
+        if (wx != 0.f) {
 #pragma unroll
             for (int q = 0; q < T; ++q)
                 if (q == nw) { wl[q] = ow; ww[q] = wx; }
@@ -202,9 +208,16 @@ __global__ __launch_bounds__(kBlock) void k_up_bwd_taps(const u32x4* __restrict_
         }
     }
     float acc[8];
+    const u32x4* db = dy + (n * g.Ho * g.Wo) * c8t + c8s + c8;
+    if (nh > T || nw > T) {
+        // more nonzero lines than the host's bound allowed for (float rounding of r * o): the plain
+        // loop, same terms in the same order -- never a dropped tap
+        up_bwd_sum(db, g, i, j, oh0, oh1, ow0, ow1, c8t, acc);
+        dx[t] = pack8(acc);
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-    const u32x4* db = dy + (n * g.Ho * g.Wo) * c8t + c8s + c8;
     for (int a = 0; a < nh; ++a) {
         int row = 0;
         float wy = 0.f;

@@ -231,9 +231,19 @@ def pointwise_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
             and x.is_contiguous() and (x.shape[2] * x.shape[3]) % 4 == 0
             and conv.weight.dtype in (torch.float32, torch.bfloat16)
             and ((torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
-                 or (x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16))):
+                 or (x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16))
+            and _pw_fits(x.shape[0], x.shape[1], conv.weight.shape[0], x.shape[2] * x.shape[3])):
         return _HipPointwise.apply(x, conv.weight)
     return conv(x)
+
+
+_INT_MAX = 2**31 - 1
+
+
+def _pw_fits(N: int, Cin: int, Cout: int, HW: int) -> bool:
+    """The index limits lss_pw_conv / lss_pw_wrw enforce (they return EINVAL past them): larger
+    activations stay on MIOpen instead of raising."""
+    return N * max(Cin, Cout) * HW < _INT_MAX and N * ((HW + 31) // 32) < _INT_MAX
 
 
 def depthwise_same_pads(conv: "Conv2dStaticSamePadding") -> Tuple[int, int, int, int]:

@@ -6,8 +6,9 @@ optimizer's own state tensors (``step``, ``exp_avg``, ``exp_avg_sq``, created as
 ``opt.state_dict()`` stays what torch would save and either path can continue the other. The gradient
 norm is fp32 over all the tensors' gradients; the gradients themselves are left unclipped (nothing reads
 them after the step). Kernels: ``lss_clip_adam`` (include/lss_convs.h). Anything it does not cover
-(amsgrad, maximize, several parameter groups, tensor learning rates, CPU tensors, other dtypes) keeps
-torch's path (``supported``).
+(amsgrad, maximize, several parameter groups, tensor learning rates, CPU tensors, other dtypes, an Adam
+that is neither ``capturable`` nor ``fused``, whose ``step`` torch keeps on the host) keeps torch's path
+(``supported``).
 """
 from __future__ import annotations
 
@@ -27,6 +28,10 @@ def supported(opt: torch.optim.Optimizer, params: Sequence[torch.Tensor]) -> boo
         return False
     g = opt.param_groups[0]
     if g.get("amsgrad") or g.get("maximize") or g.get("differentiable") or g.get("decoupled_weight_decay"):
+        return False
+    if not (g.get("capturable") or g.get("fused")):
+        # torch keeps such an Adam's `step` on the host; the device step this path keeps would change
+        # its state_dict and cost the next torch step a sync per tensor
         return False
     if any(isinstance(g[k], torch.Tensor) for k in ("lr", "eps", "weight_decay")) or \
             any(isinstance(b, torch.Tensor) for b in g["betas"]):

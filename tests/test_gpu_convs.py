@@ -394,3 +394,22 @@ def test_bn_relu_nhwc_backward_recomputes_output(dtype):
     tol = dict(rtol=1e-3, atol=1e-3) if dtype == torch.float32 else dict(rtol=2e-2, atol=5e-2)
     torch.testing.assert_close(y.float(), ref.detach(), **tol)
     torch.testing.assert_close(xd.grad.float(), xr.grad, **tol)
+
+
+@pytest.mark.parametrize("Hi,Wi,Ho,Wo", [(10, 13, 37, 50), (7, 9, 13, 29), (25, 25, 101, 99)])
+def test_upsample_noninteger_ratio_vs_fp64(Hi, Wi, Ho, Wo):
+    """lss_upsample_* at output sizes that are not integer multiples (align_corners ratios r = (Hi - 1) /
+    (Ho - 1) whose r * o rounds across line boundaries): every nonzero tap reaches the backward, whether
+    k_up_bwd_taps holds it in its list or falls back to the plain loop."""
+    g = torch.Generator().manual_seed(Hi * 100 + Wo)
+    cl = torch.channels_last
+    x = torch.randn(2, 16, Hi, Wi, generator=g).bfloat16()
+    xd = x.to(DEV).contiguous(memory_format=cl).requires_grad_(True)
+    y = R._UpsampleCat.apply(xd, None, Ho, Wo)
+    xr = x.double().requires_grad_(True)
+    ref = F.interpolate(xr, size=(Ho, Wo), mode="bilinear", align_corners=True)
+    torch.testing.assert_close(y.detach().cpu().double(), ref.detach(), rtol=8e-3, atol=8e-3)
+    dy = torch.randn(y.shape, generator=g).bfloat16()
+    y.backward(dy.to(DEV).contiguous(memory_format=cl))
+    ref.backward(dy.double())
+    torch.testing.assert_close(xd.grad.cpu().double(), xr.grad, rtol=1e-2, atol=2e-2)

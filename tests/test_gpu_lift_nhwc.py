@@ -212,3 +212,23 @@ def test_model_under_flat_params_takes_the_prepacked_weight():
     torch.cuda.synchronize()
     assert calls == [False, True]
     assert torch.equal(seen[0], seen[1])
+
+
+def test_depthnet_wgrad_partials_fp32_vs_fp64():
+    """The split-K depthnet weight gradient (ops._bmm_f32 + a slice-order sum) on zero-mean pixel
+    gradients, whose sums cancel: every element within one bf16 rounding of the fp64 GEMM of the same
+    bf16 operands (bf16 partials, rounded before the sum, were not)."""
+    from lss_carla_amd import ops
+    g = torch.Generator().manual_seed(5)
+    npix, O, K = 8448, 105, 512
+    dd = (torch.randn(npix, O, generator=g) * 1e-2).bfloat16()
+    fm = torch.randn(npix, K, generator=g).bfloat16()
+    S = ops._wgrad_splits(npix)
+    ddd, fmd = dd.to(DEV), fm.to(DEV)
+    part = ops._bmm_f32(ddd.view(S, npix // S, O).transpose(1, 2), fmd.view(S, npix // S, K))
+    assert part.dtype == torch.float32
+    got = part.sum(0).bfloat16().double().cpu()
+    want = dd.double().t() @ fm.double()
+    err = (got - want).abs()
+    bound = want.abs() * 2.0 ** -8 + 1e-6 * want.abs().max()
+    assert bool((err <= bound).all()), float((err / (want.abs() + 1e-30)).max())

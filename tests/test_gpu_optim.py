@@ -70,3 +70,34 @@ def test_clip_adam_graph_replay_and_unsupported_cases():
     assert not optim.supported(torch.optim.Adam(ps, lr=1e-3, amsgrad=True), ps)
     assert not optim.supported(torch.optim.AdamW(ps, lr=1e-3), ps)
     assert not optim.supported(opt, ps[:2])
+
+
+def test_clip_adam_nan_gradient_poisons_like_torch():
+    """One NaN gradient entry: torch's clip_grad_norm_ turns the clip factor NaN (clamp(max=1) passes NaN),
+    so every gradient and then every parameter goes NaN; lss_clip_adam must do the same, not step the
+    other tensors unclipped."""
+    ps_a, g = _setup(3)
+    ps_b = [p.detach().clone().requires_grad_(True) for p in ps_a]
+    opt_a = torch.optim.Adam(ps_a, lr=1e-3, fused=True, capturable=True)
+    opt_b = torch.optim.Adam(ps_b, lr=1e-3, fused=True, capturable=True)
+    grads = [torch.randn(p.shape, generator=g).to(DEV) for p in ps_a]
+    grads[3][7] = float("nan")
+    for p, q, gr in zip(ps_a, ps_b, grads):
+        p.grad, q.grad = gr.clone(), gr.clone()
+    optim.ClipAdam(opt_a).step(5.0)
+    torch.nn.utils.clip_grad_norm_(ps_b, 5.0)
+    opt_b.step()
+    for p, q in zip(ps_a, ps_b):
+        assert torch.isnan(q).all(), "torch's reference behaviour changed"
+        assert torch.isnan(p).all()
+
+
+def test_clip_adam_only_for_device_step_adams():
+    """A plain (foreach) Adam keeps `step` on the host: ClipAdam leaves it to torch, so its state_dict and
+    a later torch step are what torch alone would give."""
+    ps, _ = _setup(4)
+    for p in ps:
+        p.grad = torch.ones_like(p)
+    assert not optim.supported(torch.optim.Adam(ps, lr=1e-3), ps)
+    assert optim.supported(torch.optim.Adam(ps, lr=1e-3, fused=True), ps)
+    assert optim.supported(torch.optim.Adam(ps, lr=1e-3, capturable=True), ps)

@@ -153,3 +153,12 @@ def test_hip_adam_only_for_plain_cuda_adam():
         p.grad = torch.ones_like(p)
     assert not optim.supported(torch.optim.Adam(ps, lr=1e-3), ps)  # CPU tensors
     assert not optim.supported(torch.optim.SGD(ps, lr=1e-3), ps)
+
+
+def test_pointwise_conv_size_guard():
+    """pointwise_conv routes to lss_pw_conv / lss_pw_wrw only inside the index limits those kernels check
+    (EINVAL past them); larger activations stay on the framework conv."""
+    from lss_carla_amd import efficientnet as E
+    assert E._pw_fits(48, 512, 105, 176)
+    assert not E._pw_fits(4096, 1152, 192, 704)        # N * C * HW >= 2^31
+    assert E._pw_fits(1, 2**20, 1, 2047) and not E._pw_fits(1, 2**20, 1, 2048)
