@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 21
+#define LSS_ABI_VERSION 22
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;
@@ -121,7 +121,8 @@ int lss_csr_build(const int32_t* cell_of, const int32_t* slot_of, int32_t nprime
  * use; cell_count is zero-filled before the first lss_geometry_cells / lss_cells_from_geom that
  * counts into it; every call leaves both zero-filled again. One call at a time per workspace (the
  * caller orders calls that share one: ops.py records the stream and event of its last use).
- * Workspace header, 4 uint32: [0] unused, [1] sticky count of look-back timeouts (a block that
+ * Workspace header, 4 uint32: [0] overflow-record counter of the ordered plans (below; 0 between
+ * calls), [1] sticky count of look-back timeouts (a block that
  * waited its spin limit for a predecessor sums that predecessor's counts itself: the output is exact
  * either way), [2] spin-limit override (0: the built-in limit; s > 0: s - 1 polls -- tests of the
  * timeout path), [3] unused. */
@@ -130,6 +131,33 @@ int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t npr
                      int32_t* cell_count, int32_t ncells, const lss_dims_t* dims,
                      int32_t* cell_start, long long* sorted_key, int32_t* sorted_row,
                      void* scratch, void* workspace, lss_stream_t stream);
+
+/* Ordered plans (ABI 22): the same CSR as lss_csr_build, bit for bit, in three kernels (geometry,
+ * look-back scan, scatter) -- no sort pass after the scatter. The geometry kernel gives every kept
+ * point its rank among the points of its cell in its own 256-point block (lower point ids first)
+ * and appends one record (block, points) per distinct (block, cell) to the cell's list in `lists`;
+ * the scatter places point p at cell_start[cell] + (the cell's points in lower blocks) + rank.
+ * cell_word (ncells int32) packs the cell's point count (low 20 bits) and its record count (high
+ * bits): zero-filled before the first call, as cell_count is for lss_csr_build_ws, and left
+ * zero-filled by every lss_csr_build_ordered. `lists`: lss_csr_lists_bytes(ncells, nprime) bytes,
+ * 16-B aligned, no initialisation. `workspace`: as lss_csr_build_ws's (its word 0 counts overflow
+ * records: cells shared by more than 8 blocks). A sample may hold fewer than 2^20 - 512 points
+ * (N*D*H*W, or points_per_batch); larger returns LSS_EUNSUPPORTED (use lss_geometry_cells +
+ * lss_csr_build_ws). One plan at a time per (cell_word, lists, workspace).
+ * Replaces: ranks = ...; sorts = ranks.argsort(); x, geom_feats, ranks = x[sorts], ... (src/models.py:225-231). */
+size_t lss_csr_lists_bytes(int32_t ncells, int32_t nprime);
+int lss_geometry_cells_ordered(const float* frustum, const float* rots, const float* trans,
+                               const float* kinv, const float* pinv, const float* post_trans,
+                               const lss_dims_t* dims, const lss_grid_t* grid,
+                               float* out_geom, int32_t* cell_of, int32_t* cell_word, int32_t* rank_of,
+                               void* lists, void* workspace, lss_stream_t stream);
+int lss_cells_from_geom_ordered(const float* geom, int32_t nprime, int32_t points_per_batch,
+                                const lss_grid_t* grid, int32_t* cell_of, int32_t* cell_word,
+                                int32_t* rank_of, void* lists, void* workspace, lss_stream_t stream);
+int lss_csr_build_ordered(const int32_t* cell_of, const int32_t* rank_of, int32_t nprime,
+                          int32_t* cell_word, int32_t ncells, const lss_dims_t* dims, const void* lists,
+                          int32_t* cell_start, long long* sorted_key, int32_t* sorted_row,
+                          void* workspace, lss_stream_t stream);
 
 /* Lift, part 1 (CamEncode.get_depth_dist + layout, src/models.py:49-59, 192-202):
  * depth (B*N, D, H, W) fp32 = softmax over D of depthnet_out[:, :D];

@@ -18,7 +18,7 @@ DEBUG_LIB_PATH = os.path.join(_HERE, "liblss_hip_debug.so")  # LSS_DEBUG=1: devi
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 
 class Dims(ctypes.Structure):
@@ -61,6 +61,10 @@ SIGNATURES = {
     "lss_csr_build": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p]),
     "lss_csr_workspace_bytes": (ctypes.c_size_t, [_i32]),
     "lss_csr_build_ws": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p, _p]),
+    "lss_csr_lists_bytes": (ctypes.c_size_t, [_i32, _i32]),
+    "lss_geometry_cells_ordered": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _DIMS, _GRID, _p, _p, _p, _p, _p, _p, _p]),
+    "lss_cells_from_geom_ordered": (ctypes.c_int, [_p, _i32, _i32, _GRID, _p, _p, _p, _p, _p, _p]),
+    "lss_csr_build_ordered": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _DIMS, _p, _p, _p, _p, _p, _p]),
     "lss_lift_prep": (ctypes.c_int, [_p, _i32, _DIMS, _p, _p, _i32, _p]),
     "lss_depthnet_lift": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p]),
     "lss_depthnet_lift_nhwc": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _DIMS, _p, _p, _i32, _p]),

@@ -340,6 +340,124 @@ __global__ __launch_bounds__(kGeoBlock) void k_cells_from_geom(const float* __re
     emit_cell_block(p, cell, cell_of, cell_count, slot_of, live, hash);
 }
 
+// ---- ordered plan (lss_geometry_cells_ordered + lss_csr_build_ordered, ABI 22): every kept point's
+// position in the canonical CSR (ascending cell, then ascending point id) follows from the counts
+// alone, so no sort pass (k_csr_canon) is needed after the scatter.
+//   in the block: a point's rank among the block's points of its cell is the number of LOWER threads
+//     with that cell -- one bit per thread in a 256-bit mask per hash slot (LDS), popcounts below;
+//   across blocks: the one returning device atomic per distinct (block, cell) adds
+//     (1 << kOrdCountBits) | n to the cell's word, and the entry index it returns (the high bits)
+//     places the record (logical block, n) in the cell's list of kOrdList records (or, past them,
+//     in an overflow area through a counter in the workspace header: never at c1-c5, at most 8
+//     blocks share a cell at c5). The scatter then sums the counts of the cell's records from lower
+//     blocks: that is the number of the cell's points with a lower point id in other blocks.
+// Points of logical block lb are [256 lb, 256 lb + 256) (XCD-contiguous blocks, xcd_block), so block
+// order is point order. Cell words: points in the low kOrdCountBits bits, records in the high bits.
+constexpr int kOrdCountBits = 20;
+constexpr int kOrdCountMask = (1 << kOrdCountBits) - 1;
+constexpr int kOrdList = 8;                 // records per cell held in the cell's list
+constexpr int kGeoWaves = kGeoBlock / kWave;
+static_assert(kGeoBlock == 256, "records pack n (<= 256) into 9 bits");
+
+struct GeoHashOrd {
+    int key[kGeoHash];
+    unsigned long long mask[kGeoHash][kGeoWaves];  // bit l of word w: thread 64 w + l holds this cell
+};
+
+__device__ __forceinline__ void emit_cell_block_ordered(int lb, int p, int cell, int32_t* __restrict__ cell_of,
+                                                        int32_t* __restrict__ cell_word, int32_t* __restrict__ rank_of,
+                                                        int32_t* __restrict__ list, int2* __restrict__ ovf,
+                                                        unsigned* __restrict__ ovf_count, bool live,
+                                                        GeoHashOrd& h) {
+    if (live) cell_of[p] = cell;
+    for (int i = threadIdx.x; i < kGeoHash; i += kGeoBlock) h.key[i] = -1;
+    unsigned long long* m = &h.mask[0][0];
+    for (int i = threadIdx.x; i < kGeoHash * kGeoWaves; i += kGeoBlock) m[i] = 0ull;
+    __syncthreads();
+    const bool kept = live && cell >= 0;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int at = 0;
+    if (kept) {
+        at = (int)(((unsigned)cell * 2654435761u) >> (32 - kGeoHashBits));
+        for (;;) {
+            const int prev = atomicCAS(&h.key[at], -1, cell);
+            if (prev == -1 || prev == cell) break;
+            at = (at + 1) & (kGeoHash - 1);
+        }
+        atomicOr(&h.mask[at][wave], 1ull << lane);
+    }
+    __syncthreads();
+    int rank = 0;
+    if (kept) {
+#pragma unroll
+        for (int w = 0; w < kGeoWaves; ++w) {
+            const unsigned long long mw = h.mask[at][w];
+            rank += w < wave ? __popcll(mw) : (w == wave ? __popcll(mw & ((1ull << lane) - 1ull)) : 0);
+        }
+    }
+    for (int i = threadIdx.x; i < kGeoHash; i += kGeoBlock) {
+        const int c = h.key[i];
+        if (c >= 0) {
+            int n = 0;
+#pragma unroll
+            for (int w = 0; w < kGeoWaves; ++w) n += __popcll(h.mask[i][w]);
+            const int old = atomicAdd(cell_word + c, (1 << kOrdCountBits) | n);
+            const int idx = (int)((unsigned)old >> kOrdCountBits);
+            const int rec = (lb << 9) | n;
+            if (idx < kOrdList) {
+                list[(size_t)c * kOrdList + idx] = rec;
+            } else {
+                const unsigned o = atomicAdd(ovf_count, 1u);
+                ovf[o] = make_int2(c, rec);
+            }
+        }
+    }
+    if (live) rank_of[p] = kept ? rank : -1;
+}
+
+__global__ __launch_bounds__(kGeoBlock) void k_geometry_cells_ord(
+    const float* __restrict__ frustum, const float* __restrict__ rots, const float* __restrict__ trans,
+    const float* __restrict__ kinv, const float* __restrict__ pinv, const float* __restrict__ post_trans,
+    int N, int DHW, int nprime, lss_grid_t g, float* __restrict__ out_geom, int32_t* __restrict__ cell_of,
+    int32_t* __restrict__ cell_word, int32_t* __restrict__ rank_of, int32_t* __restrict__ list,
+    int2* __restrict__ ovf, unsigned* __restrict__ ovf_count) {
+    const int lb = xcd_block();
+    if (lb * kGeoBlock >= nprime) return;  // block-uniform (padding blocks of the XCD-contiguous grid)
+    const int p0 = lb * kGeoBlock + threadIdx.x;
+    const bool live = p0 < nprime;
+    const int p = live ? p0 : nprime - 1;  // dead lanes recompute the last point, then write nothing
+    const int cam = p / DHW;
+    const int f = p - cam * DHW;
+    const int b = cam / N;
+    float e[3];
+    geometry_point(frustum, rots, trans, kinv, pinv, post_trans, cam, f, e);
+    if (out_geom != nullptr && live) {
+        out_geom[3 * (size_t)p + 0] = e[0];
+        out_geom[3 * (size_t)p + 1] = e[1];
+        out_geom[3 * (size_t)p + 2] = e[2];
+    }
+    const int cell = live ? quantize_cell(e[0], e[1], e[2], g, b) : -1;
+    __shared__ GeoHashOrd hash;
+    emit_cell_block_ordered(lb, p, cell, cell_of, cell_word, rank_of, list, ovf, ovf_count, live, hash);
+}
+
+__global__ __launch_bounds__(kGeoBlock) void k_cells_from_geom_ord(const float* __restrict__ geom, int nprime, int ppb,
+                                                                   lss_grid_t g, int32_t* __restrict__ cell_of,
+                                                                   int32_t* __restrict__ cell_word,
+                                                                   int32_t* __restrict__ rank_of,
+                                                                   int32_t* __restrict__ list, int2* __restrict__ ovf,
+                                                                   unsigned* __restrict__ ovf_count) {
+    const int lb = xcd_block();
+    if (lb * kGeoBlock >= nprime) return;
+    const int p0 = lb * kGeoBlock + threadIdx.x;
+    const bool live = p0 < nprime;
+    const int p = live ? p0 : nprime - 1;
+    const int cell =
+        live ? quantize_cell(geom[3 * (size_t)p], geom[3 * (size_t)p + 1], geom[3 * (size_t)p + 2], g, p / ppb) : -1;
+    __shared__ GeoHashOrd hash;
+    emit_cell_block_ordered(lb, p, cell, cell_of, cell_word, rank_of, list, ovf, ovf_count, live, hash);
+}
+
 // ----------------------------------------------------------------------------- CSR (counting sort)
 // Exclusive scan of 1024 thread totals inside a block; returns the thread's exclusive prefix.
 // Inclusive scan over the 64 lanes on DPP (integer adds: exact in any order): the sum of the 4 lanes up
@@ -458,8 +576,9 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const int32_t* __restrict__ 
 // timeout only costs time; the sticky timeout word counts them. The scatter re-zeroes the ticket and
 // the granules after the scan, so every call starts from zeros.
 constexpr unsigned kScanSpinLimit = 1u << 22;
-struct ScanWs {  // lss_csr_workspace_bytes: [unused, timeouts, spin_limit_override, pad][granule x nb]
-    unsigned unused, timeouts;
+struct ScanWs {  // lss_csr_workspace_bytes: [ovf_count, timeouts, spin_limit_override, pad][granule x nb]
+    unsigned ovf_count;  // ordered plans: records past a cell's list (reset by k_scatter_ord)
+    unsigned timeouts;
     unsigned spin_override;  // 0: kScanSpinLimit polls; s > 0: s - 1 polls (tests of the timeout path)
     unsigned pad;
 };
@@ -469,7 +588,7 @@ struct ScanWs {  // lss_csr_workspace_bytes: [unused, timeouts, spin_limit_overr
 // {status 1, sum of its kScanItems counts}, summed by the whole wave from `cnt`. jb = the block each
 // lane polled (>= 0 wherever x == 0).
 __device__ unsigned long long scan_fill_missing(unsigned long long x, int jb, const int32_t* __restrict__ cnt,
-                                                int ncells, int lane) {
+                                                int ncells, int lane, int cmask) {
     unsigned long long miss = __ballot(x == 0ull);
     while (miss) {
         const int l = __builtin_ctzll(miss);
@@ -477,7 +596,7 @@ __device__ unsigned long long scan_fill_missing(unsigned long long x, int jb, co
         const int blk = __builtin_amdgcn_readlane(jb, l);
         const int lo = blk * kScanItems, hi = min(lo + kScanItems, ncells);
         int s = 0;
-        for (int i = lo + lane; i < hi; i += kWave) s += cnt[i];
+        for (int i = lo + lane; i < hi; i += kWave) s += cnt[i] & cmask;
         s = wave_sum_i(s);
         if (lane == l) x = (1ull << 32) | (unsigned)s;
     }
@@ -490,8 +609,10 @@ __device__ __forceinline__ void st_agent(unsigned long long* p, unsigned long lo
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// cmask: the count bits of a cell word (-1: plain counts; kOrdCountMask: ordered-plan words)
 __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restrict__ cnt, int ncells,
-                                                        ScanWs* __restrict__ ws, int32_t* __restrict__ cell_start) {
+                                                        ScanWs* __restrict__ ws, int32_t* __restrict__ cell_start,
+                                                        int cmask) {
     __shared__ int s_wave[32];
     __shared__ int s_total;
     __shared__ int s_prefix;
@@ -513,6 +634,10 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
         if (base + 2 < ncells) c4.z = cnt[base + 2];
         if (base + 3 < ncells) c4.w = cnt[base + 3];
     }
+    c4.x &= cmask;
+    c4.y &= cmask;
+    c4.z &= cmask;
+    c4.w &= cmask;
     const int excl = block_exclusive_scan_1024(c4.x + c4.y + c4.z + c4.w, s_wave, &s_total);
     if (threadIdx.x < kWave) {
         const int lane = threadIdx.x;
@@ -537,8 +662,8 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(const int32_t* __restric
                         // stop waiting: the unpublished predecessors' aggregates from their counts
                         if (!gave_up && lane == 0) atomicAdd(&ws->timeouts, 1u);
                         gave_up = true;
-                        x0 = scan_fill_missing(x0, j0, cnt, ncells, lane);
-                        x1 = scan_fill_missing(x1, j1, cnt, ncells, lane);
+                        x0 = scan_fill_missing(x0, j0, cnt, ncells, lane, cmask);
+                        x1 = scan_fill_missing(x1, j1, cnt, ncells, lane, cmask);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
@@ -589,6 +714,78 @@ __global__ __launch_bounds__(kBlock) void k_scatter_ws(const int32_t* __restrict
     if (t < nb) reinterpret_cast<unsigned long long*>(ws + 1)[t] = 0ull;
 }
 
+__device__ __forceinline__ int point_row(int p, int DHW, int HW) {
+    const int cam = p / DHW;
+    return cam * HW + (p - cam * DHW) % HW;  // pixel of point p = its context row
+}
+
+// Ordered scatter (lss_csr_build_ordered): point p of cell c goes straight to its canonical position
+// cell_start[c] + (the cell's points in lower blocks, summed from the cell's records) + (its rank in
+// its block), with its key and context row; entries [total, nprime) get the sentinel key. Then the
+// reset for the next plan: the cell words, the scan's granules and the overflow counter (nothing in
+// this launch reads them). Points are taken in XCD-contiguous blocks (xcd_block), as the geometry and
+// the splat's chunk waves take them, so each sample's CSR entries are written from the XCD that reads
+// them. The grid covers max(nprime, ncells) threads.
+__device__ __forceinline__ void ord_rec(int rec, int n_c, int myblk, int& seen, int& before) {
+    if (seen < n_c) {
+        const int n = rec & 511;
+        seen += n;
+        before += (rec >> 9) < myblk ? n : 0;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_scatter_ord(const int32_t* __restrict__ cell_of,
+                                                        const int32_t* __restrict__ rank_of, int nprime,
+                                                        const int32_t* __restrict__ cell_start,
+                                                        const int32_t* __restrict__ list,
+                                                        const int2* __restrict__ ovf, int DHW, int HW,
+                                                        long long* __restrict__ key_out, int32_t* __restrict__ row_out,
+                                                        int32_t* __restrict__ cell_word, int ncells,
+                                                        ScanWs* __restrict__ ws) {
+    static_assert(kBlock == kGeoBlock, "one scatter block = one geometry block of points");
+    const int t = xcd_block() * kBlock + threadIdx.x;
+    if (t < nprime) {
+        const int total = min(cell_start[ncells], nprime);
+        const int cell = cell_of[t];
+        const int r = rank_of[t];
+        if (cell >= 0) {
+            const int c = dchk(cell, ncells, kDbgCell);
+            const int a = cell_start[c], z = cell_start[c + 1];
+            const int4 l0 = *reinterpret_cast<const int4*>(list + (size_t)c * kOrdList);
+            const int4 l1 = *reinterpret_cast<const int4*>(list + (size_t)c * kOrdList + 4);
+            const int n_c = z - a;
+            const int myblk = t / kGeoBlock;
+            int seen = 0, before = 0;
+            ord_rec(l0.x, n_c, myblk, seen, before);
+            ord_rec(l0.y, n_c, myblk, seen, before);
+            ord_rec(l0.z, n_c, myblk, seen, before);
+            ord_rec(l0.w, n_c, myblk, seen, before);
+            ord_rec(l1.x, n_c, myblk, seen, before);
+            ord_rec(l1.y, n_c, myblk, seen, before);
+            ord_rec(l1.z, n_c, myblk, seen, before);
+            ord_rec(l1.w, n_c, myblk, seen, before);
+            // more than kOrdList blocks share the cell: its other records, in the overflow area's valid
+            // prefix (the counter restarts at 0 every plan; the records of this cell end before the
+            // cell's points are all accounted for, so nothing past that prefix is read)
+            for (int o = 0; seen < n_c && o < nprime; ++o) {
+                const int2 v = ovf[o];
+                if (v.x == c) ord_rec(v.y, n_c, myblk, seen, before);
+            }
+            dassert(seen == n_c, kDbgScatterPos, seen, n_c);
+            const int at = dchk(a + before + r, total, kDbgScatterPos);
+            dassert(before + r < n_c, kDbgScatterPos, before + r, n_c);
+            key_out[at] = ((long long)cell << 32) | (unsigned)t;
+            row_out[at] = point_row(t, DHW, HW);
+        }
+        if (t >= total) key_out[t] = -1ll;  // sentinel tail
+    }
+    const int g = blockIdx.x * kBlock + threadIdx.x;  // the reset, in launch order
+    if (g < ncells) cell_word[g] = 0;
+    const int nb = (ncells + kScanItems - 1) / kScanItems;
+    if (g < nb) reinterpret_cast<unsigned long long*>(ws + 1)[g] = 0ull;
+    if (g == 0) ws->ovf_count = 0u;
+}
+
 // The sorted list is cut into 64-entry chunks; the wave of chunk w owns the cells that START
 // in [64w, 64w + 64). It reads entries [64w - 1, 64w + 128): the owned cells (<= 64 entries each;
 // a longer last cell is flagged `big`) and the entry before the chunk (a cell that started earlier).
@@ -630,10 +827,6 @@ __device__ __forceinline__ int pick(int r0, int r1, int idx) {  // idx uniform, 
     return idx < kWave ? __builtin_amdgcn_readlane(r0, idx) : __builtin_amdgcn_readlane(r1, idx - kWave);
 }
 
-__device__ __forceinline__ int point_row(int p, int DHW, int HW) {
-    const int cam = p / DHW;
-    return cam * HW + (p - cam * DHW) % HW;  // pixel of point p = its context row
-}
 
 // Canonical CSR order: inside every cell the entries are sorted by point id (so every later
 // reduction over a cell is deterministic without sorting again), and each entry's context-row
@@ -2557,12 +2750,86 @@ int lss_csr_build_ws(const int32_t* cell_of, const int32_t* slot_of, int32_t npr
     long long* tmp_key = reinterpret_cast<long long*>(static_cast<char*>(scratch) + poff);
     ScanWs* ws = static_cast<ScanWs*>(workspace);
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_scan_lookback, dim3(nb), dim3(1024), 0, s, cell_count, ncells, ws, cell_start);
+    hipLaunchKernelGGL(k_scan_lookback, dim3(nb), dim3(1024), 0, s, cell_count, ncells, ws, cell_start, -1);
     hipLaunchKernelGGL(k_scatter_ws, dim3(grid_blocks(std::max(nprime, ncells), kBlock)), dim3(kBlock), 0, s, cell_of,
                        slot_of, nprime, cell_start, tmp_key, cell_count, ncells, ws);
     const int nchunks = (nprime + kWave - 1) / kWave;
     hipLaunchKernelGGL(k_csr_canon, dim3(xcd_grid(grid_blocks(nchunks, kBlock / kWave))), dim3(kBlock), 0, s, tmp_key,
                        cell_start + ncells, nchunks, nprime, DHW, HW, sorted_key, sorted_row);
+    debug_check_csr(cell_start, ncells, cell_of, nprime, s);
+    return launch_status();
+}
+
+// ---- ordered plans (ABI 22)
+// lists buffer: [ncells * kOrdList int32 records][nprime int2 overflow records], 16-B aligned parts
+static size_t ord_list_bytes(int32_t ncells) {
+    return ((sizeof(int32_t) * (size_t)ncells * kOrdList) + 255) & ~(size_t)255;
+}
+size_t lss_csr_lists_bytes(int32_t ncells, int32_t nprime) {
+    if (ncells <= 0 || nprime <= 0) return 0;
+    return ord_list_bytes(ncells) + sizeof(int2) * (size_t)nprime;
+}
+// points of one sample (the most a cell can hold) and blocks per sample must fit the cell word's fields
+static bool ord_fits(long ppb) { return ppb > 0 && ppb < (1L << kOrdCountBits) - 2L * kGeoBlock; }
+
+int lss_geometry_cells_ordered(const float* frustum, const float* rots, const float* trans, const float* kinv,
+                               const float* pinv, const float* post_trans, const lss_dims_t* dims,
+                               const lss_grid_t* grid, float* out_geom, int32_t* cell_of, int32_t* cell_word,
+                               int32_t* rank_of, void* lists, void* workspace, lss_stream_t stream) {
+    if (!dims_ok(dims) || !grid_ok(grid) || !frustum || !rots || !trans || !kinv || !pinv || !post_trans || !cell_of ||
+        !cell_word || !rank_of || !lists || !workspace || (reinterpret_cast<uintptr_t>(lists) & 15))
+        return LSS_EINVAL;
+    const long DHW = (long)dims->D * dims->H * dims->W;
+    const long nprime = (long)dims->B * dims->N * DHW;
+    if (nprime >= INT_MAX || !ord_fits((long)dims->N * DHW)) return LSS_EUNSUPPORTED;
+    const int ncells = grid->nx[0] * grid->nx[1] * grid->nx[2] * dims->B;
+    int32_t* list = static_cast<int32_t*>(lists);
+    int2* ovf = reinterpret_cast<int2*>(static_cast<char*>(lists) + ord_list_bytes(ncells));
+    hipLaunchKernelGGL(k_geometry_cells_ord, dim3(xcd_grid(grid_blocks(nprime, kGeoBlock))), dim3(kGeoBlock), 0,
+                       (hipStream_t)stream, frustum, rots, trans, kinv, pinv, post_trans, dims->N, (int)DHW,
+                       (int)nprime, *grid, out_geom, cell_of, cell_word, rank_of, list, ovf,
+                       &static_cast<ScanWs*>(workspace)->ovf_count);
+    return launch_status();
+}
+
+int lss_cells_from_geom_ordered(const float* geom, int32_t nprime, int32_t points_per_batch, const lss_grid_t* grid,
+                                int32_t* cell_of, int32_t* cell_word, int32_t* rank_of, void* lists,
+                                void* workspace, lss_stream_t stream) {
+    if (!geom || !cell_of || !cell_word || !rank_of || !lists || !workspace || nprime <= 0 || points_per_batch <= 0 ||
+        !grid_ok(grid) || (reinterpret_cast<uintptr_t>(lists) & 15) || nprime % points_per_batch != 0)
+        return LSS_EINVAL;
+    if (!ord_fits(points_per_batch)) return LSS_EUNSUPPORTED;
+    const int ncells = grid->nx[0] * grid->nx[1] * grid->nx[2] * (nprime / points_per_batch);
+    int32_t* list = static_cast<int32_t*>(lists);
+    int2* ovf = reinterpret_cast<int2*>(static_cast<char*>(lists) + ord_list_bytes(ncells));
+    hipLaunchKernelGGL(k_cells_from_geom_ord, dim3(xcd_grid(grid_blocks(nprime, kGeoBlock))), dim3(kGeoBlock), 0,
+                       (hipStream_t)stream, geom, nprime, points_per_batch, *grid, cell_of, cell_word, rank_of, list,
+                       ovf, &static_cast<ScanWs*>(workspace)->ovf_count);
+    return launch_status();
+}
+
+int lss_csr_build_ordered(const int32_t* cell_of, const int32_t* rank_of, int32_t nprime, int32_t* cell_word,
+                          int32_t ncells, const lss_dims_t* dims, const void* lists, int32_t* cell_start,
+                          long long* sorted_key, int32_t* sorted_row, void* workspace, lss_stream_t stream) {
+    if (!cell_of || !rank_of || !cell_word || !lists || !cell_start || !sorted_key || !sorted_row || !workspace ||
+        nprime <= 0 || ncells <= 0 || (reinterpret_cast<uintptr_t>(lists) & 15))
+        return LSS_EINVAL;
+    int DHW = nprime, HW = nprime;  // no dims: the row of point p is p (per-point rows)
+    if (dims != nullptr) {
+        if (!dims_ok(dims)) return LSS_EINVAL;
+        DHW = dims->D * dims->H * dims->W;
+        HW = dims->H * dims->W;
+        if ((long)dims->B * dims->N * DHW != nprime) return LSS_EINVAL;
+    }
+    const int nb = (ncells + kScanItems - 1) / kScanItems;
+    ScanWs* ws = static_cast<ScanWs*>(workspace);
+    const int32_t* list = static_cast<const int32_t*>(lists);
+    const int2* ovf = reinterpret_cast<const int2*>(static_cast<const char*>(lists) + ord_list_bytes(ncells));
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_scan_lookback, dim3(nb), dim3(1024), 0, s, cell_word, ncells, ws, cell_start, kOrdCountMask);
+    hipLaunchKernelGGL(k_scatter_ord, dim3(xcd_grid(grid_blocks(std::max(nprime, ncells), kBlock))), dim3(kBlock), 0, s,
+                       cell_of, rank_of, nprime, cell_start, list, ovf, DHW, HW, sorted_key, sorted_row, cell_word,
+                       ncells, ws);
     debug_check_csr(cell_start, ncells, cell_of, nprime, s);
     return launch_status();
 }

@@ -179,6 +179,8 @@ class PlanWs:
         self.counts = torch.zeros(ncells, device=dev, dtype=torch.int32)
         self.workspace = torch.zeros(int(lib.lss_csr_workspace_bytes(ncells)), device=dev, dtype=torch.uint8)
         self.scratch = torch.empty(int(lib.lss_csr_scratch_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
+        # ordered plans' per-cell block records (no initialisation needed)
+        self.lists = torch.empty(int(lib.lss_csr_lists_bytes(ncells, nprime)), device=dev, dtype=torch.uint8)
         self.last_stream = None
         self.last_event = None
 
@@ -227,6 +229,15 @@ class _PlanWorkspace:
 
 PLAN_WS = _PlanWorkspace()
 USE_PLAN_WS = True  # False: a count memset + lss_csr_build (two-kernel scan) per plan
+# with a persistent workspace: ordered plans (lss_geometry_cells_ordered + lss_csr_build_ordered, three
+# kernels, every point written at its canonical position) instead of lss_geometry_cells +
+# lss_csr_build_ws (four kernels: arrival-order slots, then k_csr_canon sorts each cell)
+USE_PLAN_ORDERED = True
+_ORD_MAX_SAMPLE_POINTS = (1 << 20) - 512  # lss_geometry_cells_ordered's limit (points per sample)
+
+
+def _ordered(ws, points_per_sample: int) -> bool:
+    return ws is not None and USE_PLAN_ORDERED and points_per_sample < _ORD_MAX_SAMPLE_POINTS
 
 
 def _plan_counts(dev: torch.device, ncells: int, nprime: int):
@@ -260,14 +271,21 @@ def _counted_plan(dev: torch.device, ws: Optional[PlanWs], launch_cells, build_c
     return out
 
 
-def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None):
-    """Counting sort into the canonical CSR (lss_csr_build[_ws]): cell_start, sorted_key, sorted_row."""
+def _build_csr(cell_of, slot_of, counts, dims, ncells: int, dev, ws=None, ordered=False):
+    """Counting sort into the canonical CSR (lss_csr_build[_ws|_ordered]): cell_start, sorted_key,
+    sorted_row."""
     lib = _lib.load()
     B, N, D, H, W = dims
     nprime = B * N * D * H * W
     cell_start = torch.empty(ncells + 1, device=dev, dtype=torch.int32)
     sorted_key = torch.empty(nprime, device=dev, dtype=torch.int64)
     sorted_row = torch.empty(nprime, device=dev, dtype=torch.int32)
+    if ordered:
+        _lib.check(lib.lss_csr_build_ordered(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
+                                             make_dims(*dims), _lib.ptr(ws.lists), _lib.ptr(cell_start),
+                                             _lib.ptr(sorted_key), _lib.ptr(sorted_row), _lib.ptr(ws.workspace),
+                                             _lib.stream_handle(dev)), "lss_csr_build_ordered")
+        return cell_start, sorted_key, sorted_row
     if ws is not None:
         _lib.check(lib.lss_csr_build_ws(_lib.ptr(cell_of), _lib.ptr(slot_of), nprime, _lib.ptr(counts), ncells,
                                         make_dims(*dims), _lib.ptr(cell_start), _lib.ptr(sorted_key),
@@ -305,8 +323,15 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
         slot_of = torch.empty(nprime, device=dev, dtype=torch.int32)
     dims = make_dims(B, N, D, H, W)
     g = grid.c_struct()
+    ordered = want_csr and _ordered(ws, N * D * H * W)
 
     def launch_cells():
+        if ordered:
+            _lib.check(lib.lss_geometry_cells_ordered(
+                _lib.ptr(fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv), _lib.ptr(pt), dims, g,
+                _lib.ptr(geom), _lib.ptr(cell_of), _lib.ptr(counts), _lib.ptr(slot_of), _lib.ptr(ws.lists),
+                _lib.ptr(ws.workspace), _lib.stream_handle(dev)), "lss_geometry_cells_ordered")
+            return
         _lib.check(lib.lss_geometry_cells(_lib.ptr(fr), _lib.ptr(ro), _lib.ptr(tr), _lib.ptr(kinv), _lib.ptr(pinv),
                                           _lib.ptr(pt), dims, g, _lib.ptr(geom), _lib.ptr(cell_of), _lib.ptr(counts),
                                           _lib.ptr(slot_of), _lib.stream_handle(dev)), "lss_geometry_cells")
@@ -315,7 +340,8 @@ def plan_from_cameras(frustum: torch.Tensor, rots, trans, intrins, post_rots, po
         launch_cells()
         return SplatPlan((B, N, D, H, W), grid, cell_of, None, None, None, geom)
     cell_start, sorted_key, sorted_row = _counted_plan(
-        dev, ws, launch_cells, lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws))
+        dev, ws, launch_cells,
+        lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws, ordered))
     return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, geom)
 
 
@@ -330,14 +356,22 @@ def plan_from_geom(geom: torch.Tensor, grid: GridSpec) -> SplatPlan:
     cell_of = torch.empty(nprime, device=dev, dtype=torch.int32)
     counts, ws = _plan_counts(dev, ncells, nprime)
     slot_of = torch.empty(nprime, device=dev, dtype=torch.int32)
+    ordered = _ordered(ws, nprime // B)
 
     def launch_cells():
+        if ordered:
+            _lib.check(lib.lss_cells_from_geom_ordered(_lib.ptr(gm), nprime, nprime // B, grid.c_struct(),
+                                                       _lib.ptr(cell_of), _lib.ptr(counts), _lib.ptr(slot_of),
+                                                       _lib.ptr(ws.lists), _lib.ptr(ws.workspace),
+                                                       _lib.stream_handle(dev)), "lss_cells_from_geom_ordered")
+            return
         _lib.check(lib.lss_cells_from_geom(_lib.ptr(gm), nprime, nprime // B, grid.c_struct(), _lib.ptr(cell_of),
                                            _lib.ptr(counts), _lib.ptr(slot_of), _lib.stream_handle(dev)),
                    "lss_cells_from_geom")
 
     cell_start, sorted_key, sorted_row = _counted_plan(
-        dev, ws, launch_cells, lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws))
+        dev, ws, launch_cells,
+        lambda: _build_csr(cell_of, slot_of, counts, (B, N, D, H, W), ncells, dev, ws, ordered))
     return SplatPlan((B, N, D, H, W), grid, cell_of, cell_start, sorted_key, sorted_row, None)
 
 
@@ -589,10 +623,11 @@ class DepthnetLiftSplat(torch.autograd.Function):
             if need[1]:
                 # split-K as a batched GEMM: one (O x npix) x (npix x K) product gives hipBLASLt only
                 # (O / 64) x (K / 64) = 16 tiles for 8,448-long dot products (76 us at c3); KSPLIT slices of
-                # the pixels fill the chip, their bf16 partials summed in fp32 (slice order)
+                # the pixels fill the chip, their partials kept in fp32 (bf16 partials would be rounded
+                # before the sum, and pixel-gradient sums cancel) and summed in slice order
                 S = _wgrad_splits(npix)
-                part = torch.bmm(dd.view(S, npix // S, O).transpose(1, 2), fm.view(S, npix // S, K))
-                d_w = part.sum(0, dtype=torch.float32).view(weight.shape).to(weight.dtype)
+                part = _bmm_f32(dd.view(S, npix // S, O).transpose(1, 2), fm.view(S, npix // S, K))
+                d_w = part.sum(0).view(weight.shape).to(weight.dtype)
             if need[2]:
                 # per-channel sums straight from the NCHW d(logits) (torch's dim-0 reduction of the
                 # pixel-major copy ran on 128 threads: 89 us at c3)
@@ -605,6 +640,28 @@ class DepthnetLiftSplat(torch.autograd.Function):
             d_dn, feat, weight, [weight.shape[0]], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
             [need[0], need[1], need[2]])
         return d_feat, d_w, d_b, None, None, None, None
+
+
+_BMM_F32_OUT = {}
+
+
+def _bmm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bf16 x bf16 batched GEMM with fp32 outputs (torch.bmm's out_dtype overload, one rounding per
+    element); where this torch build lacks that overload for the device, an fp32 GEMM of the same
+    bf16 values (exact products, fp32 sums). Probed once per device, outside any capture (the eager
+    warm-up steps come first)."""
+    dev = a.device
+    ok = _BMM_F32_OUT.get(dev)
+    if ok is None:
+        try:
+            t = torch.ones(1, 2, 2, device=dev, dtype=torch.bfloat16)
+            ok = torch.bmm(t, t, out_dtype=torch.float32).dtype == torch.float32
+        except (RuntimeError, TypeError, NotImplementedError):
+            ok = False
+        _BMM_F32_OUT[dev] = ok
+    if ok:
+        return torch.bmm(a, b, out_dtype=torch.float32)
+    return torch.bmm(a.float(), b.float())
 
 
 def depthnet_lift_splat(feat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, plan: SplatPlan,

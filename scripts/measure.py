@@ -19,6 +19,7 @@ Steps:
                                       limits) over bench.py (eager steps) for kernels matching REGEX:
                                       per-kernel averages in NAME.txt
   kbench:NAME:args                    scripts/kbench.py with args, log kept
+  py:NAME:script args                 python scripts/<script> args (a diagnostics script), log kept
   lib:VARIANT                         later steps load lss-carla_amd/variants/VARIANT.so (product: the default)
 """
 from __future__ import annotations
@@ -44,7 +45,13 @@ def run(cmd, log_path, limit, env=None, cwd=REPO) -> int:
     t0 = time.time()
     full = ["timeout", "-k", "10", str(limit)] + cmd
     with open(log_path, "w") as fh:
-        rc = subprocess.call(full, stdout=fh, stderr=subprocess.STDOUT, env=env, cwd=cwd)
+        proc = subprocess.Popen(full, stdout=fh, stderr=subprocess.STDOUT, env=env, cwd=cwd)
+        while True:  # a heartbeat: a first step compiling library kernels can be silent for minutes
+            try:
+                rc = proc.wait(timeout=50)
+                break
+            except subprocess.TimeoutExpired:
+                print(f"  ... {os.path.basename(log_path)} running, {time.time() - t0:.0f} s", flush=True)
     print(f"  rc={rc} in {time.time() - t0:.0f} s ({os.path.basename(log_path)})", flush=True)
     return rc
 
@@ -142,7 +149,10 @@ def step_pmc(out, spec):
         return rc
     pat = re.compile(regex)
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+    files = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
+    if files and os.path.getsize(files[0]) < 32 << 20:  # kept for scripts/step_roofline.py
+        shutil.copy(files[0], os.path.join(out, f"{name}_counter_collection.csv"))
+    for f in files:
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
             if pat.search(k):
@@ -169,6 +179,15 @@ def step_kbench(out, spec):
     return rc
 
 
+def step_py(out, spec):
+    name, _, extra = spec.partition(":")
+    args = shlex.split(extra)
+    log = os.path.join(out, f"{name}.log")
+    rc = run([PY, "-u", os.path.join("scripts", args[0])] + args[1:], log, 600)
+    print(tail(log, 40), flush=True)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", required=True)
@@ -178,7 +197,7 @@ def main():
     os.makedirs(out, exist_ok=True)
     os.chdir(REPO)
     fns = {"tests": step_tests, "smoke": step_smoke, "bench": step_bench, "trace": step_trace, "pmc": step_pmc,
-           "kbench": step_kbench}
+           "kbench": step_kbench, "py": step_py}
     for s in a.steps:
         kind, _, spec = s.partition(":")
         print(f"== {s}", flush=True)

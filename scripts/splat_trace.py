@@ -84,9 +84,19 @@ def main():
     print("chunk rest (t3-t2)   ", q(rel[has2, 3] - rel[has2, 2]))
     print("chunk total (t3-t0)  ", q(rel[c, 3] - rel[c, 0]))
     print("chunk end            ", q(rel[c, 3]))
-    print("zero start           ", q(rel[z, 0]))
-    print("zero total           ", q(rel[z, 3] - rel[z, 0]))
-    print("zero end             ", q(rel[z, 3]))
+    if z.any():
+        print("zero start           ", q(rel[z, 0]))
+        print("zero total           ", q(rel[z, 3] - rel[z, 0]))
+        print("zero end             ", q(rel[z, 3]))
+    # start skew between XCDs: per XCC, the waves' start-time percentiles (is the ramp dispatch or XCD start?)
+    xcc = (buf[:, 4] >> np.uint64(32)).astype(np.int64)
+    for x in range(8):
+        for nm, msk in (("chunk", c), ("zero", z)):
+            sel = msk & (xcc == x)
+            if sel.any():
+                print(f"xcc {x} {nm:5s} waves {sel.sum():5d} start p0 {rel[sel, 0].min():5.2f} p10 "
+                      f"{np.percentile(rel[sel, 0], 10):5.2f} p50 {np.percentile(rel[sel, 0], 50):5.2f} "
+                      f"max {rel[sel, 0].max():5.2f}  end max {rel[sel, 3].max():5.2f}")
     # the slowest chunk waves and their chunks
     sk = plan.sorted_key.cpu().numpy()
     tot = int(plan.cell_start[-1])

@@ -552,3 +552,36 @@ def test_random_shapes_fwd_bwd_vs_oracle(seed, B, N, fH, fW, D, half, dx, Z, bf1
     want_g = ref.lift_splat_backward_fp64(dn_in.numpy(), geom, gd.float().cpu().numpy(), dx_, bx_, nx_, D, 64)
     tol = ATOL if dtype == torch.float32 else 2e-2
     np.testing.assert_allclose(dnd.grad.float().cpu().numpy(), want_g, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("crowd", [3, 11])
+def test_ordered_plan_overflow_records_exact(crowd):
+    """Ordered plans (lss_cells_from_geom_ordered + lss_csr_build_ordered): a cell fed by `crowd` blocks of
+    256 points -- more than the 8 records a cell's list holds at 11, so 3 of its records go through the
+    overflow area -- and a second sample of scattered points. The CSR equals the four-kernel path's bit
+    for bit (ascending cell, then point id), over two consecutive plans, and the counts, scan state and
+    overflow counter come back zero-filled."""
+    grid = ops.GridSpec.from_conf(syn.grid_conf())
+    B, N, D, H, W = 2, 1, 16, 8, 22              # 2,816 points per sample = 11 blocks
+    g = torch.Generator().manual_seed(crowd)
+    geom = (torch.rand(B, N, D, H, W, 3, generator=g) - 0.5) * torch.tensor([100.0, 100.0, 20.0])
+    flat = geom.view(B, -1, 3)
+    flat[0, : crowd * 256] = torch.tensor([1.1, -2.3, 0.4])   # one cell, `crowd` blocks
+    gd = geom.to(DEV)
+    old, ops.USE_PLAN_ORDERED = ops.USE_PLAN_ORDERED, False
+    try:
+        want = ops.plan_from_geom(gd, grid)
+    finally:
+        ops.USE_PLAN_ORDERED = old
+    for _ in range(2):
+        got = ops.plan_from_geom(gd, grid)
+        torch.cuda.synchronize()
+        assert torch.equal(got.cell_start, want.cell_start)
+        assert torch.equal(got.sorted_key, want.sorted_key)
+        kept = int(want.cell_start[-1])
+        assert torch.equal(got.sorted_row[:kept], want.sorted_row[:kept])
+    w = ops.PLAN_WS.get(DEV, grid.ncells(B), B * N * D * H * W, create=False)
+    words = w.workspace.view(torch.int32).cpu().numpy()
+    assert int(w.counts.abs().sum()) == 0 and words[0] == 0 and not words[4:].any()
+    big = int((want.cell_start[1:] - want.cell_start[:-1]).max())
+    assert big == crowd * 256

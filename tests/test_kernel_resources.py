@@ -16,7 +16,7 @@ import pytest
 from lss_carla_amd import _lib
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-HOT = ("k_geometry_cells", "k_scan_lookback", "k_scatter_ws", "k_csr_canon", "k_lift_prep", "k_depthnet_lift2",
+HOT = ("k_geometry_cells", "k_scan_lookback", "k_scatter_ws", "k_scatter_ord", "k_cells_from_geom_ord", "k_csr_canon", "k_lift_prep", "k_depthnet_lift2",
        "k_depthnet_lift3", "k_splat_fwd_nhwc", "k_splat_fwd_nchw2", "k_splat_bwd_tile", "k_splat_bwd_reg",
        "k_bev_rows")
 
