@@ -150,6 +150,23 @@ int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int3
                int32_t act, int32_t ngroups, float* partial, float* coef, float* dgamma, float* dbeta, void* dx,
                void* dresidual, void* stream);
 
+/* lss_bn_fwd / lss_bn_bwd with a sync workspace (lss_bn_sync_words() uint32, zero-filled once; every
+ * call leaves it zero-filled; one call at a time per workspace; NULL = the calls above). For NCHW bf16
+ * maps with several groups per channel (lss_bn_groups > 1), statistics and apply then run in ONE launch:
+ * the blocks of a channel hold their groups in registers and meet on the channel's counters in the
+ * workspace (bounded waits; a block that gives up recomputes the statistics itself). Same outputs,
+ * bit for bit. The workspace's last word overrides the wait bound (0: built in; s > 0: s - 1 polls). */
+int lss_bn_sync_words(void);
+int lss_bn_fwd2(const void* x, const void* residual, int32_t dtype, int32_t layout, int32_t N, int32_t C, int32_t HW,
+                const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
+                float* running_var, long long* num_batches_tracked, int32_t act, int32_t ngroups, float* partial,
+                float* save_mean, float* save_rstd, float* scale, float* shift, void* y, uint32_t* sync,
+                void* stream);
+int lss_bn_bwd2(const void* dy, const void* x, const void* y, int32_t dtype, int32_t layout, int32_t N, int32_t C,
+                int32_t HW, const float* scale, const float* shift, const float* save_mean, const float* save_rstd,
+                int32_t act, int32_t ngroups, float* partial, float* coef, float* dgamma, float* dbeta, void* dx,
+                void* dresidual, uint32_t* sync, void* stream);
+
 /* Bilinear upsampling with align_corners=True (nn.Upsample(mode="bilinear", align_corners=True),
  * src/models.py:19, 109) fused with Up's channel concatenation (torch.cat([x2, x1], 1),
  * src/models.py:33). All tensors channels-last bf16, 16-byte aligned, C1 and C2 multiples of 8,

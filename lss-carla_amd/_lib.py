@@ -108,6 +108,11 @@ SIGNATURES = {
                                   _p, _p, _p, _i32, _i32, _p, _p, _p, _p, _p, _p, _p]),
     "lss_bn_bwd": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p,
                                   _p, _p, _p, _p, _p]),
+    "lss_bn_sync_words": (ctypes.c_int, []),
+    "lss_bn_fwd2": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, ctypes.c_float, ctypes.c_float,
+                                   _p, _p, _p, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "lss_bn_bwd2": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p,
+                                   _p, _p, _p, _p, _p, _p]),
     "lss_upsample_cat_fwd": (ctypes.c_int, [_p, _p] + [_i32] * 7 + [_p, _p]),
     "lss_upsample_bwd": (ctypes.c_int, [_p] + [_i32] * 7 + [_p, _p]),
     "lss_se_fwd": (ctypes.c_int, [_p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p, _p]),

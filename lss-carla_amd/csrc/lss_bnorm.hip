@@ -585,6 +585,270 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_fused_reg_nchw(const bf16* __
     }
 }
 
+// ---- NCHW with G > 1 groups per channel, bf16: statistics and apply in ONE launch (lss_bn_fwd2 /
+// lss_bn_bwd2 with a sync workspace). Block b = (channel c = b / G, group q = b % G), so the G blocks of
+// a channel are consecutive in dispatch order (a cluster). Each block holds its group of the channel
+// (images [N q / G, N (q + 1) / G)) in registers, publishes its partial pair with an agent-scope store,
+// arrives on the channel's counter and waits for the other G - 1 blocks of its cluster, folds the G
+// pairs in group order and applies from its registers: x (and dy) read once instead of twice, one
+// launch instead of two. Same sums in the same order as k_bn_stats_nchw + k_bn_apply_nchw (and the
+// backward pair), so the same bits. The wait is bounded: a block that gives up recomputes every
+// group's pair from memory itself (same code, same order: exact), so a cluster whose blocks are not
+// all resident only costs time. The last block to leave re-zeroes the channel's two counters.
+constexpr unsigned kBnSpinLimit = 1u << 20;
+constexpr int kBnClusterMaxG = 64;  // (the timeout path's LDS pairs)
+constexpr int kBnClusterIT = 8;     // 16-B vectors per thread held in registers
+constexpr int kBnSyncMaxC = 4096;   // channels a sync workspace covers (two counters each, + the spin word)
+
+__device__ __forceinline__ void st_pair_agent(float* p, float a, float b) {
+    const unsigned long long v = ((unsigned long long)__float_as_uint(b) << 32) | __float_as_uint(a);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 ld_pair_agent(const float* p) {
+    const unsigned long long v =
+        __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_float2(__uint_as_float((unsigned)v), __uint_as_float((unsigned)(v >> 32)));
+}
+
+// thread 0: publish (a, b) as group q's pair, arrive, wait for the cluster; true = all G arrived.
+// limit_word (the workspace's last word): 0 = kBnSpinLimit polls, s > 0 = s - 1 (tests of the timeout path)
+__device__ __forceinline__ bool cluster_publish_wait(float* __restrict__ partial, size_t at, float a, float b,
+                                                     unsigned* arrive, int G, const unsigned* limit_word) {
+    st_pair_agent(partial + at, a, b);
+    __threadfence();  // the pair before the arrival
+    atomicAdd(arrive, 1u);
+    const unsigned lo = *limit_word;
+    const unsigned limit = lo ? lo - 1u : kBnSpinLimit;
+    for (unsigned spins = 0;; ++spins) {
+        if (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)G) {
+            __threadfence();
+            return true;
+        }
+        if (spins >= limit) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+__device__ __forceinline__ void cluster_leave(unsigned* arrive, unsigned* leave, int G) {
+    if (atomicAdd(leave, 1u) == (unsigned)G - 1u) {
+        atomicExch(arrive, 0u);
+        atomicExch(leave, 0u);
+    }
+}
+
+// wave 0: the G pairs of channel c in fold_groups' order (lanes over groups, then a butterfly), from
+// the published pairs or, after a timeout, from the block's own recomputation in LDS
+__device__ __forceinline__ void fold_cluster(const float* __restrict__ partial, int c, int G, bool published,
+                                             const float (*s_pairs)[2], float& a, float& b) {
+    a = 0.f;
+    b = 0.f;
+    for (int q = threadIdx.x; q < G; q += kWave) {
+        const float2 v = published ? ld_pair_agent(partial + ((size_t)c * G + q) * 2) : make_float2(s_pairs[q][0], s_pairs[q][1]);
+        a += v.x;
+        b += v.y;
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, kWave);
+        b += __shfl_xor(b, o, kWave);
+    }
+}
+
+template <int V>
+__global__ __launch_bounds__(kBlock) void k_bn_cluster_nchw(const bf16* __restrict__ x, const bf16* __restrict__ res,
+                                                            BnGeo g, int G, float* __restrict__ partial, BnParams P,
+                                                            int act, unsigned* __restrict__ sync,
+                                                            bf16* __restrict__ y) {
+    __shared__ float s_red[2][kBlock / kWave];
+    __shared__ float s_pairs[kBnClusterMaxG][2];
+    __shared__ float s_coef[2];
+    __shared__ int s_ok;
+    const int c = blockIdx.x / G, q = blockIdx.x - c * G;
+    const int n0 = (int)((long)g.N * q / G), n1 = (int)((long)g.N * (q + 1) / G);
+    const int per = g.HW / V, count = per * (n1 - n0);
+    const bf16* xc = x + ((size_t)n0 * g.C + c) * g.HW;  // (chan_vec over the group's images)
+    PackedBf16<V> raw[kBnClusterIT];
+#pragma unroll
+    for (int it = 0; it < kBnClusterIT; ++it)
+        raw[it].load(xc + chan_vec(g, 0, per, count, (int)threadIdx.x + it * kBlock, V) + (size_t)0);
+    const float k = first_nchw(x, c, g);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int it = 0; it < kBnClusterIT; ++it) {
+        if ((int)threadIdx.x + it * kBlock < count) {
+            float v[V];
+            raw[it].get(v);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const float d = v[j] - k;
+                s1 += d;
+                s2 = fmaf(d, d, s2);
+            }
+        }
+    }
+    block_pair_sum(s1, s2, s_red);
+    unsigned* arrive = sync + 2 * c;
+    if (threadIdx.x == 0)
+        s_ok = cluster_publish_wait(partial, ((size_t)c * G + q) * 2, s1, s2, arrive, G, sync + 2 * kBnSyncMaxC);
+    __syncthreads();
+    const bool ok = s_ok;
+    if (!ok) {  // (never expected) every group's pair from memory, in k_bn_stats_nchw's order
+        for (int qq = 0; qq < G; ++qq) {
+            float a = 0.f, b = 0.f;
+            for_chunk_nchw<V, bf16>(g, G, c, qq, [&](size_t i) {
+                float v[V];
+                ldv<V>(x + i, v);
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const float d = v[j] - k;
+                    a += d;
+                    b = fmaf(d, d, b);
+                }
+            });
+            block_pair_sum(a, b, s_red);
+            if (threadIdx.x == 0) {
+                s_pairs[qq][0] = a;
+                s_pairs[qq][1] = b;
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x < kWave) {
+        float f1, f2;
+        fold_cluster(partial, c, G, ok, s_pairs, f1, f2);
+        float sc, sh;
+        finalize_channel(f1, f2, k, (float)g.N * (float)g.HW, c, g.C, P, q == 0 && threadIdx.x == 0, sc, sh);
+        if (threadIdx.x == 0) {
+            s_coef[0] = sc;
+            s_coef[1] = sh;
+            cluster_leave(arrive, arrive + 1, G);
+        }
+    }
+    __syncthreads();
+    const float sc = s_coef[0], sh = s_coef[1];
+#pragma unroll
+    for (int it = 0; it < kBnClusterIT; ++it) {
+        const int e = (int)threadIdx.x + it * kBlock;
+        if (e < count) {
+            const size_t i = ((size_t)n0 * g.C + c) * g.HW + chan_vec(g, 0, per, count, e, V);
+            float v[V], r[V];
+            raw[it].get(v);
+            if (res) ldv<V>(res + i, r);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                float z = fmaf(v[j], sc, sh);
+                if (res) z += r[j];
+                v[j] = act_fwd(z, act);
+            }
+            stv<V>(y + i, v);
+        }
+    }
+}
+
+template <int V, bool RELU>
+__global__ __launch_bounds__(kBlock) void k_bn_bwd_cluster_nchw(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                                const bf16* __restrict__ y, BnGeo g, int G,
+                                                                const float* __restrict__ stats, float* __restrict__ partial,
+                                                                int act, unsigned* __restrict__ sync,
+                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                                bf16* __restrict__ dx, bf16* __restrict__ dres) {
+    __shared__ float s_red[2][kBlock / kWave];
+    __shared__ float s_pairs[kBnClusterMaxG][2];
+    __shared__ float s_coef[2];
+    __shared__ int s_ok;
+    const int c = blockIdx.x / G, q = blockIdx.x - c * G;
+    const int n0 = (int)((long)g.N * q / G), n1 = (int)((long)g.N * (q + 1) / G);
+    const int per = g.HW / V, count = per * (n1 - n0);
+    const size_t base = ((size_t)n0 * g.C + c) * g.HW;
+    PackedBf16<V> rd[kBnClusterIT], rx[kBnClusterIT], ry[RELU ? kBnClusterIT : 1];
+#pragma unroll
+    for (int it = 0; it < kBnClusterIT; ++it) {
+        const size_t i = base + chan_vec(g, 0, per, count, (int)threadIdx.x + it * kBlock, V);
+        rd[it].load(dy + i);
+        rx[it].load(x + i);
+        if constexpr (RELU) ry[it].load(y + i);
+    }
+    const float mean = stats[c], rstd = stats[g.C + c], sc = stats[2 * g.C + c], sh = stats[3 * g.C + c];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int it = 0; it < kBnClusterIT; ++it) {
+        if ((int)threadIdx.x + it * kBlock < count) {
+            float d[V], xv[V], yv[V];
+            rd[it].get(d);
+            rx[it].get(xv);
+            if constexpr (RELU) ry[it].get(yv);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const float gr = grad_pre(d[j], RELU ? yv[j] : 0.f, fmaf(xv[j], sc, sh), act);
+                sg += gr;
+                sgx = fmaf(gr, (xv[j] - mean) * rstd, sgx);
+            }
+        }
+    }
+    block_pair_sum(sg, sgx, s_red);
+    unsigned* arrive = sync + 2 * c;
+    if (threadIdx.x == 0)
+        s_ok = cluster_publish_wait(partial, ((size_t)c * G + q) * 2, sg, sgx, arrive, G, sync + 2 * kBnSyncMaxC);
+    __syncthreads();
+    const bool ok = s_ok;
+    if (!ok) {
+        for (int qq = 0; qq < G; ++qq) {
+            float a = 0.f, b = 0.f;
+            for_chunk_nchw<V, bf16>(g, G, c, qq, [&](size_t i) {
+                float d[V], xv[V], yv[V];
+                ldv<V>(dy + i, d);
+                ldv<V>(x + i, xv);
+                if constexpr (RELU) ldv<V>(y + i, yv);
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const float gr = grad_pre(d[j], RELU ? yv[j] : 0.f, fmaf(xv[j], sc, sh), act);
+                    a += gr;
+                    b = fmaf(gr, (xv[j] - mean) * rstd, b);
+                }
+            });
+            block_pair_sum(a, b, s_red);
+            if (threadIdx.x == 0) {
+                s_pairs[qq][0] = a;
+                s_pairs[qq][1] = b;
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x < kWave) {
+        float fg, fgx;
+        fold_cluster(partial, c, G, ok, s_pairs, fg, fgx);
+        if (threadIdx.x == 0) {
+            if (q == 0) {
+                if (dgamma) dgamma[c] = fgx;
+                if (dbeta) dbeta[c] = fg;
+            }
+            const float n = (float)g.N * (float)g.HW;
+            s_coef[0] = fg / n;
+            s_coef[1] = fgx / n;
+            cluster_leave(arrive, arrive + 1, G);
+        }
+    }
+    __syncthreads();
+    const float mg = s_coef[0], mgx = s_coef[1];
+#pragma unroll
+    for (int it = 0; it < kBnClusterIT; ++it) {
+        const int e = (int)threadIdx.x + it * kBlock;
+        if (e < count) {
+            const size_t i = base + chan_vec(g, 0, per, count, e, V);
+            float d[V], xv[V], yv[V], o[V], gr[V];
+            rd[it].get(d);
+            rx[it].get(xv);
+            if constexpr (RELU) ry[it].get(yv);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                gr[j] = grad_pre(d[j], RELU ? yv[j] : 0.f, fmaf(xv[j], sc, sh), act);
+                o[j] = sc * (gr[j] - mg - (xv[j] - mean) * rstd * mgx);
+            }
+            stv<V>(dx + i, o);
+            if (dres) stv<V>(dres + i, gr);
+        }
+    }
+}
+
 // ============================================================================= NHWC (channels-last)
 // block q: pixels [M q / G, M (q+1) / G) x all C channels; thread = 8 consecutive channels of a pixel.
 // Partials (C, G, 2) as in NCHW; a separate fold kernel (one wave per channel) turns them into the
@@ -978,6 +1242,18 @@ template <typename T> inline bool fused_reg(int V, long cnt) {
 
 inline int vec_nchw(int HW) { return HW % 8 == 0 ? 8 : (HW % 4 == 0 ? 4 : 1); }
 
+#ifndef LSS_BN_CLUSTER
+#define LSS_BN_CLUSTER 1  // NCHW, G > 1: the cluster kernels when a sync workspace is given (lss_bn_*2)
+#endif
+
+// NCHW bf16 with several groups per channel, each group's vectors held in registers
+template <typename T> inline bool cluster_ok(const uint32_t* sync, int G, int V, const BnGeo& g) {
+    if (!LSS_BN_CLUSTER || sync == nullptr || !std::is_same<T, bf16>::value || V != 8) return false;
+    if (G < 2 || G > kBnClusterMaxG || g.C > kBnSyncMaxC) return false;
+    const long imgs = (g.N + G - 1) / G;  // images of the largest group
+    return imgs * (g.HW / V) <= (long)kBnClusterIT * kBlock;
+}
+
 inline int apply_blocks(const BnGeo& g) {  // grid-stride elementwise passes: up to 8 blocks per CU
     const long nv = (long)g.N * g.HW * g.C / 8;
     const long b = (nv + kBlock - 1) / kBlock;
@@ -998,10 +1274,22 @@ int lss_bn_groups(int32_t N, int32_t C, int32_t HW, int32_t layout) {
     return (int)(g < 1 ? 1 : (g > N ? N : g));
 }
 
+int lss_bn_sync_words(void) { return 2 * kBnSyncMaxC + 1; }
+
 int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layout, int32_t N, int32_t C, int32_t HW,
                const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
                float* running_var, long long* num_batches_tracked, int32_t act, int32_t ngroups, float* partial,
                float* save_mean, float* save_rstd, float* scale, float* shift, void* y, void* stream) {
+    return lss_bn_fwd2(x, residual, dtype, layout, N, C, HW, gamma, beta, eps, momentum, running_mean, running_var,
+                       num_batches_tracked, act, ngroups, partial, save_mean, save_rstd, scale, shift, y, nullptr,
+                       stream);
+}
+
+int lss_bn_fwd2(const void* x, const void* residual, int32_t dtype, int32_t layout, int32_t N, int32_t C, int32_t HW,
+                const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
+                float* running_var, long long* num_batches_tracked, int32_t act, int32_t ngroups, float* partial,
+                float* save_mean, float* save_rstd, float* scale, float* shift, void* y, uint32_t* sync,
+                void* stream) {
     const BnGeo g{N, C, HW};
     if (!x || !y || !partial || !save_mean || !save_rstd || !scale || !shift || ngroups <= 0 || !bn_ok(g, layout))
         return LSS_CONV_EINVAL;
@@ -1032,7 +1320,10 @@ int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layou
             const int V = vec_nchw(HW);                                                                            \
             const dim3 gr(C * G), bl(kBlock);                                                                      \
             const long cnt = (long)N * (HW / V);                                                                   \
-            if (G == 1 && LSS_BN_FUSED && fused_reg<T>(V, cnt)) {                                                  \
+            if (cluster_ok<T>(sync, G, V, g)) {                                                                    \
+                hipLaunchKernelGGL((k_bn_cluster_nchw<8>), gr, bl, 0, s, (const bf16*)xx, (const bf16*)rr, g, G,   \
+                                   partial, P, (int)act, (unsigned*)sync, (bf16*)yy);                              \
+            } else if (G == 1 && LSS_BN_FUSED && fused_reg<T>(V, cnt)) {                                           \
                 if (V == 8 && cnt <= 4 * kBlock)                                                                   \
                     hipLaunchKernelGGL((k_bn_fused_reg_nchw<8, 4>), gr, bl, 0, s, (const bf16*)xx,                \
                                        (const bf16*)rr, g, P, (int)act, (bf16*)yy);                                \
@@ -1073,6 +1364,14 @@ int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int3
                int32_t HW, const float* scale, const float* shift, const float* save_mean, const float* save_rstd,
                int32_t act, int32_t ngroups, float* partial, float* coef, float* dgamma, float* dbeta, void* dx,
                void* dresidual, void* stream) {
+    return lss_bn_bwd2(dy, x, y, dtype, layout, N, C, HW, scale, shift, save_mean, save_rstd, act, ngroups, partial,
+                       coef, dgamma, dbeta, dx, dresidual, nullptr, stream);
+}
+
+int lss_bn_bwd2(const void* dy, const void* x, const void* y, int32_t dtype, int32_t layout, int32_t N, int32_t C,
+                int32_t HW, const float* scale, const float* shift, const float* save_mean, const float* save_rstd,
+                int32_t act, int32_t ngroups, float* partial, float* coef, float* dgamma, float* dbeta, void* dx,
+                void* dresidual, uint32_t* sync, void* stream) {
     const BnGeo g{N, C, HW};
     if (!dy || !x || !scale || !shift || !save_mean || !save_rstd || !partial || !coef || !dx || ngroups <= 0 ||
         !bn_ok(g, layout))
@@ -1106,7 +1405,15 @@ int lss_bn_bwd(const void* dy, const void* x, const void* y, int32_t dtype, int3
             const int V = vec_nchw(HW);                                                                            \
             const dim3 gr(C * G), bl(kBlock);                                                                      \
             const long cnt = (long)N * (HW / V);                                                                   \
-            if (G == 1 && LSS_BN_FUSED && fused_reg<T>(V, cnt)) {                                                  \
+            if (cluster_ok<T>(sync, G, V, g)) {                                                                    \
+                const bf16 *db = (const bf16*)d, *xb = (const bf16*)xx, *yb = (const bf16*)yy;                     \
+                if (act == LSS_ACT_RELU)                                                                           \
+                    hipLaunchKernelGGL((k_bn_bwd_cluster_nchw<8, true>), gr, bl, 0, s, db, xb, yb, g, G, stats,    \
+                                       partial, (int)act, (unsigned*)sync, dgamma, dbeta, (bf16*)o, (bf16*)orr);   \
+                else                                                                                               \
+                    hipLaunchKernelGGL((k_bn_bwd_cluster_nchw<8, false>), gr, bl, 0, s, db, xb, yb, g, G, stats,   \
+                                       partial, (int)act, (unsigned*)sync, dgamma, dbeta, (bf16*)o, (bf16*)orr);   \
+            } else if (G == 1 && LSS_BN_FUSED && fused_reg<T>(V, cnt)) {                                           \
                 const bf16 *db = (const bf16*)d, *xb = (const bf16*)xx, *yb = (const bf16*)yy;                     \
                 if (V == 8 && cnt <= 4 * kBlock)                                                                   \
                     hipLaunchKernelGGL((k_bn_bwd_fused_reg_nchw<8, 4>), gr, bl, 0, s, db, xb, yb, g, stats,       \

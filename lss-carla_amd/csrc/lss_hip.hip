@@ -752,7 +752,6 @@ __global__ __launch_bounds__(kBlock) void k_scatter_ord(const int32_t* __restric
             const int c = dchk(cell, ncells, kDbgCell);
             const int a = cell_start[c], z = cell_start[c + 1];
             const int4 l0 = *reinterpret_cast<const int4*>(list + (size_t)c * kOrdList);
-            const int4 l1 = *reinterpret_cast<const int4*>(list + (size_t)c * kOrdList + 4);
             const int n_c = z - a;
             const int myblk = t / kGeoBlock;
             int seen = 0, before = 0;
@@ -760,10 +759,13 @@ __global__ __launch_bounds__(kBlock) void k_scatter_ord(const int32_t* __restric
             ord_rec(l0.y, n_c, myblk, seen, before);
             ord_rec(l0.z, n_c, myblk, seen, before);
             ord_rec(l0.w, n_c, myblk, seen, before);
-            ord_rec(l1.x, n_c, myblk, seen, before);
-            ord_rec(l1.y, n_c, myblk, seen, before);
-            ord_rec(l1.z, n_c, myblk, seen, before);
-            ord_rec(l1.w, n_c, myblk, seen, before);
+            if (seen < n_c) {  // more than 4 blocks share the cell (none at c1-c4, ~1 % of c5's occupied cells)
+                const int4 l1 = *reinterpret_cast<const int4*>(list + (size_t)c * kOrdList + 4);
+                ord_rec(l1.x, n_c, myblk, seen, before);
+                ord_rec(l1.y, n_c, myblk, seen, before);
+                ord_rec(l1.z, n_c, myblk, seen, before);
+                ord_rec(l1.w, n_c, myblk, seen, before);
+            }
             // more than kOrdList blocks share the cell: its other records, in the overflow area's valid
             // prefix (the counter restarts at 0 every plan; the records of this cell end before the
             // cell's points are all accounted for, so nothing past that prefix is read)

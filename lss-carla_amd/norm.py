@@ -22,6 +22,22 @@ USE_HIP_BN = True
 RECOMPUTE_RELU_Y = True
 ACT = {"none": 0, "relu": 1, "swish": 2}
 NCHW, NHWC = 0, 1
+# NCHW maps with several groups per channel: statistics + apply in one launch per direction (the
+# lss_bn_*2 cluster kernels), through a per-device sync workspace (zero-filled once, left zero-filled)
+USE_BN_CLUSTER = True
+_SYNC = {}
+
+
+def _sync(dev: torch.device):
+    if not USE_BN_CLUSTER:
+        return None
+    w = _SYNC.get(dev)
+    if w is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None  # (created by the eager warm-up steps, before any capture)
+        w = torch.zeros(int(_lib.load().lss_bn_sync_words()), device=dev, dtype=torch.int32)
+        _SYNC[dev] = w
+    return w
 
 
 def _layout(x: torch.Tensor) -> Optional[int]:
@@ -59,11 +75,11 @@ class _BnAct(torch.autograd.Function):
                 counter = bn.num_batches_tracked
         rm = bn.running_mean if bn.track_running_stats else None
         rv = bn.running_var if bn.track_running_stats else None
-        _lib.check(lib.lss_bn_fwd(_lib.ptr(x), _lib.ptr(residual), _lib.dtype_code(x.dtype), layout, N, C, HW,
-                                  _lib.ptr(weight), _lib.ptr(bias), float(bn.eps), float(momentum), _lib.ptr(rm),
-                                  _lib.ptr(rv), _lib.ptr(counter), act, groups, _lib.ptr(partial), _lib.ptr(stats[0]),
-                                  _lib.ptr(stats[1]), _lib.ptr(stats[2]), _lib.ptr(stats[3]), _lib.ptr(y), st),
-                   "lss_bn_fwd")
+        _lib.check(lib.lss_bn_fwd2(_lib.ptr(x), _lib.ptr(residual), _lib.dtype_code(x.dtype), layout, N, C, HW,
+                                   _lib.ptr(weight), _lib.ptr(bias), float(bn.eps), float(momentum), _lib.ptr(rm),
+                                   _lib.ptr(rv), _lib.ptr(counter), act, groups, _lib.ptr(partial),
+                                   _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]), _lib.ptr(stats[3]),
+                                   _lib.ptr(y), _lib.ptr(_sync(dev)), st), "lss_bn_fwd2")
         # ReLU's backward needs y; in channels-last without a residual the kernels recompute it from x
         # (lss_bn_bwd), so y is neither kept nor read again
         keep_y = act == ACT["relu"] and (layout == NCHW or residual is not None or not RECOMPUTE_RELU_Y)
@@ -87,11 +103,11 @@ class _BnAct(torch.autograd.Function):
         dbeta = torch.empty(C, **f32)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if has_res else None
-        _lib.check(lib.lss_bn_bwd(_lib.ptr(dy), _lib.ptr(x), _lib.ptr(y), _lib.dtype_code(x.dtype), layout, N, C,
-                                  H * W, _lib.ptr(stats[2]), _lib.ptr(stats[3]), _lib.ptr(stats[0]),
-                                  _lib.ptr(stats[1]), act, groups, _lib.ptr(partial), _lib.ptr(coef),
-                                  _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dx), _lib.ptr(dres),
-                                  _lib.stream_handle(dev)), "lss_bn_bwd")
+        _lib.check(lib.lss_bn_bwd2(_lib.ptr(dy), _lib.ptr(x), _lib.ptr(y), _lib.dtype_code(x.dtype), layout, N, C,
+                                   H * W, _lib.ptr(stats[2]), _lib.ptr(stats[3]), _lib.ptr(stats[0]),
+                                   _lib.ptr(stats[1]), act, groups, _lib.ptr(partial), _lib.ptr(coef),
+                                   _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dx), _lib.ptr(dres),
+                                   _lib.ptr(_sync(dev)), _lib.stream_handle(dev)), "lss_bn_bwd2")
         return dx, dgamma, dbeta, dres, None, None, None
 
 

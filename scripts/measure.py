@@ -74,8 +74,10 @@ def bench_args(extra: str) -> list:
 
 def step_tests(out, spec):
     args = shlex.split(spec) if spec else []
+    if not any(a.startswith("tests") for a in args):
+        args = ["tests"] + args
     log = os.path.join(out, "gpu_tests.log")
-    rc = run([PY, "-u", "-m", "pytest", "tests", "-m", "gpu", "-q", "-rs", "-p", "no:cacheprovider",
+    rc = run([PY, "-u", "-m", "pytest", "-m", "gpu", "-q", "-rs", "-p", "no:cacheprovider",
               "--timeout", "200", "--timeout-method", "thread"] + args, log, 1000)
     print(tail(log, 3), flush=True)
     return rc

@@ -413,3 +413,52 @@ def test_upsample_noninteger_ratio_vs_fp64(Hi, Wi, Ho, Wo):
     y.backward(dy.to(DEV).contiguous(memory_format=cl))
     ref.backward(dy.double())
     torch.testing.assert_close(xd.grad.cpu().double(), xr.grad, rtol=1e-2, atol=2e-2)
+
+
+def _bn_run(x, res, act, dy, seed):
+    """one bn_act forward + backward on a fresh module; every output the kernels produce"""
+    C = x.shape[1]
+    torch.manual_seed(seed)
+    bn = torch.nn.BatchNorm2d(C, eps=1e-3, momentum=0.01).to(DEV).train()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_(0.0, 0.1)
+    xd = x.clone().requires_grad_(True)
+    rd = res.clone().requires_grad_(True) if res is not None else None
+    y = Nm.bn_act(bn, xd, act, rd)
+    y.backward(dy)
+    out = [y.detach(), xd.grad, bn.weight.grad, bn.bias.grad, bn.running_mean.clone(), bn.running_var.clone()]
+    return out + ([rd.grad] if rd is not None else [])
+
+
+@pytest.mark.parametrize("spin", [0, 1])
+@pytest.mark.parametrize("act,with_res", [("swish", False), ("none", True), ("relu", False)])
+@pytest.mark.parametrize("N,C,H,W", [(48, 32, 64, 176), (48, 24, 32, 88), (48, 80, 16, 44), (16, 16, 33, 40)])
+def test_bn_cluster_kernels_bit_identical(N, C, H, W, act, with_res, spin):
+    """NCHW bf16 with several groups per channel: the one-launch cluster kernels (lss_bn_fwd2 / lss_bn_bwd2
+    with a sync workspace) against the two-launch statistics + apply kernels, bit for bit -- outputs,
+    gradients, running statistics. spin = 1 sets the workspace's wait bound to 0 polls, so every block
+    takes the timeout path (recomputes every group's statistics itself): still bit-identical. The
+    workspace's counters come back zero-filled."""
+    g = torch.Generator().manual_seed(N + C + H)
+    x = (torch.randn(N, C, H, W, generator=g) * 2 + 3).bfloat16().to(DEV)
+    res = torch.randn(N, C, H, W, generator=g).bfloat16().to(DEV) if with_res else None
+    dy = torch.randn(N, C, H, W, generator=g).bfloat16().to(DEV)
+    from lss_carla_amd import _lib
+    lib = _lib.load()
+    assert lib.lss_bn_groups(N, C, H * W, 0) > 1
+    old = Nm.USE_BN_CLUSTER
+    try:
+        Nm.USE_BN_CLUSTER = False
+        want = _bn_run(x, res, act, dy, 1)
+        Nm.USE_BN_CLUSTER = True
+        sync = Nm._sync(DEV)
+        sync[-1] = spin
+        got = _bn_run(x, res, act, dy, 1)
+        torch.cuda.synchronize()
+    finally:
+        Nm.USE_BN_CLUSTER = old
+        Nm._sync(DEV)[-1] = 0
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
+    assert int(Nm._sync(DEV)[:-1].abs().sum()) == 0, "cluster counters not re-zeroed"
