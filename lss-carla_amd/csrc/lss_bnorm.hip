@@ -598,7 +598,9 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_fused_reg_nchw(const bf16* __
 constexpr unsigned kBnSpinLimit = 1u << 20;
 constexpr int kBnClusterMaxG = 64;  // (the timeout path's LDS pairs)
 constexpr int kBnClusterIT = 8;     // 16-B vectors per thread held in registers
-constexpr int kBnSyncMaxC = 4096;   // channels a sync workspace covers (two counters each, + the spin word)
+constexpr int kBnSyncMaxC = 4096;   // channels a sync workspace covers (+ the spin word)
+constexpr int kBnSyncStride = 32;   // words per channel: its two counters alone in a 128-B line (a line
+                                    // shared by the counters of many channels serialised every poll)
 
 __device__ __forceinline__ void st_pair_agent(float* p, float a, float b) {
     const unsigned long long v = ((unsigned long long)__float_as_uint(b) << 32) | __float_as_uint(a);
@@ -614,18 +616,18 @@ __device__ __forceinline__ float2 ld_pair_agent(const float* p) {
 // limit_word (the workspace's last word): 0 = kBnSpinLimit polls, s > 0 = s - 1 (tests of the timeout path)
 __device__ __forceinline__ bool cluster_publish_wait(float* __restrict__ partial, size_t at, float a, float b,
                                                      unsigned* arrive, int G, const unsigned* limit_word) {
+    // the R2 hand-off (cdna_hip_programming.md, Guideline 16): the pair written through (sc1) and
+    // retired (vmcnt counts stores) before the arrival; readers poll and read with sc1 loads. No fence:
+    // an agent-scope fence writes back / invalidates the whole L2 of the XCD, per block
     st_pair_agent(partial + at, a, b);
-    __threadfence();  // the pair before the arrival
-    atomicAdd(arrive, 1u);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned lo = *limit_word;
     const unsigned limit = lo ? lo - 1u : kBnSpinLimit;
     for (unsigned spins = 0;; ++spins) {
-        if (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)G) {
-            __threadfence();
-            return true;
-        }
+        if (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)G) return true;
         if (spins >= limit) return false;
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(8);
     }
 }
 __device__ __forceinline__ void cluster_leave(unsigned* arrive, unsigned* leave, int G) {
@@ -653,7 +655,7 @@ __device__ __forceinline__ void fold_cluster(const float* __restrict__ partial, 
     }
 }
 
-template <int V>
+template <int V, int IT>
 __global__ __launch_bounds__(kBlock) void k_bn_cluster_nchw(const bf16* __restrict__ x, const bf16* __restrict__ res,
                                                             BnGeo g, int G, float* __restrict__ partial, BnParams P,
                                                             int act, unsigned* __restrict__ sync,
@@ -666,14 +668,14 @@ __global__ __launch_bounds__(kBlock) void k_bn_cluster_nchw(const bf16* __restri
     const int n0 = (int)((long)g.N * q / G), n1 = (int)((long)g.N * (q + 1) / G);
     const int per = g.HW / V, count = per * (n1 - n0);
     const bf16* xc = x + ((size_t)n0 * g.C + c) * g.HW;  // (chan_vec over the group's images)
-    PackedBf16<V> raw[kBnClusterIT];
+    PackedBf16<V> raw[IT];
 #pragma unroll
-    for (int it = 0; it < kBnClusterIT; ++it)
+    for (int it = 0; it < IT; ++it)
         raw[it].load(xc + chan_vec(g, 0, per, count, (int)threadIdx.x + it * kBlock, V) + (size_t)0);
     const float k = first_nchw(x, c, g);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int it = 0; it < kBnClusterIT; ++it) {
+    for (int it = 0; it < IT; ++it) {
         if ((int)threadIdx.x + it * kBlock < count) {
             float v[V];
             raw[it].get(v);
@@ -686,9 +688,10 @@ __global__ __launch_bounds__(kBlock) void k_bn_cluster_nchw(const bf16* __restri
         }
     }
     block_pair_sum(s1, s2, s_red);
-    unsigned* arrive = sync + 2 * c;
+    unsigned* arrive = sync + (size_t)c * kBnSyncStride;
     if (threadIdx.x == 0)
-        s_ok = cluster_publish_wait(partial, ((size_t)c * G + q) * 2, s1, s2, arrive, G, sync + 2 * kBnSyncMaxC);
+        s_ok = cluster_publish_wait(partial, ((size_t)c * G + q) * 2, s1, s2, arrive, G,
+                                    sync + (size_t)kBnSyncMaxC * kBnSyncStride);
     __syncthreads();
     const bool ok = s_ok;
     if (!ok) {  // (never expected) every group's pair from memory, in k_bn_stats_nchw's order
@@ -726,7 +729,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_cluster_nchw(const bf16* __restri
     __syncthreads();
     const float sc = s_coef[0], sh = s_coef[1];
 #pragma unroll
-    for (int it = 0; it < kBnClusterIT; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int e = (int)threadIdx.x + it * kBlock;
         if (e < count) {
             const size_t i = ((size_t)n0 * g.C + c) * g.HW + chan_vec(g, 0, per, count, e, V);
@@ -744,7 +747,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_cluster_nchw(const bf16* __restri
     }
 }
 
-template <int V, bool RELU>
+template <int V, int IT, bool RELU>
 __global__ __launch_bounds__(kBlock) void k_bn_bwd_cluster_nchw(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                                 const bf16* __restrict__ y, BnGeo g, int G,
                                                                 const float* __restrict__ stats, float* __restrict__ partial,
@@ -759,9 +762,9 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_cluster_nchw(const bf16* __re
     const int n0 = (int)((long)g.N * q / G), n1 = (int)((long)g.N * (q + 1) / G);
     const int per = g.HW / V, count = per * (n1 - n0);
     const size_t base = ((size_t)n0 * g.C + c) * g.HW;
-    PackedBf16<V> rd[kBnClusterIT], rx[kBnClusterIT], ry[RELU ? kBnClusterIT : 1];
+    PackedBf16<V> rd[IT], rx[IT], ry[RELU ? IT : 1];
 #pragma unroll
-    for (int it = 0; it < kBnClusterIT; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const size_t i = base + chan_vec(g, 0, per, count, (int)threadIdx.x + it * kBlock, V);
         rd[it].load(dy + i);
         rx[it].load(x + i);
@@ -770,7 +773,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_cluster_nchw(const bf16* __re
     const float mean = stats[c], rstd = stats[g.C + c], sc = stats[2 * g.C + c], sh = stats[3 * g.C + c];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
-    for (int it = 0; it < kBnClusterIT; ++it) {
+    for (int it = 0; it < IT; ++it) {
         if ((int)threadIdx.x + it * kBlock < count) {
             float d[V], xv[V], yv[V];
             rd[it].get(d);
@@ -785,9 +788,10 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_cluster_nchw(const bf16* __re
         }
     }
     block_pair_sum(sg, sgx, s_red);
-    unsigned* arrive = sync + 2 * c;
+    unsigned* arrive = sync + (size_t)c * kBnSyncStride;
     if (threadIdx.x == 0)
-        s_ok = cluster_publish_wait(partial, ((size_t)c * G + q) * 2, sg, sgx, arrive, G, sync + 2 * kBnSyncMaxC);
+        s_ok = cluster_publish_wait(partial, ((size_t)c * G + q) * 2, sg, sgx, arrive, G,
+                                    sync + (size_t)kBnSyncMaxC * kBnSyncStride);
     __syncthreads();
     const bool ok = s_ok;
     if (!ok) {
@@ -830,7 +834,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_cluster_nchw(const bf16* __re
     __syncthreads();
     const float mg = s_coef[0], mgx = s_coef[1];
 #pragma unroll
-    for (int it = 0; it < kBnClusterIT; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int e = (int)threadIdx.x + it * kBlock;
         if (e < count) {
             const size_t i = base + chan_vec(g, 0, per, count, e, V);
@@ -1246,10 +1250,25 @@ inline int vec_nchw(int HW) { return HW % 8 == 0 ? 8 : (HW % 4 == 0 ? 4 : 1); }
 #define LSS_BN_CLUSTER 1  // NCHW, G > 1: the cluster kernels when a sync workspace is given (lss_bn_*2)
 #endif
 
-// NCHW bf16 with several groups per channel, each group's vectors held in registers
-template <typename T> inline bool cluster_ok(const uint32_t* sync, int G, int V, const BnGeo& g) {
+// vectors per thread the largest group of a channel needs
+inline int cluster_it(int G, int V, const BnGeo& g) {
+    const long imgs = (g.N + G - 1) / G;
+    return (int)((imgs * (g.HW / V) + kBlock - 1) / kBlock);
+}
+
+// NCHW bf16 with several groups per channel, each group's vectors held in registers. Where it pays
+// (c3 trunk, per-layer A/B of the step's graph replays against stats + apply, profiles/r06/
+// bn_cluster_ab.txt): a block that has published waits for the whole channel, so a grid that does not
+// fit the resident slots in one round (4 blocks per CU at the cluster kernels' 100-128 VGPRs) loses
+// the overlap two launches give -- forward: 1,536 blocks 31-33 us vs 24-26, 4,608 blocks 86 vs 57;
+// at <= 960 blocks 8.5-15.4 vs 11.1-16.9 us. The backward (two tensors read, three written or read
+// again) also wins at 1,536-2,304 blocks of 3-12 images per group (30.6-40.6 vs 32.5-44.7 us), not at
+// one image per group (G = 48 at 64 x 176: 43.9 vs 39.0; forward 768 blocks: 15.5 vs 14.2).
+template <typename T> inline bool cluster_ok(const uint32_t* sync, int G, int V, const BnGeo& g, bool bwd) {
     if (!LSS_BN_CLUSTER || sync == nullptr || !std::is_same<T, bf16>::value || V != 8) return false;
     if (G < 2 || G > kBnClusterMaxG || g.C > kBnSyncMaxC) return false;
+    const long blocks = (long)g.C * G;
+    if (g.N / G < 2 || blocks > (bwd ? 2304 : 1024)) return false;
     const long imgs = (g.N + G - 1) / G;  // images of the largest group
     return imgs * (g.HW / V) <= (long)kBnClusterIT * kBlock;
 }
@@ -1274,7 +1293,7 @@ int lss_bn_groups(int32_t N, int32_t C, int32_t HW, int32_t layout) {
     return (int)(g < 1 ? 1 : (g > N ? N : g));
 }
 
-int lss_bn_sync_words(void) { return 2 * kBnSyncMaxC + 1; }
+int lss_bn_sync_words(void) { return kBnSyncMaxC * kBnSyncStride + 1; }
 
 int lss_bn_fwd(const void* x, const void* residual, int32_t dtype, int32_t layout, int32_t N, int32_t C, int32_t HW,
                const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
@@ -1320,9 +1339,13 @@ int lss_bn_fwd2(const void* x, const void* residual, int32_t dtype, int32_t layo
             const int V = vec_nchw(HW);                                                                            \
             const dim3 gr(C * G), bl(kBlock);                                                                      \
             const long cnt = (long)N * (HW / V);                                                                   \
-            if (cluster_ok<T>(sync, G, V, g)) {                                                                    \
-                hipLaunchKernelGGL((k_bn_cluster_nchw<8>), gr, bl, 0, s, (const bf16*)xx, (const bf16*)rr, g, G,   \
-                                   partial, P, (int)act, (unsigned*)sync, (bf16*)yy);                              \
+            if (cluster_ok<T>(sync, G, V, g, false)) {                                                             \
+                if (cluster_it(G, V, g) <= 6)                                                                      \
+                    hipLaunchKernelGGL((k_bn_cluster_nchw<8, 6>), gr, bl, 0, s, (const bf16*)xx, (const bf16*)rr,  \
+                                       g, G, partial, P, (int)act, (unsigned*)sync, (bf16*)yy);                    \
+                else                                                                                               \
+                    hipLaunchKernelGGL((k_bn_cluster_nchw<8, 8>), gr, bl, 0, s, (const bf16*)xx, (const bf16*)rr,  \
+                                       g, G, partial, P, (int)act, (unsigned*)sync, (bf16*)yy);                    \
             } else if (G == 1 && LSS_BN_FUSED && fused_reg<T>(V, cnt)) {                                           \
                 if (V == 8 && cnt <= 4 * kBlock)                                                                   \
                     hipLaunchKernelGGL((k_bn_fused_reg_nchw<8, 4>), gr, bl, 0, s, (const bf16*)xx,                \
@@ -1405,14 +1428,23 @@ int lss_bn_bwd2(const void* dy, const void* x, const void* y, int32_t dtype, int
             const int V = vec_nchw(HW);                                                                            \
             const dim3 gr(C * G), bl(kBlock);                                                                      \
             const long cnt = (long)N * (HW / V);                                                                   \
-            if (cluster_ok<T>(sync, G, V, g)) {                                                                    \
+            if (cluster_ok<T>(sync, G, V, g, true)) {                                                              \
                 const bf16 *db = (const bf16*)d, *xb = (const bf16*)xx, *yb = (const bf16*)yy;                     \
-                if (act == LSS_ACT_RELU)                                                                           \
-                    hipLaunchKernelGGL((k_bn_bwd_cluster_nchw<8, true>), gr, bl, 0, s, db, xb, yb, g, G, stats,    \
+                const bool it6 = cluster_it(G, V, g) <= 6;                                                         \
+                if (act == LSS_ACT_RELU && it6)                                                                    \
+                    hipLaunchKernelGGL((k_bn_bwd_cluster_nchw<8, 6, true>), gr, bl, 0, s, db, xb, yb, g, G, stats, \
                                        partial, (int)act, (unsigned*)sync, dgamma, dbeta, (bf16*)o, (bf16*)orr);   \
+                else if (act == LSS_ACT_RELU)                                                                      \
+                    hipLaunchKernelGGL((k_bn_bwd_cluster_nchw<8, 8, true>), gr, bl, 0, s, db, xb, yb, g, G, stats, \
+                                       partial, (int)act, (unsigned*)sync, dgamma, dbeta, (bf16*)o, (bf16*)orr);   \
+                else if (it6)                                                                                      \
+                    hipLaunchKernelGGL((k_bn_bwd_cluster_nchw<8, 6, false>), gr, bl, 0, s, db, xb, yb, g, G,       \
+                                       stats, partial, (int)act, (unsigned*)sync, dgamma, dbeta, (bf16*)o,         \
+                                       (bf16*)orr);                                                                \
                 else                                                                                               \
-                    hipLaunchKernelGGL((k_bn_bwd_cluster_nchw<8, false>), gr, bl, 0, s, db, xb, yb, g, G, stats,   \
-                                       partial, (int)act, (unsigned*)sync, dgamma, dbeta, (bf16*)o, (bf16*)orr);   \
+                    hipLaunchKernelGGL((k_bn_bwd_cluster_nchw<8, 8, false>), gr, bl, 0, s, db, xb, yb, g, G,       \
+                                       stats, partial, (int)act, (unsigned*)sync, dgamma, dbeta, (bf16*)o,         \
+                                       (bf16*)orr);                                                                \
             } else if (G == 1 && LSS_BN_FUSED && fused_reg<T>(V, cnt)) {                                           \
                 const bf16 *db = (const bf16*)d, *xb = (const bf16*)xx, *yb = (const bf16*)yy;                     \
                 if (V == 8 && cnt <= 4 * kBlock)                                                                   \
