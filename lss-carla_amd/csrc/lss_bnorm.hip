@@ -433,6 +433,8 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_fused_nchw(const T* __restric
     });
 }
 
+// (IT = 5 for the trunk's 8 x 22 maps at B*N = 48: 1,056 vectors, one over IT = 4's reach; with IT = 8
+// the backward's 130 VGPRs held 3 blocks per CU, 1.5 rounds for 1,152 channels)
 // bf16, one group per channel, at most IT vectors of V elements per thread: the same two launches'
 // work with every load of the channel issued up front and the channel held in registers (packed
 // bf16) between the statistics and the apply -- one read of x (and dy) instead of two, and no
@@ -1350,6 +1352,9 @@ int lss_bn_fwd2(const void* x, const void* residual, int32_t dtype, int32_t layo
                 if (V == 8 && cnt <= 4 * kBlock)                                                                   \
                     hipLaunchKernelGGL((k_bn_fused_reg_nchw<8, 4>), gr, bl, 0, s, (const bf16*)xx,                \
                                        (const bf16*)rr, g, P, (int)act, (bf16*)yy);                                \
+                else if (V == 8 && cnt <= 5 * kBlock)                                                              \
+                    hipLaunchKernelGGL((k_bn_fused_reg_nchw<8, 5>), gr, bl, 0, s, (const bf16*)xx,                \
+                                       (const bf16*)rr, g, P, (int)act, (bf16*)yy);                                \
                 else if (V == 8)                                                                                   \
                     hipLaunchKernelGGL((k_bn_fused_reg_nchw<8, 8>), gr, bl, 0, s, (const bf16*)xx,                \
                                        (const bf16*)rr, g, P, (int)act, (bf16*)yy);                                \
@@ -1449,6 +1454,9 @@ int lss_bn_bwd2(const void* dy, const void* x, const void* y, int32_t dtype, int
                 const bf16 *db = (const bf16*)d, *xb = (const bf16*)xx, *yb = (const bf16*)yy;                     \
                 if (V == 8 && cnt <= 4 * kBlock)                                                                   \
                     hipLaunchKernelGGL((k_bn_bwd_fused_reg_nchw<8, 4>), gr, bl, 0, s, db, xb, yb, g, stats,       \
+                                       (int)act, dgamma, dbeta, (bf16*)o, (bf16*)orr);                             \
+                else if (V == 8 && cnt <= 5 * kBlock)                                                              \
+                    hipLaunchKernelGGL((k_bn_bwd_fused_reg_nchw<8, 5>), gr, bl, 0, s, db, xb, yb, g, stats,       \
                                        (int)act, dgamma, dbeta, (bf16*)o, (bf16*)orr);                             \
                 else if (V == 8)                                                                                   \
                     hipLaunchKernelGGL((k_bn_bwd_fused_reg_nchw<8, 8>), gr, bl, 0, s, db, xb, yb, g, stats,       \
