@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <algorithm>
+#include <type_traits>
 #include <limits.h>
 #include <stdint.h>
 
@@ -549,6 +550,291 @@ int dw_wgt_lds(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, fl
     return launch_status();
 }
 
+// ---- narrow planes (the trunk's 8 x 22 and 4 x 11 maps: Wo in {22, 11}), whole planes per block. The
+// register-tiled kernels above issue ~100 two-byte loads per thread on these (lanes 8 B apart; 0.6-1.4
+// TB/s, profiles/r06/step_roofline.json), and their rows of 22 / 11 elements are not 16-B aligned,
+// which kept them off the LDS kernels' vector staging. But a block's consecutive planes are ONE
+// contiguous run of memory: staged here with flat 16-B loads into zero-padded fp32 LDS planes; a
+// thread computes one output row (WO outputs; every staged value it reads feeds all the taps that
+// reach it); the outputs go back through LDS as one contiguous run of 16-B stores.
+template <typename T>
+__device__ __forceinline__ void ldv16(const T* p, float* o);  // 16 B -> 16 / sizeof(T) floats
+template <> __device__ __forceinline__ void ldv16<bf16>(const bf16* p, float* o) { unpack8(*reinterpret_cast<const uint4*>(p), o); }
+template <> __device__ __forceinline__ void ldv16<float>(const float* p, float* o) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+}
+
+// f(i, v) for the n elements of the run at src: 16-B loads when the run allows them (src 16-B aligned,
+// n a multiple of the vector), else one element per load
+template <typename T, typename F>
+__device__ __forceinline__ void for_run(const T* __restrict__ src, int n, F&& f) {
+    constexpr int V = 16 / sizeof(T);
+    if ((reinterpret_cast<uintptr_t>(src) & 15) == 0 && n % V == 0) {
+        for (int i = threadIdx.x; i < n / V; i += kBlock) {
+            float v[V];
+            ldv16<T>(src + (size_t)i * V, v);
+#pragma unroll
+            for (int j = 0; j < V; ++j) f(i * V + j, v[j]);
+        }
+    } else {
+        for (int i = threadIdx.x; i < n; i += kBlock) f(i, ld(src + i));
+    }
+}
+
+// VW consecutive elements -> fp32, in loads of up to 16 B (the caller guarantees the alignment)
+template <int VW, typename T>
+__device__ __forceinline__ void ld_vec(const T* __restrict__ p, float* o) {
+    constexpr int B = VW * (int)sizeof(T);
+    if constexpr (B >= 16) {
+        constexpr int E = 16 / (int)sizeof(T);
+#pragma unroll
+        for (int k = 0; k < VW; k += E) ldv16<T>(p + k, o + k);
+    } else if constexpr (B == 8 && sizeof(T) == 2) {
+        const uint2 u = *reinterpret_cast<const uint2*>(p);
+        o[0] = __uint_as_float(u.x << 16); o[1] = __uint_as_float(u.x & 0xFFFF0000u);
+        o[2] = __uint_as_float(u.y << 16); o[3] = __uint_as_float(u.y & 0xFFFF0000u);
+    } else if constexpr (B == 8) {
+        const float2 a = *reinterpret_cast<const float2*>(p);
+        o[0] = a.x; o[1] = a.y;
+    } else if constexpr (B == 4 && sizeof(T) == 2) {
+        const unsigned u = *reinterpret_cast<const unsigned*>(p);
+        o[0] = __uint_as_float(u << 16); o[1] = __uint_as_float(u & 0xFFFF0000u);
+    } else {
+#pragma unroll
+        for (int k = 0; k < VW; ++k) o[k] = ld(p + k);
+    }
+}
+
+// f(pl, e, v) for element e of plane pl, over np planes of n elements each at x + (first + pl * step) * n:
+// one flat loop over every plane's VW-element vectors, so all their loads are in flight together
+template <int VW, typename T, typename F>
+__device__ __forceinline__ void for_planes_v(const T* __restrict__ x, size_t first, size_t step, int np, int n, F&& f) {
+    const int nv = n / VW;
+    for (int i = threadIdx.x; i < np * nv; i += kBlock) {
+        const int pl = i / nv, v = i - pl * nv;
+        float vals[VW];
+        ld_vec<VW, T>(x + (first + (size_t)pl * step) * n + (size_t)v * VW, vals);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) f(pl, v * VW + j, vals[j]);
+    }
+}
+template <typename T, typename F>
+__device__ __forceinline__ void for_planes(const T* __restrict__ x, size_t first, size_t step, int np, int n, F&& f) {
+    // (plane bases are n elements apart: n % VW == 0 keeps every vector aligned on an aligned tensor)
+    if (n % 8 == 0) for_planes_v<8, T>(x, first, step, np, n, f);
+    else if (n % 4 == 0) for_planes_v<4, T>(x, first, step, np, n, f);
+    else if (n % 2 == 0) for_planes_v<2, T>(x, first, step, np, n, f);
+    else for_planes_v<1, T>(x, first, step, np, n, f);
+}
+
+// the run [0, n) of s (T in LDS) to dst: 16-B stores when aligned
+template <typename T>
+__device__ __forceinline__ void store_run(T* __restrict__ dst, const T* __restrict__ s, int n) {
+    constexpr int V = 16 / sizeof(T);
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0 && n % V == 0) {
+        for (int i = threadIdx.x; i < n / V; i += kBlock)
+            *reinterpret_cast<uint4*>(dst + (size_t)i * V) = *reinterpret_cast<const uint4*>(s + (size_t)i * V);
+    } else {
+        for (int i = threadIdx.x; i < n; i += kBlock) dst[i] = s[i];
+    }
+}
+
+__device__ __forceinline__ void to_t(float* p, float v) { *p = v; }
+__device__ __forceinline__ void to_t(bf16* p, float v) { *p = __float2bfloat16(v); }
+
+// one input plane element (r, c) into its padded LDS slot (never read if it lies past the reach)
+__device__ __forceinline__ void put_padded(float* __restrict__ plane, int r, int c, int pt, int pl, int LH, int LW,
+                                          float v) {
+    const int rr = r + pt, cc = c + pl;
+    if (rr < LH && cc < LW) plane[rr * LW + cc] = v;
+}
+
+template <int K, int S, int WO>
+struct PlaneGeo {
+    static constexpr int LW = (WO - 1) * S + K;
+    __host__ __device__ static int LH(int Ho) { return (Ho - 1) * S + K; }
+};
+
+// forward (and stride-1 backward-data with flip): block = PB consecutive planes
+template <int K, int S, int WO, typename T>
+__global__ __launch_bounds__(kBlock) void k_dw_fwd_planes(const T* __restrict__ x, const float* __restrict__ w,
+                                                          DwGeo g, int flip, int PB, T* __restrict__ y) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    using PG = PlaneGeo<K, S, WO>;
+    constexpr int LW = PG::LW;
+    const int LH = PG::LH(g.Ho), plane_f = LH * LW;
+    const int p0 = blockIdx.x * PB, np = min(PB, g.nplanes - p0);
+    const int HiWi = g.Hi * g.Wi, HoWo = g.Ho * WO;
+    float* s_w = smem;                                   // [PB][K*K]
+    float* s_x = s_w + ((PB * K * K + 3) & ~3);          // [PB][LH][LW]
+    T* s_y = reinterpret_cast<T*>(s_x + ((PB * plane_f + 3) & ~3));  // [PB][Ho][WO], 16-B aligned
+    for (int i = threadIdx.x; i < np * plane_f; i += kBlock) s_x[i] = 0.f;
+    for (int i = threadIdx.x; i < np * K * K; i += kBlock) {
+        const int pl = i / (K * K), t = i - pl * (K * K);
+        s_w[i] = w[(size_t)((p0 + pl) % g.C) * K * K + (flip ? K * K - 1 - t : t)];
+    }
+    __syncthreads();
+    for_run(x + (size_t)p0 * HiWi, np * HiWi, [&](int f, float v) {
+        const int pl = f / HiWi, rem = f - pl * HiWi;
+        const int r = rem / g.Wi;
+        put_padded(s_x + pl * plane_f, r, rem - r * g.Wi, g.pt, g.pl, LH, LW, v);
+    });
+    __syncthreads();
+    for (int it = threadIdx.x; it < np * g.Ho; it += kBlock) {
+        const int pl = it / g.Ho, oh = it - pl * g.Ho;
+        const float* xs = s_x + pl * plane_f + oh * S * LW;
+        const float* wk = s_w + pl * K * K;
+        float acc[WO];
+#pragma unroll
+        for (int j = 0; j < WO; ++j) acc[j] = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh) {
+            float v[LW];
+#pragma unroll
+            for (int q = 0; q < LW; ++q) v[q] = xs[kh * LW + q];
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) {
+                const float wv = wk[kh * K + kw];
+#pragma unroll
+                for (int j = 0; j < WO; ++j) acc[j] = fmaf(v[j * S + kw], wv, acc[j]);
+            }
+        }
+        T* o = s_y + pl * HoWo + oh * WO;
+#pragma unroll
+        for (int j = 0; j < WO; ++j) to_t(o + j, acc[j]);
+    }
+    __syncthreads();
+    store_run(y + (size_t)p0 * HoWo, s_y, np * HoWo);
+}
+
+// weight-gradient partials: block (channel c, image group q); PB images' planes of x and dy staged at
+// a time; a thread takes output rows; fixed reduction order (the thread's rows in order, then wave
+// shuffles, then waves in order)
+template <int K, int S, int WO, typename T>
+__global__ __launch_bounds__(kBlock) void k_dw_wgt_planes(const T* __restrict__ x, const T* __restrict__ dy, DwGeo g,
+                                                          int nimg, int ngroups, int PB, float* __restrict__ partial) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    __shared__ float s_red[kBlock / kWave][K * K];
+    using PG = PlaneGeo<K, S, WO>;
+    constexpr int LW = PG::LW;
+    const int LH = PG::LH(g.Ho), plane_f = LH * LW;
+    const int c = blockIdx.x % g.C, q = blockIdx.x / g.C;
+    const int n0 = (int)((long)nimg * q / ngroups), n1 = (int)((long)nimg * (q + 1) / ngroups);
+    const int HiWi = g.Hi * g.Wi, HoWo = g.Ho * WO;
+    float* s_x = smem;                                   // [PB][LH][LW]
+    float* s_d = s_x + PB * plane_f;                     // [PB][Ho][WO]
+    float acc[K * K];
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
+    for (int nb = n0; nb < n1; nb += PB) {
+        const int np = min(PB, n1 - nb);
+        __syncthreads();  // the previous chunk's readers are done
+        for (int i = threadIdx.x; i < np * plane_f; i += kBlock) s_x[i] = 0.f;
+        __syncthreads();
+        const size_t first = (size_t)nb * g.C + c;  // plane (image nb, channel c); images g.C planes apart
+        for_planes(x, first, (size_t)g.C, np, HiWi, [&](int pl, int f, float v) {
+            const int r = f / g.Wi;
+            put_padded(s_x + pl * plane_f, r, f - r * g.Wi, g.pt, g.pl, LH, LW, v);
+        });
+        for_planes(dy, first, (size_t)g.C, np, HoWo, [&](int pl, int f, float v) { s_d[pl * HoWo + f] = v; });
+        __syncthreads();
+        for (int it = threadIdx.x; it < np * g.Ho; it += kBlock) {
+            const int pl = it / g.Ho, oh = it - pl * g.Ho;
+            const float* xs = s_x + pl * plane_f + oh * S * LW;
+            const float* ds = s_d + pl * HoWo + oh * WO;
+            float d[WO];
+#pragma unroll
+            for (int j = 0; j < WO; ++j) d[j] = ds[j];
+#pragma unroll
+            for (int kh = 0; kh < K; ++kh) {
+                float v[LW];
+#pragma unroll
+                for (int qq = 0; qq < LW; ++qq) v[qq] = xs[kh * LW + qq];
+#pragma unroll
+                for (int kw = 0; kw < K; ++kw) {
+                    float a = acc[kh * K + kw];
+#pragma unroll
+                    for (int j = 0; j < WO; ++j) a = fmaf(d[j], v[j * S + kw], a);
+                    acc[kh * K + kw] = a;
+                }
+            }
+        }
+    }
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) {
+        float v = acc[i];
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+        if (lane == 0) s_red[wave][i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < K * K) {
+        float t = 0.f;
+#pragma unroll
+        for (int jw = 0; jw < kBlock / kWave; ++jw) t += s_red[jw][threadIdx.x];
+        partial[((size_t)c * ngroups + q) * K * K + threadIdx.x] = t;
+    }
+}
+
+#ifndef LSS_DW_PLANES
+#define LSS_DW_PLANES 1  // experiment switch: 0 = the register-tiled kernels on the narrow planes
+#endif
+constexpr int kDwPlanesLdsMax = 48 * 1024;  // bytes of LDS a planes block may use
+
+// the planes kernels take Wo in {22, 11} (the trunk's narrow maps), a staged plane holding every input
+// element a tap reaches; PB = planes per block: one output row per thread, within the LDS budget
+template <int K, int S, int WO>
+inline int dw_planes_pb(const DwGeo& g, int extra_floats_per_plane, int elt) {
+    if (!LSS_DW_PLANES || g.Wo != WO) return 0;
+    using PG = PlaneGeo<K, S, WO>;
+    const int plane_bytes = 4 * (PG::LH(g.Ho) * PG::LW + extra_floats_per_plane) + elt * g.Ho * WO;
+    int pb = std::max(1, kBlock / g.Ho);
+    while (pb > 1 && pb * plane_bytes + 4 * pb * K * K + 64 > kDwPlanesLdsMax) --pb;
+    return pb * plane_bytes + 4 * pb * K * K + 64 <= kDwPlanesLdsMax ? pb : 0;
+}
+
+template <int K, int S, typename T>
+int dw_fwd_planes(const void* x, const float* w, DwGeo g, int flip, void* y, hipStream_t s) {
+    // (stride 2: slower than the register-tiled kernel, 21.9 / 21.0 vs 15.3 / 19.1 us in the c3 step)
+    if (S != 1) return 1;
+    auto go = [&](auto wo_tag) -> int {
+        constexpr int WO = decltype(wo_tag)::value;
+        const int pb = dw_planes_pb<K, S, WO>(g, 0, (int)sizeof(T));
+        if (pb == 0) return 1;
+        using PG = PlaneGeo<K, S, WO>;
+        const size_t lds = 4 * ((((size_t)pb * K * K + 3) & ~(size_t)3) +
+                                (((size_t)pb * PG::LH(g.Ho) * PG::LW + 3) & ~(size_t)3)) +
+                           sizeof(T) * (size_t)pb * g.Ho * WO;
+        const long blocks = ((long)g.nplanes + pb - 1) / pb;
+        if (blocks > INT_MAX) return 1;
+        hipLaunchKernelGGL((k_dw_fwd_planes<K, S, WO, T>), dim3((unsigned)blocks), dim3(kBlock), lds, s, (const T*)x,
+                           w, g, flip, pb, (T*)y);
+        return 0;
+    };
+    if (g.Wo == 22) return go(std::integral_constant<int, 22>{});
+    if (g.Wo == 11) return go(std::integral_constant<int, 11>{});
+    return 1;
+}
+
+template <int K, int S, typename T>
+int dw_wgt_planes(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, hipStream_t s) {
+    auto go = [&](auto wo_tag) -> int {
+        constexpr int WO = decltype(wo_tag)::value;
+        const int pb = dw_planes_pb<K, S, WO>(g, g.Ho * WO, 0);
+        if (pb == 0) return 1;
+        using PG = PlaneGeo<K, S, WO>;
+        const size_t lds = 4 * (size_t)pb * (PG::LH(g.Ho) * PG::LW + g.Ho * WO);
+        hipLaunchKernelGGL((k_dw_wgt_planes<K, S, WO, T>), dim3(g.C * ngroups), dim3(kBlock), lds, s, (const T*)x,
+                           (const T*)dy, g, nimg, ngroups, pb, partial);
+        return 0;
+    };
+    if (g.Wo == 22) return go(std::integral_constant<int, 22>{});
+    if (g.Wo == 11) return go(std::integral_constant<int, 11>{});
+    return 1;
+}
+
 // dispatch over (K, S, T)
 template <template <int, int, typename> class F, typename... A>
 int dispatch_kst(int K, int S, int dtype, A... a) {
@@ -570,6 +856,7 @@ template <int K, int S, typename T>
 struct Fwd {
     static int run(const void* x, const float* w, DwGeo g, int flip, void* y, hipStream_t s) {
         if (LSS_DW_LDS && dw_lds_ok<K, S>(g, x, y)) return dw_fwd_lds<K, S, T>(x, w, g, flip, y, s);
+        if (dw_fwd_planes<K, S, T>(x, w, g, flip, y, s) == 0) return launch_status();
         constexpr int TH = Tile<S>::TH, TW = Tile<S>::TW;
         const long n = (long)g.nplanes * ((g.Ho + TH - 1) / TH) * ((g.Wo + TW - 1) / TW);
         hipLaunchKernelGGL((k_dw_fwd<K, S, TH, TW, T>), dim3(blocks_for(n)), dim3(kBlock), 0, s, (const T*)x, w, g,
@@ -599,6 +886,7 @@ template <int K, int S, typename T>
 struct BwdWeight {
     static int run(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, hipStream_t s) {
         if (LSS_DW_LDS && dw_lds_ok<K, S>(g, x, dy)) return dw_wgt_lds<K, S, T>(x, dy, g, nimg, ngroups, partial, s);
+        if (dw_wgt_planes<K, S, T>(x, dy, g, nimg, ngroups, partial, s) == 0) return launch_status();
         hipLaunchKernelGGL((k_dw_bwd_weight<K, S, 4, S == 1 ? 4 : 2, T>), dim3(g.C * ngroups), dim3(kBlock), 0, s,
                            (const T*)x, (const T*)dy, g, nimg, ngroups, partial);
         return launch_status();
