@@ -1580,8 +1580,9 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
 //     point id per cell, the NCHW tile kernel's order, so both layouts agree bit for bit); each
 //     finished cell's row is stored straight to the BEV. No global load follows a store, so stores
 //     never sit in front of a load's wait.
-//   zero waves: kZeroUnits x 64 consecutive cells each; the rows of the empty cells are written as
-//     zeros with 16-B non-temporal stores, so every BEV element is written exactly once.
+//   zero waves: zu x 64 consecutive cells each (zu <= kMaxZeroUnits, chosen per launch); the rows of
+//     the empty cells are written as zeros with 16-B non-temporal stores, so every BEV element is
+//     written exactly once.
 // The CSR's sentinel tail (key -1 past the last entry, lss_csr_build) spares a load of the count.
 #ifndef LSS_SPLAT_ROLES
 #define LSS_SPLAT_ROLES 0  // experiments only: 1 runs the chunk waves alone, 2 the zero fill alone
@@ -1595,12 +1596,17 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
 #ifndef LSS_SPLAT_SKIP
 #define LSS_SPLAT_SKIP 0  // experiments only (wrong sums): 1 rows from 8 L1-resident rows, 2 one depth line, 4 no row stores
 #endif
-// 64-cell zero-fill units per wave: 1 (2-16 with their cell_start loads in flight together measured
-// slower, as did dispatching the zero fill first or interleaved with the chunks: rounds 3-4)
+// 64-cell zero-fill units per zero wave, zu in [1, kMaxZeroUnits], chosen per launch (splat_zero_units):
+// the fewest that let every chunk wave AND every zero wave be resident at once. At c3 the 5,386 chunk
+// waves leave 1,782 of the 7,168 wave slots, so 1 unit per wave (5,000 zero waves) ran the last 3,200
+// zero waves as a second generation behind the chunk waves; 3 units (1,667 waves) fit: in-step 12.21 ->
+// 11.63 us (2 units: 11.98, 4: 11.78; profiles/r06/splat_zu_ab.txt). When the chunk waves alone fill
+// the slots (c5) the zero fill is a second generation anyway and keeps 1 unit per wave. (Rounds 3-4
+// measured 2-16 units slower with 6 resident waves per SIMD, where no zu made the grid one generation.)
 #ifndef LSS_SPLAT_ZU
-#define LSS_SPLAT_ZU 1
+#define LSS_SPLAT_ZU 0  // experiments only: > 0 forces that many units per zero wave
 #endif
-constexpr int kZeroUnits = LSS_SPLAT_ZU;
+constexpr int kMaxZeroUnits = 4;
 constexpr int kSplatWaves = 4;  // waves per block of the channels-last splat (waves are independent;
                                 // 2 / 7 / 8 measured slower, round 4)
 constexpr int kSplatBlock = kSplatWaves * kWave;
@@ -1609,21 +1615,21 @@ constexpr int kSplatBlock = kSplatWaves * kWave;
 #endif
 constexpr int kSplatMinWaves = LSS_SPLAT_OCC;  // occupancy floor (waves per SIMD): 72 VGPRs, 16 KB LDS per block
 
-// Zero-fill units [u0, u0 + kZeroUnits): cells [64u, 64u + 64) each; empty cells' rows written as zeros.
+// Zero-fill units [u0, u0 + zu): cells [64u, 64u + 64) each; empty cells' rows written as zeros.
 template <typename OutT>
-__device__ void zero_empty_rows(int u0, const int32_t* __restrict__ cell_start, const BevGeo& g,
+__device__ void zero_empty_rows(int u0, int zu, const int32_t* __restrict__ cell_start, const BevGeo& g,
                                 OutT* __restrict__ out, int lane) {
-    unsigned long long emask[kZeroUnits];
+    unsigned long long emask[kMaxZeroUnits];
 #pragma unroll
-    for (int i = 0; i < kZeroUnits; ++i) {
+    for (int i = 0; i < kMaxZeroUnits; ++i) {  // every unit's cell starts in flight together
         const int k = (u0 + i) * kWave + lane;
         bool empty = false;
-        if (k < g.ncells) empty = cell_start[k] == cell_start[k + 1];
+        if (i < zu && k < g.ncells) empty = cell_start[k] == cell_start[k + 1];
         emask[i] = __ballot(empty);
     }
     constexpr int EPL = 16 / sizeof(OutT), LPR = kC / EPL, RPS = kWave / LPR;
 #pragma unroll
-    for (int i = 0; i < kZeroUnits; ++i) {
+    for (int i = 0; i < kMaxZeroUnits; ++i) {
         const int k0 = (u0 + i) * kWave;
         for (int r0 = 0; r0 < kWave; r0 += RPS) {
             const int r = r0 + lane / LPR;
@@ -1876,7 +1882,7 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
                                                            const long long* __restrict__ sorted_key,
                                                            const int32_t* __restrict__ sorted_row, BevGeo g,
                                                            int nprime, int nchunk_blocks, int nzero_blocks,
-                                                           OutT* __restrict__ out) {
+                                                           int zu, OutT* __restrict__ out) {
     __shared__ EntryMeta s_meta[kSplatWaves][2 * kWave];
     __shared__ __attribute__((aligned(16))) float s_part[kSplatWaves][RowSlice<RT>::NG * kC];
     const int lane = threadIdx.x & 63;
@@ -1909,10 +1915,10 @@ __global__ __launch_bounds__(kSplatBlock, kSplatMinWaves) void k_splat_fwd_nhwc(
         if (LSS_SPLAT_ROLES == 1) return;
         const int zb = x * nzg + zgi;
         if (zb >= nzero_blocks) return;
-        const int u = (zb * kSplatWaves + wave) * kZeroUnits;
+        const int u = (zb * kSplatWaves + wave) * zu;
         [[maybe_unused]] const int zslot = nchunk_blocks * kSplatWaves + zb * kSplatWaves + wave;
         LSS_STAMP(zslot, 0);
-        if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, cell_start, g, out, lane);
+        if (u * kWave < g.ncells) zero_empty_rows<OutT>(u, zu, cell_start, g, out, lane);
         LSS_STAMP(zslot, 3);
 #if LSS_TRACE
         if (lane == 0 && zslot < 16384) g_lss_trace[zslot][4] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
@@ -2564,6 +2570,17 @@ inline int device_cus() {
     return n;
 }
 
+// Zero-fill units per zero wave of k_splat_fwd_nhwc: the fewest (<= kMaxZeroUnits) with which the chunk
+// waves and the zero waves are all resident at once (kSplatMinWaves waves per SIMD, 4 SIMDs per CU);
+// 1 when no choice fits.
+inline int splat_zero_units(long chunk_waves, long units) {
+    if (LSS_SPLAT_ZU > 0) return std::min(LSS_SPLAT_ZU, kMaxZeroUnits);
+    const long slots = (long)device_cus() * 4 * kSplatMinWaves;
+    for (int zu = 1; zu <= kMaxZeroUnits; ++zu)
+        if (chunk_waves + grid_blocks(grid_blocks(units, zu), kSplatWaves) * (long)kSplatWaves <= slots) return zu;
+    return 1;
+}
+
 inline int choose_yt(int Y) {
     if (Y <= kYtMax) return Y;
     for (int t = kYtMax; t >= 16; t -= 4)
@@ -2992,18 +3009,19 @@ int lss_splat_fwd(const float* depth, const void* ctx_t, int32_t ctx_dtype, cons
         g.nrows = sg.nrows;
         const int nchunks = grid_blocks(nprime, kWave);
         const int nchunk_blocks = grid_blocks(nchunks, kSplatWaves);
-        const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), kZeroUnits), kSplatWaves);
+        const int zu = splat_zero_units(nchunk_blocks * kSplatWaves, grid_blocks(g.ncells, kWave));
+        const int nzero_blocks = grid_blocks(grid_blocks(grid_blocks(g.ncells, kWave), zu), kSplatWaves);
         const dim3 gr(8 * (grid_blocks(nchunk_blocks, 8) + grid_blocks(nzero_blocks, 8))), bl(kSplatBlock);
 // kernel-stamped events only when asked for: a plain launch is what a hipGraph capture records
 #define LSS_NHWC_FWD(F, RT, T)                                                                                     \
     do {                                                                                                           \
         if (e0 || e1)                                                                                              \
             hipExtLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, e0, e1, 0, depth, (const RT*)rows,   \
-                                  cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks,      \
+                                  cell_start, sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, zu,  \
                                   (T*)out);                                                                        \
         else                                                                                                       \
             hipLaunchKernelGGL((k_splat_fwd_nhwc<F, RT, T>), gr, bl, 0, s, depth, (const RT*)rows, cell_start,     \
-                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, (T*)out);           \
+                               sorted_key, sorted_row, g, nprime, nchunk_blocks, nzero_blocks, zu, (T*)out);       \
     } while (0)
         if (out_dtype == LSS_F32) {
             if (!fused) LSS_NHWC_FWD(false, float, float);
