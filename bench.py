@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--hip-pw", type=int, default=2,
                     help="trunk 1x1 convs: 2 = forward/backward-data on lss_pw_conv and weight gradients on lss_pw_wrw, "
                          "1 = lss_pw_wrw only, 0 = MIOpen")
+    ap.add_argument("--flip-bwd", type=int, default=1,
+                    help="stride-1 3x3 convs: backward-data as a forward conv of the flipped weight (models.USE_FLIP_BWD)")
     ap.add_argument("--plan-at", default="dropout", choices=("trunk", "dropout", "lift"),
                     help="plan kernels in front of the trunk, the dropout or the fused lift")
     ap.add_argument("--plan-ordered", type=int, default=1,
@@ -329,6 +331,7 @@ def measure_in_graph(args) -> dict | None:
            "--mode", args.mode]
     # the rest of this run's configuration, so the child measures the same step
     for flag in ("miopen_find", "hip_bn", "bn_relu_y", "hip_adam", "fuse_depthnet", "hip_dropout", "hip_pw", "plan_at",
+                 "flip_bwd",
                  "plan_ordered", "trunk_channels_last", "param_groups",
                  "flat_params", "overlap_all_reduce", "dw_impl"):
         cmd += ["--" + flag.replace("_", "-"), str(getattr(args, flag))]
@@ -486,6 +489,7 @@ def build_model(args, dev, gc, dac):
     lss_optim.USE_HIP_ADAM = bool(args.hip_adam)
     models.USE_HIP_DROPOUT = bool(args.hip_dropout)
     models.PLAN_AT = args.plan_at
+    models.USE_FLIP_BWD = bool(args.flip_bwd)
     from lss_carla_amd import efficientnet
     efficientnet.USE_HIP_PW_WRW = args.hip_pw >= 1
     efficientnet.USE_HIP_PW_GEMM = args.hip_pw >= 2

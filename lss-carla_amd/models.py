@@ -46,6 +46,53 @@ from .tools import gen_dx_bx
 UP1_CHANNELS_LAST = True
 
 
+# Stride-1 3x3 convolutions (BevEncode's layer1-3 / up1 / up2 convs, CamEncode.up1) with the backward-data
+# pass run as a FORWARD convolution of dy with the flipped, transposed weight (dx = conv2d(dy, W'),
+# W'[i, o, a, b] = W[o, i, 2 - a, 2 - b]: the transposed convolution of stride 1, padding 1). MIOpen's
+# find gives these shapes its CK forward kernels (0.29-0.33 of the bf16 MFMA peak at c3) where its
+# backward-data solvers (ASM implicit GEMM) run at 0.13-0.29; the weight gradient stays MIOpen's.
+USE_FLIP_BWD = True
+
+
+def _flip_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    return (USE_FLIP_BWD and x.is_cuda and x.dim() == 4 and conv.kernel_size == (3, 3) and conv.stride == (1, 1)
+            and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.padding_mode == "zeros" and torch.is_grad_enabled()
+            and (x.requires_grad or conv.weight.requires_grad))
+
+
+class _Conv3x3(torch.autograd.Function):
+    """conv2d(x, w, stride 1, padding 1); backward-data as conv2d(dy, flip(w^T)) (see USE_FLIP_BWD)."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return F.conv2d(x, w, None, 1, 1)
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        dx = dw = None
+        fmt = torch.channels_last if w.is_contiguous(memory_format=torch.channels_last) else torch.contiguous_format
+        if need[0]:
+            wt = w.transpose(0, 1).flip(2, 3).contiguous(memory_format=fmt)
+            dx = F.conv2d(dy, wt, None, 1, 1)
+        if need[1]:
+            dw = torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1]
+        return dx, dw
+
+
+def conv3x3(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """conv(x), through _Conv3x3 where eligible (same parameters, same forward)."""
+    if _flip_eligible(conv, x):
+        return _Conv3x3.apply(x, conv.weight)
+    return conv(x)
+
+
 class Up(nn.Module):
     """Upsample x1, concatenate with x2, two conv-BN-ReLU (src/models.py:15-34)."""
 
@@ -66,16 +113,16 @@ class Up(nn.Module):
         if resample.USE_HIP_UPSAMPLE and resample._eligible(x1) and resample._eligible(x2):
             # channels-last bf16 (BevEncode under autocast): upsample + cat in one kernel
             x = resample.upsample_cat(x1, x2, int(self.up.scale_factor))
-            x = bn_act(c[1], c[0](x), "relu")
-            return bn_act(c[4], c[3](x), "relu")
+            x = bn_act(c[1], conv3x3(c[0], x), "relu")
+            return bn_act(c[4], conv3x3(c[3], x), "relu")
         if x1.is_cuda and not x1.is_contiguous(memory_format=torch.channels_last):
             # PyTorch's NCHW bilinear kernel parallelises over output pixels only (a 8x22 map:
             # 176 threads, each looping over N*C); the channels-last kernel covers every element.
             x1 = self.up(x1.contiguous(memory_format=torch.channels_last)).contiguous()
         else:
             x1 = self.up(x1)
-        x = bn_act(c[1], c[0](torch.cat([x2, x1], dim=1)), "relu")
-        return bn_act(c[4], c[3](x), "relu")
+        x = bn_act(c[1], conv3x3(c[0], torch.cat([x2, x1], dim=1)), "relu")
+        return bn_act(c[4], conv3x3(c[3], x), "relu")
 
 
 _TRUNK_WEIGHTS_NOTED = set()
@@ -232,8 +279,8 @@ class BasicBlock(nn.Module):
             identity = x
         else:
             identity = bn_act(self.downsample[1], conv1x1(self.downsample[0], x))
-        out = bn_act(self.bn1, self.conv1(x), "relu")
-        return bn_act(self.bn2, self.conv2(out), "relu", residual=identity)
+        out = bn_act(self.bn1, conv3x3(self.conv1, x), "relu")
+        return bn_act(self.bn2, conv3x3(self.conv2, out), "relu", residual=identity)
 
 
 def _resnet_layer(inplanes, planes, blocks, stride):
@@ -365,7 +412,7 @@ class BevEncode(nn.Module):
             x = resample.upsample_cat(x, None, int(u[0].scale_factor))
         else:
             x = u[0](x)
-        return conv1x1(u[4], bn_act(u[2], u[1](x), "relu"))
+        return conv1x1(u[4], bn_act(u[2], conv3x3(u[1], x), "relu"))
 
 
 class LiftSplatShoot(nn.Module):
