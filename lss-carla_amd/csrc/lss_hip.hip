@@ -1607,8 +1607,11 @@ __device__ float reduce_big_cell(int start, int nprime, const long long* __restr
 #define LSS_SPLAT_ZU 0  // experiments only: > 0 forces that many units per zero wave
 #endif
 constexpr int kMaxZeroUnits = 4;
-constexpr int kSplatWaves = 4;  // waves per block of the channels-last splat (waves are independent;
-                                // 2 / 7 / 8 measured slower, round 4)
+#ifndef LSS_SPLAT_WAVES
+#define LSS_SPLAT_WAVES 4
+#endif
+constexpr int kSplatWaves = LSS_SPLAT_WAVES;  // waves per block of the channels-last splat (waves are
+                                              // independent; 2 / 7 / 8 measured slower, round 4)
 constexpr int kSplatBlock = kSplatWaves * kWave;
 #ifndef LSS_SPLAT_OCC
 #define LSS_SPLAT_OCC 7

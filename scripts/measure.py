@@ -128,7 +128,9 @@ def step_trace(out, spec):
                 subprocess.call([PY, os.path.join(REPO, "scripts", script), tr] + args, stdout=fh,
                                 stderr=subprocess.STDOUT)
         keep = os.path.join(out, f"{name}_kernel_trace.csv")
-        if os.path.getsize(tr) < 48 << 20:
+        # gpurun copies back at most 64 MiB of gpurun_out/: keep a trace only while the tag stays < 40 MiB
+        used = sum(os.path.getsize(os.path.join(out, f)) for f in os.listdir(out))
+        if used + os.path.getsize(tr) < 40 << 20:
             shutil.copy(tr, keep)
         print(tail(os.path.join(out, f"{name}_hot_steps.txt"), 12), flush=True)
     shutil.rmtree(d, ignore_errors=True)
