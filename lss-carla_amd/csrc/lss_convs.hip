@@ -283,11 +283,141 @@ inline bool geo_ok(int N, int C, int Hi, int Wi, int K, int S, int Ho, int Wo) {
 constexpr int kDwLdsFloats = 8192;  // staged input per block (32 KB)
 
 struct DwBand {
-    int BHo, PB, LW, LHmax, nbands;  // output rows per band, planes per block, LDS row width / rows
+    int BHo, PB, LW, LHmax, nbands;  // output rows per band, planes per block, LDS row stride / rows
 };
 
+// "v if c else 0" without a branch (the mask laundered through an empty asm, so the compiler cannot
+// sink the load that produced v into a conditional block: such blocks serialise loads that should all
+// be in flight together)
+__device__ __forceinline__ unsigned dw_keep_mask(bool c) {
+    unsigned m = c ? 0xFFFFFFFFu : 0u;
+    asm("" : "+v"(m));
+    return m;
+}
+__device__ __forceinline__ uint4 dw_keep(bool c, uint4 v) {
+    const unsigned m = dw_keep_mask(c);
+    return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+}
+
+// LDS column of input column iw: iw + kDwCol (so the 8-element chunks of a row land 8-B aligned:
+// vector LDS writes); the left padding columns sit just below kDwCol, zero-filled with the right ones.
+constexpr int kDwCol = 4;
+// staged 16-B input chunks per thread per round: every load of a round in flight together (the loop
+// that loaded, converted and wrote one chunk per iteration waited a memory round trip per iteration)
+constexpr int kDwStageU = 8;
+
+// Stage np planes (global plane stride gps elements) x LH rows from input row ih0 into LDS planes of
+// lps floats (row stride LW): LDS (pl, r, c) = x[plane pl][ih0 + r][c - kDwCol], zero outside x.
 template <typename T>
-__device__ __forceinline__ void dw_stage(const T* __restrict__ xp, int Hi, int Wi, int ih0, int LH, int LW, int pl,
+__device__ __forceinline__ void dw_stage(const T* __restrict__ xp, size_t gps, int np, int Hi, int Wi, int ih0, int LH,
+                                         int LW, int lps, float* __restrict__ dst) {
+    if (Wi % 8 == 0) {  // 8-element row chunks: 16-B (bf16) / 2 x 16-B (fp32) loads, all of a round in flight
+        const int cpr = Wi / 8, per = LH * cpr, n = np * per;
+        constexpr int U = sizeof(T) == 2 ? kDwStageU : kDwStageU / 2;
+        constexpr int NV = sizeof(T) == 2 ? 1 : 2;  // 16-B pieces per chunk
+        for (int i0 = threadIdx.x; i0 < n; i0 += U * kBlock) {
+            uint4 raw[U][NV];
+            const int nu = (n - (i0 - (int)threadIdx.x) + kBlock - 1) / kBlock;  // loads this round (block-uniform)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {  // clamped addresses, unconditional loads, masked values
+                if (u >= nu) break;
+                const int i = min(i0 + u * kBlock, n - 1);
+                const int pl = i / per, rem = i - pl * per, r = rem / cpr, ch = rem - r * cpr;
+                const int ih = ih0 + r;
+                const bool ok = ih >= 0 && ih < Hi;
+                const uint4* src = reinterpret_cast<const uint4*>(xp + pl * gps + (size_t)min(max(ih, 0), Hi - 1) * Wi + 8 * ch);
+#pragma unroll
+                for (int h = 0; h < NV; ++h) raw[u][h] = dw_keep(ok, src[h]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {  // every load issued before the first LDS write (no sinking)
+                if (u >= nu) break;
+#pragma unroll
+                for (int h = 0; h < NV; ++h) asm volatile("" : : "v"(raw[u][h].x), "v"(raw[u][h].y), "v"(raw[u][h].z), "v"(raw[u][h].w));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {  // (a clamped chunk rewrites chunk n - 1 with its own values)
+                if (u >= nu) break;
+                const int i = min(i0 + u * kBlock, n - 1);
+                const int pl = i / per, rem = i - pl * per, r = rem / cpr, ch = rem - r * cpr;
+                float2* d = reinterpret_cast<float2*>(dst + pl * lps + r * LW + kDwCol + 8 * ch);  // 8-B aligned
+                float v[8];
+                if constexpr (sizeof(T) == 2) {
+                    unpack8(raw[u][0], v);
+                } else {
+                    const float4 a = __builtin_bit_cast(float4, raw[u][0]), b = __builtin_bit_cast(float4, raw[u][1]);
+                    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) d[k] = make_float2(v[2 * k], v[2 * k + 1]);
+            }
+        }
+        const int npad = LW - Wi;  // columns [0, kDwCol) and [kDwCol + Wi, LW)
+        for (int i = threadIdx.x; i < np * LH * npad; i += kBlock) {
+            const int pr = i / npad, k = i - pr * npad;
+            const int pl = pr / LH, r = pr - pl * LH;
+            dst[pl * lps + r * LW + (k < kDwCol ? k : Wi + k)] = 0.f;
+        }
+    } else {
+        for (int i = threadIdx.x; i < np * LH * LW; i += kBlock) {
+            const int pr = i / LW, c = i - pr * LW;
+            const int pl = pr / LH, r = pr - pl * LH;
+            const int ih = ih0 + r, iw = c - kDwCol;
+            dst[pl * lps + r * LW + c] =
+                (ih >= 0 && ih < Hi && iw >= 0 && iw < Wi) ? ld(xp + pl * gps + (size_t)ih * Wi + iw) : 0.f;
+        }
+    }
+}
+
+template <int SEG, typename T>
+__device__ __forceinline__ void store_seg(T* __restrict__ p, const float* v, int n) {
+    if (n == SEG) {
+        if constexpr (sizeof(T) == 2 && SEG == 8) {
+            *reinterpret_cast<uint4*>(p) = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+            return;
+        } else if constexpr (sizeof(T) == 2 && SEG == 4) {
+            *reinterpret_cast<uint2*>(p) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+            return;
+        } else if constexpr (sizeof(T) == 2 && SEG == 2) {
+            *reinterpret_cast<unsigned*>(p) = pack2(v[0], v[1]);
+            return;
+        } else if constexpr (sizeof(T) == 4 && SEG % 4 == 0) {
+#pragma unroll
+            for (int k = 0; k < SEG; k += 4) *reinterpret_cast<float4*>(p + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+            return;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < SEG; ++k)
+        if (k < n) st(p + k, v[k]);
+}
+
+template <int SEG, typename T>
+__device__ __forceinline__ void load_seg(const T* __restrict__ p, float* v, int n) {
+    if (n == SEG) {
+        if constexpr (sizeof(T) == 2 && SEG == 8) {
+            unpack8(*reinterpret_cast<const uint4*>(p), v);
+            return;
+        } else if constexpr (sizeof(T) == 2 && SEG == 4) {
+            const uint2 r = *reinterpret_cast<const uint2*>(p);
+            v[0] = __uint_as_float(r.x << 16); v[1] = __uint_as_float(r.x & 0xFFFF0000u);
+            v[2] = __uint_as_float(r.y << 16); v[3] = __uint_as_float(r.y & 0xFFFF0000u);
+            return;
+        } else if constexpr (sizeof(T) == 4 && SEG % 4 == 0) {
+#pragma unroll
+            for (int k = 0; k < SEG; k += 4) {
+                const float4 a = *reinterpret_cast<const float4*>(p + k);
+                v[k] = a.x; v[k + 1] = a.y; v[k + 2] = a.z; v[k + 3] = a.w;
+            }
+            return;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < SEG; ++k) v[k] = k < n ? ld(p + k) : 0.f;
+}
+
+template <typename T>
+__device__ __forceinline__ void dw_stage_seg(const T* __restrict__ xp, int Hi, int Wi, int ih0, int LH, int LW, int pl,
                                          bool vec8, float* __restrict__ dst) {
     // LDS rows r = input rows ih0 + r, columns c = input columns c - pl; zero outside the input
     if (vec8) {  // Wi % 8 == 0: 8-element row chunks, 16-B (bf16) loads; the pad columns separately
@@ -326,51 +456,12 @@ __device__ __forceinline__ void dw_stage(const T* __restrict__ xp, int Hi, int W
     }
 }
 
-template <int SEG, typename T>
-__device__ __forceinline__ void store_seg(T* __restrict__ p, const float* v, int n) {
-    if (n == SEG) {
-        if constexpr (sizeof(T) == 2 && SEG == 8) {
-            *reinterpret_cast<uint4*>(p) = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
-            return;
-        } else if constexpr (sizeof(T) == 2 && SEG == 4) {
-            *reinterpret_cast<uint2*>(p) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-            return;
-        } else if constexpr (sizeof(T) == 2 && SEG == 2) {
-            *reinterpret_cast<unsigned*>(p) = pack2(v[0], v[1]);
-            return;
-        } else if constexpr (sizeof(T) == 4 && SEG % 4 == 0) {
-#pragma unroll
-            for (int k = 0; k < SEG; k += 4) *reinterpret_cast<float4*>(p + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
-            return;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < SEG; ++k)
-        if (k < n) st(p + k, v[k]);
-}
-
-template <int SEG, typename T>
-__device__ __forceinline__ void load_seg(const T* __restrict__ p, float* v, int n) {
-    if (n == SEG) {
-        if constexpr (sizeof(T) == 2 && SEG == 8) {
-            unpack8(*reinterpret_cast<const uint4*>(p), v);
-            return;
-        } else if constexpr (sizeof(T) == 4 && SEG % 4 == 0) {
-#pragma unroll
-            for (int k = 0; k < SEG; k += 4) {
-                const float4 a = *reinterpret_cast<const float4*>(p + k);
-                v[k] = a.x; v[k + 1] = a.y; v[k + 2] = a.z; v[k + 3] = a.w;
-            }
-            return;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < SEG; ++k) v[k] = k < n ? ld(p + k) : 0.f;
-}
-
-// y (forward or stride-1 backward-data with flip): block = (PB consecutive planes, band of BHo output rows)
+// Round-5 segment kernel (the 5 x 5 and stride-2 forwards, where it measured faster than the tile
+// mapping below): its own staging (column iw at iw + pl, row stride (Wo - 1) S + K) and SEG consecutive
+// outputs of one row per thread. y (forward or stride-1 backward-data with flip): block = (PB
+// consecutive planes, band of BHo output rows)
 template <int K, int S, int SEG, typename T>
-__global__ __launch_bounds__(kBlock) void k_dw_fwd_lds(const T* __restrict__ x, const float* __restrict__ w, DwGeo g,
+__global__ __launch_bounds__(kBlock) void k_dw_fwd_lds_seg(const T* __restrict__ x, const float* __restrict__ w, DwGeo g,
                                                        int flip, DwBand bd, T* __restrict__ y) {
     extern __shared__ float smem[];
     float* s_w = smem;                    // [PB][K*K]
@@ -385,7 +476,7 @@ __global__ __launch_bounds__(kBlock) void k_dw_fwd_lds(const T* __restrict__ x, 
     }
     const bool vec8 = g.Wi % 8 == 0;
     for (int pl = 0; pl < np; ++pl)
-        dw_stage(x + (size_t)(p0 + pl) * g.Hi * g.Wi, g.Hi, g.Wi, oh0 * S - g.pt, LH, bd.LW, g.pl, vec8,
+        dw_stage_seg(x + (size_t)(p0 + pl) * g.Hi * g.Wi, g.Hi, g.Wi, oh0 * S - g.pt, LH, bd.LW, g.pl, vec8,
                  s_x + pl * bd.LHmax * bd.LW);
     __syncthreads();
     const int nseg = (g.Wo + SEG - 1) / SEG;
@@ -416,18 +507,90 @@ __global__ __launch_bounds__(kBlock) void k_dw_fwd_lds(const T* __restrict__ x, 
     }
 }
 
+// Compute mapping of the LDS kernels: consecutive threads take consecutive output COLUMNS of a row
+// group (TH output rows of one plane), so a wave's LDS reads of a tap are consecutive words (no bank
+// conflicts; the round-5 mapping gave each thread SEG consecutive outputs, lanes 8 words apart: 8-way
+// conflicts that made these kernels LDS-bound), and each staged input row a thread reads feeds every
+// output row of its group it overlaps (vertical reuse: ((TH - 1) S + K) K reads for TH K^2 FMAs).
+constexpr int kDwTH = 4;
+// output columns per thread: TW consecutive outputs (one 4 * TW-byte store per row for bf16; the
+// single-column form issued 8x the store instructions of the 16-B segment form and measured slower)
+constexpr int kDwTW = 4;
+// which LDS kernels take the TH x TW tile mapping (per-layer A/B, c3 step, profiles/r06/dw_tile_ab.txt):
+// every weight gradient and the 3 x 3 stride-1 forward (27.9 vs 32.1 us at 64 x 176; weight gradients
+// 33.6 vs 42.5, 46.3 vs 65.5); 5 x 5 and stride-2 forwards keep the segment mapping (57 vs 38 us: their
+// threads' input columns 4 S words apart conflict in the LDS banks again)
+__host__ __device__ constexpr bool dw_tile_map(int K, int S, bool fwd) { return !fwd || (K == 3 && S == 1); }
+
+// y (forward or stride-1 backward-data with flip): block = (PB consecutive planes, band of BHo output rows)
+template <int K, int S, int SEG, typename T>
+__global__ __launch_bounds__(kBlock) void k_dw_fwd_lds(const T* __restrict__ x, const float* __restrict__ w, DwGeo g,
+                                                       int flip, DwBand bd, T* __restrict__ y) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int TH = kDwTH, TR = (TH - 1) * S + K;  // output rows per thread, input rows they read
+    const int band = blockIdx.x % bd.nbands, pg = blockIdx.x / bd.nbands;
+    const int p0 = pg * bd.PB, np = min(bd.PB, g.nplanes - p0);
+    const int oh0 = band * bd.BHo, nrow = min(bd.BHo, g.Ho - oh0);
+    const int LH = (nrow - 1) * S + K;
+    const int lps = bd.LHmax * bd.LW;
+    float* s_x = smem;                    // [PB][LHmax][LW] (8-B aligned rows)
+    float* s_w = smem + bd.PB * lps;      // [PB][K*K]
+    dw_stage(x + (size_t)p0 * g.Hi * g.Wi, (size_t)g.Hi * g.Wi, np, g.Hi, g.Wi, oh0 * S - g.pt, LH, bd.LW, lps, s_x);
+    for (int i = threadIdx.x; i < np * K * K; i += kBlock) {
+        const int pl = i / (K * K), t = i - pl * (K * K);
+        s_w[i] = w[(size_t)((p0 + pl) % g.C) * K * K + (flip ? K * K - 1 - t : t)];
+    }
+    __syncthreads();
+    const int col0 = kDwCol - g.pl;
+    constexpr int TW = kDwTW, CW = (TW - 1) * S + K;  // output columns per thread, input columns they read
+    const int nrg = (nrow + TH - 1) / TH, ncg = g.Wo / TW;  // (Wo % TW == 0: dw_lds_ok)
+    const int items = np * nrg * ncg;
+    for (int it = threadIdx.x; it < items; it += kBlock) {
+        const int pr = it / ncg, ow = (it - pr * ncg) * TW;
+        const int pl = pr / nrg, rg = pr - pl * nrg;
+        const float* wk = s_w + pl * K * K;
+        const float* xs = s_x + pl * lps + (rg * TH * S) * bd.LW + ow * S + col0;
+        float acc[TH][TW];
+#pragma unroll
+        for (int j = 0; j < TH; ++j)
+#pragma unroll
+            for (int c = 0; c < TW; ++c) acc[j][c] = 0.f;
+#pragma unroll
+        for (int t = 0; t < TR; ++t) {  // input row t of the group (rows past the band's end: never stored)
+            float v[CW];
+#pragma unroll
+            for (int q = 0; q < CW; ++q) v[q] = xs[min(t, LH - 1 - rg * TH * S) * bd.LW + q];
+#pragma unroll
+            for (int j = 0; j < TH; ++j) {
+                const int kh = t - j * S;
+                if (kh >= 0 && kh < K)
+#pragma unroll
+                    for (int kw = 0; kw < K; ++kw) {
+                        const float wv = wk[kh * K + kw];
+#pragma unroll
+                        for (int c = 0; c < TW; ++c) acc[j][c] = fmaf(v[c * S + kw], wv, acc[j][c]);
+                    }
+            }
+        }
+        T* yp = y + ((size_t)(p0 + pl) * g.Ho + oh0 + rg * TH) * g.Wo + ow;
+#pragma unroll
+        for (int j = 0; j < TH; ++j)
+            if (rg * TH + j < nrow) store_seg<TW>(yp + (size_t)j * g.Wo, acc[j], TW);
+    }
+}
+
 // weight-gradient partials: block (channel c, image group q), PB images of the group staged at a time
 template <int K, int S, int SEG, typename T>
 __global__ __launch_bounds__(kBlock) void k_dw_wgt_lds(const T* __restrict__ x, const T* __restrict__ dy, DwGeo g,
                                                        int nimg, int ngroups, DwBand bd, float* __restrict__ partial) {
-    extern __shared__ float smem[];
-    float* s_x = smem;  // [PB][LH][LW]
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int TH = kDwTH, TR = (TH - 1) * S + K;
+    float* s_x = smem;  // [PB][LHmax][LW]
     __shared__ float s_red[kBlock / kWave][K * K];
     const int c = blockIdx.x % g.C, q = blockIdx.x / g.C;
     const int n0 = (int)((long)nimg * q / ngroups), n1 = (int)((long)nimg * (q + 1) / ngroups);
-    const int nseg = (g.Wo + SEG - 1) / SEG;
-    constexpr int CW = (SEG - 1) * S + K;
-    const bool vec8 = g.Wi % 8 == 0;
+    const int lps = bd.LHmax * bd.LW;
+    const int col0 = kDwCol - g.pl;
     float acc[K * K];
 #pragma unroll
     for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
@@ -437,27 +600,41 @@ __global__ __launch_bounds__(kBlock) void k_dw_wgt_lds(const T* __restrict__ x, 
             const int oh0 = band * bd.BHo, nrow = min(bd.BHo, g.Ho - oh0);
             const int LH = (nrow - 1) * S + K;
             __syncthreads();  // the previous chunk's readers are done with s_x
-            for (int pl = 0; pl < np; ++pl)
-                dw_stage(x + ((size_t)(nb + pl) * g.C + c) * g.Hi * g.Wi, g.Hi, g.Wi, oh0 * S - g.pt, LH, bd.LW, g.pl,
-                         vec8, s_x + pl * bd.LHmax * bd.LW);
+            dw_stage(x + ((size_t)nb * g.C + c) * g.Hi * g.Wi, (size_t)g.C * g.Hi * g.Wi, np, g.Hi, g.Wi,
+                     oh0 * S - g.pt, LH, bd.LW, lps, s_x);
             __syncthreads();
-            const int items = np * nrow * nseg;
+            constexpr int TW = kDwTW, CW = (TW - 1) * S + K;
+            const int nrg = (nrow + TH - 1) / TH, ncg = g.Wo / TW;
+            const int items = np * nrg * ncg;
             for (int it = threadIdx.x; it < items; it += kBlock) {
-                const int pl = it / (nrow * nseg), rem = it - pl * (nrow * nseg);
-                const int r = rem / nseg, sg = rem - r * nseg;
-                const int ow0 = sg * SEG, nv = min(SEG, g.Wo - ow0);
-                float d[SEG];
-                load_seg<SEG>(dy + (((size_t)(nb + pl) * g.C + c) * g.Ho + oh0 + r) * g.Wo + ow0, d, nv);
-                const float* xs = s_x + pl * bd.LHmax * bd.LW + (r * S) * bd.LW + ow0 * S;
+                const int pr = it / ncg, ow = (it - pr * ncg) * TW;
+                const int pl = pr / nrg, rg = pr - pl * nrg;
+                // the group's dy values (clamped rows, zeroed past the band: every load issued before the first use)
+                const T* dp = dy + (((size_t)(nb + pl) * g.C + c) * g.Ho + oh0 + rg * TH) * g.Wo + ow;
+                float d[TH][TW];
 #pragma unroll
-                for (int kh = 0; kh < K; ++kh) {
+                for (int j = 0; j < TH; ++j) load_seg<TW>(dp + (size_t)min(j, nrow - 1 - rg * TH) * g.Wo, d[j], TW);
+#pragma unroll
+                for (int j = 0; j < TH; ++j)
+                    if (rg * TH + j >= nrow)
+#pragma unroll
+                        for (int cc = 0; cc < TW; ++cc) d[j][cc] = 0.f;
+                const float* xs = s_x + pl * lps + (rg * TH * S) * bd.LW + ow * S + col0;
+#pragma unroll
+                for (int t = 0; t < TR; ++t) {
                     float v[CW];
 #pragma unroll
-                    for (int qq = 0; qq < CW; ++qq) v[qq] = xs[kh * bd.LW + qq];
+                    for (int qq = 0; qq < CW; ++qq) v[qq] = xs[min(t, LH - 1 - rg * TH * S) * bd.LW + qq];
 #pragma unroll
-                    for (int kw = 0; kw < K; ++kw)
+                    for (int j = 0; j < TH; ++j) {
+                        const int kh = t - j * S;
+                        if (kh >= 0 && kh < K)
 #pragma unroll
-                        for (int j = 0; j < SEG; ++j) acc[kh * K + kw] = fmaf(d[j], v[j * S + kw], acc[kh * K + kw]);
+                            for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+                                for (int cc = 0; cc < TW; ++cc)
+                                    acc[kh * K + kw] = fmaf(d[j][cc], v[cc * S + kw], acc[kh * K + kw]);
+                    }
                 }
             }
         }
@@ -482,13 +659,18 @@ __global__ __launch_bounds__(kBlock) void k_dw_wgt_lds(const T* __restrict__ x, 
 // bands and planes per block for the LDS kernels: the whole plane when it fits, several planes per
 // block while the block has fewer than ~2 output segments per thread
 template <int K, int S>
-inline DwBand dw_band(const DwGeo& g, int seg, int max_planes) {
+inline DwBand dw_band(const DwGeo& g, int seg, int max_planes, bool tile) {
     DwBand b;
-    b.LW = (g.Wo - 1) * S + K;
+    // row stride: the data at kDwCol, every compute read of the last (possibly partial) segment inside
+    // the row; LW = 2 (mod 4): rows 8-B aligned for the staging writes, and consecutive rows start 2
+    // banks apart (a stride of 0 mod 8 lined every row's segments up on the same banks: 32 -> 49 us at
+    // block 0's 64 x 176 planes)
+    (void)seg;
+    b.LW = ((kDwCol - g.pl + (g.Wo - 1) * S + K + 1) & ~3) + 2;
     const int full = (g.Ho - 1) * S + K;
     if (full * b.LW <= kDwLdsFloats) {
         b.BHo = g.Ho;
-        const int per_plane = g.Ho * ((g.Wo + seg - 1) / seg);
+        const int per_plane = tile ? ((g.Ho + kDwTH - 1) / kDwTH) * (g.Wo / kDwTW) : g.Ho * (g.Wo / seg);  // items
         int pb = std::max(1, kDwLdsFloats / (full * b.LW));
         pb = std::min(pb, std::max(1, (2 * kBlock + per_plane - 1) / per_plane));
         b.PB = std::max(1, std::min(pb, max_planes));
@@ -513,13 +695,50 @@ inline bool dw_lds_ok(const DwGeo& g, const void* a, const void* b) {
 
 inline int dw_seg(int Wo) { return Wo % 8 == 0 ? 8 : Wo % 4 == 0 ? 4 : Wo % 2 == 0 ? 2 : 1; }
 
+// the round-5 band for the segment kernel: LDS rows of exactly (Wo - 1) S + K floats
+template <int K, int S>
+inline DwBand dw_band_seg(const DwGeo& g, int seg, int max_planes) {
+    DwBand b;
+    b.LW = (g.Wo - 1) * S + K;
+    const int full = (g.Ho - 1) * S + K;
+    if (full * b.LW <= kDwLdsFloats) {
+        b.BHo = g.Ho;
+        const int per_plane = g.Ho * ((g.Wo + seg - 1) / seg);
+        int pb = std::max(1, kDwLdsFloats / (full * b.LW));
+        pb = std::min(pb, std::max(1, (2 * kBlock + per_plane - 1) / per_plane));
+        b.PB = std::max(1, std::min(pb, max_planes));
+    } else {
+        b.BHo = std::max(1, (kDwLdsFloats / b.LW - K) / S + 1);
+        b.PB = 1;
+    }
+    b.LHmax = (b.BHo - 1) * S + K;
+    b.nbands = (g.Ho + b.BHo - 1) / b.BHo;
+    return b;
+}
+
 template <int K, int S, typename T>
 int dw_fwd_lds(const void* x, const float* w, DwGeo g, int flip, void* y, hipStream_t s) {
     const int seg = dw_seg(g.Wo);
-    const DwBand b = dw_band<K, S>(g, seg, g.nplanes);
+    if constexpr (!dw_tile_map(K, S, true)) {
+        const DwBand b = dw_band_seg<K, S>(g, seg, g.nplanes);
+        const long blocks = (long)b.nbands * ((g.nplanes + b.PB - 1) / b.PB);
+        // slack past the staged rows: the last segment of a row reads up to (SEG - 1) * S columns past Wo
+        const size_t lds = sizeof(float) * ((size_t)b.PB * K * K + (size_t)b.PB * b.LHmax * b.LW + 8 * S + K);
+        if (blocks > INT_MAX) return LSS_CONV_EINVAL;
+#define LSS_DW_FWD_SEG(SG) hipLaunchKernelGGL((k_dw_fwd_lds_seg<K, S, SG, T>), dim3((unsigned)blocks), dim3(kBlock), lds, \
+                                              s, (const T*)x, w, g, flip, b, (T*)y)
+        switch (seg) {
+            case 8: LSS_DW_FWD_SEG(8); break;
+            case 4: LSS_DW_FWD_SEG(4); break;
+            case 2: LSS_DW_FWD_SEG(2); break;
+            default: LSS_DW_FWD_SEG(1); break;
+        }
+#undef LSS_DW_FWD_SEG
+        return launch_status();
+    }
+    const DwBand b = dw_band<K, S>(g, seg, g.nplanes, dw_tile_map(K, S, true));
     const long blocks = (long)b.nbands * ((g.nplanes + b.PB - 1) / b.PB);
-    // slack past the staged rows: the last segment of a row reads up to (SEG - 1) * S columns past Wo
-    const size_t lds = sizeof(float) * ((size_t)b.PB * K * K + (size_t)b.PB * b.LHmax * b.LW + 8 * S + K);
+    const size_t lds = sizeof(float) * ((size_t)b.PB * b.LHmax * b.LW + (size_t)b.PB * K * K);
     if (blocks > INT_MAX) return LSS_CONV_EINVAL;
 #define LSS_DW_FWD(SG) hipLaunchKernelGGL((k_dw_fwd_lds<K, S, SG, T>), dim3((unsigned)blocks), dim3(kBlock), lds, s, \
                                           (const T*)x, w, g, flip, b, (T*)y)
@@ -536,8 +755,8 @@ int dw_fwd_lds(const void* x, const float* w, DwGeo g, int flip, void* y, hipStr
 template <int K, int S, typename T>
 int dw_wgt_lds(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, hipStream_t s) {
     const int seg = dw_seg(g.Wo);
-    const DwBand b = dw_band<K, S>(g, seg, (nimg + ngroups - 1) / ngroups);
-    const size_t lds = sizeof(float) * ((size_t)b.PB * b.LHmax * b.LW + 8 * S + K);
+    const DwBand b = dw_band<K, S>(g, seg, (nimg + ngroups - 1) / ngroups, dw_tile_map(K, S, false));
+    const size_t lds = sizeof(float) * ((size_t)b.PB * b.LHmax * b.LW);
 #define LSS_DW_WGT(SG) hipLaunchKernelGGL((k_dw_wgt_lds<K, S, SG, T>), dim3(g.C * ngroups), dim3(kBlock), lds, s, \
                                           (const T*)x, (const T*)dy, g, nimg, ngroups, b, partial)
     switch (seg) {

@@ -122,7 +122,7 @@ def step_trace(out, spec):
         shutil.copy(st, os.path.join(out, f"{name}_kernel_stats.csv"))
     if tr:
         for script, suffix, args in (("hot_steps.py", "hot_steps.txt", ["5", "23"]),
-                                     ("step_kernels.py", "step_kernels.txt", ["5", "23", "40"]),
+                                     ("step_kernels.py", "step_kernels.txt", ["5", "23", "400"]),
                                      ("steady_summary.py", "steady_summary.json", [])):
             with open(os.path.join(out, f"{name}_{suffix}"), "w") as fh:
                 subprocess.call([PY, os.path.join(REPO, "scripts", script), tr] + args, stdout=fh,
