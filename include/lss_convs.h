@@ -80,6 +80,15 @@ int lss_pw_conv(const void* x, const void* a, int32_t a_layout, int32_t N, int32
 int lss_scale_add(const void* x, const void* u, float keep, const void* res, int64_t N, int64_t per, void* y,
                   void* stream);
 
+/* (ABI 23) The weight of a stride-1, padding-(K-1)/2 transposed convolution as a forward one:
+ * wt[i][o][a][b] = w[o][i][K-1-a][K-1-b], written channels-last ((I, O, K, K) with memory order
+ * i, a, b, o). w is (O, I, K, K), NCHW (contiguous) or NHWC (channels-last) per w_layout; dtype fp32 or
+ * bf16. dx = conv2d(dy, wt) is the backward-data of y = conv2d(x, w) (models._Conv3x3: MIOpen's forward
+ * kernels instead of its backward-data ones). Replaces w.transpose(0, 1).flip(2, 3).contiguous(...),
+ * two torch kernels. */
+int lss_conv_flip_weight(const void* w, int32_t dtype, int32_t O, int32_t I, int32_t K, int32_t w_layout,
+                         void* wt, void* stream);
+
 /* Dropout (CamEncode.dropout = nn.Dropout(0.2), src/models.py:44, 53), training mode: y = x / keep where
  * a counter-based draw keeps the element (probability keep), else 0; n elements of dtype (fp32 or bf16)
  * in memory order (any memory format), n * sizeof(dtype) % 16 == 0, 16-B aligned. The mask is a pure

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LSS_ABI_VERSION 22
+#define LSS_ABI_VERSION 23
 
 typedef struct lss_dims {
     int32_t B, N, D, H, W, C;

@@ -18,7 +18,7 @@ DEBUG_LIB_PATH = os.path.join(_HERE, "liblss_hip_debug.so")  # LSS_DEBUG=1: devi
 
 F32, BF16 = 0, 1
 NCHW, NHWC = 0, 1
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 
 class Dims(ctypes.Structure):
@@ -96,6 +96,7 @@ SIGNATURES = {
     "lss_bce_logits": (ctypes.c_int, [_p, _i32, _p, ctypes.c_int64, ctypes.c_float, _p, _p, _p, _p]),
     "lss_bce_partials": (ctypes.c_int64, [ctypes.c_int64]),
     "lss_channel_sums": (ctypes.c_int, [_p, _i32, _i32, _i32, _i32, _p, _p]),
+    "lss_conv_flip_weight": (ctypes.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "lss_clip_adam_partials": (ctypes.c_int, []),
     "lss_clip_adam": (ctypes.c_int, [_i32, _p, _p, _p, _p, _p, _p, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                      ctypes.c_float, ctypes.c_float, ctypes.c_float, _p, _p]),

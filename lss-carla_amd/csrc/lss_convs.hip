@@ -1953,6 +1953,93 @@ int lss_scale_add(const void* x, const void* u, float keep, const void* res, int
 }
 
 
+}  // extern "C"
+
+namespace {
+// wt[i][o][a][b] = w[o][i][K-1-a][K-1-b], written channels-last ([i][a][b][o] in memory): the weight of a
+// stride-1 transposed convolution as a forward one (models._Conv3x3's backward-data). One thread per
+// output element, consecutive threads along o (coalesced writes; the reads are a 1.2 MB weight, in L2).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_conv_flip_weight(const T* __restrict__ w, int O, int I, int K, int cl_in,
+                                                             T* __restrict__ wt) {
+    const long e = (long)blockIdx.x * kBlock + threadIdx.x;
+    const long n = (long)O * I * K * K;
+    if (e >= n) return;
+    const int o = (int)(e % O);
+    long r = e / O;
+    const int b = (int)(r % K);
+    r /= K;
+    const int a = (int)(r % K);
+    const int i = (int)(r / K);
+    const int ka = K - 1 - a, kb = K - 1 - b;
+    const long src = cl_in ? (((long)o * K + ka) * K + kb) * I + i : (((long)o * I + i) * K + ka) * K + kb;
+    wt[e] = w[src];
+}
+
+// The tiled form: per tap, a 64 x 64 (o, i) tile read along i (coalesced for channels-last weights,
+// whose innermost index is i; 9-element strides for contiguous ones) and written along o (wt's innermost)
+// through an LDS transpose (odd row stride); each thread's 16 loads are issued together (a loop that
+// loaded and stored one element per iteration took 11 us per weight: 16 dependent round trips).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_conv_flip_weight_cl(const T* __restrict__ w, int O, int I, int K, int cl,
+                                                                T* __restrict__ wt) {
+    __shared__ T tile[64][65];
+    const int ti = (I + 63) / 64, to = (O + 63) / 64;
+    int b = blockIdx.x;
+    const int it = b % ti;
+    b /= ti;
+    const int ot = b % to;
+    const int tap = b / to;  // output tap (a, b) = (tap / K, tap % K); source tap K*K - 1 - tap
+    const int i0 = it * 64, o0 = ot * 64, src_tap = K * K - 1 - tap;
+    const long so = (long)K * K * I, si = cl ? 1 : K * K, st = cl ? I : 1;
+    const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+    constexpr int R = 64 / (kBlock / 64);
+    T v[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {  // rows o, columns i (clamped addresses, all loads in flight)
+        const int o = min(o0 + r0 + k * (kBlock / 64), O - 1), i = min(i0 + c, I - 1);
+        v[k] = w[o * so + src_tap * st + i * si];
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) tile[r0 + k * (kBlock / 64)][c] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < R; ++k) {  // rows i, columns o
+        const int i = i0 + r0 + k * (kBlock / 64), o = o0 + c;
+        if (o < O && i < I) wt[((long)i * K * K + tap) * O + o] = tile[c][r0 + k * (kBlock / 64)];
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int lss_conv_flip_weight(const void* w, int32_t dtype, int32_t O, int32_t I, int32_t K, int32_t w_layout, void* wt,
+                         void* stream) {
+    if (!w || !wt || O <= 0 || I <= 0 || K <= 0 || (dtype != LSS_CONV_BF16 && dtype != LSS_CONV_F32) ||
+        (w_layout != LSS_CONV_NCHW && w_layout != LSS_CONV_NHWC))
+        return LSS_CONV_EINVAL;
+    const long n = (long)O * I * K * K;
+    if (n >= INT_MAX) return LSS_CONV_EINVAL;
+    const int cl = w_layout == LSS_CONV_NHWC;
+    const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    if (O >= 64 && I >= 64) {
+        const unsigned gcl = (unsigned)(((I + 63) / 64) * ((O + 63) / 64) * K * K);
+        if (dtype == LSS_CONV_BF16)
+            hipLaunchKernelGGL(k_conv_flip_weight_cl<bf16>, dim3(gcl), dim3(kBlock), 0, s, (const bf16*)w, O, I, K, cl,
+                               (bf16*)wt);
+        else
+            hipLaunchKernelGGL(k_conv_flip_weight_cl<float>, dim3(gcl), dim3(kBlock), 0, s, (const float*)w, O, I, K,
+                               cl, (float*)wt);
+    } else if (dtype == LSS_CONV_BF16)
+        hipLaunchKernelGGL(k_conv_flip_weight<bf16>, dim3(grid), dim3(kBlock), 0, s, (const bf16*)w, O, I, K, cl, (bf16*)wt);
+    else
+        hipLaunchKernelGGL(k_conv_flip_weight<float>, dim3(grid), dim3(kBlock), 0, s, (const float*)w, O, I, K, cl,
+                           (float*)wt);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
 int lss_dropout(const void* x, int32_t dtype, int64_t n, const uint64_t* seed, float keep, void* y, const void* prefetch,
                 int64_t prefetch_bytes, void* stream) {
     const int esz = dtype == LSS_CONV_BF16 ? 2 : dtype == LSS_CONV_F32 ? 4 : 0;

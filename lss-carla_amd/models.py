@@ -76,14 +76,26 @@ class _Conv3x3(torch.autograd.Function):
         x, w = ctx.saved_tensors
         need = ctx.needs_input_grad
         dx = dw = None
-        fmt = torch.channels_last if w.is_contiguous(memory_format=torch.channels_last) else torch.contiguous_format
         if need[0]:
-            wt = w.transpose(0, 1).flip(2, 3).contiguous(memory_format=fmt)
-            dx = F.conv2d(dy, wt, None, 1, 1)
+            dx = F.conv2d(dy, _flip_weight(w), None, 1, 1)
         if need[1]:
             dw = torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                                                      [False, True, False])[1]
         return dx, dw
+
+
+def _flip_weight(w: torch.Tensor) -> torch.Tensor:
+    """W'[i, o, a, b] = W[o, i, 2 - a, 2 - b], channels-last, in one lss_conv_flip_weight launch."""
+    O, I, K, _ = w.shape
+    if w.is_contiguous(memory_format=torch.channels_last):
+        lay = _lib.NHWC
+    else:
+        w, lay = w.contiguous(), _lib.NCHW
+    wt = torch.empty(I, O, K, K, device=w.device, dtype=w.dtype, memory_format=torch.channels_last)
+    lib = _lib.load()
+    _lib.check(lib.lss_conv_flip_weight(_lib.ptr(w), _lib.dtype_code(w.dtype), O, I, K, lay, _lib.ptr(wt),
+                                        _lib.stream_handle(w.device)), "lss_conv_flip_weight")
+    return wt
 
 
 def conv3x3(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:

@@ -90,3 +90,19 @@ def test_bevencode_flip_on_off():
     assert grads[0].keys() == grads[1].keys()
     for n in grads[0]:
         assert _rel(grads[0][n], grads[1][n]) < 3e-2, n
+
+
+@pytest.mark.parametrize("cl", [True, False], ids=["channels_last", "contiguous"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32], ids=["bf16", "fp32"])
+@pytest.mark.parametrize("O,I,K", [(256, 320, 3), (128, 256, 3), (40, 48, 5)])
+def test_flip_weight_kernel_exact(O, I, K, dtype, cl):
+    """lss_conv_flip_weight == w.transpose(0, 1).flip(2, 3), bit for bit, channels-last output."""
+    torch.manual_seed(O + I + K)
+    w = torch.randn(O, I, K, K, device=DEV).to(dtype)
+    if cl:
+        w = w.contiguous(memory_format=torch.channels_last)
+    got = models._flip_weight(w)
+    torch.cuda.synchronize()
+    want = w.transpose(0, 1).flip(2, 3)
+    assert got.shape == (I, O, K, K) and got.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(got, want)
