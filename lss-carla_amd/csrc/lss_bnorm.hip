@@ -41,6 +41,12 @@ constexpr int kWave = 64;
 #ifndef LSS_BN_GMAX
 #define LSS_BN_GMAX 4096
 #endif
+#ifndef LSS_BN_NHWC_ELEMS
+#define LSS_BN_NHWC_ELEMS 32768  // NHWC statistics: elements per block (128 per thread; 8 K: 1013 vs 966-978 us of NHWC BN per c3 step, profiles/r06/bn_nhwc_groups_ab.txt)
+#endif
+#ifndef LSS_BN_NHWC_GMIN
+#define LSS_BN_NHWC_GMIN 512  // ... but at least this many blocks where each still gets >= 8 K elements
+#endif
 constexpr int kMaxGroupsNhwc = 4096;  // partial groups the ABI accepts (NHWC)
 constexpr int kGroupsNhwc = LSS_BN_GMAX;  // groups lss_bn_groups picks at most (NHWC)
 
@@ -969,7 +975,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_stats_nhwc(const T* __restrict__ 
 // A lane's pairs of one channel's partials (groups lane, lane + 64, ...) added in that order, kFoldBatch
 // loads in flight at a time: the loop that loaded one pair per iteration waited a cache round trip per
 // 64 groups (up to 64 of them in sequence: a 14-19 us fold at 2,500-4,096 groups).
-constexpr int kFoldBatch = 16;
+constexpr int kFoldBatch = 16;  // (32, one batch per lane at c3, measured no faster: launch-bound)
 __device__ __forceinline__ void fold_lane_pairs(const float* __restrict__ p, int G, int lane, float& s1, float& s2) {
     int q = lane;
     for (; q + (kFoldBatch - 1) * kWave < G; q += kFoldBatch * kWave) {
@@ -1288,7 +1294,12 @@ extern "C" {
 int lss_bn_groups(int32_t N, int32_t C, int32_t HW, int32_t layout) {
     const long per_chan = (long)N * HW;
     if (layout == LSS_CONV_NHWC) {
-        const long g = per_chan * C / 8192;  // ~8 K elements (32 per thread) per block
+        // ~LSS_BN_NHWC_ELEMS elements per block, but at least LSS_BN_NHWC_GMIN blocks where the tensor
+        // has >= 8 K elements for each
+        const long tot = per_chan * C;
+        long g = tot / LSS_BN_NHWC_ELEMS;
+        const long gmin = std::min<long>(LSS_BN_NHWC_GMIN, tot / 8192);
+        if (g < gmin) g = gmin;
         return (int)(g < 1 ? 1 : (g > kGroupsNhwc ? kGroupsNhwc : g));
     }
     const long g = per_chan / 8192;  // ~8 K elements of one channel per block

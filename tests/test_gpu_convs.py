@@ -347,8 +347,8 @@ def test_drop_connect_add_eval_is_plain_add():
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_bn_relu_nhwc_backward_recomputes_output(dtype):
     """Channels-last ReLU without a residual: lss_bn_bwd with y = NULL (the output recomputed from x and
-    the saved scale / shift) gives the same bits as with the forward's y; at a shape with 2,500 partial
-    groups per channel (the fold's batched loads and its tail), and against torch's BN on the GPU."""
+    the saved scale / shift) gives the same bits as with the forward's y, with 2,500 partial groups per
+    channel through the C ABI (the fold's batched loads and its tail), and against torch's BN on the GPU."""
     from lss_carla_amd import _lib
     lib = _lib.load()
     N, C, H, W = 4, 128, 200, 200
@@ -363,8 +363,10 @@ def test_bn_relu_nhwc_backward_recomputes_output(dtype):
     xd = x.clone().requires_grad_(True)
     y = Nm.bn_act(bn, xd, "relu")
     y.backward(dy)
-    groups = int(lib.lss_bn_groups(N, C, H * W, Nm.NHWC))
-    assert groups > 64 * 16  # the fold's batched loop runs
+    # the C-ABI passes below use more partial groups than lss_bn_groups picks (625 here), so the fold's
+    # batched loop (32 loads per lane) and its tail both run
+    groups = 2500
+    assert groups > 64 * 32 and groups <= 4096
     # the same forward again for its saved statistics, then both backward forms through the C ABI
     stats = torch.empty(4, C, device=DEV)
     partial = torch.empty(C, groups, 2, device=DEV)
@@ -386,7 +388,9 @@ def test_bn_relu_nhwc_backward_recomputes_output(dtype):
         outs.append((dx, dg, db))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
-    assert torch.equal(outs[1][0], xd.grad)
+    # bn_act (lss_bn_groups' 625 groups) vs these 2,500: the same sums in another fold order
+    close = dict(rtol=1e-5, atol=1e-6) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-3)
+    torch.testing.assert_close(outs[1][0].float(), xd.grad.float(), **close)
     # torch's fp32 BN + ReLU on the GPU
     xr = x.float().requires_grad_(True)
     ref = F.relu(F.batch_norm(xr, None, None, bn.weight.detach(), bn.bias.detach(), training=True, eps=1e-5))
