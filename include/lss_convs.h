@@ -51,6 +51,17 @@ int lss_head1_blocks(int32_t P);
 int lss_head1_fwd(const void* x, const float* w, const float* bias, int32_t P, int32_t C, void* y, void* stream);
 int lss_head1_bwd(const void* x, const void* dy, const float* w, int32_t P, int32_t C, void* dx, float* partial,
                   void* stream);
+/* (ABI 23) BevEncode's up2 tail -- BN + ReLU + the one-channel head -- without the normalised map:
+ * lss_head1_fwd2 / lss_head1_bwd2 with bn_stats = the batch norm's saved (4, C) statistics (mean, rstd,
+ * scale, shift; from lss_bn_fwd2 with y = NULL) read x as the batch norm's INPUT and use
+ * bf16(relu(fmaf(x, scale, shift))) -- the value lss_bn_fwd's ReLU apply would have stored -- in its
+ * place (bn_stats = NULL: lss_head1_fwd / lss_head1_bwd). lss_head1_bwd2 with dx = NULL writes no input
+ * gradient (bn_stats required): lss_bn_bwd_rank1 takes it as bf16(dy[r] w[c]) itself. Bit-identical to
+ * the unfused sequence (tests/test_gpu_convs.py). */
+int lss_head1_fwd2(const void* x, const float* w, const float* bias, int32_t P, int32_t C, const float* bn_stats,
+                   void* y, void* stream);
+int lss_head1_bwd2(const void* x, const void* dy, const float* w, int32_t P, int32_t C, const float* bn_stats,
+                   void* dx, float* partial, void* stream);
 
 /* Weight gradient of a 1x1 convolution (no bias, stride 1) over NCHW contiguous bf16 activations:
  * dw (Cout, Cin) = sum over n < N, q < HW of dy[n][co][q] * x[n][ci][q], fp32 accumulation, written as
@@ -175,6 +186,15 @@ int lss_bn_bwd2(const void* dy, const void* x, const void* y, int32_t dtype, int
                 int32_t HW, const float* scale, const float* shift, const float* save_mean, const float* save_rstd,
                 int32_t act, int32_t ngroups, float* partial, float* coef, float* dgamma, float* dbeta, void* dx,
                 void* dresidual, uint32_t* sync, void* stream);
+/* (ABI 23) NHWC bf16 batch-norm backward whose incoming gradient is the rank-1 product
+ * dy[p][c] = bf16(g1[p] * w1[c]) (g1: N*HW bf16, w1: C fp32), computed in the kernels instead of read --
+ * the gradient the one-channel head hands back (lss_head1_bwd2 with dx = NULL). Otherwise lss_bn_bwd's
+ * NHWC path with y = NULL, no residual; act LSS_ACT_NONE or LSS_ACT_RELU. And lss_bn_fwd / lss_bn_fwd2
+ * accept y = NULL for LSS_CONV_NHWC: statistics, saved stats and running stats only, no apply pass. */
+int lss_bn_bwd_rank1(const void* g1, const float* w1, const void* x, int32_t N, int32_t C, int32_t HW,
+                     const float* scale, const float* shift, const float* save_mean, const float* save_rstd,
+                     int32_t act, int32_t ngroups, float* partial, float* coef, float* dgamma, float* dbeta, void* dx,
+                     void* stream);
 
 /* Bilinear upsampling with align_corners=True (nn.Upsample(mode="bilinear", align_corners=True),
  * src/models.py:19, 109) fused with Up's channel concatenation (torch.cat([x2, x1], 1),

@@ -91,6 +91,10 @@ SIGNATURES = {
     "lss_head1_blocks": (ctypes.c_int, [_i32]),
     "lss_head1_fwd": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _p]),
     "lss_head1_bwd": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _p, _p]),
+    "lss_head1_fwd2": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _p, _p]),
+    "lss_head1_bwd2": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _p, _p, _p]),
+    "lss_bn_bwd_rank1": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p, _p, _p, _p,
+                                        _p]),
     "lss_scale_add": (ctypes.c_int, [_p, _p, ctypes.c_float, _p, ctypes.c_int64, ctypes.c_int64, _p, _p]),
     "lss_dropout": (ctypes.c_int, [_p, _i32, ctypes.c_int64, _p, ctypes.c_float, _p, _p, ctypes.c_int64, _p]),
     "lss_bce_logits": (ctypes.c_int, [_p, _i32, _p, ctypes.c_int64, ctypes.c_float, _p, _p, _p, _p]),

@@ -1063,11 +1063,29 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_nhwc(const T* __restrict__ 
     }
 }
 
-template <typename T>
+// Rank-1 incoming gradient (R1): dy[p][c] = bf16(g1[p] * w1[c]), computed instead of loaded -- the
+// gradient a 1x1 conv to ONE channel (lss_head1_bwd2) hands back, bit for bit, never materialised.
+struct Rank1 {
+    const bf16* g1;   // per pixel row
+    const float* w1;  // per channel
+};
+template <bool R1, typename T>
+__device__ __forceinline__ void load_dy8(const T* __restrict__ dy, int idx, int c0, const BnGeo& g, const Rank1& r1,
+                                         const float* w8, float* d) {
+    if constexpr (R1) {
+        const float gv = __bfloat162float(r1.g1[(idx - c0) / g.C]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = __bfloat162float(__float2bfloat16(gv * w8[j]));
+    } else {
+        ldv<8>(dy + idx, d);
+    }
+}
+
+template <typename T, bool R1 = false>
 __global__ __launch_bounds__(kBlock) void k_bn_bwd_stats_nhwc(const T* __restrict__ dy, const T* __restrict__ x,
                                                               const T* __restrict__ y, BnGeo g, int G,
                                                               const float* __restrict__ stats, int act,
-                                                              float* __restrict__ partial) {
+                                                              float* __restrict__ partial, Rank1 r1 = {}) {
     extern __shared__ float s_dyn[];  // [waves][C][2]
     const int cg = g.C / 8;
     const int c0 = ((int)threadIdx.x % cg) * 8;
@@ -1080,6 +1098,9 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_stats_nhwc(const T* __restric
         sh[j] = stats[3 * g.C + c0 + j];
     }
     float a[8] = {}, b[8] = {};
+    float w8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w8[j] = R1 ? r1.w1[c0 + j] : 0.f;
     const bool relu = act == LSS_ACT_RELU;
     constexpr int R = LSS_BN_STATS_R;
     for_rows_nhwc<R>(g, G, blockIdx.x, [&](const int* idx, int n) {
@@ -1087,7 +1108,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_stats_nhwc(const T* __restric
 #pragma unroll
         for (int u = 0; u < R; ++u) {
             if (u >= n) continue;
-            ldv<8>(dy + idx[u], d[u]);
+            load_dy8<R1>(dy, idx[u], c0, g, r1, w8, d[u]);
             ldv<8>(x + idx[u], xv[u]);
             if (relu && y) ldv<8>(y + idx[u], yv[u]);
         }
@@ -1185,15 +1206,18 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_rows_nhwc(const T* __restri
 // dx = scale g + B x + K with B = -scale rstd mean(g xhat), K = -scale (mean(g) - mean rstd mean(g xhat))
 // (the grid-stride form's scale (g - mean(g) - (x - mean) rstd mean(g xhat)) regrouped: 4 coefficients
 // per channel held in registers)
-template <typename T>
+template <typename T, bool R1 = false>
 __global__ __launch_bounds__(kBlock) void k_bn_bwd_apply_rows_nhwc(const T* __restrict__ dy, const T* __restrict__ x,
                                                                    const T* __restrict__ y, BnGeo g,
                                                                    const float* __restrict__ stats,
                                                                    const float* __restrict__ coef, int act,
-                                                                   T* __restrict__ dx, T* __restrict__ dres) {
+                                                                   T* __restrict__ dx, T* __restrict__ dres,
+                                                                   Rank1 r1 = {}) {
     constexpr int R = 2;
     const int c0 = ((int)threadIdx.x % (g.C >> 3)) * 8;
-    float sc[8], sh[8], kb[8], kk[8];
+    float sc[8], sh[8], kb[8], kk[8], w8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w8[j] = R1 ? r1.w1[c0 + j] : 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int c = c0 + j;
@@ -1210,7 +1234,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_apply_rows_nhwc(const T* __re
 #pragma unroll
         for (int u = 0; u < R; ++u)
             if (u < n) {
-                ldv<8>(dy + idx[u], d[u]);
+                load_dy8<R1>(dy, idx[u], c0, g, r1, w8, d[u]);
                 ldv<8>(x + idx[u], xv[u]);
                 if (relu && y) ldv<8>(y + idx[u], yv[u]);
             }
@@ -1323,7 +1347,10 @@ int lss_bn_fwd2(const void* x, const void* residual, int32_t dtype, int32_t layo
                 float* save_mean, float* save_rstd, float* scale, float* shift, void* y, uint32_t* sync,
                 void* stream) {
     const BnGeo g{N, C, HW};
-    if (!x || !y || !partial || !save_mean || !save_rstd || !scale || !shift || ngroups <= 0 || !bn_ok(g, layout))
+    // y == NULL (NHWC only): statistics and the running-stat update, no apply pass (a consumer that
+    // applies scale / shift itself: lss_head1_fwd2)
+    if (!x || (!y && layout != LSS_CONV_NHWC) || !partial || !save_mean || !save_rstd || !scale || !shift ||
+        ngroups <= 0 || !bn_ok(g, layout))
         return LSS_CONV_EINVAL;
     if (act != LSS_ACT_NONE && act != LSS_ACT_RELU && act != LSS_ACT_SWISH) return LSS_CONV_EINVAL;
     // the saved statistics are one (4, C) array: mean, rstd, scale, shift
@@ -1342,7 +1369,8 @@ int lss_bn_fwd2(const void* x, const void* residual, int32_t dtype, int32_t layo
             hipLaunchKernelGGL(k_bn_stats_nhwc<T>, dim3(G), dim3(kBlock), kNhwcStatsLds * C * sizeof(float), s, xx, \
                                g, G, partial);                                                                     \
             hipLaunchKernelGGL(k_bn_fold_nhwc<T>, dim3((C + 3) / 4), dim3(kBlock), 0, s, partial, G, xx, g, P);   \
-            if (LSS_BN_ROWS)                                                                                       \
+            if (!yy) {                                                                                             \
+            } else if (LSS_BN_ROWS)                                                                                \
                 hipLaunchKernelGGL(k_bn_apply_rows_nhwc<T>, dim3(apply_blocks(g)), dim3(kBlock), 0, s, xx, rr, g,  \
                                    save_mean, (int)act, yy);                                                       \
             else                                                                                                   \
@@ -1510,6 +1538,30 @@ int lss_bn_bwd2(const void* dy, const void* x, const void* y, int32_t dtype, int
     else if (dtype == LSS_CONV_BF16) LSS_BN_BWD(bf16);
     else return LSS_CONV_EINVAL;
 #undef LSS_BN_BWD
+    return launch_status();
+}
+
+
+int lss_bn_bwd_rank1(const void* g1, const float* w1, const void* x, int32_t N, int32_t C, int32_t HW,
+                     const float* scale, const float* shift, const float* save_mean, const float* save_rstd,
+                     int32_t act, int32_t ngroups, float* partial, float* coef, float* dgamma, float* dbeta, void* dx,
+                     void* stream) {
+    const BnGeo g{N, C, HW};
+    if (!g1 || !w1 || !x || !scale || !shift || !save_mean || !save_rstd || !partial || !coef || !dx || ngroups <= 0 ||
+        ngroups > kMaxGroupsNhwc || !bn_ok(g, LSS_CONV_NHWC))
+        return LSS_CONV_EINVAL;
+    if (save_rstd != save_mean + C || scale != save_mean + 2 * C || shift != save_mean + 3 * C) return LSS_CONV_EINVAL;
+    if (act != LSS_ACT_NONE && act != LSS_ACT_RELU) return LSS_CONV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const int G = ngroups;
+    const Rank1 r1{(const bf16*)g1, w1};
+    const bf16* xx = (const bf16*)x;
+    hipLaunchKernelGGL((k_bn_bwd_stats_nhwc<bf16, true>), dim3(G), dim3(kBlock), kNhwcStatsLds * C * sizeof(float), s,
+                       (const bf16*)nullptr, xx, (const bf16*)nullptr, g, G, save_mean, (int)act, partial, r1);
+    hipLaunchKernelGGL(k_bn_bwd_fold_nhwc, dim3((C + 3) / 4), dim3(kBlock), 0, s, partial, G, g, dgamma, dbeta, coef);
+    hipLaunchKernelGGL((k_bn_bwd_apply_rows_nhwc<bf16, true>), dim3(apply_blocks(g)), dim3(kBlock), 0, s,
+                       (const bf16*)nullptr, xx, (const bf16*)nullptr, g, save_mean, coef, (int)act, (bf16*)dx,
+                       (bf16*)nullptr, r1);
     return launch_status();
 }
 

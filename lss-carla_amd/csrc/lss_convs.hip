@@ -1118,15 +1118,32 @@ struct BwdWeight {
 // reads 4 rows per instruction (16 lanes x 16 B = one 128-channel row), fp32 accumulation.
 constexpr int kHeadRows = 256;  // rows per block (64 per wave)
 
+// BN mode (bnst = a batch norm's saved (4, C) statistics, NHWC): the input row is the batch norm's INPUT and
+// each value goes through the apply pass's arithmetic first -- bf16(relu(fmaf(x, scale, shift))), what
+// lss_bn_fwd's ReLU apply would have stored -- so the normalised map is never materialised.
+__device__ __forceinline__ void head_bn8(const float* __restrict__ bnst, int C, int c0, float* sc, float* sh) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        sc[i] = bnst ? bnst[2 * C + c0 + i] : 1.f;
+        sh[i] = bnst ? bnst[3 * C + c0 + i] : 0.f;
+    }
+}
+__device__ __forceinline__ float head_in(float v, bool bn, float sc, float sh) {
+    return bn ? __bfloat162float(__float2bfloat16(fmaxf(fmaf(v, sc, sh), 0.f))) : v;
+}
+
 template <int LPR>  // lanes per row: C / 8
 __global__ __launch_bounds__(kBlock) void k_head1_fwd(const uint4* __restrict__ x, const float* __restrict__ w,
-                                                      const float* __restrict__ bias, int P, bf16* __restrict__ y) {
+                                                      const float* __restrict__ bias, int P, bf16* __restrict__ y,
+                                                      const float* __restrict__ bnst) {
     constexpr int RPI = kWave / LPR;  // rows per wave instruction
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int col = lane % LPR, sub = lane / LPR;
-    float wv[8];
+    float wv[8], sc[8], sh[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) wv[i] = w[col * 8 + i];
+    const bool bn = bnst != nullptr;
+    head_bn8(bnst, LPR * 8, col * 8, sc, sh);
     const float b = bias ? *bias : 0.f;  // (a device value: a captured graph replays with the current bias)
     const int r0 = blockIdx.x * kHeadRows + wave * (kHeadRows / 4);
 #pragma unroll 4
@@ -1138,8 +1155,9 @@ __global__ __launch_bounds__(kBlock) void k_head1_fwd(const uint4* __restrict__ 
             const unsigned u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                acc = fmaf(__uint_as_float(u[i] << 16), wv[2 * i], acc);
-                acc = fmaf(__uint_as_float(u[i] & 0xFFFF0000u), wv[2 * i + 1], acc);
+                acc = fmaf(head_in(__uint_as_float(u[i] << 16), bn, sc[2 * i], sh[2 * i]), wv[2 * i], acc);
+                acc = fmaf(head_in(__uint_as_float(u[i] & 0xFFFF0000u), bn, sc[2 * i + 1], sh[2 * i + 1]), wv[2 * i + 1],
+                           acc);
             }
         }
 #pragma unroll
@@ -1150,19 +1168,23 @@ __global__ __launch_bounds__(kBlock) void k_head1_fwd(const uint4* __restrict__ 
 
 // dx[r, c] = dy[r] * w[c] (bf16); partial[block][c] = sum over the block's rows of dy[r] * x[r, c],
 // partial[block][C] = sum of dy[r] (fixed reduction order: deterministic).
+// (BN mode as k_head1_fwd's; dx == NULL: no input gradient written -- the batch norm's backward takes it
+// as the rank-1 product bf16(dy[r] w[c]) itself, lss_bn_bwd_rank1)
 template <int LPR>
 __global__ __launch_bounds__(kBlock) void k_head1_bwd(const uint4* __restrict__ x, const bf16* __restrict__ dy,
                                                       const float* __restrict__ w, int P, uint4* __restrict__ dx,
-                                                      float* __restrict__ partial) {
+                                                      float* __restrict__ partial, const float* __restrict__ bnst) {
     constexpr int RPI = kWave / LPR;
     constexpr int C = LPR * 8;
     __shared__ float s_part[4][C + 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int col = lane % LPR, sub = lane / LPR;
-    float wv[8], acc[8] = {};
+    float wv[8], acc[8] = {}, sc[8], sh[8];
     float dsum = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) wv[i] = w[col * 8 + i];
+    const bool bn = bnst != nullptr;
+    head_bn8(bnst, C, col * 8, sc, sh);
     const int r0 = blockIdx.x * kHeadRows + wave * (kHeadRows / 4);
 #pragma unroll 4
     for (int it = 0; it < kHeadRows / 4 / RPI; ++it) {
@@ -1174,14 +1196,15 @@ __global__ __launch_bounds__(kBlock) void k_head1_bwd(const uint4* __restrict__ 
             unsigned o[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float lo = __uint_as_float(u[i] << 16), hi = __uint_as_float(u[i] & 0xFFFF0000u);
+                const float lo = head_in(__uint_as_float(u[i] << 16), bn, sc[2 * i], sh[2 * i]);
+                const float hi = head_in(__uint_as_float(u[i] & 0xFFFF0000u), bn, sc[2 * i + 1], sh[2 * i + 1]);
                 acc[2 * i] = fmaf(g, lo, acc[2 * i]);
                 acc[2 * i + 1] = fmaf(g, hi, acc[2 * i + 1]);
                 const bf16 a = __float2bfloat16(g * wv[2 * i]), c = __float2bfloat16(g * wv[2 * i + 1]);
                 o[i] = (unsigned)*reinterpret_cast<const unsigned short*>(&a) |
                        ((unsigned)*reinterpret_cast<const unsigned short*>(&c) << 16);
             }
-            dx[(size_t)r * LPR + col] = make_uint4(o[0], o[1], o[2], o[3]);
+            if (dx) dx[(size_t)r * LPR + col] = make_uint4(o[0], o[1], o[2], o[3]);
             if (col == 0) dsum += g;
         }
     }
@@ -1787,31 +1810,43 @@ extern "C" {
 int lss_head1_blocks(int32_t P) { return P > 0 ? (P + kHeadRows - 1) / kHeadRows : 0; }
 
 int lss_head1_fwd(const void* x, const float* w, const float* bias, int32_t P, int32_t C, void* y, void* stream) {
+    return lss_head1_fwd2(x, w, bias, P, C, nullptr, y, stream);
+}
+int lss_head1_fwd2(const void* x, const float* w, const float* bias, int32_t P, int32_t C, const float* bn_stats,
+                   void* y, void* stream) {
     if (!x || !w || !y || P <= 0 || C <= 0 || C % 8 != 0 || 64 % (C / 8) != 0) return LSS_CONV_EINVAL;
     const dim3 gr(lss_head1_blocks(P)), bl(kBlock);
     hipStream_t s = (hipStream_t)stream;
+#define LSS_HEAD1_FWD(L) \
+    hipLaunchKernelGGL((k_head1_fwd<L>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y, bn_stats)
     switch (C / 8) {
-        case 16: hipLaunchKernelGGL((k_head1_fwd<16>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
-        case 8: hipLaunchKernelGGL((k_head1_fwd<8>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
-        case 32: hipLaunchKernelGGL((k_head1_fwd<32>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
-        case 64: hipLaunchKernelGGL((k_head1_fwd<64>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
-        case 4: hipLaunchKernelGGL((k_head1_fwd<4>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
-        case 2: hipLaunchKernelGGL((k_head1_fwd<2>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
-        case 1: hipLaunchKernelGGL((k_head1_fwd<1>), gr, bl, 0, s, (const uint4*)x, w, bias, P, (bf16*)y); break;
+        case 16: LSS_HEAD1_FWD(16); break;
+        case 8: LSS_HEAD1_FWD(8); break;
+        case 32: LSS_HEAD1_FWD(32); break;
+        case 64: LSS_HEAD1_FWD(64); break;
+        case 4: LSS_HEAD1_FWD(4); break;
+        case 2: LSS_HEAD1_FWD(2); break;
+        case 1: LSS_HEAD1_FWD(1); break;
         default: return LSS_CONV_EINVAL;
     }
+#undef LSS_HEAD1_FWD
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
-
 int lss_head1_bwd(const void* x, const void* dy, const float* w, int32_t P, int32_t C, void* dx, float* partial,
                   void* stream) {
-    if (!x || !dy || !w || !dx || !partial || P <= 0 || C <= 0 || C % 8 != 0 || 64 % (C / 8) != 0)
+    if (!dx) return LSS_CONV_EINVAL;
+    return lss_head1_bwd2(x, dy, w, P, C, nullptr, dx, partial, stream);
+}
+int lss_head1_bwd2(const void* x, const void* dy, const float* w, int32_t P, int32_t C, const float* bn_stats, void* dx,
+                   float* partial, void* stream) {
+    if (!x || !dy || !w || (!dx && !bn_stats) || !partial || P <= 0 || C <= 0 || C % 8 != 0 || 64 % (C / 8) != 0)
         return LSS_CONV_EINVAL;
     const dim3 gr(lss_head1_blocks(P)), bl(kBlock);
     hipStream_t s = (hipStream_t)stream;
 #define LSS_HEAD1_BWD(L)                                                                                          \
-    hipLaunchKernelGGL((k_head1_bwd<L>), gr, bl, 0, s, (const uint4*)x, (const bf16*)dy, w, P, (uint4*)dx, partial)
+    hipLaunchKernelGGL((k_head1_bwd<L>), gr, bl, 0, s, (const uint4*)x, (const bf16*)dy, w, P, (uint4*)dx, partial, \
+                       bn_stats)
     switch (C / 8) {
         case 16: LSS_HEAD1_BWD(16); break;
         case 8: LSS_HEAD1_BWD(8); break;

@@ -38,6 +38,7 @@ from torch import nn
 from . import _lib, ops
 from .efficientnet import EfficientNetB0
 from . import resample
+from . import norm
 from .norm import bn_act
 from .tools import gen_dx_bx
 
@@ -352,6 +353,91 @@ def _head1_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
 
 
 USE_HIP_HEAD1 = True  # BevEncode's last conv (one output channel) on lss_head1_* instead of a hipBLASLt GEMV
+# BevEncode's up2 tail, BN + ReLU + that conv, without the normalised map (_BnReluHead1)
+USE_BN_HEAD = True
+
+
+class _BnReluHead1(torch.autograd.Function):
+    """conv1x1_to_one_channel(relu(bn(x))) for channels-last bf16 maps in training mode (BevEncode.up2[2:5],
+    src/models.py:111-115), the normalised map never written: lss_bn_fwd2 with y = NULL (statistics,
+    running stats), then lss_head1_fwd2 applies scale / shift / ReLU to each value as it reads x (the
+    value the BN apply would have stored); backward: lss_head1_bwd2 (head weight / bias gradients from
+    the recomputed map, no input gradient written) and lss_bn_bwd_rank1 (the BN backward with the head's
+    gradient bf16(dout[p] w[c]) computed in its kernels). The same kernels' arithmetic in the same order
+    as bn_act + _Head1x1: bit-identical outputs and gradients (tests/test_gpu_convs.py). At c3 this
+    skips 82 MB written and 82 MB read in the forward, 82 MB written and 164 MB read in the backward."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
+    def forward(ctx, x, gamma, beta, hw, hb, bn: nn.BatchNorm2d):
+        lib = _lib.load()
+        N, C, H, W = x.shape
+        HW, P = H * W, N * H * W
+        dev = x.device
+        st = _lib.stream_handle(dev)
+        groups = int(lib.lss_bn_groups(N, C, HW, norm.NHWC))
+        f32 = dict(device=dev, dtype=torch.float32)
+        partial = torch.empty(C, groups, 2, **f32)
+        stats = torch.empty(4, C, **f32)  # save_mean, save_rstd, scale, shift
+        momentum, counter, rm, rv = norm.running_args(bn)
+        _lib.check(lib.lss_bn_fwd2(_lib.ptr(x), None, _lib.BF16, norm.NHWC, N, C, HW, _lib.ptr(gamma), _lib.ptr(beta),
+                                   float(bn.eps), float(momentum), _lib.ptr(rm), _lib.ptr(rv), _lib.ptr(counter),
+                                   norm.ACT["relu"], groups, _lib.ptr(partial), _lib.ptr(stats[0]), _lib.ptr(stats[1]),
+                                   _lib.ptr(stats[2]), _lib.ptr(stats[3]), None, None, st), "lss_bn_fwd2")
+        w = hw.detach().to(torch.bfloat16).reshape(C).float()  # the bf16 operands, as _Head1x1 takes them
+        b = hb.detach().to(torch.bfloat16).float().reshape(1) if hb is not None else None
+        y = torch.empty(N, 1, H, W, device=dev, dtype=torch.bfloat16)
+        _lib.check(lib.lss_head1_fwd2(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), P, C, _lib.ptr(stats), _lib.ptr(y), st),
+                   "lss_head1_fwd2")
+        ctx.save_for_backward(x, stats, w)
+        # under autocast the head's operands are its bf16 casts, so its parameter gradients come back
+        # rounded to bf16 (as _Head1x1's, whose inputs autocast casts)
+        cast = torch.is_autocast_enabled("cuda")
+        ctx.meta = (groups, hw.shape, torch.bfloat16 if cast else hw.dtype, hw.dtype,
+                    None if hb is None else (torch.bfloat16 if cast else hb.dtype), None if hb is None else hb.dtype)
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dout):
+        lib = _lib.load()
+        x, stats, w = ctx.saved_tensors
+        groups, wshape, wdtype, wdtype_out, bdtype, bdtype_out = ctx.meta
+        N, C, H, W = x.shape
+        P = N * H * W
+        dev = x.device
+        st = _lib.stream_handle(dev)
+        dout = dout.to(torch.bfloat16).contiguous()
+        part = torch.empty(int(lib.lss_head1_blocks(P)), C + 1, device=dev, dtype=torch.float32)
+        _lib.check(lib.lss_head1_bwd2(_lib.ptr(x), _lib.ptr(dout), _lib.ptr(w), P, C, _lib.ptr(stats), None,
+                                      _lib.ptr(part), st), "lss_head1_bwd2")
+        tot = part.sum(0)
+        dw = tot[:C].reshape(wshape).to(wdtype).to(wdtype_out)
+        db = tot[C:].to(bdtype).to(bdtype_out) if bdtype is not None else None
+        f32 = dict(device=dev, dtype=torch.float32)
+        partial = torch.empty(C, groups, 2, **f32)
+        coef = torch.empty(C, 2, **f32)
+        dgamma = torch.empty(C, **f32)
+        dbeta = torch.empty(C, **f32)
+        dx = torch.empty_like(x)
+        _lib.check(lib.lss_bn_bwd_rank1(_lib.ptr(dout), _lib.ptr(w), _lib.ptr(x), N, C, H * W, _lib.ptr(stats[2]),
+                                        _lib.ptr(stats[3]), _lib.ptr(stats[0]), _lib.ptr(stats[1]), norm.ACT["relu"],
+                                        groups, _lib.ptr(partial), _lib.ptr(coef), _lib.ptr(dgamma), _lib.ptr(dbeta),
+                                        _lib.ptr(dx), st), "lss_bn_bwd_rank1")
+        return dx, dgamma, dbeta, dw, db, None
+
+
+def bn_relu_head1(bn: nn.BatchNorm2d, head: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """head(relu(bn(x))) with head a 1x1 conv to one channel: _BnReluHead1 where eligible (the benched
+    BevEncode: training mode, channels-last bf16 under autocast), else bn_act + conv1x1."""
+    C = x.shape[1] if x.dim() == 4 else 0
+    ok = (USE_BN_HEAD and norm.USE_HIP_BN and USE_HIP_HEAD1 and bn.training and bn.affine and x.is_cuda
+          and x.dim() == 4 and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
+          and head.out_channels == 1 and head.kernel_size == (1, 1) and head.stride == (1, 1) and head.groups == 1
+          and C % 8 == 0 and 64 % (C // 8) == 0 and 256 % (C // 8) == 0 and _head1_eligible(head, x))
+    if not ok:
+        return conv1x1(head, bn_act(bn, x, "relu"))
+    return _BnReluHead1.apply(x, bn.weight, bn.bias, head.weight, head.bias, bn)
 
 
 def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
@@ -424,7 +510,7 @@ class BevEncode(nn.Module):
             x = resample.upsample_cat(x, None, int(u[0].scale_factor))
         else:
             x = u[0](x)
-        return conv1x1(u[4], bn_act(u[2], conv3x3(u[1], x), "relu"))
+        return bn_relu_head1(u[2], u[4], conv3x3(u[1], x))
 
 
 class LiftSplatShoot(nn.Module):

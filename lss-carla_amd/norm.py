@@ -48,6 +48,22 @@ def _layout(x: torch.Tensor) -> Optional[int]:
     return None
 
 
+def running_args(bn: nn.BatchNorm2d):
+    """(momentum, num_batches_tracked counter or None, running_mean, running_var) for lss_bn_fwd*, with
+    PyTorch's update rule (the counter is incremented by the kernel; a cumulative average needs it here)."""
+    momentum = bn.momentum if bn.momentum is not None else 0.0
+    counter = None
+    if bn.track_running_stats and bn.num_batches_tracked is not None:
+        if bn.momentum is None:  # cumulative moving average: the factor needs the count on the host
+            bn.num_batches_tracked.add_(1)
+            momentum = 1.0 / float(bn.num_batches_tracked.item())
+        else:
+            counter = bn.num_batches_tracked
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    return momentum, counter, rm, rv
+
+
 class _BnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, bn: nn.BatchNorm2d, act: int, layout: int):
@@ -65,16 +81,7 @@ class _BnAct(torch.autograd.Function):
         f32 = dict(device=dev, dtype=torch.float32)
         partial = torch.empty(C, groups, 2, **f32)
         stats = torch.empty(4, C, **f32)  # save_mean, save_rstd, scale, shift
-        momentum = bn.momentum if bn.momentum is not None else 0.0
-        counter = None  # num_batches_tracked: incremented by the kernel
-        if bn.track_running_stats and bn.num_batches_tracked is not None:
-            if bn.momentum is None:  # cumulative moving average: the factor needs the count on the host
-                bn.num_batches_tracked.add_(1)
-                momentum = 1.0 / float(bn.num_batches_tracked.item())
-            else:
-                counter = bn.num_batches_tracked
-        rm = bn.running_mean if bn.track_running_stats else None
-        rv = bn.running_var if bn.track_running_stats else None
+        momentum, counter, rm, rv = running_args(bn)
         _lib.check(lib.lss_bn_fwd2(_lib.ptr(x), _lib.ptr(residual), _lib.dtype_code(x.dtype), layout, N, C, HW,
                                    _lib.ptr(weight), _lib.ptr(bias), float(bn.eps), float(momentum), _lib.ptr(rm),
                                    _lib.ptr(rv), _lib.ptr(counter), act, groups, _lib.ptr(partial),

@@ -466,3 +466,39 @@ def test_bn_cluster_kernels_bit_identical(N, C, H, W, act, with_res, spin):
     for a, b in zip(got, want):
         assert torch.equal(a, b)
     assert int(Nm._sync(DEV)[:-1].abs().sum()) == 0, "cluster counters not re-zeroed"
+
+
+# ----------------------------------------------------------------------------- BevEncode up2 tail
+@pytest.mark.parametrize("shape", [(2, 128, 64, 64), (1, 64, 30, 50)])
+def test_bn_relu_head1_fused_bit_identical(shape):
+    """models._BnReluHead1 (BN statistics only, the head applying scale / shift / ReLU as it reads, the BN
+    backward taking the head's rank-1 gradient) == bn_act + _Head1x1 bit for bit: the output, d(x), the BN
+    weight / bias gradients, the head weight / bias gradients and the running statistics."""
+    import copy
+    from lss_carla_amd import models as M
+    N, C, H, W = shape
+    torch.manual_seed(C + H)
+    bn = torch.nn.BatchNorm2d(C).to(DEV).train()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C) + 0.5)
+        bn.bias.copy_(torch.randn(C) * 0.2)
+    head = torch.nn.Conv2d(C, 1, 1).to(DEV).to(memory_format=torch.channels_last)
+    x = (torch.randn(N, C, H, W, device=DEV) + 0.2).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dout = torch.randn(N, 1, H, W, device=DEV).to(torch.bfloat16)
+    res = []
+    for fused in (True, False):
+        b, h = copy.deepcopy(bn), copy.deepcopy(head)
+        xi = x.clone().requires_grad_(True)
+        M.USE_BN_HEAD = fused
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = M.bn_relu_head1(b, h, xi)
+        finally:
+            M.USE_BN_HEAD = True
+        out.backward(dout)
+        torch.cuda.synchronize()
+        res.append((out.detach(), xi.grad, b.weight.grad, b.bias.grad, h.weight.grad, h.bias.grad,
+                    b.running_mean, b.running_var, b.num_batches_tracked))
+    for a, c in zip(*res):
+        assert torch.equal(a, c)
+    assert int(res[0][-1]) == 1
