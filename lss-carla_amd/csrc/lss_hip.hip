@@ -2266,7 +2266,7 @@ __global__ __launch_bounds__(kBlock) void k_splat_bwd_reg(const GT* __restrict__
 
 // k_splat_bwd_tile shape for bf16 gradient rows, D <= 48 (experiment switches for build_variant)
 #ifndef LSS_BWD_WAVES
-#define LSS_BWD_WAVES 8
+#define LSS_BWD_WAVES 4  // round 6: 4 pixels per block, 8.6 vs 9.0-9.2 us in-step (profiles/r06/splat_bwd_shape_ab.txt)
 #endif
 #ifndef LSS_BWD_PPW
 #define LSS_BWD_PPW 1
@@ -2288,7 +2288,10 @@ constexpr int kBwdBigWaves = LSS_BWD_WAVES, kBwdBigPpw = LSS_BWD_PPW, kBwdBigMin
 // and leaves d_logits / d_ctx in an LDS tile that the block writes channel by channel in runs of RUN
 // consecutive pixels of one image.
 //
-// Tile shape: 8 waves x 1 pixel (the product). A one-round shape -- 4 waves x 3 pixels, all of c3's
+// Tile shape: 4 waves x 1 pixel (the product since round 6: with 71 VGPRs a CU holds 7 such blocks, 28
+// waves, where it held 3 blocks of 8 -- 24 waves: in-step 8.60 / 8.64 vs 8.96-9.21 us on the same boxes;
+// 4 x 1 at 6 or 8 waves per SIMD: 8.69 / 12.3 us, the VGPR cap spills; profiles/r06/splat_bwd_shape_ab.txt).
+// Before: 8 waves x 1 pixel. A one-round shape -- 4 waves x 3 pixels, all of c3's
 // 8,448 pixels resident at once (704 blocks for 768 slots) where 8 x 1 needs 1,056 blocks for 768
 // -- measured no faster (in-step 9.7 vs 9.5 us with the DPP reductions, 11.8 vs 11.7 before them;
 // profiles/r05/prof_ab_bwd_*): the per-pixel reduction, not the block rounds, was the long phase.
