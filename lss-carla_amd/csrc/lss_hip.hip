@@ -1277,6 +1277,10 @@ __global__ __launch_bounds__(kDn2Block) void k_depthnet_lift2(const bf16* __rest
 // plain 16-B LDS reads. Rows past the tile's pixel count are clamped copies of its last row and only
 // feed output columns that are never written. A fragments and epilogue (bias, bf16 rounding, softmax,
 // context rows) as k_depthnet_lift2; identical results.
+#ifndef LSS_DN3_BPC
+#define LSS_DN3_BPC 1  // experiments: lift blocks per CU (2 -- 512 blocks of ~17 pixels at c3, two resident per
+                       // CU -- measured 11.0 vs 8.9 us in-step, profiles/r06/lift_blocks_per_cu_ab.txt)
+#endif
 constexpr int kDn3Waves = 8;             // 8 x 16 = 128 output rows >= D + C
 constexpr int kDn3Block = kDn3Waves * kWave;
 constexpr int kDn3MaxPix = 48;           // pixels per block at most: three 16-column MFMA tiles
@@ -1314,7 +1318,7 @@ __global__ __launch_bounds__(kBlock) void k_depthnet_pack(const WT* __restrict__
 // the compiler budgets 128 (the 4 waves per SIMD two blocks' LDS would allow) and kept the feature
 // loads in scratch: stores behind vmcnt waits, reloads behind a vmcnt(0) -- the stage serialised.
 template <int K, bool PACKED>
-__global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_depthnet_lift3(const bf16* __restrict__ feat,
+__global__ __launch_bounds__(kDn3Block) __attribute__((amdgpu_waves_per_eu(1, 2 * LSS_DN3_BPC))) void k_depthnet_lift3(const bf16* __restrict__ feat,
                                                               const bf16* __restrict__ weight,
                                                               const bf16* __restrict__ bias, int D, int HW,
                                                               int npix, int nlift, float* __restrict__ depth,
@@ -2933,7 +2937,8 @@ static int depthnet_lift_nhwc(const void* feat, const void* weight, bool packed,
     if (npix >= INT_MAX / 2) return LSS_EUNSUPPORTED;
     // one block per CU, more only when a CU's share would pass kDn3MaxPix pixels; never more than
     // the pixels (every block holds at least one)
-    const long nlift = std::min<long>(npix, std::max<long>(device_cus(), (npix + kDn3MaxPix - 1) / kDn3MaxPix));
+    const long nlift = std::min<long>(npix, std::max<long>((long)LSS_DN3_BPC * device_cus(),
+                                                           (npix + kDn3MaxPix - 1) / kDn3MaxPix));
     hipStream_t s = (hipStream_t)stream;
     if (packed)
         hipLaunchKernelGGL((k_depthnet_lift3<512, true>), dim3(xcd_grid(nlift)), dim3(kDn3Block), 0, s, (const bf16*)feat,
