@@ -211,6 +211,13 @@ int lss_upsample_cat_fwd(const void* x, const void* skip, int32_t N, int32_t Hi,
  * fp32, fixed order), no atomics. The skip's gradient is dy's first C2 channels (a view). */
 int lss_upsample_bwd(const void* dy, int32_t N, int32_t Hi, int32_t Wi, int32_t C1, int32_t C2, int32_t Ho,
                      int32_t Wo, void* dx, void* stream);
+/* (ABI 23) The same with chan_scale (nullable, N x C1 fp32): x's channel c of image n scaled by
+ * chan_scale[n C1 + c] after the interpolation, and the input gradient by the same factor -- BevEncode's
+ * Dropout2d (src/models.py:110: a per-(image, channel) 0 or 1 / (1 - p)) folded into up2's upsample. */
+int lss_upsample_cat_fwd2(const void* x, const void* skip, int32_t N, int32_t Hi, int32_t Wi, int32_t C1, int32_t C2,
+                          int32_t Ho, int32_t Wo, const float* chan_scale, void* y, void* stream);
+int lss_upsample_bwd2(const void* dy, int32_t N, int32_t Hi, int32_t Wi, int32_t C1, int32_t C2, int32_t Ho,
+                      int32_t Wo, const float* chan_scale, void* dx, void* stream);
 
 /* Squeeze-and-excitation of an MBConv block (efficientnet_pytorch MBConvBlock, used by CamEncode's
  * trunk, src/models.py:43): y = x * sigmoid(W2 swish(W1 mean_hw(x) + b1) + b2), x / y (N, C, HW)

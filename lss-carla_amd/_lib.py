@@ -120,6 +120,8 @@ SIGNATURES = {
                                    _p, _p, _p, _p, _p, _p]),
     "lss_upsample_cat_fwd": (ctypes.c_int, [_p, _p] + [_i32] * 7 + [_p, _p]),
     "lss_upsample_bwd": (ctypes.c_int, [_p] + [_i32] * 7 + [_p, _p]),
+    "lss_upsample_cat_fwd2": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p, _p]),
+    "lss_upsample_bwd2": (ctypes.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p, _p]),
     "lss_se_fwd": (ctypes.c_int, [_p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p, _p]),
     "lss_se_bwd": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "lss_se_wgrad": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),

@@ -82,8 +82,10 @@ __device__ __forceinline__ float line_weight(float r, int o, int in, int i) {
     return w;
 }
 
+// cs (nullable): a per-(image, channel) scale of x's channels (N x C1 fp32): BevEncode's Dropout2d mask
+// (src/models.py:110), applied to the interpolated values (and to the input gradient in the backward)
 __global__ __launch_bounds__(kBlock) void k_up_cat_fwd(const u32x4* __restrict__ x, const u32x4* __restrict__ skip,
-                                                       UpGeo g, u32x4* __restrict__ y) {
+                                                       UpGeo g, u32x4* __restrict__ y, const float* __restrict__ cs) {
     const int c8s = g.C2 >> 3, c81 = g.C1 >> 3, c8t = c8s + c81;
     const int total = g.N * g.Ho * g.Wo * c8t;
     const int t = blockIdx.x * kBlock + threadIdx.x;
@@ -109,6 +111,11 @@ __global__ __launch_bounds__(kBlock) void k_up_cat_fwd(const u32x4* __restrict__
     unpack8(xb[(r1 + w.i0 + w.ip) * c81], d);
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = h0l * (w0l * a[k] + w1l * b[k]) + h1l * (w0l * c[k] + w1l * d[k]);
+    if (cs) {
+        const float* m = cs + (size_t)n * g.C1 + (c8 - c8s) * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] *= m[k];
+    }
     y[t] = pack8(o);
 }
 
@@ -139,7 +146,15 @@ __device__ __forceinline__ void up_bwd_sum(const u32x4* __restrict__ db, const U
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_up_bwd(const u32x4* __restrict__ dy, UpGeo g, u32x4* __restrict__ dx) {
+__device__ __forceinline__ void up_scale(const float* __restrict__ cs, const UpGeo& g, int n, int c8, float acc[8]) {
+    if (!cs) return;
+    const float* m = cs + (size_t)n * g.C1 + c8 * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] *= m[k];
+}
+
+__global__ __launch_bounds__(kBlock) void k_up_bwd(const u32x4* __restrict__ dy, UpGeo g, u32x4* __restrict__ dx,
+                                                   const float* __restrict__ cs) {
     const int c8s = g.C2 >> 3, c81 = g.C1 >> 3, c8t = c8s + c81;
     const int total = g.N * g.Hi * g.Wi * c81;
     const int t = blockIdx.x * kBlock + threadIdx.x;
@@ -155,6 +170,7 @@ __global__ __launch_bounds__(kBlock) void k_up_bwd(const u32x4* __restrict__ dy,
     out_range(g.rw, j, g.Wo, ow0, ow1);
     float acc[8];
     up_bwd_sum(dy + (n * g.Ho * g.Wo) * c8t + c8s + c8, g, i, j, oh0, oh1, ow0, ow1, c8t, acc);
+    up_scale(cs, g, n, c8, acc);
     dx[t] = pack8(acc);
 }
 
@@ -167,7 +183,8 @@ __global__ __launch_bounds__(kBlock) void k_up_bwd(const u32x4* __restrict__ dy,
 #define LSS_UP_BWD_V2 1
 #endif
 template <int T>
-__global__ __launch_bounds__(kBlock) void k_up_bwd_taps(const u32x4* __restrict__ dy, UpGeo g, u32x4* __restrict__ dx) {
+__global__ __launch_bounds__(kBlock) void k_up_bwd_taps(const u32x4* __restrict__ dy, UpGeo g, u32x4* __restrict__ dx,
+                                                        const float* __restrict__ cs) {
     const int c8s = g.C2 >> 3, c81 = g.C1 >> 3, c8t = c8s + c81;
     const int total = g.N * g.Hi * g.Wi * c81;
     const int t = blockIdx.x * kBlock + threadIdx.x;
@@ -213,6 +230,7 @@ __global__ __launch_bounds__(kBlock) void k_up_bwd_taps(const u32x4* __restrict_
         // more nonzero lines than the host's bound allowed for (float rounding of r * o): the plain
         // loop, same terms in the same order -- never a dropped tap
         up_bwd_sum(db, g, i, j, oh0, oh1, ow0, ow1, c8t, acc);
+        up_scale(cs, g, n, c8, acc);
         dx[t] = pack8(acc);
         return;
     }
@@ -238,6 +256,7 @@ __global__ __launch_bounds__(kBlock) void k_up_bwd_taps(const u32x4* __restrict_
             }
         }
     }
+    up_scale(cs, g, n, c8, acc);
     dx[t] = pack8(acc);
 }
 
@@ -269,17 +288,27 @@ extern "C" {
 
 int lss_upsample_cat_fwd(const void* x, const void* skip, int32_t N, int32_t Hi, int32_t Wi, int32_t C1, int32_t C2,
                          int32_t Ho, int32_t Wo, void* y, void* stream) {
+    return lss_upsample_cat_fwd2(x, skip, N, Hi, Wi, C1, C2, Ho, Wo, nullptr, y, stream);
+}
+
+int lss_upsample_cat_fwd2(const void* x, const void* skip, int32_t N, int32_t Hi, int32_t Wi, int32_t C1, int32_t C2,
+                          int32_t Ho, int32_t Wo, const float* chan_scale, void* y, void* stream) {
     if (!x || !y || !up_ok(N, Hi, Wi, C1, C2, Ho, Wo) || (C2 > 0 && !skip)) return LSS_CONV_EINVAL;
     if (!aligned16(x) || !aligned16(y) || (C2 > 0 && !aligned16(skip))) return LSS_CONV_EINVAL;
     const UpGeo g = make_geo(N, Hi, Wi, C1, C2, Ho, Wo);
     const int total = N * Ho * Wo * ((C1 + C2) / 8);
     hipLaunchKernelGGL(k_up_cat_fwd, dim3((total + kBlock - 1) / kBlock), dim3(kBlock), 0, (hipStream_t)stream,
-                       (const u32x4*)x, (const u32x4*)skip, g, (u32x4*)y);
+                       (const u32x4*)x, (const u32x4*)skip, g, (u32x4*)y, chan_scale);
     return launch_status();
 }
 
 int lss_upsample_bwd(const void* dy, int32_t N, int32_t Hi, int32_t Wi, int32_t C1, int32_t C2, int32_t Ho,
                      int32_t Wo, void* dx, void* stream) {
+    return lss_upsample_bwd2(dy, N, Hi, Wi, C1, C2, Ho, Wo, nullptr, dx, stream);
+}
+
+int lss_upsample_bwd2(const void* dy, int32_t N, int32_t Hi, int32_t Wi, int32_t C1, int32_t C2, int32_t Ho,
+                      int32_t Wo, const float* chan_scale, void* dx, void* stream) {
     if (!dy || !dx || !up_ok(N, Hi, Wi, C1, C2, Ho, Wo) || !aligned16(dy) || !aligned16(dx)) return LSS_CONV_EINVAL;
     const UpGeo g = make_geo(N, Hi, Wi, C1, C2, Ho, Wo);
     const int total = N * Hi * Wi * (C1 / 8);
@@ -288,13 +317,13 @@ int lss_upsample_bwd(const void* dy, int32_t N, int32_t Hi, int32_t Wi, int32_t 
     const dim3 gr((total + kBlock - 1) / kBlock), bl(kBlock);
     if (LSS_UP_BWD_V2 && need <= 6)
         hipLaunchKernelGGL(k_up_bwd_taps<6>, gr, bl, 0, (hipStream_t)stream,
-                       (const u32x4*)dy, g, (u32x4*)dx);
+                       (const u32x4*)dy, g, (u32x4*)dx, chan_scale);
     else if (LSS_UP_BWD_V2 && need <= 10)
         hipLaunchKernelGGL(k_up_bwd_taps<10>, gr, bl, 0, (hipStream_t)stream,
-                       (const u32x4*)dy, g, (u32x4*)dx);
+                       (const u32x4*)dy, g, (u32x4*)dx, chan_scale);
     else
         hipLaunchKernelGGL(k_up_bwd, gr, bl, 0, (hipStream_t)stream,
-                       (const u32x4*)dy, g, (u32x4*)dx);
+                       (const u32x4*)dy, g, (u32x4*)dx, chan_scale);
     return launch_status();
 }
 

@@ -462,6 +462,18 @@ def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     return y.permute(0, 3, 1, 2)  # (N, O, H, W), channels-last strides
 
 
+def _dropout2d_scale(d: nn.Dropout2d, x: torch.Tensor):
+    """The (N, C) factor nn.Dropout2d multiplies x by (0 or 1 / (1 - p) per image and channel, drawn the
+    way torch's feature dropout draws it: bernoulli_(1 - p) then div_(1 - p) in x's dtype), or None when
+    it is the identity (eval, p = 0)."""
+    if not d.training or d.p == 0:
+        return None
+    if d.p == 1:
+        return torch.zeros(x.shape[0], x.shape[1], device=x.device)
+    noise = torch.empty(x.shape[0], x.shape[1], device=x.device, dtype=x.dtype)
+    return noise.bernoulli_(1 - d.p).div_(1 - d.p).float()
+
+
 class BevEncode(nn.Module):
     """ResNet-18 stem + layer1-3 + two Up stages (src/models.py:92-130).
 
@@ -504,12 +516,14 @@ class BevEncode(nn.Module):
         x = bn_act(self.bn1, self.conv1(x), "relu")
         x1 = self.layer1(x)
         x = self.layer3(self.layer2(x1))
-        x = self.dropout(self.up1(x, x1))
+        x = self.up1(x, x1)
         u = self.up2  # Upsample, conv, BN, ReLU, conv
         if resample.USE_HIP_UPSAMPLE and resample._eligible(x):
-            x = resample.upsample_cat(x, None, int(u[0].scale_factor))
+            # Dropout2d folded into the upsample: its (N, C) mask scales the interpolated channels (and
+            # the gradient) inside lss_upsample_cat_fwd2 / lss_upsample_bwd2, not as two passes over x
+            x = resample.upsample_cat(x, None, int(u[0].scale_factor), _dropout2d_scale(self.dropout, x))
         else:
-            x = u[0](x)
+            x = u[0](self.dropout(x))
         return bn_relu_head1(u[2], u[4], conv3x3(u[1], x))
 
 

@@ -27,15 +27,17 @@ def _eligible(t: Optional[torch.Tensor]) -> bool:
 
 class _UpsampleCat(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, skip, Ho: int, Wo: int):
+    def forward(ctx, x, skip, Ho: int, Wo: int, chan_scale=None):
         lib = _lib.load()
         N, C1, Hi, Wi = x.shape
         C2 = skip.shape[1] if skip is not None else 0
         y = torch.empty(N, C2 + C1, Ho, Wo, device=x.device, dtype=torch.bfloat16,
                         memory_format=torch.channels_last)
-        _lib.check(lib.lss_upsample_cat_fwd(_lib.ptr(x), _lib.ptr(skip), N, Hi, Wi, C1, C2, Ho, Wo, _lib.ptr(y),
-                                            _lib.stream_handle(x.device)), "lss_upsample_cat_fwd")
+        _lib.check(lib.lss_upsample_cat_fwd2(_lib.ptr(x), _lib.ptr(skip), N, Hi, Wi, C1, C2, Ho, Wo,
+                                             _lib.ptr(chan_scale), _lib.ptr(y), _lib.stream_handle(x.device)),
+                   "lss_upsample_cat_fwd2")
         ctx.geo = (N, Hi, Wi, C1, C2, Ho, Wo)
+        ctx.save_for_backward(chan_scale)
         return y
 
     @staticmethod
@@ -44,17 +46,24 @@ class _UpsampleCat(torch.autograd.Function):
         N, Hi, Wi, C1, C2, Ho, Wo = ctx.geo
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = torch.empty(N, C1, Hi, Wi, device=dy.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
-        _lib.check(lib.lss_upsample_bwd(_lib.ptr(dy), N, Hi, Wi, C1, C2, Ho, Wo, _lib.ptr(dx),
-                                        _lib.stream_handle(dy.device)), "lss_upsample_bwd")
+        (chan_scale,) = ctx.saved_tensors
+        _lib.check(lib.lss_upsample_bwd2(_lib.ptr(dy), N, Hi, Wi, C1, C2, Ho, Wo, _lib.ptr(chan_scale), _lib.ptr(dx),
+                                         _lib.stream_handle(dy.device)), "lss_upsample_bwd2")
         dskip = dy[:, :C2] if C2 else None
-        return dx, dskip, None, None
+        return dx, dskip, None, None, None
 
 
-def upsample_cat(x: torch.Tensor, skip: Optional[torch.Tensor], scale_factor: int) -> torch.Tensor:
-    """cat([skip, bilinear_upsample(x, scale_factor, align_corners=True)], dim=1); skip may be None."""
+def upsample_cat(x: torch.Tensor, skip: Optional[torch.Tensor], scale_factor: int,
+                 chan_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """cat([skip, bilinear_upsample(x * chan_scale, scale_factor, align_corners=True)], dim=1); skip and
+    chan_scale (an (N, C) per-channel factor: a Dropout2d mask) may be None."""
     Ho, Wo = x.shape[2] * scale_factor, x.shape[3] * scale_factor
+    if chan_scale is not None:
+        chan_scale = chan_scale.reshape(x.shape[0], x.shape[1]).float().contiguous()
     if (USE_HIP_UPSAMPLE and _eligible(x) and _eligible(skip) and x.shape[2] > 1 and x.shape[3] > 1
             and (skip is None or (skip.shape[0] == x.shape[0] and tuple(skip.shape[2:]) == (Ho, Wo)))):
-        return _UpsampleCat.apply(x, skip, Ho, Wo)
+        return _UpsampleCat.apply(x, skip, Ho, Wo, chan_scale)
+    if chan_scale is not None:
+        x = x * chan_scale.view(x.shape[0], x.shape[1], 1, 1).to(x.dtype)
     up = F.interpolate(x, scale_factor=scale_factor, mode="bilinear", align_corners=True)
     return up if skip is None else torch.cat([skip, up], dim=1)

@@ -502,3 +502,43 @@ def test_bn_relu_head1_fused_bit_identical(shape):
     for a, c in zip(*res):
         assert torch.equal(a, c)
     assert int(res[0][-1]) == 1
+
+
+# ----------------------------------------------------------------------------- Dropout2d in the upsample
+@pytest.mark.parametrize("N,C,H,W,s", [(2, 256, 25, 25, 2), (3, 64, 10, 13, 4)])
+def test_upsample_channel_scale_vs_fp64(N, C, H, W, s):
+    """upsample_cat(x, None, s, chan_scale=m) == bilinear_upsample(x * m) (fp64 of the same bf16 values,
+    one bf16 rounding), and d(x) = m * upsample_bwd(dy); m a Dropout2d mask with zeroed channels."""
+    g = torch.Generator().manual_seed(N + C + H)
+    cl = torch.channels_last
+    x = torch.randn(N, C, H, W, generator=g).bfloat16()
+    m = (torch.rand(N, C, generator=g) > 0.3).float() * (1 / 0.7)
+    xd = x.to(DEV).contiguous(memory_format=cl).requires_grad_(True)
+    y = R.upsample_cat(xd, None, s, m.to(DEV))
+    xr = x.double().requires_grad_(True)
+    ref = F.interpolate(xr * m.double().view(N, C, 1, 1), scale_factor=s, mode="bilinear", align_corners=True)
+    torch.testing.assert_close(y.detach().cpu().double(), ref.detach(), rtol=8e-3, atol=8e-3)
+    zero = m == 0
+    assert (y.detach().cpu()[zero] == 0).all()  # dropped channels exactly zero
+    dy = torch.randn(y.shape, generator=g).bfloat16()
+    y.backward(dy.to(DEV).contiguous(memory_format=cl))
+    ref.backward(dy.double())
+    torch.testing.assert_close(xd.grad.cpu().double(), xr.grad, rtol=1e-2, atol=2e-2)
+    assert (xd.grad.cpu()[zero] == 0).all()
+
+
+def test_bevencode_dropout2d_mask_matches_torch():
+    """models._dropout2d_scale draws the mask torch's Dropout2d draws (same generator calls, same dtype):
+    with the same seed, x * mask == F.dropout2d(x) bit for bit; eval and p = 0 give None."""
+    from lss_carla_amd import models as M
+    d = torch.nn.Dropout2d(0.1).train()
+    x = torch.randn(8, 256, 4, 4, device=DEV).bfloat16()
+    torch.manual_seed(5)
+    m = M._dropout2d_scale(d, x)
+    torch.manual_seed(5)
+    ref = F.dropout2d(x, 0.1, True)
+    got = x * m.view(8, 256, 1, 1).to(x.dtype)
+    assert torch.equal(got, ref)
+    assert 0 < int((m == 0).sum()) < m.numel()
+    assert M._dropout2d_scale(d.eval(), x) is None
+    assert M._dropout2d_scale(torch.nn.Dropout2d(0.0).train(), x) is None
