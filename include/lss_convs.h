@@ -40,6 +40,12 @@ int lss_dwconv_bwd_data(const void* dy, int32_t dtype, const float* w, int32_t N
 int lss_dwconv_bwd_weight(const void* x, const void* dy, int32_t dtype, int32_t N, int32_t C, int32_t Hi, int32_t Wi,
                           int32_t K, int32_t stride, int32_t pad_top, int32_t pad_left, int32_t Ho, int32_t Wo,
                           int32_t ngroups, float* partial, void* stream);
+/* (ABI 23) lss_dwconv_bwd_weight that also folds the partials: the last of each channel's ngroups blocks
+ * to finish sums them in group order into dw (C, K*K) fp32 -- no separate reduction launch. sync: the
+ * batch-norm sync workspace (lss_bn_sync_words int32, zero-filled; left zero-filled), C <= 4096. */
+int lss_dwconv_bwd_weight2(const void* x, const void* dy, int32_t dtype, int32_t N, int32_t C, int32_t Hi,
+                           int32_t Wi, int32_t K, int32_t stride, int32_t pad_top, int32_t pad_left, int32_t Ho,
+                           int32_t Wo, int32_t ngroups, float* partial, uint32_t* sync, float* dw, void* stream);
 
 /* 1x1 convolution to one output channel (BevEncode's last conv, up2.4: 128 -> outC = 1,
  * src/models.py:115) over channels-last bf16 rows x (P, C), C % 8 == 0 and 64 % (C / 8) == 0:

@@ -88,6 +88,7 @@ SIGNATURES = {
     "lss_dwconv_fwd": (ctypes.c_int, [_p, _i32, _p] + [_i32] * 10 + [_p, _p]),
     "lss_dwconv_bwd_data": (ctypes.c_int, [_p, _i32, _p] + [_i32] * 10 + [_p, _p]),
     "lss_dwconv_bwd_weight": (ctypes.c_int, [_p, _p, _i32] + [_i32] * 11 + [_p, _p]),
+    "lss_dwconv_bwd_weight2": (ctypes.c_int, [_p, _p] + [_i32] * 12 + [_p, _p, _p, _p]),
     "lss_head1_blocks": (ctypes.c_int, [_i32]),
     "lss_head1_fwd": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _p]),
     "lss_head1_bwd": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _p, _p]),

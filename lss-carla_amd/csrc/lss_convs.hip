@@ -187,13 +187,53 @@ __global__ __launch_bounds__(kBlock) void k_dw_bwd_data_s2(const T* __restrict__
     });
 }
 
+// Weight-gradient fold (optional, DwFold.sync != NULL): the ngroups partials of a channel are summed by the
+// LAST of its blocks to finish, in group order, into dw[c][tap] -- the separate fold launch (a torch sum,
+// 5-8 us at c3) is gone. Hand-off as the batch-norm cluster kernels': the partials written through with
+// agent-scope stores and retired (vmcnt counts stores) before the agent-scope counter add; the last block
+// reads them with agent-scope loads and re-zeroes the counter. Nothing waits, so nothing can stall. The
+// counter of channel c is word c * kDwSyncStride + 2 of the batch-norm sync workspace (lss_bn_sync_words:
+// zero-filled, left zero-filled by every user; words 0 and 1 of a channel's line are the BN clusters').
+struct DwFold {
+    unsigned* sync;
+    float* dw;
+};
+constexpr int kDwSyncStride = 32;
+constexpr int kDwSyncMaxC = 4096;
+__device__ __forceinline__ void dw_finish(float* __restrict__ partial, int c, int q, int ngroups, int KK, float v,
+                                          const DwFold& f) {
+    const int t = threadIdx.x;
+    const size_t base = (size_t)c * ngroups * KK;
+    if (!f.sync) {
+        if (t < KK) partial[base + (size_t)q * KK + t] = v;
+        return;
+    }
+    if (t >= kWave) return;  // wave 0 (KK <= 25 lanes hold the block's values)
+    unsigned* pu = reinterpret_cast<unsigned*>(partial);
+    if (t < KK) __hip_atomic_store(pu + base + (size_t)q * KK + t, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's partial stores retired
+    unsigned* ctr = f.sync + (size_t)c * kDwSyncStride + 2;
+    int last = 0;
+    if (t == 0) last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)ngroups - 1u;
+    last = __shfl(last, 0, kWave);
+    if (!last) return;
+    if (t < KK) {
+        float a = 0.f;
+        for (int qq = 0; qq < ngroups; ++qq)
+            a += __uint_as_float(__hip_atomic_load(pu + base + (size_t)qq * KK + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        f.dw[(size_t)c * KK + t] = a;
+    }
+    if (t == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Backward-weight partials: block (group q, channel c) sums, over images n in its group and every
 // output element, dy[n][c][oh][ow] * x[n][c][oh*S - pt + kh][ow*S - pl + kw] for each tap; a thread
 // takes TH x TW output tiles of the group's flat (image, tile) space.
 // partial[(c * ngroups + q) * K*K + tap]; fixed reduction order (wave shuffles, then waves in order).
 template <int K, int S, int TH, int TW, typename T>
 __global__ __launch_bounds__(kBlock) void k_dw_bwd_weight(const T* __restrict__ x, const T* __restrict__ dy, DwGeo g,
-                                                          int nimg, int ngroups, float* __restrict__ partial) {
+                                                          int nimg, int ngroups, float* __restrict__ partial,
+                                                          DwFold fold) {
     __shared__ float s_red[kBlock / kWave][K * K];
     const int c = blockIdx.x % g.C, q = blockIdx.x / g.C;
     const int n0 = (int)((long)nimg * q / ngroups), n1 = (int)((long)nimg * (q + 1) / ngroups);
@@ -251,12 +291,12 @@ __global__ __launch_bounds__(kBlock) void k_dw_bwd_weight(const T* __restrict__ 
         if (lane == 0) s_red[wave][i] = v;
     }
     __syncthreads();
+    float s = 0.f;
     if (threadIdx.x < K * K) {
-        float s = 0.f;
 #pragma unroll
         for (int jw = 0; jw < kBlock / kWave; ++jw) s += s_red[jw][threadIdx.x];
-        partial[((size_t)c * ngroups + q) * K * K + threadIdx.x] = s;
     }
+    dw_finish(partial, c, q, ngroups, K * K, s, fold);
 }
 
 inline int blocks_for(long n) { return (int)((n + kBlock - 1) / kBlock); }
@@ -582,7 +622,8 @@ __global__ __launch_bounds__(kBlock) void k_dw_fwd_lds(const T* __restrict__ x, 
 // weight-gradient partials: block (channel c, image group q), PB images of the group staged at a time
 template <int K, int S, int SEG, typename T>
 __global__ __launch_bounds__(kBlock) void k_dw_wgt_lds(const T* __restrict__ x, const T* __restrict__ dy, DwGeo g,
-                                                       int nimg, int ngroups, DwBand bd, float* __restrict__ partial) {
+                                                       int nimg, int ngroups, DwBand bd, float* __restrict__ partial,
+                                                       DwFold fold) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int TH = kDwTH, TR = (TH - 1) * S + K;
     float* s_x = smem;  // [PB][LHmax][LW]
@@ -648,12 +689,12 @@ __global__ __launch_bounds__(kBlock) void k_dw_wgt_lds(const T* __restrict__ x, 
         if (lane == 0) s_red[wave][i] = v;
     }
     __syncthreads();
+    float t = 0.f;
     if (threadIdx.x < K * K) {
-        float t = 0.f;
 #pragma unroll
         for (int jw = 0; jw < kBlock / kWave; ++jw) t += s_red[jw][threadIdx.x];
-        partial[((size_t)c * ngroups + q) * K * K + threadIdx.x] = t;
     }
+    dw_finish(partial, c, q, ngroups, K * K, t, fold);
 }
 
 // bands and planes per block for the LDS kernels: the whole plane when it fits, several planes per
@@ -753,12 +794,13 @@ int dw_fwd_lds(const void* x, const float* w, DwGeo g, int flip, void* y, hipStr
 }
 
 template <int K, int S, typename T>
-int dw_wgt_lds(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, hipStream_t s) {
+int dw_wgt_lds(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, DwFold fold,
+               hipStream_t s) {
     const int seg = dw_seg(g.Wo);
     const DwBand b = dw_band<K, S>(g, seg, (nimg + ngroups - 1) / ngroups, dw_tile_map(K, S, false));
     const size_t lds = sizeof(float) * ((size_t)b.PB * b.LHmax * b.LW);
 #define LSS_DW_WGT(SG) hipLaunchKernelGGL((k_dw_wgt_lds<K, S, SG, T>), dim3(g.C * ngroups), dim3(kBlock), lds, s, \
-                                          (const T*)x, (const T*)dy, g, nimg, ngroups, b, partial)
+                                          (const T*)x, (const T*)dy, g, nimg, ngroups, b, partial, fold)
     switch (seg) {
         case 8: LSS_DW_WGT(8); break;
         case 4: LSS_DW_WGT(4); break;
@@ -932,7 +974,8 @@ __global__ __launch_bounds__(kBlock) void k_dw_fwd_planes(const T* __restrict__ 
 // shuffles, then waves in order)
 template <int K, int S, int WO, typename T>
 __global__ __launch_bounds__(kBlock) void k_dw_wgt_planes(const T* __restrict__ x, const T* __restrict__ dy, DwGeo g,
-                                                          int nimg, int ngroups, int PB, float* __restrict__ partial) {
+                                                          int nimg, int ngroups, int PB, float* __restrict__ partial,
+                                                          DwFold fold) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     __shared__ float s_red[kBlock / kWave][K * K];
     using PG = PlaneGeo<K, S, WO>;
@@ -989,12 +1032,12 @@ __global__ __launch_bounds__(kBlock) void k_dw_wgt_planes(const T* __restrict__ 
         if (lane == 0) s_red[wave][i] = v;
     }
     __syncthreads();
+    float t = 0.f;
     if (threadIdx.x < K * K) {
-        float t = 0.f;
 #pragma unroll
         for (int jw = 0; jw < kBlock / kWave; ++jw) t += s_red[jw][threadIdx.x];
-        partial[((size_t)c * ngroups + q) * K * K + threadIdx.x] = t;
     }
+    dw_finish(partial, c, q, ngroups, K * K, t, fold);
 }
 
 #ifndef LSS_DW_PLANES
@@ -1038,7 +1081,8 @@ int dw_fwd_planes(const void* x, const float* w, DwGeo g, int flip, void* y, hip
 }
 
 template <int K, int S, typename T>
-int dw_wgt_planes(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, hipStream_t s) {
+int dw_wgt_planes(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, DwFold fold,
+                  hipStream_t s) {
     auto go = [&](auto wo_tag) -> int {
         constexpr int WO = decltype(wo_tag)::value;
         const int pb = dw_planes_pb<K, S, WO>(g, g.Ho * WO, 0);
@@ -1046,7 +1090,7 @@ int dw_wgt_planes(const void* x, const void* dy, DwGeo g, int nimg, int ngroups,
         using PG = PlaneGeo<K, S, WO>;
         const size_t lds = 4 * (size_t)pb * (PG::LH(g.Ho) * PG::LW + g.Ho * WO);
         hipLaunchKernelGGL((k_dw_wgt_planes<K, S, WO, T>), dim3(g.C * ngroups), dim3(kBlock), lds, s, (const T*)x,
-                           (const T*)dy, g, nimg, ngroups, pb, partial);
+                           (const T*)dy, g, nimg, ngroups, pb, partial, fold);
         return 0;
     };
     if (g.Wo == 22) return go(std::integral_constant<int, 22>{});
@@ -1103,11 +1147,13 @@ struct BwdData {
 
 template <int K, int S, typename T>
 struct BwdWeight {
-    static int run(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, hipStream_t s) {
-        if (LSS_DW_LDS && dw_lds_ok<K, S>(g, x, dy)) return dw_wgt_lds<K, S, T>(x, dy, g, nimg, ngroups, partial, s);
-        if (dw_wgt_planes<K, S, T>(x, dy, g, nimg, ngroups, partial, s) == 0) return launch_status();
+    static int run(const void* x, const void* dy, DwGeo g, int nimg, int ngroups, float* partial, DwFold fold,
+                   hipStream_t s) {
+        if (LSS_DW_LDS && dw_lds_ok<K, S>(g, x, dy))
+            return dw_wgt_lds<K, S, T>(x, dy, g, nimg, ngroups, partial, fold, s);
+        if (dw_wgt_planes<K, S, T>(x, dy, g, nimg, ngroups, partial, fold, s) == 0) return launch_status();
         hipLaunchKernelGGL((k_dw_bwd_weight<K, S, 4, S == 1 ? 4 : 2, T>), dim3(g.C * ngroups), dim3(kBlock), 0, s,
-                           (const T*)x, (const T*)dy, g, nimg, ngroups, partial);
+                           (const T*)x, (const T*)dy, g, nimg, ngroups, partial, fold);
         return launch_status();
     }
 };
@@ -1970,7 +2016,19 @@ int lss_dwconv_bwd_weight(const void* x, const void* dy, int32_t dtype, int32_t 
     if (!x || !dy || !partial || ngroups <= 0 || ngroups > N || !geo_ok(N, C, Hi, Wi, K, stride, Ho, Wo))
         return LSS_CONV_EINVAL;
     const DwGeo g{C, Hi, Wi, Ho, Wo, pad_top, pad_left, N * C};
-    return dispatch_kst<BwdWeight>(K, stride, dtype, x, dy, g, (int)N, (int)ngroups, partial, (hipStream_t)stream);
+    return dispatch_kst<BwdWeight>(K, stride, dtype, x, dy, g, (int)N, (int)ngroups, partial, DwFold{nullptr, nullptr},
+                                   (hipStream_t)stream);
+}
+
+int lss_dwconv_bwd_weight2(const void* x, const void* dy, int32_t dtype, int32_t N, int32_t C, int32_t Hi, int32_t Wi,
+                           int32_t K, int32_t stride, int32_t pad_top, int32_t pad_left, int32_t Ho, int32_t Wo,
+                           int32_t ngroups, float* partial, uint32_t* sync, float* dw, void* stream) {
+    if (!x || !dy || !partial || !sync || !dw || ngroups <= 0 || ngroups > N || C > kDwSyncMaxC ||
+        !geo_ok(N, C, Hi, Wi, K, stride, Ho, Wo))
+        return LSS_CONV_EINVAL;
+    const DwGeo g{C, Hi, Wi, Ho, Wo, pad_top, pad_left, N * C};
+    return dispatch_kst<BwdWeight>(K, stride, dtype, x, dy, g, (int)N, (int)ngroups, partial, DwFold{sync, dw},
+                                   (hipStream_t)stream);
 }
 
 int lss_scale_add(const void* x, const void* u, float keep, const void* res, int64_t N, int64_t per, void* y,

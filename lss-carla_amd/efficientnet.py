@@ -152,9 +152,19 @@ class _HipDepthwise(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             groups = max(1, min(N, (N * Ho * Wo) // 8192))
             part = torch.empty(C, groups, K * K, device=x.device, dtype=torch.float32)
-            _lib.check(lib.lss_dwconv_bwd_weight(_lib.ptr(x), _lib.ptr(dy), code, N, C, Hi, Wi, K, stride, pt, pl,
-                                                 Ho, Wo, groups, _lib.ptr(part), st), "lss_dwconv_bwd_weight")
-            dw = part.sum(1).view(C, 1, K, K).to(wdtype)
+            from .norm import _sync
+            sync = _sync(x.device) if C <= 4096 else None
+            if sync is not None:
+                # the channel's last block folds the partials (lss_dwconv_bwd_weight2): no reduction launch
+                dw32 = torch.empty(C, K * K, device=x.device, dtype=torch.float32)
+                _lib.check(lib.lss_dwconv_bwd_weight2(_lib.ptr(x), _lib.ptr(dy), code, N, C, Hi, Wi, K, stride, pt,
+                                                      pl, Ho, Wo, groups, _lib.ptr(part), _lib.ptr(sync),
+                                                      _lib.ptr(dw32), st), "lss_dwconv_bwd_weight2")
+                dw = dw32.view(C, 1, K, K).to(wdtype)
+            else:
+                _lib.check(lib.lss_dwconv_bwd_weight(_lib.ptr(x), _lib.ptr(dy), code, N, C, Hi, Wi, K, stride, pt,
+                                                     pl, Ho, Wo, groups, _lib.ptr(part), st), "lss_dwconv_bwd_weight")
+                dw = part.sum(1).view(C, 1, K, K).to(wdtype)
         return dx, dw, None, None
 
 

@@ -542,3 +542,34 @@ def test_bevencode_dropout2d_mask_matches_torch():
     assert 0 < int((m == 0).sum()) < m.numel()
     assert M._dropout2d_scale(d.eval(), x) is None
     assert M._dropout2d_scale(torch.nn.Dropout2d(0.0).train(), x) is None
+
+
+def test_depthwise_weight_grad_folded_in_kernel():
+    """lss_dwconv_bwd_weight2: the channel's last block folds the group partials (no torch reduction):
+    equal to the unfolded partials summed in group order up to fp32 rounding, the same bits on every call,
+    and the sync workspace left zero-filled."""
+    from lss_carla_amd import _lib, norm
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(3)
+    N, C, H, W, K = 48, 40, 32, 88, 3
+    x = torch.randn(N, C, H, W, generator=g).to(torch.bfloat16).to(DEV)
+    dy = torch.randn(N, C, H, W, generator=g).to(torch.bfloat16).to(DEV)
+    groups = max(1, min(N, (N * H * W) // 8192))
+    assert groups > 1
+    st = _lib.stream_handle(DEV)
+    part = torch.empty(C, groups, K * K, device=DEV)
+    _lib.check(lib.lss_dwconv_bwd_weight(_lib.ptr(x), _lib.ptr(dy), _lib.BF16, N, C, H, W, K, 1, 1, 1, H, W, groups,
+                                         _lib.ptr(part), st), "unfolded")
+    want = part.double().sum(1)
+    sync = norm._sync(DEV)
+    outs = []
+    for _ in range(2):
+        part2 = torch.empty(C, groups, K * K, device=DEV)
+        dw = torch.empty(C, K * K, device=DEV)
+        _lib.check(lib.lss_dwconv_bwd_weight2(_lib.ptr(x), _lib.ptr(dy), _lib.BF16, N, C, H, W, K, 1, 1, 1, H, W, groups,
+                                              _lib.ptr(part2), _lib.ptr(sync), _lib.ptr(dw), st), "folded")
+        torch.cuda.synchronize()
+        outs.append(dw.clone())
+    assert torch.equal(outs[0], outs[1])
+    torch.testing.assert_close(outs[0].double(), want, rtol=1e-5, atol=1e-3)
+    assert int(sync.abs().sum()) == 0
