@@ -200,12 +200,17 @@ struct DwFold {
 };
 constexpr int kDwSyncStride = 32;
 constexpr int kDwSyncMaxC = 4096;
-__device__ __forceinline__ void dw_finish(float* __restrict__ partial, int c, int q, int ngroups, int KK, float v,
+template <int KK>
+__device__ __forceinline__ void dw_finish(float* __restrict__ partial, int c, int q, int ngroups, float v,
                                           const DwFold& f) {
     const int t = threadIdx.x;
     const size_t base = (size_t)c * ngroups * KK;
     if (!f.sync) {
         if (t < KK) partial[base + (size_t)q * KK + t] = v;
+        return;
+    }
+    if (ngroups == 1) {  // the block is the channel: no hand-off
+        if (t < KK) f.dw[(size_t)c * KK + t] = v;
         return;
     }
     if (t >= kWave) return;  // wave 0 (KK <= 25 lanes hold the block's values)
@@ -217,12 +222,27 @@ __device__ __forceinline__ void dw_finish(float* __restrict__ partial, int c, in
     if (t == 0) last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)ngroups - 1u;
     last = __shfl(last, 0, kWave);
     if (!last) return;
-    if (t < KK) {
-        float a = 0.f;
-        for (int qq = 0; qq < ngroups; ++qq)
-            a += __uint_as_float(__hip_atomic_load(pu + base + (size_t)qq * KK + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        f.dw[(size_t)c * KK + t] = a;
+    // lanes over groups (each lane's KK partials loaded together), then a butterfly per tap: fixed order
+    float a[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) a[k] = 0.f;
+    for (int qq = t; qq < ngroups; qq += kWave) {
+        unsigned u[KK];
+#pragma unroll
+        for (int k = 0; k < KK; ++k)
+            u[k] = __hip_atomic_load(pu + base + (size_t)qq * KK + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < KK; ++k) a[k] += __uint_as_float(u[k]);
     }
+    float mine = 0.f;
+#pragma unroll
+    for (int k = 0; k < KK; ++k) {
+        float s = a[k];
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
+        if (t == k) mine = s;
+    }
+    if (t < KK) f.dw[(size_t)c * KK + t] = mine;
     if (t == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -296,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void k_dw_bwd_weight(const T* __restrict__ 
 #pragma unroll
         for (int jw = 0; jw < kBlock / kWave; ++jw) s += s_red[jw][threadIdx.x];
     }
-    dw_finish(partial, c, q, ngroups, K * K, s, fold);
+    dw_finish<K * K>(partial, c, q, ngroups, s, fold);
 }
 
 inline int blocks_for(long n) { return (int)((n + kBlock - 1) / kBlock); }
@@ -694,7 +714,7 @@ __global__ __launch_bounds__(kBlock) void k_dw_wgt_lds(const T* __restrict__ x, 
 #pragma unroll
         for (int jw = 0; jw < kBlock / kWave; ++jw) t += s_red[jw][threadIdx.x];
     }
-    dw_finish(partial, c, q, ngroups, K * K, t, fold);
+    dw_finish<K * K>(partial, c, q, ngroups, t, fold);
 }
 
 // bands and planes per block for the LDS kernels: the whole plane when it fits, several planes per
@@ -1037,7 +1057,7 @@ __global__ __launch_bounds__(kBlock) void k_dw_wgt_planes(const T* __restrict__ 
 #pragma unroll
         for (int jw = 0; jw < kBlock / kWave; ++jw) t += s_red[jw][threadIdx.x];
     }
-    dw_finish(partial, c, q, ngroups, K * K, t, fold);
+    dw_finish<K * K>(partial, c, q, ngroups, t, fold);
 }
 
 #ifndef LSS_DW_PLANES

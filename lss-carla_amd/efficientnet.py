@@ -19,6 +19,7 @@ convolutions, which run on this package's HIP kernels (include/lss_convs.h) on t
 from __future__ import annotations
 
 import math
+import os
 from types import SimpleNamespace
 from typing import List, Tuple
 
@@ -39,6 +40,9 @@ B0_STAGES = (
     (1, 3, 1, 6, 192, 320),
 )
 BN_MOMENTUM = 1 - 0.99
+# depthwise weight gradient folded by each channel's last block (lss_dwconv_bwd_weight2); LSS_DW_FOLD=0 keeps
+# the partial buffer + torch reduction (A/B in profiles/r06/dw_wgrad_fold.txt)
+DW_FOLD = os.environ.get("LSS_DW_FOLD", "1") != "0"
 BN_EPS = 1e-3
 IMAGE_SIZE = 224
 
@@ -153,7 +157,7 @@ class _HipDepthwise(torch.autograd.Function):
             groups = max(1, min(N, (N * Ho * Wo) // 8192))
             part = torch.empty(C, groups, K * K, device=x.device, dtype=torch.float32)
             from .norm import _sync
-            sync = _sync(x.device) if C <= 4096 else None
+            sync = _sync(x.device) if C <= 4096 and DW_FOLD else None
             if sync is not None:
                 # the channel's last block folds the partials (lss_dwconv_bwd_weight2): no reduction launch
                 dw32 = torch.empty(C, K * K, device=x.device, dtype=torch.float32)

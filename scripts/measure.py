@@ -211,6 +211,13 @@ def main():
             else:
                 os.environ["LSS_LIB"] = os.path.join(REPO, "lss-carla_amd", "variants", spec + ".so")
             continue
+        if kind == "env":  # env:NAME=VALUE for the steps that follow (env:NAME= unsets)
+            k, _, v = spec.partition("=")
+            if v:
+                os.environ[k] = v
+            else:
+                os.environ.pop(k, None)
+            continue
         rc = fns[kind](out, spec)
         if rc != 0:
             print(f"step {s!r} failed (rc={rc}); stopping", flush=True)

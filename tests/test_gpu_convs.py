@@ -544,21 +544,26 @@ def test_bevencode_dropout2d_mask_matches_torch():
     assert M._dropout2d_scale(torch.nn.Dropout2d(0.0).train(), x) is None
 
 
-def test_depthwise_weight_grad_folded_in_kernel():
+@pytest.mark.parametrize("N,C,H,W,K,S,pad,Ho", [(48, 40, 32, 88, 3, 1, 1, 32), (48, 24, 22, 22, 5, 1, 2, 22),
+                                                 (48, 24, 11, 11, 5, 1, 2, 11), (48, 16, 22, 22, 3, 2, 0, 11)],
+                         ids=["lds-3x3", "planes-22", "planes-11-one-group", "planes-s2"])
+def test_depthwise_weight_grad_folded_in_kernel(N, C, H, W, K, S, pad, Ho):
     """lss_dwconv_bwd_weight2: the channel's last block folds the group partials (no torch reduction):
     equal to the unfolded partials summed in group order up to fp32 rounding, the same bits on every call,
     and the sync workspace left zero-filled."""
     from lss_carla_amd import _lib, norm
     lib = _lib.load()
     g = torch.Generator().manual_seed(3)
-    N, C, H, W, K = 48, 40, 32, 88, 3
     x = torch.randn(N, C, H, W, generator=g).to(torch.bfloat16).to(DEV)
-    dy = torch.randn(N, C, H, W, generator=g).to(torch.bfloat16).to(DEV)
-    groups = max(1, min(N, (N * H * W) // 8192))
-    assert groups > 1
+    dy = torch.randn(N, C, Ho, Ho, generator=g).to(torch.bfloat16).to(DEV)
+    groups = max(1, min(N, (N * Ho * Ho) // 8192))
+    # fp64 reference: padded (TF 'same' pads the far side for stride 2) grouped-conv weight gradient
+    far = (Ho - 1) * S + K - H - pad
+    xp = torch.nn.functional.pad(x.double(), (pad, far, pad, far))
+    ref = torch.nn.grad.conv2d_weight(xp, (C, 1, K, K), dy.double(), stride=S, groups=C).view(C, K * K)
     st = _lib.stream_handle(DEV)
     part = torch.empty(C, groups, K * K, device=DEV)
-    _lib.check(lib.lss_dwconv_bwd_weight(_lib.ptr(x), _lib.ptr(dy), _lib.BF16, N, C, H, W, K, 1, 1, 1, H, W, groups,
+    _lib.check(lib.lss_dwconv_bwd_weight(_lib.ptr(x), _lib.ptr(dy), _lib.BF16, N, C, H, W, K, S, pad, pad, Ho, Ho, groups,
                                          _lib.ptr(part), st), "unfolded")
     want = part.double().sum(1)
     sync = norm._sync(DEV)
@@ -566,10 +571,11 @@ def test_depthwise_weight_grad_folded_in_kernel():
     for _ in range(2):
         part2 = torch.empty(C, groups, K * K, device=DEV)
         dw = torch.empty(C, K * K, device=DEV)
-        _lib.check(lib.lss_dwconv_bwd_weight2(_lib.ptr(x), _lib.ptr(dy), _lib.BF16, N, C, H, W, K, 1, 1, 1, H, W, groups,
+        _lib.check(lib.lss_dwconv_bwd_weight2(_lib.ptr(x), _lib.ptr(dy), _lib.BF16, N, C, H, W, K, S, pad, pad, Ho, Ho, groups,
                                               _lib.ptr(part2), _lib.ptr(sync), _lib.ptr(dw), st), "folded")
         torch.cuda.synchronize()
         outs.append(dw.clone())
     assert torch.equal(outs[0], outs[1])
     torch.testing.assert_close(outs[0].double(), want, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(outs[0].double(), ref, rtol=1e-4, atol=1e-2)
     assert int(sync.abs().sum()) == 0
