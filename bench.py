@@ -69,6 +69,7 @@ def parse():
     ap.add_argument("--dtype", default="", choices=["", "bf16", "fp32"])
     ap.add_argument("--bev-layout", default="", choices=["", "nhwc", "nchw"])
     ap.add_argument("--trunk-channels-last", type=int, default=0)
+    ap.add_argument("--up1-channels-last", type=int, default=1)
     ap.add_argument("--dw-impl", default="hip", choices=["hip", "miopen", "native", "fp32"],
                     help="depthwise convs of the trunk: HIP kernels, MIOpen, PyTorch native, MIOpen in fp32")
     ap.add_argument("--miopen-find", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
@@ -332,7 +333,7 @@ def measure_in_graph(args) -> dict | None:
     # the rest of this run's configuration, so the child measures the same step
     for flag in ("miopen_find", "hip_bn", "bn_relu_y", "hip_adam", "fuse_depthnet", "hip_dropout", "hip_pw", "plan_at",
                  "flip_bwd",
-                 "plan_ordered", "trunk_channels_last", "param_groups",
+                 "plan_ordered", "trunk_channels_last", "up1_channels_last", "param_groups",
                  "flat_params", "overlap_all_reduce", "dw_impl"):
         cmd += ["--" + flag.replace("_", "-"), str(getattr(args, flag))]
     try:
@@ -482,6 +483,10 @@ def build_model(args, dev, gc, dac):
         model.bevencode.to(memory_format=torch.channels_last)
     if args.trunk_channels_last:
         model.camencode.to(memory_format=torch.channels_last)
+    elif args.up1_channels_last:
+        # CamEncode.up1's 3x3 convs see channels-last maps: channels-last weights spare MIOpen's weight
+        # copy per forward and the layout-changing gradient copy into the flat parameters
+        model.camencode.up1.to(memory_format=torch.channels_last)
     from lss_carla_amd import norm, models
     norm.USE_HIP_BN = bool(args.hip_bn)
     norm.RECOMPUTE_RELU_Y = args.bn_relu_y == "recompute"

@@ -23,6 +23,8 @@ from __future__ import annotations
 
 from typing import Dict, List, Tuple
 
+import os
+
 import torch
 from torch import nn
 
@@ -85,13 +87,37 @@ class _Materialize(torch.autograd.Function):
         return d_master, None
 
 
+GATHER_SPLIT = os.environ.get("LSS_FLAT_GATHER_SPLIT", "1") != "0"
+
+
 def _gather(dst_views, grads, buf) -> None:
     """Copy the per-parameter gradients into their views of buf (unused parameters: zero)."""
     if any(g is None for g in grads):
         buf.zero_()
-    pairs = [(d, g) for d, g in zip(dst_views, grads) if g is not None]
-    if pairs:
+    pairs = [(d, _restride(g, d)) for d, g in zip(dst_views, grads) if g is not None]
+    # _foreach_copy_ takes its multi-tensor route only when EVERY pair has the same dtype and strides;
+    # one odd pair (a channels-last conv weight gradient into a contiguous view) would send all of them
+    # through a strided copy each: the odd ones are copied on their own
+    if not GATHER_SPLIT:  # (A/B: the single _foreach_copy_ of round 5)
         torch._foreach_copy_([d for d, _ in pairs], [g.to(d.dtype) for d, g in pairs])
+        return
+    fast = [(d, g) for d, g in pairs if g.dtype == d.dtype and g.stride() == d.stride()]
+    if fast:
+        torch._foreach_copy_([d for d, _ in fast], [g for _, g in fast])
+    for d, g in pairs:
+        if g.dtype != d.dtype or g.stride() != d.stride():
+            d.copy_(g)
+
+
+def _restride(g: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
+    """g re-viewed with d's strides when the two differ only on size-1 dimensions (a 1x1 conv weight's
+    gradient in (O, I, 1, 1) contiguous strides against a channels-last parameter view): the same memory
+    order, so _foreach_copy_ keeps its one-launch multi-tensor route instead of a strided copy per tensor."""
+    if g.shape != d.shape or g.stride() == d.stride() or not g.is_contiguous():
+        return g
+    if all(gs == ds for gs, ds, n in zip(g.stride(), d.stride(), d.shape) if n != 1):
+        return g.as_strided(d.shape, d.stride())
+    return g
 
 
 class FlatParams:
