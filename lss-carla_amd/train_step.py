@@ -26,6 +26,7 @@ off-by-default options; its measurements stay in profiles/r03.)
 """
 from __future__ import annotations
 
+import time
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -143,14 +144,22 @@ class TrainStep:
                     on_warmup(i)
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
+        mode = "global"
+        if self.collectives:
+            # the process group's watchdog thread polls the warm-up's all-reduce events (every 100 ms)
+            # until it reaps them; one such query during a global-mode capture aborts the process
+            # ("operation not permitted when stream is capturing", seen in a world-size-1 RCCL run).
+            # Let it reap the completed works, and restrict the capture's checks to this thread.
+            time.sleep(0.5)
+            mode = "thread_local"
         g_fb, g_up = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_fb):
+        with torch.cuda.graph(g_fb, capture_error_mode=mode):
             # detached: holding the captured autograd graph would keep its AccumulateGrad nodes
             # (bound to the capture stream) alive into later eager steps. The gradients allocated
             # here (graph pool) are what graph B and the all-reduce read on every replay.
             self.static_loss = self.forward_backward().detach()
         self.graph_grads = [p.grad for p in self.params]
-        with torch.cuda.graph(g_up, pool=g_fb.pool()):
+        with torch.cuda.graph(g_up, pool=g_fb.pool(), capture_error_mode=mode):
             self.update()
         self.graphs = (g_fb, g_up)
 
