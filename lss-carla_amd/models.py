@@ -440,6 +440,25 @@ def bn_relu_head1(bn: nn.BatchNorm2d, head: nn.Conv2d, x: torch.Tensor) -> torch
     return _BnReluHead1.apply(x, bn.weight, bn.bias, head.weight, head.bias, bn)
 
 
+class _Subsample(torch.autograd.Function):
+    """x[:, :, ::s, ::s] as a channels-last copy (what F.linear over the pixels needs anyway), its gradient
+    scattered into one zero-filled map: two SliceBackward nodes each allocated, zero-filled and copied a
+    map of their own (the H slice's at full size), and matmul cloned the strided view in the forward."""
+
+    @staticmethod
+    def forward(ctx, x, s):
+        fmt = torch.contiguous_format if x.is_contiguous() else torch.channels_last
+        ctx.meta = (x.shape, s, fmt)
+        return x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
+
+    @staticmethod
+    def backward(ctx, g):
+        shape, s, fmt = ctx.meta
+        dx = torch.empty(shape, device=g.device, dtype=g.dtype, memory_format=fmt).zero_()
+        dx[:, :, ::s, ::s] = g
+        return dx, None
+
+
 def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """A 1x1 nn.Conv2d (stride s, no padding) applied as a GEMM over the channels of every s-th pixel
     (F.linear: hipBLASLt) on CUDA maps, with the module's own weight and bias (same math). MIOpen's
@@ -456,7 +475,7 @@ def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     if s == 1 and _head1_eligible(conv, x):
         return _Head1x1.apply(x, conv.weight, conv.bias)
     if s > 1:
-        x = x[:, :, ::s, ::s]
+        x = _Subsample.apply(x, s)
     w = conv.weight.reshape(conv.out_channels, conv.in_channels)
     y = F.linear(x.permute(0, 2, 3, 1), w, conv.bias)  # (N, H, W, O)
     return y.permute(0, 3, 1, 2)  # (N, O, H, W), channels-last strides
